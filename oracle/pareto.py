@@ -1,0 +1,92 @@
+"""Oracle: Pareto filter, 2-D cell decomposition and exact hypervolume (fp64 numpy).
+
+TEST INFRASTRUCTURE ONLY — see oracle/__init__.py.
+
+* ``calc_pf`` restates util_functions.py:64-77: the first front of
+  ``pygmo.fast_non_dominated_sorting`` (pygmo>=2.0, absent here): the rows no other row
+  Pareto-dominates, in ascending row order, duplicates kept; fewer than 2 rows → identity.
+* ``decompose_into_cells`` restates the 2-D WFG-style decomposition of emo.py:55-152
+  (≡ util_functions.py:414-517) in closed form; pinned against the
+  reference implementation's own output (tests/golden/cells.npz).
+* ``hypervolume`` is the exact dominated volume that ``pygmo.hypervolume(PF).compute(r)``
+  (util_functions.py:198-206) and pymoo's ``HV`` (optimisers.py:216-220) return.
+"""
+import numpy as np
+
+
+def dominates_matrix(Y):
+    Y = np.asarray(Y, np.float64)
+    le = np.all(Y[:, None, :] <= Y[None, :, :], axis=2)
+    lt = np.any(Y[:, None, :] < Y[None, :, :], axis=2)
+    return le & lt          # D[a, b]: a dominates b
+
+
+def calc_pf(Y):
+    Y = np.asarray(Y, np.float64)
+    if len(Y) < 2:
+        return Y
+    D = dominates_matrix(Y)
+    first = ~np.any(D, axis=0)
+    return Y[first]
+
+
+def decompose_into_cells(pf, ideal_point, max_point):
+    """Closed form of emo.py:55-152 for 2 objectives → (P+1, 2, 2) [upper, lower].
+
+    PF sorted by f1 ascending (emo.py:126; Python's stable ``sorted``), p_1..p_P:
+      cell 0    : upper = (p1.f1, max(p1.f2, R1)),  lower = (I0, I1)            (emo.py:142-148)
+      cell j    : upper = (p_{j+1}.f1, p_j.f2),      lower = (max(p_j.f1, I0), max(I0, I1))   (1 ≤ j < P)
+      cell P    : upper = (max(pP.f1, R0), pP.f2),    lower = (max(pP.f1, I0), max(I0, I1))
+    Quirk 5 (reference-exact): the lower bound of cells j ≥ 1 is
+    ``np.maximum(np.rot90(incl)[-1], hv[-1])`` (emo.py:102) with incl = [p, ideal], so its
+    f2 coordinate is max(I0, I1) — ideal's f1 leaks into f2; it equals I1 only when I0 ≤ I1.
+    """
+    pf = np.asarray(pf, np.float64).reshape(-1, 2)
+    I = np.asarray(ideal_point, np.float64)
+    R = np.asarray(max_point, np.float64)
+    order = np.argsort(pf[:, 0], kind="stable")
+    p = pf[order]
+    P = len(p)
+    cells = np.empty((P + 1, 2, 2))
+    cells[0, 0] = (p[0, 0], max(p[0, 1], R[1]))
+    cells[0, 1] = (I[0], I[1])
+    lo2 = max(I[0], I[1])
+    for j in range(1, P):
+        cells[j, 0] = (p[j, 0], p[j - 1, 1])
+        cells[j, 1] = (max(p[j - 1, 0], I[0]), lo2)
+    cells[P, 0] = (max(p[P - 1, 0], R[0]), p[P - 1, 1])
+    cells[P, 1] = (max(p[P - 1, 0], I[0]), lo2)
+    return cells
+
+
+def hypervolume(pts, r):
+    """Exact hypervolume of the region dominated by ``pts`` and bounded by ``r`` (k = 2 or 3)."""
+    pts = np.asarray(pts, np.float64)
+    r = np.asarray(r, np.float64)
+    if len(pts) == 0:
+        return 0.0
+    pts = pts[np.all(pts < r, axis=1)]
+    if len(pts) == 0:
+        return 0.0
+    k = pts.shape[1]
+    if k == 2:
+        return _hv2d(pts, r)
+    if k == 3:
+        zs = np.unique(pts[:, 2])
+        total = 0.0
+        for i, z in enumerate(zs):
+            z_next = zs[i + 1] if i + 1 < len(zs) else r[2]
+            total += _hv2d(pts[pts[:, 2] <= z][:, :2], r[:2]) * (z_next - z)
+        return total
+    raise NotImplementedError("hypervolume: k must be 2 or 3")
+
+
+def _hv2d(pts, r):
+    p = pts[np.lexsort((pts[:, 1], pts[:, 0]))]
+    total = 0.0
+    best_f2 = r[1]
+    for x, y in p:
+        if y < best_f2:
+            total += (r[0] - x) * (best_f2 - y)
+            best_f2 = y
+    return total

@@ -1,0 +1,286 @@
+"""Generate the golden fixtures in tests/golden/*.npz from the reference's OWN functions.
+
+Runs only in the build container (it reads /root/reference, which never travels to the
+GPU box).  The committed .npz files hold inputs and expected outputs only.
+
+The reference (aje220/OptiMOBO v0.2.1, pure Python) imports three third-party packages
+that are not installed here: pygmo, GPy and pymoo (requirements.txt:1-5).  The
+acquisition arithmetic we pin lives in the reference's own files and only needs those
+packages for module-level imports and two pygmo algorithms, so we register minimal test
+doubles in ``sys.modules`` before importing:
+  * ``pygmo.fast_non_dominated_sorting`` → first-front filter (oracle.pareto.calc_pf rule);
+  * ``pygmo.hypervolume(pts).compute(r)`` → exact HV that raises ValueError when a point is
+    not inside the reference box, like pagmo's ``assert_minimisation``;
+  * empty ``GPy`` / ``pymoo`` names (never called on the pinned paths).
+``model.predict`` is supplied by ``ConstModel`` (duck typing, as the reference's own
+callers pass GPy models): it returns fixed (μ, σ²) so the reference acquisition code runs
+its arithmetic on known posterior moments.  numpy 2.x removed ``np.product`` (used at
+util_functions.py:410, emo.py:220); it is aliased to ``np.prod``.
+
+GP posterior fixtures come from scikit-learn's GaussianProcessRegressor (independent of
+both GPy and this build) with the reference's kernel (Matern-5/2 ARD, noise 0 + 1e-8).
+
+Usage:  python tests/golden/make_golden.py
+"""
+import os
+import sys
+import types
+
+import numpy as np
+from scipy.stats import qmc, norm
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, REPO)
+
+from oracle import pareto as opareto  # noqa: E402
+from oracle import gp as ogp  # noqa: E402
+
+
+# ----------------------------------------------------------------------------- doubles
+def _install_doubles():
+    np.product = np.prod
+
+    pg = types.ModuleType("pygmo")
+
+    def fast_non_dominated_sorting(Y):
+        Y = np.asarray(Y, np.float64)
+        D = opareto.dominates_matrix(Y)
+        first = np.nonzero(~np.any(D, axis=0))[0]
+        return [list(first)], None, None, None
+
+    class hypervolume:
+        def __init__(self, pts):
+            self.pts = np.atleast_2d(np.asarray(pts, np.float64))
+
+        def compute(self, r):
+            r = np.asarray(r, np.float64)
+            for p in self.pts:
+                if np.any(p > r) or np.all(p == r):
+                    raise ValueError("Reference point is invalid: points must dominate it")
+            return opareto.hypervolume(self.pts, r)
+
+    pg.fast_non_dominated_sorting = fast_non_dominated_sorting
+    pg.hypervolume = hypervolume
+    sys.modules["pygmo"] = pg
+
+    gpy = types.ModuleType("GPy")
+    gpy.kern = types.SimpleNamespace()
+    gpy.models = types.SimpleNamespace()
+    gpy.plotting = types.SimpleNamespace(change_plotting_library=lambda *a, **k: None)
+    sys.modules["GPy"] = gpy
+
+    for name in ["pymoo", "pymoo.util", "pymoo.util.ref_dirs", "pymoo.indicators", "pymoo.indicators.hv",
+                 "pymoo.gradient", "pymoo.gradient.toolbox", "pymoo.util.cache", "pymoo.util.misc"]:
+        sys.modules[name] = types.ModuleType(name)
+    sys.modules["pymoo.util.ref_dirs"].get_reference_directions = None
+    sys.modules["pymoo.indicators.hv"].HV = None
+    sys.modules["pymoo.util.cache"].Cache = lambda f: f
+    sys.modules["pymoo.util.misc"].at_least_2d_array = None
+    sys.path.insert(0, REF)
+
+
+class ConstModel:
+    """Duck-typed stand-in for a fitted GPy model: predict → fixed (μ (1,1), σ² (1,1))."""
+
+    def __init__(self, mu, var):
+        self.mu, self.var = float(mu), float(var)
+
+    def predict(self, X):
+        return np.array([[self.mu]]), np.array([[self.var]])
+
+
+def cached_samples(k, m, seed=0):
+    """optimisers.py:121-141 (_get_cached_samples) with an explicit seed."""
+    s = qmc.Sobol(d=k, scramble=True, seed=seed).random_base2(m=m)
+    return np.asarray(list(zip(*[norm.ppf(s[:, i]) for i in range(k)])))
+
+
+def zdt1(X):
+    f1 = X[:, 0]
+    g = 1 + 9.0 / (X.shape[1] - 1) * np.sum(X[:, 1:], axis=1)
+    return np.column_stack([f1, g * (1 - np.sqrt(f1 / g))])
+
+
+def random_pf(rng, P, k=2):
+    """A mutually non-dominated set of P points in [0,1]^k (k=2: a curved front)."""
+    if k == 2:
+        x = np.sort(rng.uniform(0.02, 0.98, P))
+        return np.column_stack([x, 1 - np.sqrt(x)])
+    pts = rng.uniform(0, 1, (P * 8, k))
+    pts = pts / np.linalg.norm(pts, axis=1, keepdims=True)
+    pf = opareto.calc_pf(pts)
+    return pf[:P]
+
+
+# ----------------------------------------------------------------------------- fixtures
+def make_posterior(rng):
+    for n, d in [(20, 2), (128, 6), (512, 6)]:
+        X = rng.uniform(0, 1, (n, d))
+        Y = zdt1(X) if d > 1 else X
+        ls = rng.uniform(0.2, 2.0, d)
+        out = {"X": X, "Y": Y, "lengthscale": ls}
+        # candidates: Sobol points, plus exact training points and near-duplicates
+        Xc = qmc.Sobol(d=d, scramble=True, seed=7).random_base2(m=8)
+        Xc[:4] = X[:4]
+        Xc[4:8] = X[4:8] + 1e-7
+        out["Xc"] = Xc
+        for obj in range(2):
+            var = float(np.var(Y[:, obj]))
+            mu_s, var_s = ogp.sklearn_posterior(X, Y[:, obj], ls, var, Xc)
+            out[f"variance{obj}"] = np.float64(var)
+            out[f"mu{obj}"] = mu_s
+            out[f"var{obj}"] = var_s
+        np.savez_compressed(os.path.join(HERE, f"posterior_n{n}_d{d}.npz"), **out)
+
+
+def make_ehvi2d(rng, uf):
+    cache = cached_samples(2, 5, seed=0)
+    for P in [1, 3, 9, 30]:
+        pf = random_pf(rng, P)
+        r = pf.max(axis=0) + 0.1 * (pf.max(axis=0) - pf.min(axis=0) + 0.1)
+        N = 96
+        mu = np.vstack([rng.uniform(-0.2, 1.2, N), rng.uniform(-0.2, 1.2, N)])
+        var = np.vstack([10 ** rng.uniform(-5, -0.5, N), 10 ** rng.uniform(-5, -0.5, N)])
+        var[0, -1] = -1e-9   # negative posterior variance → reference NaN (sqrt of negative)
+        ref = np.empty(N)
+        tb = np.empty(N)
+        with np.errstate(invalid="ignore"):
+            for i in range(N):
+                models = [ConstModel(mu[0, i], var[0, i]), ConstModel(mu[1, i], var[1, i])]
+                ref[i] = np.asarray(uf.EHVI(np.zeros(2), models, r, pf, cache)).reshape(-1)[0]
+                s = np.sqrt(var[:, i])
+                v = np.asarray(uf.EHVI_2D_aux(pf, r, mu[:, i], np.array([[s[0], s[1]]]))).reshape(-1)[0]
+                # the stripe the reference loop omits (util_functions.py:120)
+                last_f1 = pf[np.argsort(pf[:, 1])][-1, 0]
+                v += (uf.psi_cal(np.array([last_f1]), np.array([last_f1]), mu[0, i], s[0])
+                      * uf.psi_cal(np.array([r[1]]), np.array([r[1]]), mu[1, i], s[1]))
+                tb[i] = np.asarray(v).reshape(-1)[0]
+        np.savez_compressed(os.path.join(HERE, f"ehvi2d_P{P}.npz"), pf=pf, r=r, cache=cache, mu=mu, var=var,
+                            ehvi_reference=ref, ehvi_textbook=tb)
+
+
+def make_ehvi3d(rng, uf):
+    cache = cached_samples(3, 5, seed=0)
+    pf = random_pf(rng, 12, k=3)
+    r = np.array([1.5, 1.5, 1.5])
+    N = 48
+    mu = rng.uniform(0.0, 1.2, (3, N))
+    var = np.vstack([10 ** rng.uniform(-5, -1.5, N)] * 3)
+    var[0, :8] = 0.3          # wide distributions: samples leave the box → pygmo raises
+    ref = np.full(N, np.nan)
+    raises = np.zeros(N, bool)
+    for i in range(N):
+        models = [ConstModel(mu[j, i], var[j, i]) for j in range(3)]
+        try:
+            ref[i] = uf.EHVI_3D(np.zeros(3), models, r, pf, cache)
+        except ValueError:
+            raises[i] = True
+    np.savez_compressed(os.path.join(HERE, "ehvi3d.npz"), pf=pf, r=r, cache=cache, mu=mu, var=var,
+                        hv_pf=opareto.hypervolume(pf, r), ehvi_reference=ref, raises=raises)
+
+
+def make_cells_hvpoi(rng, uf, emo_mod):
+    out = {}
+    EMO = emo_mod.EMO
+    for t, P in enumerate([1, 2, 5, 17]):
+        pf = random_pf(rng, P)
+        ideal = pf.min(axis=0) - 0.05
+        mx = pf.max(axis=0) + 0.2
+        obj = object.__new__(EMO)
+        obj.ideal_point, obj.max_point, obj.n_obj = ideal, mx, 2
+        cells = obj.decompose_into_cells(pf)
+        cells_uf = uf.decompose_into_cells(pf, ideal, mx)
+        assert np.array_equal(cells, cells_uf)
+        N = 64
+        mu = np.vstack([rng.uniform(ideal[0] - 0.1, mx[0], N), rng.uniform(ideal[1] - 0.1, mx[1], N)])
+        var = np.vstack([10 ** rng.uniform(-6, -0.5, N), 10 ** rng.uniform(-6, -0.5, N)])
+        vals = np.empty(N)
+        for i in range(N):
+            models = [ConstModel(mu[0, i], var[0, i]), ConstModel(mu[1, i], var[1, i])]
+            vals[i] = obj.hypervolume_based_PoI(np.zeros(2), models, None, cells)
+        out.update({f"pf{t}": pf, f"ideal{t}": ideal, f"max{t}": mx, f"cells{t}": cells,
+                    f"mu{t}": mu, f"var{t}": var, f"hvpoi{t}": vals})
+    np.savez_compressed(os.path.join(HERE, "cells_hvpoi.npz"), **out)
+
+
+def make_expdec(rng, uf, sc):
+    out = {}
+    names = ["WeightedSum", "Tchebicheff", "AugmentedTchebicheff", "ModifiedTchebicheff",
+             "ExponentialWeightedCriterion", "WeightedNorm", "WeightedPower", "WeightedProduct",
+             "PBI", "IPBI", "QPBI", "APD"]
+    for k in (2, 3):
+        cache = cached_samples(k, 3 if k == 2 else 5, seed=0)
+        ideal = np.zeros(k)
+        mx = np.array([700.0, 12.0, 5.0][:k])
+        N = 48
+        mu = np.vstack([rng.uniform(0, 1.0, N) * mx[j] for j in range(k)])
+        var = np.vstack([10 ** rng.uniform(-4, 0.5, N) * mx[j] for j in range(k)])
+        w = np.array([0.3, 0.7]) if k == 2 else np.array([0.2, 0.5, 0.3])
+        out[f"k{k}_cache"], out[f"k{k}_ideal"], out[f"k{k}_max"] = cache, ideal, mx
+        out[f"k{k}_mu"], out[f"k{k}_var"], out[f"k{k}_w"] = mu, var, w
+        for name in names:
+            s = getattr(sc, name)(ideal, mx)
+            # min over a few "ysample" rows, as optimisers.py:250 does
+            ys = np.column_stack([rng.uniform(0, 1, 16) * mx[j] for j in range(k)])
+            agg_min = np.min([s(y, w) for y in ys])
+            vals = np.empty(N)
+            with np.errstate(all="ignore"):
+                for i in range(N):
+                    models = [ConstModel(mu[j, i], var[j, i]) for j in range(k)]
+                    vals[i] = uf.expected_decomposition(np.zeros(2), models, w, s, agg_min, cache)
+            out[f"k{k}_{name}_min"] = np.float64(agg_min)
+            out[f"k{k}_{name}"] = vals
+    np.savez_compressed(os.path.join(HERE, "expdec.npz"), **out)
+
+
+def make_ei(rng, opt_mod, parego_mod):
+    mono = object.__new__(opt_mod.MonoSurrogateOptimiser)
+    par = object.__new__(parego_mod.ParEGO)
+    N = 128
+    mu = rng.uniform(-1, 1, N)
+    var = 10 ** rng.uniform(-9, 0, N)
+    var[:4] = 0.0
+    best = -0.2
+    e_mono = np.empty(N)
+    e_par = np.empty(N)
+    for i in range(N):
+        m = ConstModel(mu[i], var[i])
+        e_mono[i] = mono._expected_improvement(np.zeros(3), m, best)[0]
+        e_par[i] = par._expected_improvement(np.zeros(3), m, best)[0]
+    np.savez_compressed(os.path.join(HERE, "ei.npz"), mu=mu, var=var, best=best, ei_mono=e_mono, ei_parego=e_par)
+
+
+def make_calc_pf(rng, uf):
+    out = {}
+    for t, (n, k) in enumerate([(1, 2), (40, 2), (60, 3)]):
+        Y = rng.uniform(0, 1, (n, k))
+        if n > 4:
+            Y[3] = Y[2]          # duplicate rows stay in the first front together
+        out[f"Y{t}"] = Y
+        out[f"pf{t}"] = np.asarray(uf.calc_pf(Y))
+    np.savez_compressed(os.path.join(HERE, "calc_pf.npz"), **out)
+
+
+def main():
+    _install_doubles()
+    import optimobo.util_functions as uf
+    import optimobo.scalarisations as sc
+    import optimobo.algorithms.emo as emo_mod
+    import optimobo.algorithms.optimisers as opt_mod
+    import optimobo.algorithms.parego as parego_mod
+
+    rng = np.random.default_rng(20261015)
+    make_posterior(rng)
+    make_ehvi2d(rng, uf)
+    make_ehvi3d(rng, uf)
+    make_cells_hvpoi(rng, uf, emo_mod)
+    make_expdec(rng, uf, sc)
+    make_ei(rng, opt_mod, parego_mod)
+    make_calc_pf(rng, uf)
+    print("golden fixtures written to", HERE)
+
+
+if __name__ == "__main__":
+    main()

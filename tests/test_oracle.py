@@ -1,0 +1,136 @@
+"""The oracle (CPU restatement) against the golden vectors made from the reference itself.
+
+Tolerances: both sides are fp64 numpy of the same formulas (≤1e-12 rel in practice); the
+posterior is pinned against scikit-learn's independent implementation.
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from oracle import acquisition as acq
+from oracle import gp as ogp
+from oracle import pareto
+from oracle import scalarisations as osc
+
+
+def load(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name), allow_pickle=False)
+
+
+@pytest.mark.parametrize("name", ["posterior_n20_d2.npz", "posterior_n128_d6.npz", "posterior_n512_d6.npz"])
+def test_posterior_vs_sklearn(golden_dir, name):
+    z = load(golden_dir, name)
+    for obj in range(2):
+        g = ogp.ExactGP(z["X"], z["Y"][:, obj], z["lengthscale"], float(z[f"variance{obj}"]))
+        mu, var = g.predict(z["Xc"])
+        scale = float(z[f"variance{obj}"])
+        # μ: α has large cancelling entries → compare against the posterior scale
+        np.testing.assert_allclose(mu[:, 0], z[f"mu{obj}"], rtol=1e-6, atol=1e-7 * np.sqrt(scale))
+        np.testing.assert_allclose(var[:, 0], z[f"var{obj}"], rtol=1e-6, atol=1e-9 * scale)
+
+
+@pytest.mark.parametrize("P", [1, 3, 9, 30])
+def test_ehvi2d_reference_mode(golden_dir, P):
+    z = load(golden_dir, f"ehvi2d_P{P}.npz")
+    with np.errstate(invalid="ignore"):
+        got = acq.ehvi2d(z["mu"], z["var"], z["pf"], z["r"], z["cache"], mode="reference")
+    ref = z["ehvi_reference"]
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    ok = ~np.isnan(ref)
+    np.testing.assert_allclose(got[ok], ref[ok], rtol=1e-10, atol=1e-13)
+    assert np.isnan(ref[-1])   # negative variance → NaN, as the reference
+
+
+@pytest.mark.parametrize("P", [1, 3, 9, 30])
+def test_ehvi2d_textbook_mode(golden_dir, P):
+    z = load(golden_dir, f"ehvi2d_P{P}.npz")
+    with np.errstate(invalid="ignore"):
+        got = acq.ehvi2d(z["mu"], z["var"], z["pf"], z["r"], z["cache"], mode="textbook")
+    ref = z["ehvi_textbook"]
+    ok = ~np.isnan(ref)
+    np.testing.assert_allclose(got[ok], ref[ok], rtol=1e-10, atol=1e-13)
+
+
+def test_ehvi2d_textbook_matches_monte_carlo():
+    """Textbook mode is the exact EHVI: compare against 2e5-sample MC of the HV improvement."""
+    rng = np.random.default_rng(3)
+    x = np.sort(rng.uniform(0.05, 0.95, 7))
+    pf = np.column_stack([x, 1 - np.sqrt(x)])
+    r = np.array([1.1, 1.1])
+    hv0 = pareto.hypervolume(pf, r)
+    for mu, sd in [((0.3, 0.4), (0.2, 0.15)), ((0.7, 0.1), (0.05, 0.3))]:
+        y = rng.standard_normal((200000, 2)) * np.array(sd) + np.array(mu)
+        # HV improvement of each sample, vectorised over the 2-D staircase
+        hvi = np.array([pareto.hypervolume(np.vstack([pf, s]), r) - hv0 for s in y[:4000]])
+        mc = hvi.mean()
+        ex = acq.ehvi2d(np.array(mu)[:, None], np.square(np.array(sd))[:, None], pf, r, None, mode="textbook")[0]
+        assert abs(ex - mc) < 4 * hvi.std() / np.sqrt(len(hvi)) + 1e-12
+
+
+def test_ehvi3d_reference(golden_dir):
+    z = load(golden_dir, "ehvi3d.npz")
+    val, raises = acq.ehvi3d_reference(z["mu"], z["var"], float(z["hv_pf"]), z["r"], z["cache"])
+    assert np.array_equal(raises, z["raises"])
+    ok = ~z["raises"]
+    assert ok.sum() > 10 and z["raises"].sum() > 0
+    np.testing.assert_allclose(val[ok], z["ehvi_reference"][ok], rtol=1e-10, atol=1e-14)
+    assert abs(pareto.hypervolume(z["pf"], z["r"]) - float(z["hv_pf"])) < 1e-14
+
+
+def test_cells_and_hvpoi(golden_dir):
+    z = load(golden_dir, "cells_hvpoi.npz")
+    for t in range(4):
+        cells = pareto.decompose_into_cells(z[f"pf{t}"], z[f"ideal{t}"], z[f"max{t}"])
+        np.testing.assert_array_equal(cells, z[f"cells{t}"])
+        got = acq.hvpoi(z[f"mu{t}"], z[f"var{t}"], cells)
+        np.testing.assert_allclose(got, z[f"hvpoi{t}"], rtol=1e-10, atol=1e-15)
+
+
+def test_cells_closed_form_random_fronts():
+    """Closed form vs the 2-D WFG decomposition on many random fronts (property check)."""
+    rng = np.random.default_rng(11)
+    for _ in range(200):
+        P = int(rng.integers(1, 12))
+        pf = pareto.calc_pf(rng.uniform(0, 1, (P * 3, 2)))
+        cells = pareto.decompose_into_cells(pf, [-0.1, -0.1], [1.2, 1.2])
+        # with I0 == I1 the cells tile the region below the attainment surface inside [ideal, max]
+        area = np.prod(cells[:, 0, :] - cells[:, 1, :], axis=1).sum()
+        dominated = pareto.hypervolume(pf, np.array([1.2, 1.2]))
+        assert abs(area + dominated - 1.3 * 1.3) < 1e-12
+
+
+@pytest.mark.parametrize("k", [2, 3])
+@pytest.mark.parametrize("cls", osc.ALL, ids=lambda c: c.__name__)
+def test_expected_decomposition(golden_dir, k, cls):
+    z = load(golden_dir, "expdec.npz")
+    s = cls(z[f"k{k}_ideal"], z[f"k{k}_max"])
+    with np.errstate(all="ignore"):
+        got = acq.expected_decomposition(z[f"k{k}_mu"], z[f"k{k}_var"], z[f"k{k}_cache"], s, z[f"k{k}_w"],
+                                         float(z[f"k{k}_{cls.__name__}_min"]))
+    ref = z[f"k{k}_{cls.__name__}"]
+    np.testing.assert_allclose(got, ref, rtol=1e-10, atol=1e-12)
+
+
+def test_ei(golden_dir):
+    z = load(golden_dir, "ei.npz")
+    np.testing.assert_allclose(acq.ei(z["mu"], z["var"], float(z["best"]), 0.0), z["ei_mono"], rtol=1e-12, atol=1e-300)
+    np.testing.assert_allclose(acq.ei(z["mu"], z["var"], float(z["best"]), 1e-6), z["ei_parego"], rtol=1e-12, atol=1e-300)
+
+
+def test_calc_pf(golden_dir):
+    z = load(golden_dir, "calc_pf.npz")
+    for t in range(3):
+        np.testing.assert_array_equal(pareto.calc_pf(z[f"Y{t}"]), z[f"pf{t}"])
+
+
+def test_argmax_rule():
+    v = np.array([1.0, np.nan, 3.0, 3.0, -np.inf])
+    assert acq.argmax(v) == (3.0, 2)
+    assert acq.argmax(v, offset=10) == (3.0, 12)
+    assert acq.argmax(np.array([np.nan, -np.inf])) == (-np.inf, -1)
+
+
+def test_fixture_files_present(golden_dir):
+    assert len(glob.glob(os.path.join(golden_dir, "*.npz"))) >= 12

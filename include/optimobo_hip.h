@@ -1,0 +1,146 @@
+/*
+ * optimobo_hip.h — C-ABI of liboptimobo_hip.so, the MI355X (gfx950) hot path of
+ * OptiMOBO's acquisition maximisation.
+ *
+ * The reference (aje220/OptiMOBO v0.2.1) is pure Python: its "boundary" is duck typing, not
+ * an FFI.  Each entry point below replaces one arithmetic site of the reference (cited
+ * file:line, relative to the reference root) and is bound from Python with ctypes
+ * (optimobo_amd/_lib.py; INTEGRATION.md shows the binding a maintainer would add).
+ *
+ * Conventions
+ *   - Every array argument named *_dev is a DEVICE pointer owned by the caller (e.g. a torch
+ *     tensor's data_ptr()); fp64, C-contiguous.  Small fixed-size vectors (reference point,
+ *     weights, bounds, scalarisation parameters) are HOST pointers read during the call.
+ *   - Calls are asynchronous on the context's stream (omb_set_stream), except omb_argmax
+ *     and omb_synchronize, which synchronise.  No call allocates device memory except
+ *     omb_create and omb_set_gp.
+ *   - Return 0 (OMB_OK) on success or a negative OMB_E* code; omb_last_error() describes the
+ *     last failure.  No C++ exception crosses the ABI.
+ *   - One context per device; a context is not thread-safe; different contexts are
+ *     independent.
+ *   - Posterior moments are laid out objective-major: mu_dev[o * ld + i], var_dev likewise.
+ */
+#ifndef OPTIMOBO_HIP_H
+#define OPTIMOBO_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OMB_ABI_VERSION 1
+#define OMB_MAX_OBJ 8      /* objectives held by one context */
+#define OMB_MAX_DIM 32     /* n_var */
+#define OMB_MAX_TRAIN 1024 /* n_train handled by the fused posterior kernel */
+
+enum {
+  OMB_OK = 0,
+  OMB_EINVAL = -1,   /* bad argument */
+  OMB_EHIP = -2,     /* HIP runtime error */
+  OMB_ENOMEM = -3,   /* device allocation failed */
+  OMB_ESTATE = -4,   /* objective not set (omb_set_gp) */
+  OMB_EUNSUP = -5    /* size outside what the kernels support */
+};
+
+enum { OMB_KERNEL_MATERN52 = 0, OMB_KERNEL_RBF = 1 };
+enum { OMB_EHVI_REFERENCE = 0, OMB_EHVI_TEXTBOOK = 1 };
+
+/* Scalarisation ids (optimobo/scalarisations.py:37-397) and their params[] layout. */
+enum {
+  OMB_SCAL_WS = 0,    /* WeightedSum                       params: -            */
+  OMB_SCAL_TCH = 1,   /* Tchebicheff                       params: -            */
+  OMB_SCAL_ATCH = 2,  /* AugmentedTchebicheff              params: alpha        */
+  OMB_SCAL_MTCH = 3,  /* ModifiedTchebicheff               params: alpha        */
+  OMB_SCAL_EWC = 4,   /* ExponentialWeightedCriterion      params: p            */
+  OMB_SCAL_WN = 5,    /* WeightedNorm                      params: p            */
+  OMB_SCAL_WPO = 6,   /* WeightedPower                     params: p            */
+  OMB_SCAL_WPR = 7,   /* WeightedProduct                   params: -            */
+  OMB_SCAL_PBI = 8,   /* PBI                               params: theta        */
+  OMB_SCAL_IPBI = 9,  /* IPBI                              params: theta        */
+  OMB_SCAL_QPBI = 10, /* QPBI                              params: theta, alpha, H */
+  OMB_SCAL_APD = 11   /* APD                               params: FE, FE_max, gamma */
+};
+
+typedef struct omb_ctx omb_ctx;
+
+int omb_abi_version(void);
+
+/* Create a context on HIP device `device` (own non-blocking stream). */
+int omb_create(int device, omb_ctx** out);
+int omb_destroy(omb_ctx* ctx);
+/* Run subsequent calls on `hip_stream` (a hipStream_t, e.g. torch's current stream;
+ * NULL is the HIP null stream).  omb_use_own_stream restores the context's own stream. */
+int omb_set_stream(omb_ctx* ctx, void* hip_stream);
+int omb_use_own_stream(omb_ctx* ctx);
+int omb_synchronize(omb_ctx* ctx);
+const char* omb_last_error(const omb_ctx* ctx);
+
+/* Fitted-GP state of objective `obj` — replaces the fitted GPy model
+ * (GPRegression + Matern52(ARD) with noise fixed to 0, optimisers.py:223-231).
+ *   X_dev     (n, d)  training inputs, unscaled
+ *   lengthscale_host (d) ARD lengthscales ℓ;  variance = σ_f²
+ *   alpha_dev (n)     woodbury vector (K + 1e-8 I)^-1 y
+ *   Linv_dev  (n, n)  row-major inverse of the lower Cholesky factor of K + 1e-8 I
+ * The context packs this into its own layout (Lp: MFMA-fragment order) on its stream. */
+int omb_set_gp(omb_ctx* ctx, int obj, int kernel, int n, int d, const double* X_dev,
+               const double* lengthscale_host, double variance, const double* alpha_dev,
+               const double* Linv_dev);
+
+/* K(X_train, X*) block of objective `obj` (GPy Stationary._scaled_dist + Matern52.K_of_r,
+ * the first half of model.predict at util_functions.py:156): K_dev (n, N) row-major. */
+int omb_kernel_block(omb_ctx* ctx, int obj, const double* Xc_dev, int64_t N, double* K_dev);
+
+/* Posterior μ, σ² of objectives 0..n_obj-1 at N candidates Xc_dev (N, d)
+ * (GPy PosteriorExact._raw_predict via model.predict, util_functions.py:155-158):
+ * mu_dev/var_dev (n_obj, N).  Fused K-block generation + FP64-MFMA L^-1 K* + reductions. */
+int omb_posterior(omb_ctx* ctx, int n_obj, const double* Xc_dev, int64_t N, double* mu_dev,
+                  double* var_dev);
+
+/* EHVI for 2 objectives (util_functions.py:136-167 + EHVI_2D_aux :81-128).
+ *   pf_sorted_dev (P, 2): Pareto front sorted by f2 ascending (util_functions.py:98)
+ *   r_host (2): reference (max) point;  s00, s01: np.cov(cache) entries (per-solve constants)
+ *   mode OMB_EHVI_REFERENCE: σA = σ²0·s00, σB = σ²0·s01, last stripe omitted (bug-compatible)
+ *   mode OMB_EHVI_TEXTBOOK : σA = sqrt(σ²0), σB = sqrt(σ²1), all P+1 stripes (exact EHVI) */
+int omb_ehvi2d(omb_ctx* ctx, const double* mu_dev, const double* var_dev, int64_t ld, int64_t N,
+               const double* pf_sorted_dev, int P, const double* r_host, double s00, double s01,
+               int mode, double* out_dev);
+
+/* EHVI_3D reference Monte-Carlo form (util_functions.py:170-214):
+ *   out = mean_s max(0, Π_j(r_j − s_j) − hv_pf),  s = cache·sqrt(σ²0) + μ (util_functions.py:217-237)
+ * raised_dev (N, int32, may be NULL) is set to 1 where pygmo's hypervolume would raise
+ * (a sample outside the reference box); out is NaN there. */
+int omb_ehvi3d_mc(omb_ctx* ctx, const double* mu_dev, const double* var_dev, int64_t ld, int64_t N,
+                  const double* cache_dev, int M, const double* r_host, double hv_pf, double* out_dev,
+                  int32_t* raised_dev);
+
+/* Hypervolume-based PoI of EMO (emo.py:176-228): cells_dev (C, 2, 2) [upper, lower]. */
+int omb_hvpoi(omb_ctx* ctx, const double* mu_dev, const double* var_dev, int64_t ld, int64_t N,
+              const double* cells_dev, int C, double* out_dev);
+
+/* expected_decomposition (util_functions.py:285-327) for k objectives:
+ *   cache_dev (M, k); weights/ideal/max host (k); params_host per OMB_SCAL_* (may be NULL). */
+int omb_expdec(omb_ctx* ctx, int k, const double* mu_dev, const double* var_dev, int64_t ld, int64_t N,
+               const double* cache_dev, int M, int scal_id, const double* params_host,
+               const double* weights_host, const double* ideal_host, const double* max_host,
+               double agg_min, double* out_dev);
+
+/* Expected improvement (optimisers.py:325-344 with var_eps = 0; parego.py:126-145 and
+ * keep.py:118-137 with var_eps = 1e-6). */
+int omb_ei(omb_ctx* ctx, const double* mu_dev, const double* var_dev, int64_t N, double best,
+           double var_eps, double* out_dev);
+
+/* Arg-max over vals_dev (N): lowest index among maxima, NaN and -inf never win
+ * (replaces scipy differential_evolution(lambda x: -acq(x)), optimisers.py:87,118).
+ * result_dev (2 doubles, device): {best value, best index + offset (as double)};
+ * index -1 when nothing qualifies.  Asynchronous. */
+int omb_argmax_dev(omb_ctx* ctx, const double* vals_dev, int64_t N, int64_t offset, double* result_dev);
+/* Same, synchronising and returning to host. */
+int omb_argmax(omb_ctx* ctx, const double* vals_dev, int64_t N, int64_t offset, double* best_val,
+               int64_t* best_idx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* OPTIMOBO_HIP_H */

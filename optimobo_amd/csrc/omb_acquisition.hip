@@ -1,0 +1,336 @@
+// Acquisition kernels on gfx950: EHVI-2D, EHVI-3D (reference Monte-Carlo form), HV-PoI,
+// expected decomposition over the twelve scalarisations, and EI.
+//
+// Each kernel evaluates one candidate per thread from the posterior moments produced by
+// omb_posterior; the per-iteration constant geometry (Pareto stripes, cells, the cached
+// normal samples) is staged once per workgroup in LDS and read as a broadcast.  All fp64.
+#include <math.h>
+
+#include "omb_internal.h"
+#include "omb_math.h"
+
+namespace omb {
+
+constexpr int kAcqThreads = 256;
+
+static unsigned acq_grid(int64_t N) {
+  int64_t b = (N + kAcqThreads - 1) / kAcqThreads;
+  if (b > 65536) b = 65536;
+  return (unsigned)(b < 1 ? 1 : b);
+}
+
+// ------------------------------------------------------------------------------ EHVI 2-D
+// util_functions.py:81-128 (EHVI_2D_aux) with the stripe array S = [(r0,−∞), PF↑f2, (−∞,r1)]
+// of :93-109.  φ/Φ of t_i = (y1[i]−μ0)/σA are reused by stripe i+1 (the reference evaluates
+// ψ(y1[i−1], y1[i−1]) from the same t), so each stripe costs 2 Φ + 2 φ instead of 7 calls.
+__global__ __launch_bounds__(kAcqThreads) void ehvi2d_kernel(const double* __restrict__ mu,
+                                                             const double* __restrict__ var, int64_t ld, int64_t N,
+                                                             const double* __restrict__ pf, int P, double r0,
+                                                             double r1, double s00, double s01, int mode,
+                                                             double* __restrict__ out) {
+  extern __shared__ double sm[];
+  double* y1 = sm;          // y1[0..P]
+  double* y2 = sm + P + 1;  // y2[1..P] stored at y2[i-1]
+  for (int i = threadIdx.x; i < P; i += blockDim.x) {
+    y1[i + 1] = pf[2 * i];
+    y2[i] = pf[2 * i + 1];
+  }
+  if (threadIdx.x == 0) y1[0] = r0;
+  __syncthreads();
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < N; c += (int64_t)gridDim.x * blockDim.x) {
+    const double m0 = mu[c], m1 = mu[ld + c], v0 = var[c];
+    double sA, sB;
+    if (mode == OMB_EHVI_REFERENCE) {
+      // change() scales the cached samples by sqrt(σ²0) (util_functions.py:233-235): a negative
+      // variance makes every sample NaN, and np.cov of them NaN.
+      if (!(v0 >= 0.0)) {
+        out[c] = __builtin_nan("");
+        continue;
+      }
+      sA = v0 * s00;   // c00 = σ²0·Cov(cache)00   (util_functions.py:163-167, 114-115)
+      sB = v0 * s01;   // c01 = σ²0·Cov(cache)01   (a covariance used as a std: quirk 2)
+    } else {
+      sA = sqrt(v0);
+      sB = sqrt(var[ld + c]);
+    }
+    double tp = (y1[0] - m0) / sA;
+    double cdf_p = ndtr(tp), pdf_p = npdf(tp);
+    double sum1 = 0.0, sum2 = 0.0;
+    for (int i = 1; i <= P; ++i) {
+      const double y1p = y1[i - 1], y1i = y1[i], y2i = y2[i - 1];
+      const double t = (y1i - m0) / sA;
+      const double cdf_t = ndtr(t), pdf_t = npdf(t);
+      const double u = (y2i - m1) / sB;
+      const double p2 = sB * npdf(u) + (y2i - m1) * ndtr(u);          // ψ(y2i, y2i, μ1, σB)
+      sum1 = sum1 + (y1p - y1i) * cdf_t * p2;
+      const double psi_pp = sA * pdf_p + (y1p - m0) * cdf_p;          // ψ(y1[i−1], y1[i−1], μ0, σA)
+      const double psi_pi = sA * pdf_t + (y1p - m0) * cdf_t;          // ψ(y1[i−1], y1[i],   μ0, σA)
+      sum2 = sum2 + (psi_pp - psi_pi) * p2;
+      cdf_p = cdf_t;
+      pdf_p = pdf_t;
+    }
+    double res = sum1 + sum2;
+    if (mode == OMB_EHVI_TEXTBOOK) {
+      // the stripe i = P+1 that range(1, n+1) leaves out (quirk 3): ψ(y1P,y1P,μ0,σA)·ψ(r1,r1,μ1,σB)
+      const double psiA = sA * pdf_p + (y1[P] - m0) * cdf_p;
+      const double u = (r1 - m1) / sB;
+      res += psiA * (sB * npdf(u) + (r1 - m1) * ndtr(u));
+    }
+    out[c] = res;
+  }
+}
+
+hipError_t launch_ehvi2d(hipStream_t stream, const double* mu, const double* var, int64_t ld, int64_t N,
+                         const double* pf, int P, double r0, double r1, double s00, double s01, int mode,
+                         double* out) {
+  size_t shm = sizeof(double) * (2 * P + 1);
+  hipLaunchKernelGGL(ehvi2d_kernel, dim3(acq_grid(N)), dim3(kAcqThreads), shm, stream, mu, var, ld, N, pf, P, r0, r1,
+                     s00, s01, mode, out);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------ EHVI 3-D
+// util_functions.py:170-214: samples s = cache·sqrt(σ²0) + μ (change, :217-237), then
+// mean_s max(0, Π_j(r_j − s_j) − HV(PF)).  pygmo raises ValueError when a sample is not inside
+// the reference box (some s_j > r_j, or s == r): flagged per candidate, value NaN.
+__global__ __launch_bounds__(kAcqThreads) void ehvi3d_kernel(const double* __restrict__ mu,
+                                                             const double* __restrict__ var, int64_t ld, int64_t N,
+                                                             const double* __restrict__ cache, int M, double r0,
+                                                             double r1, double r2, double hv_pf,
+                                                             double* __restrict__ out, int32_t* __restrict__ raised) {
+  extern __shared__ double sm[];
+  for (int i = threadIdx.x; i < 3 * M; i += blockDim.x) sm[i] = cache[i];
+  __syncthreads();
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < N; c += (int64_t)gridDim.x * blockDim.x) {
+    const double m0 = mu[c], m1 = mu[ld + c], m2 = mu[2 * ld + c];
+    const double sd = sqrt(var[c]);   // σ²0 for every objective (quirk 1)
+    double answer = 0.0;
+    bool bad = !(sd == sd);
+    for (int s = 0; s < M; ++s) {
+      const double x0 = sm[3 * s] * sd + m0, x1 = sm[3 * s + 1] * sd + m1, x2 = sm[3 * s + 2] * sd + m2;
+      bad |= (x0 > r0) || (x1 > r1) || (x2 > r2) || ((x0 == r0) && (x1 == r1) && (x2 == r2));
+      double h = (r0 - x0) * (r1 - x1) * (r2 - x2) - hv_pf;
+      if (h > 0.0) answer += h;
+    }
+    out[c] = bad ? __builtin_nan("") : answer / M;
+    if (raised) raised[c] = bad ? 1 : 0;
+  }
+}
+
+hipError_t launch_ehvi3d_mc(hipStream_t stream, const double* mu, const double* var, int64_t ld, int64_t N,
+                            const double* cache, int M, const double* r, double hv_pf, double* out,
+                            int32_t* raised) {
+  size_t shm = sizeof(double) * 3 * M;
+  hipLaunchKernelGGL(ehvi3d_kernel, dim3(acq_grid(N)), dim3(kAcqThreads), shm, stream, mu, var, ld, N, cache, M,
+                     r[0], r[1], r[2], hv_pf, out, raised);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------ HV-PoI
+// emo.py:192-228 with vol5 (:176-189):  s = sqrt(σ² + 1e-5);
+//   PoI = Σ_c Π_k [Φ((u_k−μ_k)/s_k) − Φ((l_k−μ_k)/s_k)],  I = Σ_c [u > μ]·Π_k(u_k − max(l_k, μ_k)).
+__global__ __launch_bounds__(kAcqThreads) void hvpoi_kernel(const double* __restrict__ mu,
+                                                            const double* __restrict__ var, int64_t ld, int64_t N,
+                                                            const double* __restrict__ cells, int C,
+                                                            double* __restrict__ out) {
+  extern __shared__ double sm[];   // C × [up0, up1, lo0, lo1]
+  for (int i = threadIdx.x; i < 4 * C; i += blockDim.x) sm[i] = cells[i];
+  __syncthreads();
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < N; c += (int64_t)gridDim.x * blockDim.x) {
+    const double m0 = mu[c], m1 = mu[ld + c];
+    const double s0 = sqrt(var[c] + 1e-5), s1 = sqrt(var[ld + c] + 1e-5);
+    double poi = 0.0, imp = 0.0;
+    for (int j = 0; j < C; ++j) {
+      const double u0 = sm[4 * j], u1 = sm[4 * j + 1], l0 = sm[4 * j + 2], l1 = sm[4 * j + 3];
+      const double p0 = ndtr((u0 - m0) / s0) - ndtr((l0 - m0) / s0);
+      const double p1 = ndtr((u1 - m1) / s1) - ndtr((l1 - m1) / s1);
+      poi = poi + p0 * p1;
+      if (u0 > m0 && u1 > m1) imp = imp + (u0 - fmax(l0, m0)) * (u1 - fmax(l1, m1));
+    }
+    out[c] = poi * imp;
+  }
+}
+
+hipError_t launch_hvpoi(hipStream_t stream, const double* mu, const double* var, int64_t ld, int64_t N,
+                        const double* cells, int C, double* out) {
+  size_t shm = sizeof(double) * 4 * C;
+  hipLaunchKernelGGL(hvpoi_kernel, dim3(acq_grid(N)), dim3(kAcqThreads), shm, stream, mu, var, ld, N, cells, C, out);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------ scalarisations
+// optimobo/scalarisations.py:37-397 on one objective vector s (k entries), normalised by
+// (s − ideal)/(max − ideal).  NaN propagates like numpy's max/sum.
+__device__ __forceinline__ double nanmax(double a, double b) { return (a != a || b != b) ? __builtin_nan("") : (a > b ? a : b); }
+
+template <int K>
+__device__ double scalarise(const ScalParams& sp, const double* s) {
+  double o[K];
+#pragma unroll
+  for (int i = 0; i < K; ++i) o[i] = (s[i] - sp.ideal[i]) / sp.range[i];
+  switch (sp.id) {
+    case OMB_SCAL_WS: {
+      double a = 0.0;
+#pragma unroll
+      for (int i = 0; i < K; ++i) a += o[i] * sp.w[i];
+      return a;
+    }
+    case OMB_SCAL_TCH: {
+      double m = sp.w[0] * o[0];
+#pragma unroll
+      for (int i = 1; i < K; ++i) m = nanmax(m, sp.w[i] * o[i]);
+      return m;
+    }
+    case OMB_SCAL_ATCH: {
+      double m = fabs(o[0]) * sp.w[0], a = fabs(o[0]);
+#pragma unroll
+      for (int i = 1; i < K; ++i) {
+        m = nanmax(m, fabs(o[i]) * sp.w[i]);
+        a += fabs(o[i]);
+      }
+      return m + sp.p[0] * a;
+    }
+    case OMB_SCAL_MTCH: {
+      double a = 0.0;
+#pragma unroll
+      for (int i = 0; i < K; ++i) a += fabs(o[i]);
+      const double right = sp.p[0] * a;
+      double m = (fabs(o[0]) + right) * sp.w[0];
+#pragma unroll
+      for (int i = 1; i < K; ++i) m = nanmax(m, (fabs(o[i]) + right) * sp.w[i]);
+      return m;
+    }
+    case OMB_SCAL_EWC: {
+      double a = 0.0;
+#pragma unroll
+      for (int i = 0; i < K; ++i) a += exp(sp.p[0] * sp.w[i] - 1.0) * exp(sp.p[0] * o[i]);
+      return a;
+    }
+    case OMB_SCAL_WN: {
+      double a = 0.0;
+#pragma unroll
+      for (int i = 0; i < K; ++i) a += pow(fabs(o[i]), sp.p[0]) * sp.w[i];
+      return pow(a, 1.0 / sp.p[0]);
+    }
+    case OMB_SCAL_WPO: {
+      double a = 0.0;
+#pragma unroll
+      for (int i = 0; i < K; ++i) a += pow(o[i], sp.p[0]) * sp.w[i];
+      return a;
+    }
+    case OMB_SCAL_WPR: {
+      double a = 1.0;
+#pragma unroll
+      for (int i = 0; i < K; ++i) a *= pow(o[i] + 100000.0, sp.w[i]);
+      return a;
+    }
+    case OMB_SCAL_PBI:
+    case OMB_SCAL_IPBI:
+    case OMB_SCAL_QPBI: {
+      double W[K];
+      double d1 = 0.0;
+#pragma unroll
+      for (int i = 0; i < K; ++i) {
+        W[i] = sp.w[i] / sp.wnorm;
+        d1 += o[i] * W[i];
+      }
+      double q = 0.0;
+#pragma unroll
+      for (int i = 0; i < K; ++i) {
+        const double e = o[i] - d1 * W[i];
+        q += e * e;
+      }
+      const double d2 = sqrt(q);
+      if (sp.id == OMB_SCAL_PBI) return d1 + sp.p[0] * d2;
+      if (sp.id == OMB_SCAL_IPBI) return sp.p[0] * d2 - d1;
+      return d1 + sp.p[0] * d2 * (d2 / sp.d_star);
+    }
+    case OMB_SCAL_APD: {
+      double q = 0.0;
+      bool zero = true;
+#pragma unroll
+      for (int i = 0; i < K; ++i) {
+        q += o[i] * o[i];
+        zero = zero && (o[i] == 0.0);
+      }
+      const double nrm = sqrt(q);                // norm_trans_f, before the zero fix-up (:384)
+      double t[K];
+      double tq = 0.0;
+#pragma unroll
+      for (int i = 0; i < K; ++i) {
+        t[i] = zero ? 1e-5 : o[i];
+        tq += t[i] * t[i];
+      }
+      const double tn = sqrt(tq);
+      double dot = 0.0;
+#pragma unroll
+      for (int i = 0; i < K; ++i) dot += (t[i] / tn) * (sp.w[i] / sp.wnorm);
+      dot = fmin(fmax(dot, -1.0), 1.0);
+      const double theta = acos(dot);
+      return (1.0 + (K * (sp.p[0] / sp.p[1])) * (theta / sp.p[2])) * nrm;
+    }
+    default:
+      return __builtin_nan("");
+  }
+}
+
+// util_functions.py:285-327: mean_j max(0, min − g(change(μ, σ²0)_j)).
+template <int K>
+__global__ __launch_bounds__(kAcqThreads) void expdec_kernel(ScalParams sp, const double* __restrict__ mu,
+                                                             const double* __restrict__ var, int64_t ld, int64_t N,
+                                                             const double* __restrict__ cache, int M,
+                                                             double* __restrict__ out) {
+  extern __shared__ double sm[];
+  for (int i = threadIdx.x; i < K * M; i += blockDim.x) sm[i] = cache[i];
+  __syncthreads();
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < N; c += (int64_t)gridDim.x * blockDim.x) {
+    double m[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) m[i] = mu[i * ld + c];
+    const double sd = sqrt(var[c]);             // σ²0 for every objective (quirk 1)
+    double acc = 0.0;
+    for (int j = 0; j < M; ++j) {
+      double s[K];
+#pragma unroll
+      for (int i = 0; i < K; ++i) s[i] = sm[j * K + i] * sd + m[i];
+      const double x = sp.agg_min - scalarise<K>(sp, s);
+      acc += (x < 0.0) ? 0.0 : x;                // np.maximum(0, x): NaN propagates
+    }
+    out[c] = acc / M;
+  }
+}
+
+hipError_t launch_expdec(hipStream_t stream, const ScalParams& sp, const double* mu, const double* var,
+                         int64_t ld, int64_t N, const double* cache, int M, double* out) {
+  size_t shm = sizeof(double) * sp.k * M;
+  dim3 g(acq_grid(N)), b(kAcqThreads);
+  switch (sp.k) {
+#define OMB_ED(KV) \
+  case KV: hipLaunchKernelGGL(expdec_kernel<KV>, g, b, shm, stream, sp, mu, var, ld, N, cache, M, out); break;
+    OMB_ED(1) OMB_ED(2) OMB_ED(3) OMB_ED(4) OMB_ED(5) OMB_ED(6) OMB_ED(7) OMB_ED(8)
+#undef OMB_ED
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------ EI
+// optimisers.py:325-344 / parego.py:126-145: σ = sqrt(σ² + eps); γ = (best − μ)/(σ + 1e-10);
+// EI = σ(γΦ(γ) + φ(γ)).
+__global__ __launch_bounds__(kAcqThreads) void ei_kernel(const double* __restrict__ mu, const double* __restrict__ var,
+                                                         int64_t N, double best, double var_eps,
+                                                         double* __restrict__ out) {
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < N; c += (int64_t)gridDim.x * blockDim.x) {
+    const double sigma = sqrt(var[c] + var_eps);
+    const double gamma = (best - mu[c]) / (sigma + 1e-10);
+    out[c] = sigma * (gamma * ndtr(gamma) + npdf(gamma));
+  }
+}
+
+hipError_t launch_ei(hipStream_t stream, const double* mu, const double* var, int64_t N, double best,
+                     double var_eps, double* out) {
+  hipLaunchKernelGGL(ei_kernel, dim3(acq_grid(N)), dim3(kAcqThreads), 0, stream, mu, var, N, best, var_eps, out);
+  return hipGetLastError();
+}
+
+}  // namespace omb

@@ -1,0 +1,361 @@
+// C-ABI of liboptimobo_hip.so (declared in include/optimobo_hip.h): context, GP state,
+// argument validation and dispatch to the kernels.  No exception crosses this boundary.
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <new>
+#include <string>
+
+#include "omb_internal.h"
+
+using namespace omb;
+
+struct ObjState {
+  bool set = false;
+  int n = 0, d = 0, DP = 0, R = 0, n_pad = 0, kind = 0;
+  double variance = 0.0;
+  double* buf = nullptr;  // one allocation: Xs | xsq | alpha | ls | Lp
+  size_t cap = 0;         // bytes
+  GPDev dev{};
+};
+
+struct omb_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  std::string err;
+  ObjState obj[OMB_MAX_OBJ];
+  double* partials = nullptr;  // argmax pass-1 output
+  double* result_dev = nullptr;
+  double* result_host = nullptr;  // pinned
+};
+
+namespace {
+
+int fail(omb_ctx* ctx, int code, const char* fmt, ...) {
+  if (ctx) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    ctx->err = buf;
+  }
+  return code;
+}
+
+int hip_fail(omb_ctx* ctx, hipError_t e, const char* where) {
+  return fail(ctx, OMB_EHIP, "%s: %s", where, hipGetErrorString(e));
+}
+
+#define OMB_HIP(ctx, call)                                   \
+  do {                                                       \
+    hipError_t e_ = (call);                                  \
+    if (e_ != hipSuccess) return hip_fail(ctx, e_, #call);   \
+  } while (0)
+
+int pad_dim(int d) {
+  const int opts[] = {2, 4, 6, 8, 16, 32};
+  for (int o : opts)
+    if (d <= o) return o;
+  return -1;
+}
+
+int enter(omb_ctx* ctx) {
+  if (!ctx) return OMB_EINVAL;
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+  return OMB_OK;
+}
+
+// GP state of objectives 0..n_obj-1, all set, sharing d.
+int gather_gp(omb_ctx* ctx, int n_obj, GPArgs* args, int* max_R) {
+  if (n_obj < 1 || n_obj > OMB_MAX_OBJ) return fail(ctx, OMB_EINVAL, "n_obj=%d outside [1, %d]", n_obj, OMB_MAX_OBJ);
+  memset(args, 0, sizeof(*args));
+  *max_R = 0;
+  for (int o = 0; o < n_obj; ++o) {
+    const ObjState& s = ctx->obj[o];
+    if (!s.set) return fail(ctx, OMB_ESTATE, "objective %d has no GP state (call omb_set_gp)", o);
+    if (s.d != ctx->obj[0].d) return fail(ctx, OMB_EINVAL, "objectives disagree on n_var (%d vs %d)", s.d, ctx->obj[0].d);
+    if (s.kind != ctx->obj[0].kind) return fail(ctx, OMB_EINVAL, "objectives disagree on kernel kind");
+    args->gp[o] = s.dev;
+    if (s.R > *max_R) *max_R = s.R;
+  }
+  args->d = ctx->obj[0].d;
+  args->DP = ctx->obj[0].DP;
+  return OMB_OK;
+}
+
+int check_moments(omb_ctx* ctx, const double* mu, const double* var, int64_t ld, int64_t N, int k, const double* out) {
+  if (!mu || !var || !out) return fail(ctx, OMB_EINVAL, "null device pointer");
+  if (N < 0) return fail(ctx, OMB_EINVAL, "N=%lld < 0", (long long)N);
+  if (k > 1 && ld < N) return fail(ctx, OMB_EINVAL, "ld=%lld < N=%lld", (long long)ld, (long long)N);
+  return OMB_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int omb_abi_version(void) { return OMB_ABI_VERSION; }
+
+int omb_create(int device, omb_ctx** out) {
+  if (!out) return OMB_EINVAL;
+  *out = nullptr;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) return OMB_EINVAL;
+  omb_ctx* ctx = new (std::nothrow) omb_ctx();
+  if (!ctx) return OMB_ENOMEM;
+  ctx->device = device;
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc(&ctx->partials, sizeof(double) * 2 * kArgmaxMaxBlocks) != hipSuccess ||
+      hipMalloc(&ctx->result_dev, sizeof(double) * 2) != hipSuccess ||
+      hipHostMalloc(&ctx->result_host, sizeof(double) * 2, hipHostMallocDefault) != hipSuccess) {
+    omb_destroy(ctx);
+    return OMB_ENOMEM;
+  }
+  ctx->stream = ctx->own_stream;
+  *out = ctx;
+  return OMB_OK;
+}
+
+int omb_destroy(omb_ctx* ctx) {
+  if (!ctx) return OMB_OK;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  for (auto& s : ctx->obj)
+    if (s.buf) (void)hipFree(s.buf);
+  if (ctx->partials) (void)hipFree(ctx->partials);
+  if (ctx->result_dev) (void)hipFree(ctx->result_dev);
+  if (ctx->result_host) (void)hipHostFree(ctx->result_host);
+  if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+  delete ctx;
+  return OMB_OK;
+}
+
+int omb_set_stream(omb_ctx* ctx, void* hip_stream) {
+  if (!ctx) return OMB_EINVAL;
+  ctx->stream = reinterpret_cast<hipStream_t>(hip_stream);
+  return OMB_OK;
+}
+
+int omb_use_own_stream(omb_ctx* ctx) {
+  if (!ctx) return OMB_EINVAL;
+  ctx->stream = ctx->own_stream;
+  return OMB_OK;
+}
+
+int omb_synchronize(omb_ctx* ctx) {
+  int rc = enter(ctx);
+  if (rc) return rc;
+  OMB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return OMB_OK;
+}
+
+const char* omb_last_error(const omb_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int omb_set_gp(omb_ctx* ctx, int obj, int kernel, int n, int d, const double* X_dev, const double* lengthscale_host,
+               double variance, const double* alpha_dev, const double* Linv_dev) {
+  int rc = enter(ctx);
+  if (rc) return rc;
+  if (obj < 0 || obj >= OMB_MAX_OBJ) return fail(ctx, OMB_EINVAL, "obj=%d outside [0, %d)", obj, OMB_MAX_OBJ);
+  if (kernel != OMB_KERNEL_MATERN52 && kernel != OMB_KERNEL_RBF) return fail(ctx, OMB_EINVAL, "unknown kernel %d", kernel);
+  if (n < 1 || n > OMB_MAX_TRAIN) return fail(ctx, OMB_EUNSUP, "n_train=%d outside [1, %d]", n, OMB_MAX_TRAIN);
+  if (d < 1 || d > OMB_MAX_DIM) return fail(ctx, OMB_EUNSUP, "n_var=%d outside [1, %d]", d, OMB_MAX_DIM);
+  if (!X_dev || !lengthscale_host || !alpha_dev || !Linv_dev) return fail(ctx, OMB_EINVAL, "null pointer");
+  for (int j = 0; j < d; ++j)
+    if (!(lengthscale_host[j] > 0.0)) return fail(ctx, OMB_EINVAL, "lengthscale[%d]=%g must be > 0", j, lengthscale_host[j]);
+  if (!(variance >= 0.0)) return fail(ctx, OMB_EINVAL, "variance=%g must be >= 0", variance);
+
+  ObjState& s = ctx->obj[obj];
+  // The previous state may still be read by queued kernels.
+  OMB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  const int DP = pad_dim(d);
+  const int R = (n + 15) / 16;
+  const int Q = (R + 3) / 4;
+  const int n_pad = kChunkRows * Q;
+  const size_t doubles = (size_t)n_pad * DP + 2 * (size_t)n_pad + DP + (size_t)packed_L_size(R);
+  const size_t bytes = doubles * sizeof(double);
+  if (bytes > s.cap) {
+    if (s.buf) (void)hipFree(s.buf);
+    s.buf = nullptr;
+    s.cap = 0;
+    if (hipMalloc(&s.buf, bytes) != hipSuccess) {
+      s.set = false;
+      return fail(ctx, OMB_ENOMEM, "hipMalloc(%zu) for objective %d", bytes, obj);
+    }
+    s.cap = bytes;
+  }
+  double* Xs = s.buf;
+  double* xsq = Xs + (size_t)n_pad * DP;
+  double* alpha_p = xsq + n_pad;
+  double* ls_p = alpha_p + n_pad;
+  double* Lp = ls_p + DP;
+  hipError_t e = launch_pack_gp(ctx->stream, n, d, DP, X_dev, lengthscale_host, alpha_dev, Linv_dev, Xs, xsq,
+                                alpha_p, Lp, R, n_pad);
+  if (e != hipSuccess) {
+    s.set = false;
+    return hip_fail(ctx, e, "pack_gp");
+  }
+  s.set = true;
+  s.n = n;
+  s.d = d;
+  s.DP = DP;
+  s.R = R;
+  s.n_pad = n_pad;
+  s.kind = kernel;
+  s.variance = variance;
+  s.dev = GPDev{Xs, xsq, alpha_p, Lp, ls_p, variance, n, R, kernel, 0};
+  return OMB_OK;
+}
+
+int omb_kernel_block(omb_ctx* ctx, int obj, const double* Xc_dev, int64_t N, double* K_dev) {
+  int rc = enter(ctx);
+  if (rc) return rc;
+  if (obj < 0 || obj >= OMB_MAX_OBJ || !ctx->obj[obj].set) return fail(ctx, OMB_ESTATE, "objective %d not set", obj);
+  if (!Xc_dev || !K_dev || N < 0) return fail(ctx, OMB_EINVAL, "bad candidate/output arguments");
+  if (N == 0) return OMB_OK;
+  GPArgs args;
+  memset(&args, 0, sizeof(args));
+  args.gp[obj] = ctx->obj[obj].dev;
+  args.d = ctx->obj[obj].d;
+  args.DP = ctx->obj[obj].DP;
+  hipError_t e = launch_kernel_block(ctx->stream, args, obj, Xc_dev, N, K_dev);
+  if (e != hipSuccess) return hip_fail(ctx, e, "kernel_block");
+  return OMB_OK;
+}
+
+int omb_posterior(omb_ctx* ctx, int n_obj, const double* Xc_dev, int64_t N, double* mu_dev, double* var_dev) {
+  int rc = enter(ctx);
+  if (rc) return rc;
+  if (!Xc_dev || !mu_dev || !var_dev || N < 0) return fail(ctx, OMB_EINVAL, "bad candidate/output arguments");
+  GPArgs args;
+  int max_R = 0;
+  rc = gather_gp(ctx, n_obj, &args, &max_R);
+  if (rc) return rc;
+  if (N == 0) return OMB_OK;
+  if ((N + 31) / 32 > 0x7fffffffLL) return fail(ctx, OMB_EUNSUP, "N=%lld too large", (long long)N);
+  hipError_t e = launch_posterior(ctx->stream, args, n_obj, max_R, Xc_dev, N, mu_dev, var_dev);
+  if (e != hipSuccess) return hip_fail(ctx, e, "posterior");
+  return OMB_OK;
+}
+
+int omb_ehvi2d(omb_ctx* ctx, const double* mu_dev, const double* var_dev, int64_t ld, int64_t N,
+               const double* pf_sorted_dev, int P, const double* r_host, double s00, double s01, int mode,
+               double* out_dev) {
+  int rc = enter(ctx);
+  if (rc) return rc;
+  if ((rc = check_moments(ctx, mu_dev, var_dev, ld, N, 2, out_dev))) return rc;
+  if (!pf_sorted_dev || P < 1 || P > 4096) return fail(ctx, OMB_EINVAL, "Pareto front size P=%d outside [1, 4096]", P);
+  if (!r_host) return fail(ctx, OMB_EINVAL, "null reference point");
+  if (mode != OMB_EHVI_REFERENCE && mode != OMB_EHVI_TEXTBOOK) return fail(ctx, OMB_EINVAL, "unknown EHVI mode %d", mode);
+  if (N == 0) return OMB_OK;
+  hipError_t e = launch_ehvi2d(ctx->stream, mu_dev, var_dev, ld, N, pf_sorted_dev, P, r_host[0], r_host[1], s00, s01,
+                               mode, out_dev);
+  if (e != hipSuccess) return hip_fail(ctx, e, "ehvi2d");
+  return OMB_OK;
+}
+
+int omb_ehvi3d_mc(omb_ctx* ctx, const double* mu_dev, const double* var_dev, int64_t ld, int64_t N,
+                  const double* cache_dev, int M, const double* r_host, double hv_pf, double* out_dev,
+                  int32_t* raised_dev) {
+  int rc = enter(ctx);
+  if (rc) return rc;
+  if ((rc = check_moments(ctx, mu_dev, var_dev, ld, N, 3, out_dev))) return rc;
+  if (!cache_dev || M < 1 || M > 4096) return fail(ctx, OMB_EINVAL, "cache size M=%d outside [1, 4096]", M);
+  if (!r_host) return fail(ctx, OMB_EINVAL, "null reference point");
+  if (N == 0) return OMB_OK;
+  hipError_t e = launch_ehvi3d_mc(ctx->stream, mu_dev, var_dev, ld, N, cache_dev, M, r_host, hv_pf, out_dev, raised_dev);
+  if (e != hipSuccess) return hip_fail(ctx, e, "ehvi3d_mc");
+  return OMB_OK;
+}
+
+int omb_hvpoi(omb_ctx* ctx, const double* mu_dev, const double* var_dev, int64_t ld, int64_t N,
+              const double* cells_dev, int C, double* out_dev) {
+  int rc = enter(ctx);
+  if (rc) return rc;
+  if ((rc = check_moments(ctx, mu_dev, var_dev, ld, N, 2, out_dev))) return rc;
+  if (!cells_dev || C < 1 || C > 4096) return fail(ctx, OMB_EINVAL, "cell count C=%d outside [1, 4096]", C);
+  if (N == 0) return OMB_OK;
+  hipError_t e = launch_hvpoi(ctx->stream, mu_dev, var_dev, ld, N, cells_dev, C, out_dev);
+  if (e != hipSuccess) return hip_fail(ctx, e, "hvpoi");
+  return OMB_OK;
+}
+
+int omb_expdec(omb_ctx* ctx, int k, const double* mu_dev, const double* var_dev, int64_t ld, int64_t N,
+               const double* cache_dev, int M, int scal_id, const double* params_host, const double* weights_host,
+               const double* ideal_host, const double* max_host, double agg_min, double* out_dev) {
+  int rc = enter(ctx);
+  if (rc) return rc;
+  if (k < 1 || k > OMB_MAX_OBJ) return fail(ctx, OMB_EINVAL, "k=%d outside [1, %d]", k, OMB_MAX_OBJ);
+  if ((rc = check_moments(ctx, mu_dev, var_dev, ld, N, k, out_dev))) return rc;
+  if (!cache_dev || M < 1 || M > 4096) return fail(ctx, OMB_EINVAL, "cache size M=%d outside [1, 4096]", M);
+  if (scal_id < OMB_SCAL_WS || scal_id > OMB_SCAL_APD) return fail(ctx, OMB_EINVAL, "unknown scalarisation %d", scal_id);
+  if (!weights_host || !ideal_host || !max_host) return fail(ctx, OMB_EINVAL, "null weights/ideal/max");
+  ScalParams sp;
+  memset(&sp, 0, sizeof(sp));
+  sp.id = scal_id;
+  sp.k = k;
+  sp.agg_min = agg_min;
+  double wq = 0.0, rsum = 0.0;
+  for (int i = 0; i < k; ++i) {
+    sp.w[i] = weights_host[i];
+    sp.ideal[i] = ideal_host[i];
+    sp.range[i] = max_host[i] - ideal_host[i];
+    wq += sp.w[i] * sp.w[i];
+    rsum += sp.range[i];
+  }
+  sp.wnorm = sqrt(wq);
+  const int np = (scal_id == OMB_SCAL_QPBI || scal_id == OMB_SCAL_APD) ? 3
+                 : (scal_id == OMB_SCAL_WS || scal_id == OMB_SCAL_TCH || scal_id == OMB_SCAL_WPR) ? 0 : 1;
+  if (np > 0 && !params_host) return fail(ctx, OMB_EINVAL, "scalarisation %d needs %d parameter(s)", scal_id, np);
+  for (int i = 0; i < np; ++i) sp.p[i] = params_host[i];
+  if (scal_id == OMB_SCAL_APD && sp.wnorm == 0.0) {
+    // scalarisations.py:392-393 substitutes 1e-5 weights (the reference then fails for k > 1).
+    for (int i = 0; i < k; ++i) sp.w[i] = 1e-5;
+    sp.wnorm = sqrt(k * 1e-10);
+  }
+  if (scal_id == OMB_SCAL_QPBI) {
+    // scalarisations.py:347: alpha * (1/H * 1/k * Σ(max − ideal))
+    sp.d_star = sp.p[1] * ((1.0 / sp.p[2]) * (1.0 / (double)k) * rsum);
+  }
+  if (N == 0) return OMB_OK;
+  hipError_t e = launch_expdec(ctx->stream, sp, mu_dev, var_dev, ld, N, cache_dev, M, out_dev);
+  if (e != hipSuccess) return hip_fail(ctx, e, "expdec");
+  return OMB_OK;
+}
+
+int omb_ei(omb_ctx* ctx, const double* mu_dev, const double* var_dev, int64_t N, double best, double var_eps,
+           double* out_dev) {
+  int rc = enter(ctx);
+  if (rc) return rc;
+  if ((rc = check_moments(ctx, mu_dev, var_dev, N, N, 1, out_dev))) return rc;
+  if (N == 0) return OMB_OK;
+  hipError_t e = launch_ei(ctx->stream, mu_dev, var_dev, N, best, var_eps, out_dev);
+  if (e != hipSuccess) return hip_fail(ctx, e, "ei");
+  return OMB_OK;
+}
+
+int omb_argmax_dev(omb_ctx* ctx, const double* vals_dev, int64_t N, int64_t offset, double* result_dev) {
+  int rc = enter(ctx);
+  if (rc) return rc;
+  if (!vals_dev || !result_dev || N < 0) return fail(ctx, OMB_EINVAL, "bad arg-max arguments");
+  hipError_t e = launch_argmax(ctx->stream, vals_dev, N, offset, ctx->partials, result_dev);
+  if (e != hipSuccess) return hip_fail(ctx, e, "argmax");
+  return OMB_OK;
+}
+
+int omb_argmax(omb_ctx* ctx, const double* vals_dev, int64_t N, int64_t offset, double* best_val, int64_t* best_idx) {
+  int rc = omb_argmax_dev(ctx, vals_dev, N, offset, ctx ? ctx->result_dev : nullptr);
+  if (rc) return rc;
+  OMB_HIP(ctx, hipMemcpyAsync(ctx->result_host, ctx->result_dev, 2 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  OMB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (best_val) *best_val = ctx->result_host[0];
+  if (best_idx) *best_idx = (int64_t)ctx->result_host[1];
+  return OMB_OK;
+}
+
+}  // extern "C"

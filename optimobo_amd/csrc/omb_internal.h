@@ -1,0 +1,84 @@
+// Internal declarations shared by the HIP translation units of liboptimobo_hip.so.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/optimobo_hip.h"
+
+namespace omb {
+
+// Rows of the training set handled per streamed K* chunk (4 row tiles of 16).
+constexpr int kChunkRows = 64;
+constexpr int kBlockThreads = 512;
+
+// Device-side state of one fitted GP (objective), built by omb_set_gp.
+struct GPDev {
+  const double* Xs;     // (n_pad, DP) training inputs / ℓ, zero padded
+  const double* xsq;    // (n_pad) Σ_j Xs[k][j]²
+  const double* alpha;  // (n_pad) woodbury vector, zero padded
+  const double* Lp;     // packed lower-triangular L^-1 in MFMA fragment order (see pack kernel)
+  const double* ls;     // (DP) lengthscales, padded with 1
+  double variance;      // σ_f²
+  int n;                // n_train
+  int R;                // row tiles = ceil(n / 16)
+  int kind;             // OMB_KERNEL_*
+  int pad_;
+};
+
+struct GPArgs {
+  GPDev gp[OMB_MAX_OBJ];
+  int d;    // true n_var (≤ DP)
+  int DP;   // padded dim used by the packed Xs
+};
+
+// ---------------------------------------------------------------------------------------
+// Launchers (host functions; each launches on `stream` and returns hipGetLastError()).
+hipError_t launch_pack_gp(hipStream_t stream, int n, int d, int DP, const double* X, const double* ls_dev,
+                          const double* alpha, const double* Linv, double* Xs, double* xsq, double* alpha_p,
+                          double* Lp, int R, int n_pad);
+
+hipError_t launch_kernel_block(hipStream_t stream, const GPArgs& args, int obj, const double* Xc, int64_t N,
+                               double* K);
+
+hipError_t launch_posterior(hipStream_t stream, const GPArgs& args, int n_obj, int max_R, const double* Xc,
+                            int64_t N, double* mu, double* var);
+
+hipError_t launch_ehvi2d(hipStream_t stream, const double* mu, const double* var, int64_t ld, int64_t N,
+                         const double* pf, int P, double r0, double r1, double s00, double s01, int mode,
+                         double* out);
+
+hipError_t launch_ehvi3d_mc(hipStream_t stream, const double* mu, const double* var, int64_t ld, int64_t N,
+                            const double* cache, int M, const double* r, double hv_pf, double* out,
+                            int32_t* raised);
+
+hipError_t launch_hvpoi(hipStream_t stream, const double* mu, const double* var, int64_t ld, int64_t N,
+                        const double* cells, int C, double* out);
+
+struct ScalParams {
+  int id;
+  int k;
+  double w[OMB_MAX_OBJ];
+  double ideal[OMB_MAX_OBJ];
+  double range[OMB_MAX_OBJ];   // max − ideal
+  double p[4];
+  double wnorm;                // ‖w‖ (PBI family)
+  double d_star;               // QPBI
+  double agg_min;
+};
+
+hipError_t launch_expdec(hipStream_t stream, const ScalParams& sp, const double* mu, const double* var,
+                         int64_t ld, int64_t N, const double* cache, int M, double* out);
+
+hipError_t launch_ei(hipStream_t stream, const double* mu, const double* var, int64_t N, double best,
+                     double var_eps, double* out);
+
+// Two-pass deterministic arg-max; `partials` must hold kArgmaxMaxBlocks (val, idx) pairs.
+constexpr int kArgmaxMaxBlocks = 1024;
+hipError_t launch_argmax(hipStream_t stream, const double* vals, int64_t N, int64_t offset, double* partials,
+                         double* result);
+
+// Packed-L^-1 size in doubles for R row tiles: Σ_{r<R} 4(r+1)·64 = 128·R·(R+1).
+inline int64_t packed_L_size(int R) { return 128ll * R * (R + 1); }
+
+}  // namespace omb

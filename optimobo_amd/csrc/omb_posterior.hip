@@ -1,0 +1,348 @@
+// GP posterior on gfx950: the K(X, X*) block and the fused posterior kernel.
+//
+// Replaces GPy's PosteriorExact._raw_predict as reached through model.predict(x[None,:]) at
+// optimobo/util_functions.py:155-158 (and emo.py:203-205, optimisers.py:336, parego.py:137):
+//     K*  = σ_f² (1 + √5 r + 5/3 r²) exp(−√5 r),  r² = ‖x/ℓ‖² + ‖x*/ℓ‖² − 2 (x/ℓ)·(x*/ℓ)
+//     μ   = K*ᵀ α
+//     σ²  = σ_f² − Σ_rows (L⁻¹ K*)²
+// All arithmetic is fp64 (fp32 fails parity by orders of magnitude).
+//
+// Fused posterior kernel (one workgroup = 512 threads = 8 waves, BN candidates):
+//   * K* is generated 64 training rows at a time ("chunk") by all 8 waves (VALU fp64) into a
+//     double-buffered LDS tile stored directly in the B-operand fragment order of
+//     v_mfma_f64_16x16x4_f64, so each wave reads a fragment as 64 consecutive doubles.
+//   * The triangular product V = L⁻¹ K* runs on FP64 MFMA: the A operand (L⁻¹) is read from a
+//     packed, fragment-ordered copy (zero blocks above the diagonal are never stored or read);
+//     it is L2-resident (1.06 MiB per objective at n = 512) and shared by every workgroup.
+//   * Row tiles (16 rows) are dealt to waves so that, for every chunk, the four SIMD pairs
+//     (waves w and w+4 share a SIMD) get equal MFMA work: tile r = 4q + ((pair + q) mod 4)
+//     of quad q, quads split between the two waves of a pair in Gray-code order.
+//   * μ accumulates in VALU during generation; σ² is a wave reduction of the squared MFMA
+//     accumulators followed by a fixed-order cross-wave LDS reduction (deterministic).
+#include "omb_internal.h"
+#include "omb_math.h"
+
+namespace omb {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+typedef double d2 __attribute__((ext_vector_type(2)));
+
+// ----------------------------------------------------------------------------- packing
+struct LsArg {
+  double v[OMB_MAX_DIM];
+};
+
+// Xs = X / ℓ (GPy Stationary._scaled_dist divides), xsq = Σ Xs², α padded, ℓ padded with 1.
+__global__ void pack_rows_kernel(int n, int d, int DP, int n_pad, const double* __restrict__ X, LsArg ls,
+                                 const double* __restrict__ alpha, double* __restrict__ Xs,
+                                 double* __restrict__ xsq, double* __restrict__ alpha_p, double* __restrict__ ls_p) {
+  int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < DP && blockIdx.x == 0) ls_p[k] = (k < d) ? ls.v[k] : 1.0;
+  if (k >= n_pad) return;
+  double s = 0.0;
+  for (int j = 0; j < DP; ++j) {
+    double v = 0.0;
+    if (k < n && j < d) v = X[(int64_t)k * d + j] / ls.v[j];
+    Xs[(int64_t)k * DP + j] = v;
+    s += v * v;
+  }
+  xsq[k] = s;
+  alpha_p[k] = (k < n) ? alpha[k] : 0.0;
+}
+
+// Packed L⁻¹: tile r (rows 16r..16r+15) holds k-steps S = 0 .. 4(r+1)-1 (columns 4S..4S+3);
+// k-steps are stored in pairs so a lane loads both of its A values with one 16-byte load:
+//     Lp[128 r (r+1) + 128 (S/2) + 2 lane + (S&1)] = L⁻¹[16r + (lane&15)][4S + (lane>>4)]
+// (A-operand map of v_mfma_f64_16x16x4_f64: lane l holds A[l&15][l>>4]).
+__global__ void pack_L_kernel(int n, const double* __restrict__ Linv, double* __restrict__ Lp) {
+  const int r = blockIdx.y;
+  const int per_tile = 256 * (r + 1);
+  double* dst = Lp + 128ll * r * (r + 1);
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < per_tile; t += gridDim.x * blockDim.x) {
+    int P = t >> 7, lane = (t & 127) >> 1, h = t & 1;
+    int S = 2 * P + h;
+    int row = 16 * r + (lane & 15), col = 4 * S + (lane >> 4);
+    double v = 0.0;
+    if (row < n && col < n && col <= row) v = Linv[(int64_t)row * n + col];
+    dst[t] = v;
+  }
+}
+
+hipError_t launch_pack_gp(hipStream_t stream, int n, int d, int DP, const double* X, const double* ls_host,
+                          const double* alpha, const double* Linv, double* Xs, double* xsq, double* alpha_p,
+                          double* Lp, int R, int n_pad) {
+  LsArg ls{};
+  for (int j = 0; j < d; ++j) ls.v[j] = ls_host[j];
+  // ls_p lives right after alpha_p (see omb_set_gp's buffer carving).
+  double* ls_p = alpha_p + n_pad;
+  hipLaunchKernelGGL(pack_rows_kernel, dim3((n_pad + 255) / 256), dim3(256), 0, stream, n, d, DP, n_pad, X, ls,
+                     alpha, Xs, xsq, alpha_p, ls_p);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(pack_L_kernel, dim3(4, R), dim3(256), 0, stream, n, Linv, Lp);
+  return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------- K block
+// Standalone K(X_train, X*) (n, N) row-major — the HBM-bound kernel of the north star.
+// Each thread owns two adjacent candidates (16-byte stores), each block 64 training rows.
+template <int DP, int KIND>
+__global__ __launch_bounds__(256) void kernel_block_kernel(GPDev g, int d, const double* __restrict__ Xc,
+                                                           int64_t N, double* __restrict__ K) {
+  constexpr int kRows = 64;
+  const int64_t c = 2 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+  if (c >= N) return;
+  const bool two = (c + 1) < N;
+  double b0[DP], b1[DP];
+  double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+  for (int j = 0; j < DP; ++j) {
+    b0[j] = (j < d) ? Xc[c * d + j] / g.ls[j] : 0.0;
+    b1[j] = (j < d && two) ? Xc[(c + 1) * d + j] / g.ls[j] : 0.0;
+    s0 += b0[j] * b0[j];
+    s1 += b1[j] * b1[j];
+  }
+  const int k0 = blockIdx.y * kRows;
+  const int k1 = min(g.n, k0 + kRows);
+  for (int k = k0; k < k1; ++k) {
+    const double* xr = g.Xs + (int64_t)k * DP;
+    double dot0 = 0.0, dot1 = 0.0;
+#pragma unroll
+    for (int j = 0; j < DP; ++j) {
+      dot0 = fma(xr[j], b0[j], dot0);
+      dot1 = fma(xr[j], b1[j], dot1);
+    }
+    const double xk = g.xsq[k];
+    double v0 = kernel_of_r2<KIND>(fma(-2.0, dot0, xk + s0), g.variance);
+    double v1 = kernel_of_r2<KIND>(fma(-2.0, dot1, xk + s1), g.variance);
+    double* dst = K + (int64_t)k * N + c;
+    if (two && ((N & 1) == 0)) {
+      *reinterpret_cast<d2*>(dst) = d2{v0, v1};
+    } else {
+      dst[0] = v0;
+      if (two) dst[1] = v1;
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------- posterior
+template <int RT, int CT, int DP, int KIND>
+__global__ __launch_bounds__(kBlockThreads, 2) void posterior_kernel(GPArgs args, const double* __restrict__ Xc,
+                                                                      int64_t N, double* __restrict__ mu_out,
+                                                                      double* __restrict__ var_out) {
+  constexpr int BN = 16 * CT;                 // candidates per workgroup
+  constexpr int KS = kChunkRows / 4;          // MFMA k-steps per chunk (16)
+  constexpr int CHUNK = kChunkRows * BN;      // doubles per LDS buffer
+  constexpr int EPT = CHUNK / kBlockThreads;  // generated K* elements per thread per chunk
+  static_assert(kBlockThreads % BN == 0, "BN must divide the block");
+  __shared__ double kbuf[2 * CHUNK];
+
+  const int obj = blockIdx.y;
+  const GPDev g = args.gp[obj];
+  const int d = args.d;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t c0 = (int64_t)blockIdx.x * BN;
+
+  // ---- this thread's generation candidate (fixed across chunks since BN | 512)
+  const int cg = tid % BN;
+  const int64_t ci = min(c0 + cg, N - 1);
+  double b[DP];
+  double csq = 0.0;
+#pragma unroll
+  for (int j = 0; j < DP; ++j) {
+    b[j] = (j < d) ? Xc[ci * d + j] / g.ls[j] : 0.0;
+    csq += b[j] * b[j];
+  }
+  const int gen_ct = cg >> 4, gen_cc = cg & 15;
+
+  // ---- row-tile slots of this wave (SIMD-pair balanced, see header)
+  const int pair = wave & 3, half = wave >> 2;
+  const int Q = (g.R + 3) >> 2;  // chunks of 64 rows
+  int slot_r[RT], slot_q[RT];
+  const double* slot_A[RT];
+#pragma unroll
+  for (int j = 0; j < RT; ++j) {
+    int q = 4 * (j >> 1) + (half ? (1 + (j & 1)) : 3 * (j & 1));
+    int r = 4 * q + ((pair + q) & 3);
+    bool ok = r < g.R;
+    slot_q[j] = ok ? q : -1;
+    slot_r[j] = ok ? r : 0;
+    slot_A[j] = g.Lp + 128ll * slot_r[j] * (slot_r[j] + 1) + 2 * lane;
+  }
+
+  d4 acc[RT][CT];
+#pragma unroll
+  for (int j = 0; j < RT; ++j)
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) acc[j][ct] = d4{0.0, 0.0, 0.0, 0.0};
+  double mu_part = 0.0;
+
+  auto generate = [&](int kc, double* buf) {
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const int e = tid + kBlockThreads * i;
+      const int kl = e / BN;
+      const int k = kc * kChunkRows + kl;
+      double val = 0.0;
+      if (k < g.n) {
+        const double* xr = g.Xs + (int64_t)k * DP;
+        double dot = 0.0;
+#pragma unroll
+        for (int j = 0; j < DP; ++j) dot = fma(xr[j], b[j], dot);
+        val = kernel_of_r2<KIND>(fma(-2.0, dot, g.xsq[k] + csq), g.variance);
+        mu_part = fma(g.alpha[k], val, mu_part);
+      }
+      buf[((kl >> 2) * CT + gen_ct) * 64 + (kl & 3) * 16 + gen_cc] = val;
+    }
+  };
+
+  auto multiply = [&](int kc, const double* buf) {
+    // k-steps of each slot inside this chunk: 16 (below the diagonal quad), 4(r mod 4 + 1)
+    // (diagonal quad), 0 (finished or empty slot).
+    int nS[RT];
+#pragma unroll
+    for (int j = 0; j < RT; ++j)
+      nS[j] = (slot_q[j] > kc) ? KS : (slot_q[j] == kc ? 4 * ((slot_r[j] & 3) + 1) : 0);
+    const int P0 = kc * (KS / 2);
+    d2 a_cur[RT], a_nxt[RT];
+#pragma unroll
+    for (int j = 0; j < RT; ++j) a_cur[j] = *reinterpret_cast<const d2*>(slot_A[j] + 128 * min(P0, 2 * slot_r[j] + 1));
+#pragma unroll
+    for (int sp = 0; sp < KS / 2; ++sp) {
+      if (sp + 1 < KS / 2) {
+#pragma unroll
+        for (int j = 0; j < RT; ++j)
+          a_nxt[j] = *reinterpret_cast<const d2*>(slot_A[j] + 128 * min(P0 + sp + 1, 2 * slot_r[j] + 1));
+      }
+      double b0[CT], b1[CT];
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        b0[ct] = buf[((2 * sp) * CT + ct) * 64 + lane];
+        b1[ct] = buf[((2 * sp + 1) * CT + ct) * 64 + lane];
+      }
+#pragma unroll
+      for (int j = 0; j < RT; ++j) {
+        if (2 * sp < nS[j]) {
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct) {
+            acc[j][ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(a_cur[j].x, b0[ct], acc[j][ct], 0, 0, 0);
+            acc[j][ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(a_cur[j].y, b1[ct], acc[j][ct], 0, 0, 0);
+          }
+        }
+      }
+      if (sp + 1 < KS / 2) {
+#pragma unroll
+        for (int j = 0; j < RT; ++j) a_cur[j] = a_nxt[j];
+      }
+    }
+  };
+
+  generate(0, kbuf);
+  __syncthreads();
+  for (int kc = 0; kc < Q; ++kc) {
+    if (kc + 1 < Q) generate(kc + 1, kbuf + ((kc + 1) & 1) * CHUNK);
+    multiply(kc, kbuf + (kc & 1) * CHUNK);
+    __syncthreads();
+  }
+
+  // ---- σ²: Σ over rows of V² — registers, then lanes {l, l^16, l^32, l^48}, then waves.
+  double part[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < RT; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) s = fma(acc[j][ct][i], acc[j][ct][i], s);
+    s += __shfl_xor(s, 16);
+    s += __shfl_xor(s, 32);
+    part[ct] = s;
+  }
+  double* red = kbuf;                 // 8 waves × BN
+  double* redmu = kbuf + 8 * BN;      // 512 partial μ
+  if (lane < 16) {
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) red[wave * BN + ct * 16 + lane] = part[ct];
+  }
+  redmu[tid] = mu_part;
+  __syncthreads();
+  if (tid < BN) {
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) s += red[w * BN + tid];
+    double m = 0.0;
+    for (int t = tid; t < kBlockThreads; t += BN) m += redmu[t];
+    const int64_t c = c0 + tid;
+    if (c < N) {
+      mu_out[(int64_t)obj * N + c] = m;
+      var_out[(int64_t)obj * N + c] = g.variance - s;
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------- dispatch
+template <int DP, int KIND>
+static hipError_t launch_posterior_dp(hipStream_t stream, const GPArgs& args, int n_obj, int max_R,
+                                      const double* Xc, int64_t N, double* mu, double* var) {
+  const int Q = (max_R + 3) / 4;
+  const int RTneed = (Q + 1) / 2;
+  if (RTneed <= 1) {
+    dim3 grid((unsigned)((N + 63) / 64), n_obj);
+    hipLaunchKernelGGL((posterior_kernel<1, 4, DP, KIND>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var);
+  } else if (RTneed <= 2) {
+    dim3 grid((unsigned)((N + 63) / 64), n_obj);
+    hipLaunchKernelGGL((posterior_kernel<2, 4, DP, KIND>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var);
+  } else if (RTneed <= 4) {
+    dim3 grid((unsigned)((N + 63) / 64), n_obj);
+    hipLaunchKernelGGL((posterior_kernel<4, 4, DP, KIND>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var);
+  } else if (RTneed <= 8) {
+    dim3 grid((unsigned)((N + 31) / 32), n_obj);
+    hipLaunchKernelGGL((posterior_kernel<8, 2, DP, KIND>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var);
+  } else {
+    return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+template <int KIND>
+static hipError_t launch_posterior_kind(hipStream_t stream, const GPArgs& args, int n_obj, int max_R,
+                                        const double* Xc, int64_t N, double* mu, double* var) {
+  switch (args.DP) {
+    case 2: return launch_posterior_dp<2, KIND>(stream, args, n_obj, max_R, Xc, N, mu, var);
+    case 4: return launch_posterior_dp<4, KIND>(stream, args, n_obj, max_R, Xc, N, mu, var);
+    case 6: return launch_posterior_dp<6, KIND>(stream, args, n_obj, max_R, Xc, N, mu, var);
+    case 8: return launch_posterior_dp<8, KIND>(stream, args, n_obj, max_R, Xc, N, mu, var);
+    case 16: return launch_posterior_dp<16, KIND>(stream, args, n_obj, max_R, Xc, N, mu, var);
+    case 32: return launch_posterior_dp<32, KIND>(stream, args, n_obj, max_R, Xc, N, mu, var);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_posterior(hipStream_t stream, const GPArgs& args, int n_obj, int max_R, const double* Xc,
+                            int64_t N, double* mu, double* var) {
+  if (args.gp[0].kind == OMB_KERNEL_RBF) return launch_posterior_kind<OMB_KERNEL_RBF>(stream, args, n_obj, max_R, Xc, N, mu, var);
+  return launch_posterior_kind<OMB_KERNEL_MATERN52>(stream, args, n_obj, max_R, Xc, N, mu, var);
+}
+
+template <int KIND>
+static hipError_t launch_kblock_kind(hipStream_t stream, const GPArgs& args, int obj, const double* Xc, int64_t N,
+                                     double* K) {
+  const GPDev& g = args.gp[obj];
+  dim3 grid((unsigned)((N + 511) / 512), (unsigned)((g.n + 63) / 64));
+  switch (args.DP) {
+#define OMB_KB(DPV) \
+  case DPV: hipLaunchKernelGGL((kernel_block_kernel<DPV, KIND>), grid, dim3(256), 0, stream, g, args.d, Xc, N, K); break;
+    OMB_KB(2) OMB_KB(4) OMB_KB(6) OMB_KB(8) OMB_KB(16) OMB_KB(32)
+#undef OMB_KB
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_kernel_block(hipStream_t stream, const GPArgs& args, int obj, const double* Xc, int64_t N,
+                               double* K) {
+  if (args.gp[obj].kind == OMB_KERNEL_RBF) return launch_kblock_kind<OMB_KERNEL_RBF>(stream, args, obj, Xc, N, K);
+  return launch_kblock_kind<OMB_KERNEL_MATERN52>(stream, args, obj, Xc, N, K);
+}
+
+}  // namespace omb

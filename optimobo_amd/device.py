@@ -1,0 +1,176 @@
+"""Device context: torch tensors as device-memory holders around the HIP C-ABI.
+
+``AcqContext`` owns one ``omb_ctx`` (one per GPU) and runs every call on torch's current
+stream, so torch events time the kernels exactly.  All arrays are fp64 CUDA (HIP) tensors;
+the context never copies candidates to the host.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _dev_f64(x, device):
+    if isinstance(x, torch.Tensor):
+        t = x.to(device=device, dtype=torch.float64)
+    else:
+        t = torch.as_tensor(np.ascontiguousarray(x, dtype=np.float64), device=device)
+    return t.contiguous()
+
+
+class AcqContext:
+    """One HIP context on ``device`` holding the fitted GPs of up to 8 objectives."""
+
+    def __init__(self, device=0):
+        if not torch.cuda.is_available():
+            raise RuntimeError("AcqContext needs a ROCm GPU (torch.cuda.is_available() is False); "
+                               "the acquisition hot path has no CPU fallback")
+        self.lib = _lib.load()
+        self.device = torch.device("cuda", device if isinstance(device, int) else torch.device(device).index or 0)
+        h = ctypes.c_void_p()
+        rc = self.lib.omb_create(self.device.index, ctypes.byref(h))
+        if rc != 0:
+            raise _lib.OMBError(rc, f"omb_create(device={self.device.index}) failed")
+        self._h = h
+        self._gp_keep = {}     # device tensors referenced by the packed GP state
+        self.gp_info = {}
+
+    # ------------------------------------------------------------------ plumbing
+    def _check(self, rc, what):
+        if rc != 0:
+            msg = self.lib.omb_last_error(self._h)
+            raise _lib.OMBError(rc, f"{what}: {msg.decode() if msg else ''}")
+
+    def _stream(self):
+        s = torch.cuda.current_stream(self.device)
+        self._check(self.lib.omb_set_stream(self._h, ctypes.c_void_p(s.cuda_stream)), "omb_set_stream")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.omb_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def synchronize(self):
+        self._check(self.lib.omb_synchronize(self._h), "omb_synchronize")
+
+    # ------------------------------------------------------------------ GP state
+    def set_gp(self, obj, X, lengthscale, variance, alpha, Linv, kernel="matern52"):
+        """Upload one fitted GP (see optimobo_amd.gp.GPState) for objective ``obj``."""
+        X = _dev_f64(X, self.device)
+        alpha = _dev_f64(np.asarray(alpha).reshape(-1) if not isinstance(alpha, torch.Tensor) else alpha.reshape(-1),
+                         self.device)
+        Linv = _dev_f64(Linv, self.device)
+        n, d = X.shape
+        if Linv.shape != (n, n) or alpha.shape[0] != n:
+            raise ValueError(f"set_gp: shapes X{tuple(X.shape)} alpha{tuple(alpha.shape)} Linv{tuple(Linv.shape)}")
+        ls = np.broadcast_to(np.asarray(lengthscale, np.float64), (d,))
+        kid = {"matern52": _lib.KERNEL_MATERN52, "rbf": _lib.KERNEL_RBF}[kernel]
+        self._stream()
+        self._check(self.lib.omb_set_gp(self._h, obj, kid, n, d, _ptr(X), _lib.darr(ls), float(variance),
+                                        _ptr(alpha), _ptr(Linv)), "omb_set_gp")
+        self._gp_keep[obj] = (X, alpha, Linv)
+        self.gp_info[obj] = dict(n=n, d=d, variance=float(variance), kernel=kernel)
+
+    def set_gp_state(self, obj, state):
+        self.set_gp(obj, state.X, state.lengthscale, state.variance, state.alpha, state.Linv, state.kernel)
+
+    # ------------------------------------------------------------------ posterior
+    def kernel_block(self, obj, Xc, out=None):
+        Xc = _dev_f64(Xc, self.device)
+        n = self.gp_info[obj]["n"]
+        N = Xc.shape[0]
+        K = out if out is not None else torch.empty((n, N), dtype=torch.float64, device=self.device)
+        self._stream()
+        self._check(self.lib.omb_kernel_block(self._h, obj, _ptr(Xc), N, _ptr(K)), "omb_kernel_block")
+        return K
+
+    def posterior(self, Xc, n_obj=None, out=None):
+        """μ, σ² (n_obj, N) of objectives 0..n_obj-1 at candidates Xc (N, d)."""
+        Xc = _dev_f64(Xc, self.device)
+        if Xc.dim() != 2:
+            raise ValueError("candidates must be (N, d)")
+        n_obj = n_obj if n_obj is not None else len(self.gp_info)
+        N = Xc.shape[0]
+        if out is None:
+            mu = torch.empty((n_obj, N), dtype=torch.float64, device=self.device)
+            var = torch.empty_like(mu)
+        else:
+            mu, var = out
+        self._stream()
+        self._check(self.lib.omb_posterior(self._h, n_obj, _ptr(Xc), N, _ptr(mu), _ptr(var)), "omb_posterior")
+        return mu, var
+
+    # ------------------------------------------------------------------ acquisitions
+    def ehvi2d(self, mu, var, pf_sorted, r, s00, s01, mode="reference", out=None):
+        N = mu.shape[1]
+        pf = _dev_f64(pf_sorted, self.device)
+        out = out if out is not None else torch.empty(N, dtype=torch.float64, device=self.device)
+        m = {"reference": _lib.EHVI_REFERENCE, "textbook": _lib.EHVI_TEXTBOOK}[mode]
+        self._stream()
+        self._check(self.lib.omb_ehvi2d(self._h, _ptr(mu), _ptr(var), mu.stride(0), N, _ptr(pf), pf.shape[0],
+                                        _lib.darr(r), float(s00), float(s01), m, _ptr(out)), "omb_ehvi2d")
+        return out
+
+    def ehvi3d_mc(self, mu, var, cache, r, hv_pf, out=None, raised=None):
+        N = mu.shape[1]
+        cache = _dev_f64(cache, self.device)
+        out = out if out is not None else torch.empty(N, dtype=torch.float64, device=self.device)
+        raised = raised if raised is not None else torch.empty(N, dtype=torch.int32, device=self.device)
+        self._stream()
+        self._check(self.lib.omb_ehvi3d_mc(self._h, _ptr(mu), _ptr(var), mu.stride(0), N, _ptr(cache), cache.shape[0],
+                                           _lib.darr(r), float(hv_pf), _ptr(out), _ptr(raised)), "omb_ehvi3d_mc")
+        return out, raised
+
+    def hvpoi(self, mu, var, cells, out=None):
+        N = mu.shape[1]
+        cells = _dev_f64(cells, self.device)
+        out = out if out is not None else torch.empty(N, dtype=torch.float64, device=self.device)
+        self._stream()
+        self._check(self.lib.omb_hvpoi(self._h, _ptr(mu), _ptr(var), mu.stride(0), N, _ptr(cells), cells.shape[0],
+                                       _ptr(out)), "omb_hvpoi")
+        return out
+
+    def expdec(self, mu, var, cache, scal_id, params, weights, ideal, max_point, agg_min, out=None):
+        k, N = mu.shape
+        cache = _dev_f64(cache, self.device)
+        out = out if out is not None else torch.empty(N, dtype=torch.float64, device=self.device)
+        self._stream()
+        self._check(self.lib.omb_expdec(self._h, k, _ptr(mu), _ptr(var), mu.stride(0), N, _ptr(cache), cache.shape[0],
+                                        int(scal_id), _lib.darr(params), _lib.darr(weights), _lib.darr(ideal),
+                                        _lib.darr(max_point), float(agg_min), _ptr(out)), "omb_expdec")
+        return out
+
+    def ei(self, mu, var, best, var_eps=0.0, out=None):
+        mu = mu.reshape(-1)
+        var = var.reshape(-1)
+        N = mu.shape[0]
+        out = out if out is not None else torch.empty(N, dtype=torch.float64, device=self.device)
+        self._stream()
+        self._check(self.lib.omb_ei(self._h, _ptr(mu), _ptr(var), N, float(best), float(var_eps), _ptr(out)), "omb_ei")
+        return out
+
+    def argmax_dev(self, vals, offset=0, out=None):
+        out = out if out is not None else torch.empty(2, dtype=torch.float64, device=self.device)
+        self._stream()
+        self._check(self.lib.omb_argmax_dev(self._h, _ptr(vals), vals.numel(), int(offset), _ptr(out)), "omb_argmax_dev")
+        return out
+
+    def argmax(self, vals, offset=0):
+        v = ctypes.c_double()
+        i = ctypes.c_int64()
+        self._stream()
+        self._check(self.lib.omb_argmax(self._h, _ptr(vals), vals.numel(), int(offset), ctypes.byref(v),
+                                        ctypes.byref(i)), "omb_argmax")
+        return v.value, i.value

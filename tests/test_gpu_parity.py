@@ -1,0 +1,244 @@
+"""GPU parity: every HIP kernel (through the C-ABI) against the oracle and the golden vectors.
+
+Tolerances (written per test): posterior μ/σ² 1e-6 relative (north_star) with an absolute
+floor tied to the posterior scale; acquisitions 1e-5 relative (north_star) — in practice the
+kernels agree to ~1e-12 because both sides are fp64 with ≤1-ulp transcendentals.  The
+arg-max must be identical (same value, same index).
+"""
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+from oracle import acquisition as oacq  # noqa: E402
+from oracle import gp as ogp  # noqa: E402
+from oracle import pareto as opar  # noqa: E402
+from oracle import scalarisations as osc  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from optimobo_amd.device import AcqContext
+    c = AcqContext(0)
+    yield c
+    c.close()
+
+
+def dev(x):
+    return torch.as_tensor(np.ascontiguousarray(x, dtype=np.float64), device="cuda:0")
+
+
+def load(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name), allow_pickle=False)
+
+
+def set_gps(ctx, X, Y, ls, variances, kernel="matern52"):
+    from optimobo_amd.gp import GPState
+    states = []
+    for o in range(Y.shape[1]):
+        st = GPState(X, Y[:, o], ls, variances[o], kernel=kernel)
+        ctx.set_gp_state(o, st)
+        states.append(st)
+    return states
+
+
+def oracle_posterior(X, Y, ls, variances, Xc, kernel="matern52"):
+    mus, vs = [], []
+    for o in range(Y.shape[1]):
+        g = ogp.ExactGP(X, Y[:, o], ls, variances[o], kernel=kernel)
+        m, v = g.predict(Xc)
+        mus.append(m[:, 0])
+        vs.append(v[:, 0])
+    return np.array(mus), np.array(vs)
+
+
+def assert_posterior(mu, var, mu_ref, var_ref, variances):
+    for o in range(mu_ref.shape[0]):
+        s = variances[o]
+        np.testing.assert_allclose(mu[o], mu_ref[o], rtol=1e-6, atol=1e-7 * np.sqrt(s))
+        np.testing.assert_allclose(var[o], var_ref[o], rtol=1e-6, atol=1e-9 * s)
+
+
+# ----------------------------------------------------------------------------- posterior
+@pytest.mark.parametrize("name", ["posterior_n20_d2.npz", "posterior_n128_d6.npz", "posterior_n512_d6.npz"])
+def test_posterior_vs_golden(ctx, golden_dir, name):
+    z = load(golden_dir, name)
+    variances = [float(z["variance0"]), float(z["variance1"])]
+    set_gps(ctx, z["X"], z["Y"], z["lengthscale"], variances)
+    mu, var = ctx.posterior(dev(z["Xc"]), n_obj=2)
+    mu, var = mu.cpu().numpy(), var.cpu().numpy()
+    golden_mu = np.array([z["mu0"], z["mu1"]])
+    golden_var = np.array([z["var0"], z["var1"]])
+    assert_posterior(mu, var, golden_mu, golden_var, variances)
+    mu_o, var_o = oracle_posterior(z["X"], z["Y"], z["lengthscale"], variances, z["Xc"])
+    assert_posterior(mu, var, mu_o, var_o, variances)
+
+
+@pytest.mark.parametrize("n,d,N", [(1, 1, 5), (16, 2, 64), (17, 3, 65), (64, 6, 1000), (100, 4, 257),
+                                   (256, 6, 333), (300, 9, 129), (512, 6, 2048), (700, 2, 100),
+                                   (1024, 6, 300), (128, 30, 200), (64, 32, 64)])
+def test_posterior_sizes(ctx, n, d, N):
+    rng = np.random.default_rng(n * 1000 + d)
+    X = rng.uniform(0, 1, (n, d))
+    Y = np.column_stack([np.sin(3 * X).sum(1), np.cos(2 * X).prod(1)])
+    ls = rng.uniform(0.2, 2.0, d) * np.sqrt(d)
+    variances = [float(np.var(Y[:, 0]) + 0.1), float(np.var(Y[:, 1]) + 0.1)]
+    set_gps(ctx, X, Y, ls, variances)
+    Xc = rng.uniform(0, 1, (N, d))
+    Xc[: min(3, N)] = X[: min(3, N)]          # candidates on training points: σ² ≈ 0
+    mu, var = ctx.posterior(dev(Xc), n_obj=2)
+    mu_o, var_o = oracle_posterior(X, Y, ls, variances, Xc)
+    assert_posterior(mu.cpu().numpy(), var.cpu().numpy(), mu_o, var_o, variances)
+
+
+def test_posterior_rbf_kernel(ctx):
+    rng = np.random.default_rng(5)
+    X = rng.uniform(0, 1, (96, 5))
+    Y = np.column_stack([X.sum(1), (X ** 2).sum(1)])
+    ls = np.full(5, 0.8)
+    variances = [1.3, 0.7]
+    set_gps(ctx, X, Y, ls, variances, kernel="rbf")
+    Xc = rng.uniform(0, 1, (500, 5))
+    mu, var = ctx.posterior(dev(Xc), n_obj=2)
+    mu_o, var_o = oracle_posterior(X, Y, ls, variances, Xc, kernel="rbf")
+    assert_posterior(mu.cpu().numpy(), var.cpu().numpy(), mu_o, var_o, variances)
+
+
+@pytest.mark.parametrize("n,d,N", [(20, 2, 100), (512, 6, 4099), (100, 30, 77)])
+def test_kernel_block(ctx, n, d, N):
+    rng = np.random.default_rng(n + d)
+    X = rng.uniform(0, 1, (n, d))
+    Y = np.column_stack([X[:, 0], X.sum(1)])
+    ls = rng.uniform(0.3, 1.5, d)
+    set_gps(ctx, X, Y, ls, [0.9, 1.7])
+    Xc = rng.uniform(0, 1, (N, d))
+    K = ctx.kernel_block(1, dev(Xc)).cpu().numpy()
+    K_ref = ogp.matern52_K(X, Xc, ls, 1.7)
+    np.testing.assert_allclose(K, K_ref, rtol=1e-12, atol=1e-14)
+
+
+def test_posterior_full_size_properties(ctx):
+    """BASELINE config 3 size (n=512, N=2^20): size-independent properties + a sampled oracle check."""
+    from scipy.stats import qmc
+    rng = np.random.default_rng(0)
+    n, d, N = 512, 6, 1 << 20
+    X = rng.uniform(0, 1, (n, d))
+    f1 = X[:, 0]
+    g = 1 + 9.0 / (d - 1) * X[:, 1:].sum(1)
+    Y = np.column_stack([f1, g * (1 - np.sqrt(f1 / g))])
+    ls = np.random.default_rng(1).uniform(0.2, 2.0, d)
+    variances = [float(np.var(Y[:, 0])), float(np.var(Y[:, 1]))]
+    set_gps(ctx, X, Y, ls, variances)
+    Xc = qmc.Sobol(d=d, scramble=False).random_base2(m=20)
+    mu, var = ctx.posterior(dev(Xc), n_obj=2)
+    mu, var = mu.cpu().numpy(), var.cpu().numpy()
+    assert np.isfinite(mu).all() and np.isfinite(var).all()
+    for o in range(2):
+        assert var[o].max() <= variances[o] * (1 + 1e-12)
+        assert var[o].min() >= -1e-8 * variances[o]
+    idx = np.sort(rng.choice(N, 4096, replace=False))
+    mu_o, var_o = oracle_posterior(X, Y, ls, variances, Xc[idx])
+    assert_posterior(mu[:, idx], var[:, idx], mu_o, var_o, variances)
+    # determinism: a second launch is bitwise identical
+    mu2, var2 = ctx.posterior(dev(Xc), n_obj=2)
+    assert np.array_equal(mu2.cpu().numpy(), mu) and np.array_equal(var2.cpu().numpy(), var)
+
+
+# ----------------------------------------------------------------------------- acquisitions
+@pytest.mark.parametrize("P", [1, 3, 9, 30])
+@pytest.mark.parametrize("mode", ["reference", "textbook"])
+def test_ehvi2d_vs_golden(ctx, golden_dir, P, mode):
+    z = load(golden_dir, f"ehvi2d_P{P}.npz")
+    pf = z["pf"]
+    pf_sorted = pf[np.argsort(pf[:, 1])]
+    s00, s01 = oacq.cache_stats(z["cache"])
+    out = ctx.ehvi2d(dev(z["mu"]), dev(z["var"]), pf_sorted, z["r"], s00, s01, mode=mode).cpu().numpy()
+    ref = z["ehvi_reference" if mode == "reference" else "ehvi_textbook"]
+    assert np.array_equal(np.isnan(out), np.isnan(ref))
+    ok = ~np.isnan(ref)
+    np.testing.assert_allclose(out[ok], ref[ok], rtol=1e-5, atol=1e-12)
+
+
+def test_ehvi3d_vs_golden(ctx, golden_dir):
+    z = load(golden_dir, "ehvi3d.npz")
+    out, raised = ctx.ehvi3d_mc(dev(z["mu"]), dev(z["var"]), z["cache"], z["r"], float(z["hv_pf"]))
+    out, raised = out.cpu().numpy(), raised.cpu().numpy().astype(bool)
+    assert np.array_equal(raised, z["raises"])
+    ok = ~z["raises"]
+    np.testing.assert_allclose(out[ok], z["ehvi_reference"][ok], rtol=1e-5, atol=1e-12)
+    assert np.isnan(out[~ok]).all()
+
+
+def test_hvpoi_vs_golden(ctx, golden_dir):
+    z = load(golden_dir, "cells_hvpoi.npz")
+    for t in range(4):
+        cells = opar.decompose_into_cells(z[f"pf{t}"], z[f"ideal{t}"], z[f"max{t}"])
+        out = ctx.hvpoi(dev(z[f"mu{t}"]), dev(z[f"var{t}"]), cells).cpu().numpy()
+        np.testing.assert_allclose(out, z[f"hvpoi{t}"], rtol=1e-5, atol=1e-14)
+
+
+@pytest.mark.parametrize("k", [2, 3])
+@pytest.mark.parametrize("cls", osc.ALL, ids=lambda c: c.__name__)
+def test_expdec_vs_golden(ctx, golden_dir, k, cls):
+    z = load(golden_dir, "expdec.npz")
+    s = cls(z[f"k{k}_ideal"], z[f"k{k}_max"])
+    out = ctx.expdec(dev(z[f"k{k}_mu"]), dev(z[f"k{k}_var"]), z[f"k{k}_cache"], cls.ID, s.params(),
+                     z[f"k{k}_w"], z[f"k{k}_ideal"], z[f"k{k}_max"], float(z[f"k{k}_{cls.__name__}_min"])).cpu().numpy()
+    ref = z[f"k{k}_{cls.__name__}"]
+    np.testing.assert_allclose(out, ref, rtol=1e-5, atol=1e-12)
+
+
+def test_ei_vs_golden(ctx, golden_dir):
+    z = load(golden_dir, "ei.npz")
+    mu, var = dev(z["mu"]), dev(z["var"])
+    np.testing.assert_allclose(ctx.ei(mu, var, float(z["best"]), 0.0).cpu().numpy(), z["ei_mono"], rtol=1e-5, atol=1e-300)
+    np.testing.assert_allclose(ctx.ei(mu, var, float(z["best"]), 1e-6).cpu().numpy(), z["ei_parego"], rtol=1e-5,
+                               atol=1e-300)
+
+
+# ----------------------------------------------------------------------------- arg-max
+def test_argmax_rules(ctx):
+    rng = np.random.default_rng(9)
+    for N in [1, 7, 255, 256, 257, 100000, 1 << 20]:
+        v = rng.standard_normal(N)
+        if N > 10:
+            v[rng.choice(N, 5, replace=False)] = np.nan
+            v[N // 3] = v[N // 2] = v.max() + 1.0      # tie → lowest index
+        val, idx = ctx.argmax(dev(v), offset=17)
+        ov, oi = oacq.argmax(v, offset=17)
+        assert (val, idx) == (ov, oi)
+    assert ctx.argmax(dev(np.array([np.nan, -np.inf]))) == (-np.inf, -1)
+    r = ctx.argmax_dev(dev(np.array([1.0, 5.0, 5.0])), offset=3).cpu().numpy()
+    assert r[0] == 5.0 and r[1] == 4.0
+
+
+def test_chain_posterior_ehvi_argmax(ctx):
+    """End to end (config-2 shape, smaller N): posterior → reference EHVI → arg-max vs the oracle chain."""
+    rng = np.random.default_rng(2)
+    n, d, N = 128, 6, 1 << 14
+    X = rng.uniform(0, 1, (n, d))
+    f1 = X[:, 0]
+    g = 1 + 9.0 / (d - 1) * X[:, 1:].sum(1)
+    Y = np.column_stack([f1, g * (1 - np.sqrt(f1 / g))])
+    ls = rng.uniform(0.2, 2.0, d)
+    variances = [float(np.var(Y[:, 0])), float(np.var(Y[:, 1]))]
+    set_gps(ctx, X, Y, ls, variances)
+    Xc = rng.uniform(0, 1, (N, d))
+    mu, var = ctx.posterior(dev(Xc), n_obj=2)
+    pf = opar.calc_pf(Y)
+    r = Y.max(0) + 0.1 * (Y.max(0) - Y.min(0))
+    from scipy.stats import norm, qmc
+    cache = norm.ppf(qmc.Sobol(d=2, scramble=True, seed=0).random_base2(m=5))
+    s00, s01 = oacq.cache_stats(cache)
+    acq = ctx.ehvi2d(mu, var, pf[np.argsort(pf[:, 1])], r, s00, s01, mode="reference")
+    val, idx = ctx.argmax(acq)
+    mu_o, var_o = oracle_posterior(X, Y, ls, variances, Xc)
+    acq_o = oacq.ehvi2d(mu_o, var_o, pf, r, cache, mode="reference")
+    np.testing.assert_allclose(acq.cpu().numpy(), acq_o, rtol=1e-5, atol=1e-12)
+    ov, oi = oacq.argmax(acq_o)
+    assert idx == oi
+    assert abs(val - ov) <= 1e-9 * abs(ov)

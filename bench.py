@@ -1,0 +1,247 @@
+#!/usr/bin/env python
+"""Benchmark: EHVI candidate evaluations per second (BASELINE.json metric, config 3).
+
+One step = the whole acquisition hot path over one resident batch of candidates on every
+GPU: fused GP posterior for both objectives (omb_posterior) → reference-mode EHVI-2D
+(omb_ehvi2d) → device arg-max (omb_argmax_dev) → cross-rank arg-max exchange (RCCL
+all-gather of 16 B).  Workload per GPU: ZDT1 (n_var=6) surrogate with n_train=512 and
+N = 2^20 unscrambled-Sobol candidates; rank g scores Sobol indices [g·N, (g+1)·N) (weak scaling).
+
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W]
+        python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N  (multi-GPU)
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+FP64_MFMA_PEAK_TFLOPS = 78.6     # MI355X dense FP64 matrix peak (AMD spec; microbench: 70.3 measured)
+HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def zdt1(X):
+    """ZDT1 (optimobo/problem.py:924-936)."""
+    f1 = X[:, 0]
+    g = 1 + 9.0 / (X.shape[1] - 1) * np.sum(X[:, 1:], axis=1)
+    return np.column_stack([f1, g * (1 - np.sqrt(f1 / g))])
+
+
+def posterior_flops_per_candidate(n, d):
+    """n(n+1) triangular L⁻¹k* + 2n ‖·‖² + 2n αᵀk* + n(2d+2) distance + ~10n Matern."""
+    return n * (n + 1) + 2 * n + 2 * n + n * (2 * d + 2) + 10 * n
+
+
+def setup_problem(n, d, seed=0):
+    rng = np.random.default_rng(seed)
+    X = rng.uniform(0.0, 1.0, (n, d))
+    Y = zdt1(X)
+    ls = np.random.default_rng(seed + 1).uniform(0.2, 2.0, d)
+    variances = [float(np.var(Y[:, 0])), float(np.var(Y[:, 1]))]
+    return X, Y, ls, variances
+
+
+def candidates(d, start, count):
+    from scipy.stats import qmc
+    s = qmc.Sobol(d=d, scramble=False)
+    if start:
+        s.fast_forward(start)
+    return s.random(count)
+
+
+def cpu_baseline(X, Y, ls, variances, pf, r, cache, Xc, seconds):
+    """The oracle (numpy fp64, batched, BLAS-threaded) on a bounded sample of the same workload."""
+    from oracle import acquisition as oacq
+    from oracle import gp as ogp
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([p.get("num_threads", 1) for p in threadpool_info()] or [1])
+    except Exception:  # pragma: no cover
+        cores = os.cpu_count() or 1
+    gps = [ogp.ExactGP(X, Y[:, o], ls, variances[o]) for o in range(2)]
+    chunk = 4096
+    done = 0
+    t0 = time.perf_counter()
+    while True:
+        xc = Xc[done % len(Xc): done % len(Xc) + chunk]
+        mus, vs = [], []
+        for g in gps:
+            m, v = g.predict(xc)
+            mus.append(m[:, 0])
+            vs.append(v[:, 0])
+        acq = oacq.ehvi2d(np.array(mus), np.array(vs), pf, r, cache, mode="reference")
+        oacq.argmax(acq)
+        done += len(xc)
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "candidates/s", "cores": int(cores), "kind": "port",
+            "sample": f"{done} of the {len(Xc)} candidates (chunks of {chunk}), oracle posterior (dtrtrs) + "
+                      f"reference-mode EHVI-2D + arg-max, {dt:.1f} s"}
+
+
+def load_traffic(n, N):
+    """HBM bytes per posterior launch from the committed rocprofv3 PMC summary, if present."""
+    path = os.path.join(REPO, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        key = f"posterior_n{n}_N{N}"
+        return t.get(key, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n-train", type=int, default=512)
+    ap.add_argument("--n-var", type=int, default=6)
+    ap.add_argument("--log2-cand", type=int, default=20, help="candidates per GPU = 2^this")
+    ap.add_argument("--mode", default="reference", choices=["reference", "textbook"])
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kblock", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world_size > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group(backend="nccl", init_method="env://")
+    device = torch.device("cuda", local_rank)
+
+    from optimobo_amd import pareto
+    from optimobo_amd.device import AcqContext
+    from optimobo_amd.gp import GPState
+    from optimobo_amd.parallel import global_argmax
+
+    n, d = args.n_train, args.n_var
+    N = 1 << args.log2_cand
+    X, Y, ls, variances = setup_problem(n, d)
+    pf = pareto.calc_pf(Y)
+    pf_sorted = pareto.stripes_2d(pf)
+    r = Y.max(axis=0) + 0.1 * (Y.max(axis=0) - Y.min(axis=0))
+    cache = pareto.cached_samples(2, 5, seed=0)
+    s00, s01 = pareto.cache_stats(cache)
+
+    ctx = AcqContext(local_rank)
+    for o in range(2):
+        ctx.set_gp_state(o, GPState(X, Y[:, o], ls, variances[o]))
+    start = rank * N
+    Xc_host = candidates(d, start, N)
+    Xc = torch.as_tensor(Xc_host, device=device)
+    pf_dev = torch.as_tensor(pf_sorted, device=device)
+    mu = torch.empty((2, N), dtype=torch.float64, device=device)
+    var = torch.empty_like(mu)
+    acq = torch.empty(N, dtype=torch.float64, device=device)
+    pair = torch.empty(2, dtype=torch.float64, device=device)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+
+    def step(i=None):
+        if i is not None:
+            ev[i][0].record()
+        ctx.posterior(Xc, 2, out=(mu, var))
+        if i is not None:
+            ev[i][1].record()
+        ctx.ehvi2d(mu, var, pf_dev, r, s00, s01, mode=args.mode, out=acq)
+        ctx.argmax_dev(acq, offset=start, out=pair)
+        return global_argmax(pair)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    if world_size > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        best = step(i)
+    torch.cuda.synchronize()
+    if world_size > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world_size > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    post_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    best = best.cpu().numpy()
+
+    # standalone K(X, X*) block: the HBM-bound kernel of the north star
+    kblock = None
+    if not args.no_kblock:
+        K = torch.empty((n, N), dtype=torch.float64, device=device)
+        ctx.kernel_block(0, Xc, out=K)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 5
+        e0.record()
+        for _ in range(reps):
+            ctx.kernel_block(0, Xc, out=K)
+        e1.record()
+        torch.cuda.synchronize()
+        kb_ms = e0.elapsed_time(e1) / reps
+        kb_bytes = 8.0 * (n + d) * N + 8.0 * n * (d + 1)      # 8(n+d) per candidate + model state
+        kblock = {"bound": "hbm", "achieved": kb_bytes / (kb_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                  "frac": kb_bytes / (kb_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "ms": kb_ms,
+                  "note": "omb_kernel_block writes K (n, N) fp64 to HBM (4 GiB at config 3)"}
+        del K
+
+    flops = 2 * posterior_flops_per_candidate(n, d) * N
+    achieved = flops / (post_ms * 1e-3) / 1e12
+    roofline = {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": load_traffic(n, N),
+                "kernel": "posterior_kernel<4,4,6,Matern52> (omb_posterior, both objectives)",
+                "ms_per_launch": post_ms}
+
+    cpu = None
+    if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(X, Y, ls, variances, pf, r, cache, Xc_host, args.cpu_seconds)
+
+    if rank == 0:
+        total = N * world_size * args.steps
+        out = {
+            "metric": "EHVI candidate evals/sec at n_train=512, 2-obj; 1/2/4/8-GPU scaling",
+            "value": total / elapsed,
+            "unit": "candidates/s",
+            "n_gpus": world_size,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": f"2-obj EHVI ({args.mode} mode), ZDT1 surrogate, n_train={n}, n_var={d}, "
+                                   f"2^{args.log2_cand} Sobol candidates per GPU (BASELINE config 3)",
+                       "n_train": n, "n_var": d, "n_obj": 2, "candidates_per_gpu": N,
+                       "global_batch": N * world_size, "parallelism": f"dp{world_size}"},
+            "roofline": roofline,
+            "roofline_kblock": kblock,
+            "cpu_baseline": cpu,
+            "best": {"value": float(best[0]), "index": int(best[1])},
+        }
+        print(json.dumps(out))
+    if world_size > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

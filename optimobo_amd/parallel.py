@@ -1,0 +1,50 @@
+"""Multi-GPU candidate sharding: one process per GPU, torch.distributed (RCCL over xGMI).
+
+The candidate batch is embarrassingly parallel: every rank holds a replica
+of the per-iteration model state (X/ℓ, α, L⁻¹, σ_f², PF/cells, cache statistics) and scores
+its own contiguous shard of candidate indices.  The only exchange is the arg-max: each rank
+contributes {best value, best global index} (16 bytes) to one all-gather, and every rank
+reduces the gathered pairs with the same rule as the device kernel (highest value, lowest
+index on ties, index −1 = no valid candidate).  The result is identical to the single-GPU
+arg-max over the concatenated batch.
+"""
+import torch
+import torch.distributed as dist
+
+
+def world():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(), dist.get_rank()
+    return 1, 0
+
+
+def shard_range(n_total, world_size, rank):
+    """Contiguous shard [start, start+count) of rank ``rank``; sizes differ by at most one."""
+    base, extra = divmod(int(n_total), int(world_size))
+    start = rank * base + min(rank, extra)
+    return start, base + (1 if rank < extra else 0)
+
+
+def reduce_pairs(pairs):
+    """pairs (W, 2) float64 {value, index}: best value, lowest index; invalid index < 0."""
+    vals = pairs[:, 0]
+    idx = pairs[:, 1]
+    valid = idx >= 0
+    if not bool(valid.any()):
+        return pairs.new_tensor([float("-inf"), -1.0])
+    v = torch.where(valid, vals, torch.full_like(vals, float("-inf")))
+    best = v.max()
+    cand = valid & (v == best)
+    big = torch.full_like(idx, float("inf"))
+    i = torch.where(cand, idx, big).min()
+    return torch.stack([best, i])
+
+
+def global_argmax(local_pair, group=None):
+    """All-gather each rank's {value, global index} pair and reduce it identically everywhere."""
+    w, _ = world()
+    if w == 1:
+        return local_pair
+    gathered = [torch.empty_like(local_pair) for _ in range(w)]
+    dist.all_gather(gathered, local_pair.contiguous(), group=group)
+    return reduce_pairs(torch.stack(gathered))

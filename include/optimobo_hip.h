@@ -44,7 +44,7 @@ enum {
 };
 
 enum { OMB_KERNEL_MATERN52 = 0, OMB_KERNEL_RBF = 1 };
-enum { OMB_EHVI_REFERENCE = 0, OMB_EHVI_TEXTBOOK = 1 };
+enum { OMB_EHVI_REFERENCE = 0, OMB_EHVI_TEXTBOOK = 1, OMB_EHVI_SIGMA = 2 };
 
 /* Scalarisation ids (optimobo/scalarisations.py:37-397) and their params[] layout. */
 enum {
@@ -101,7 +101,8 @@ int omb_posterior(omb_ctx* ctx, int n_obj, const double* Xc_dev, int64_t N, doub
  *   pf_sorted_dev (P, 2): Pareto front sorted by f2 ascending (util_functions.py:98)
  *   r_host (2): reference (max) point;  s00, s01: np.cov(cache) entries (per-solve constants)
  *   mode OMB_EHVI_REFERENCE: σA = σ²0·s00, σB = σ²0·s01, last stripe omitted (bug-compatible)
- *   mode OMB_EHVI_TEXTBOOK : σA = sqrt(σ²0), σB = sqrt(σ²1), all P+1 stripes (exact EHVI) */
+ *   mode OMB_EHVI_TEXTBOOK : σA = sqrt(σ²0), σB = sqrt(σ²1), all P+1 stripes (exact EHVI)
+ *   mode OMB_EHVI_SIGMA    : var_dev holds (σA, σB) directly — EHVI_2D_aux(PF, r, μ, σ) itself */
 int omb_ehvi2d(omb_ctx* ctx, const double* mu_dev, const double* var_dev, int64_t ld, int64_t N,
                const double* pf_sorted_dev, int P, const double* r_host, double s00, double s01,
                int mode, double* out_dev);

@@ -15,7 +15,7 @@ OMB_OK, OMB_EINVAL, OMB_EHIP, OMB_ENOMEM, OMB_ESTATE, OMB_EUNSUP = 0, -1, -2, -3
 ERROR_NAMES = {OMB_EINVAL: "OMB_EINVAL", OMB_EHIP: "OMB_EHIP", OMB_ENOMEM: "OMB_ENOMEM",
                OMB_ESTATE: "OMB_ESTATE", OMB_EUNSUP: "OMB_EUNSUP"}
 KERNEL_MATERN52, KERNEL_RBF = 0, 1
-EHVI_REFERENCE, EHVI_TEXTBOOK = 0, 1
+EHVI_REFERENCE, EHVI_TEXTBOOK, EHVI_SIGMA = 0, 1, 2
 MAX_OBJ, MAX_DIM, MAX_TRAIN = 8, 32, 1024
 
 _p = ctypes.c_void_p

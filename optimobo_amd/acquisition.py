@@ -1,0 +1,146 @@
+"""Batched acquisition engine: the device replacement for the reference's maximiser loop.
+
+The reference maximises every acquisition with ``scipy.optimize.differential_evolution``,
+calling ``acq(x)`` one candidate at a time (optimisers.py:87,118,366; emo.py:240).  Here one
+BO iteration uploads the fitted surrogates once, scores a large quasi-random candidate batch
+on the GPU (posterior → acquisition) and reduces it with the device arg-max.  With
+torch.distributed initialised, every rank scores its own contiguous shard of the Sobol
+sequence and the ranks exchange one {value, index} pair (optimobo_amd.parallel); the winning
+point is regenerated from its Sobol index on every rank, so no coordinates are broadcast.
+"""
+import numpy as np
+import torch
+from scipy.stats import qmc
+
+from . import pareto
+from .device import AcqContext
+from .gp import GPState
+from .parallel import global_argmax, shard_range, world
+
+
+def _state_of(model):
+    if isinstance(model, GPState):
+        return model
+    if hasattr(model, "state"):
+        return model.state()
+    raise TypeError(f"unsupported surrogate {type(model).__name__}: expected optimobo_amd.gp.GPRegression/GPState")
+
+
+class AcquisitionEngine:
+    """Owns one AcqContext and the fitted GP state currently resident on the device."""
+
+    def __init__(self, device=None):
+        if device is None:
+            device = torch.cuda.current_device() if torch.cuda.is_available() else 0
+        self.ctx = AcqContext(device)
+        self.device = self.ctx.device
+        self._resident = {}
+        self.n_obj = 0
+
+    # ------------------------------------------------------------------ model state
+    def load_models(self, models):
+        for o, m in enumerate(models):
+            st = _state_of(m)
+            if self._resident.get(o) is not st:
+                self.ctx.set_gp_state(o, st)
+                self._resident[o] = st
+        self.n_obj = len(models)
+        return self
+
+    def _dev(self, x):
+        return torch.as_tensor(np.ascontiguousarray(x, dtype=np.float64), device=self.device)
+
+    def posterior(self, Xc):
+        Xc = Xc if isinstance(Xc, torch.Tensor) else self._dev(np.atleast_2d(Xc))
+        return self.ctx.posterior(Xc, self.n_obj)
+
+    # ------------------------------------------------------------------ acquisitions on a batch
+    def ehvi(self, Xc, max_point, PF, cache, mode="reference"):
+        """util_functions.EHVI (2 objectives) on every row of Xc."""
+        mu, var = self.posterior(Xc)
+        s00, s01 = pareto.cache_stats(np.asarray(cache, np.float64))
+        pf = pareto.stripes_2d(PF)
+        return self.ctx.ehvi2d(mu, var, pf, np.asarray(max_point, np.float64), s00, s01, mode=mode)
+
+    def ehvi_2d_aux(self, PF, r, mu, sigma):
+        """EHVI_2D_aux(PF, r, μ, σ) with σ given directly (util_functions.py:81), batched: (2, N)."""
+        mu = self._dev(np.asarray(mu, np.float64).reshape(2, -1))
+        sig = self._dev(np.asarray(sigma, np.float64).reshape(2, -1))
+        return self.ctx.ehvi2d(mu, sig, pareto.stripes_2d(PF), np.asarray(r, np.float64), 1.0, 1.0, mode="sigma")
+
+    def ehvi3d(self, Xc, max_point, PF, cache):
+        mu, var = self.posterior(Xc)
+        hv = pareto.hypervolume(PF, max_point)
+        return self.ctx.ehvi3d_mc(mu, var, np.asarray(cache, np.float64), np.asarray(max_point, np.float64), hv)
+
+    def expected_decomposition(self, Xc, weights, agg_func, agg_min, cache):
+        mu, var = self.posterior(Xc)
+        sid, params = agg_func.device_spec()
+        return self.ctx.expdec(mu, var, np.asarray(cache, np.float64), sid, params, np.asarray(weights, np.float64),
+                               np.asarray(agg_func.ideal_point, np.float64), np.asarray(agg_func.max_point, np.float64),
+                               float(agg_min))
+
+    def hvpoi(self, Xc, cells):
+        mu, var = self.posterior(Xc)
+        return self.ctx.hvpoi(mu, var, np.ascontiguousarray(cells, dtype=np.float64))
+
+    def ei(self, Xc, best, var_eps=0.0):
+        mu, var = self.posterior(Xc)
+        return self.ctx.ei(mu[0], var[0], float(best), float(var_eps))
+
+    # ------------------------------------------------------------------ maximiser
+    def maximise(self, acq_fn, lower, upper, n_candidates=1 << 16, seed=0, refine_rounds=2, shrink=0.1):
+        """Arg-max of ``acq_fn(Xc_tensor) -> (N,) tensor`` over [lower, upper]^d.
+
+        Round 0 scores the first ``n_candidates`` points of a scrambled Sobol sequence (seeded, so
+        every rank sees the same sequence and owns one contiguous shard).  Each refinement round
+        re-centres a box ``shrink`` times smaller on the incumbent and keeps it if it improves —
+        a batched stand-in for DE's final polish.  Returns (x_best (d,), value).
+        """
+        lower = np.asarray(lower, np.float64)
+        upper = np.asarray(upper, np.float64)
+        d = lower.size
+        W, rank = world()
+        best_x, best_v = None, -np.inf
+        lo, hi = lower, upper
+        for rnd in range(refine_rounds + 1):
+            start, count = shard_range(n_candidates, W, rank)
+            sob = qmc.Sobol(d=d, scramble=True, seed=seed + rnd)
+            if start:
+                sob.fast_forward(start)
+            U = sob.random(max(count, 1))[:count]
+            Xc = self._dev(lo + U * (hi - lo)) if count else torch.empty((0, d), dtype=torch.float64,
+                                                                           device=self.device)
+            vals = acq_fn(Xc) if count else torch.empty(0, dtype=torch.float64, device=self.device)
+            pair = self.ctx.argmax_dev(vals, offset=start) if count else torch.tensor([-np.inf, -1.0],
+                                                                                     dtype=torch.float64,
+                                                                                     device=self.device)
+            g = global_argmax(pair).cpu().numpy()
+            if g[1] >= 0 and g[0] > best_v:
+                idx = int(g[1])
+                s2 = qmc.Sobol(d=d, scramble=True, seed=seed + rnd)
+                if idx:
+                    s2.fast_forward(idx)
+                best_x = lo + s2.random(1)[0] * (hi - lo)
+                best_v = float(g[0])
+            if best_x is None:
+                break
+            half = shrink ** (rnd + 1) * (upper - lower) / 2
+            lo = np.maximum(lower, best_x - half)
+            hi = np.minimum(upper, best_x + half)
+        if best_x is None:   # every candidate was NaN/−inf: fall back to the first Sobol point
+            best_x = lower + qmc.Sobol(d=d, scramble=True, seed=seed).random(1)[0] * (upper - lower)
+        return best_x, best_v
+
+
+_ENGINES = {}
+
+
+def engine_for(models, device=None):
+    """Process-wide engine per device with ``models`` resident."""
+    if device is None:
+        device = torch.cuda.current_device() if torch.cuda.is_available() else 0
+    eng = _ENGINES.get(device)
+    if eng is None:
+        eng = _ENGINES[device] = AcquisitionEngine(device)
+    return eng.load_models(models)

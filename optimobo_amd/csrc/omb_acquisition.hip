@@ -49,9 +49,12 @@ __global__ __launch_bounds__(kAcqThreads) void ehvi2d_kernel(const double* __res
       }
       sA = v0 * s00;   // c00 = σ²0·Cov(cache)00   (util_functions.py:163-167, 114-115)
       sB = v0 * s01;   // c01 = σ²0·Cov(cache)01   (a covariance used as a std: quirk 2)
-    } else {
+    } else if (mode == OMB_EHVI_TEXTBOOK) {
       sA = sqrt(v0);
       sB = sqrt(var[ld + c]);
+    } else {   // OMB_EHVI_SIGMA: EHVI_2D_aux called with σ directly
+      sA = v0;
+      sB = var[ld + c];
     }
     double tp = (y1[0] - m0) / sA;
     double cdf_p = ndtr(tp), pdf_p = npdf(tp);

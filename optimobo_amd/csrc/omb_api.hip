@@ -251,7 +251,7 @@ int omb_ehvi2d(omb_ctx* ctx, const double* mu_dev, const double* var_dev, int64_
   if ((rc = check_moments(ctx, mu_dev, var_dev, ld, N, 2, out_dev))) return rc;
   if (!pf_sorted_dev || P < 1 || P > 4096) return fail(ctx, OMB_EINVAL, "Pareto front size P=%d outside [1, 4096]", P);
   if (!r_host) return fail(ctx, OMB_EINVAL, "null reference point");
-  if (mode != OMB_EHVI_REFERENCE && mode != OMB_EHVI_TEXTBOOK) return fail(ctx, OMB_EINVAL, "unknown EHVI mode %d", mode);
+  if (mode != OMB_EHVI_REFERENCE && mode != OMB_EHVI_TEXTBOOK && mode != OMB_EHVI_SIGMA) return fail(ctx, OMB_EINVAL, "unknown EHVI mode %d", mode);
   if (N == 0) return OMB_OK;
   hipError_t e = launch_ehvi2d(ctx->stream, mu_dev, var_dev, ld, N, pf_sorted_dev, P, r_host[0], r_host[1], s00, s01,
                                mode, out_dev);

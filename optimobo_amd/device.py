@@ -117,7 +117,7 @@ class AcqContext:
         N = mu.shape[1]
         pf = _dev_f64(pf_sorted, self.device)
         out = out if out is not None else torch.empty(N, dtype=torch.float64, device=self.device)
-        m = {"reference": _lib.EHVI_REFERENCE, "textbook": _lib.EHVI_TEXTBOOK}[mode]
+        m = {"reference": _lib.EHVI_REFERENCE, "textbook": _lib.EHVI_TEXTBOOK, "sigma": _lib.EHVI_SIGMA}[mode]
         self._stream()
         self._check(self.lib.omb_ehvi2d(self._h, _ptr(mu), _ptr(var), mu.stride(0), N, _ptr(pf), pf.shape[0],
                                         _lib.darr(r), float(s00), float(s01), m, _ptr(out)), "omb_ehvi2d")

@@ -1,0 +1,196 @@
+"""CPU tests of the drop-in host surface: scalarisations, Pareto geometry, Problem, reference
+directions and the GP fit.  The product modules are checked against the oracle (which is
+itself pinned to the reference by tests/test_oracle.py)."""
+import os
+
+import numpy as np
+import pytest
+
+from optimobo_amd import pareto
+from optimobo_amd import scalarisations as sc
+from optimobo_amd.gp import GPRegression, GPState, Matern52
+from optimobo_amd.problem import ElementwiseProblem, Problem, StarmapParallelization
+from optimobo_amd.refdirs import das_dennis
+from oracle import acquisition as oacq
+from oracle import gp as ogp
+from oracle import pareto as opar
+from oracle import scalarisations as osc
+
+
+# ----------------------------------------------------------------------------- scalarisations
+@pytest.mark.parametrize("name", [c.__name__ for c in sc.ALL])
+def test_scalarisation_matches_oracle(name):
+    rng = np.random.default_rng(len(name))
+    for k in (2, 3):
+        ideal = np.zeros(k)
+        mx = np.linspace(2, 5, k)
+        w = rng.dirichlet(np.ones(k))
+        F2 = rng.uniform(-0.5, 5, (40, k))
+        ours = getattr(sc, name)(ideal, mx)
+        ref = getattr(osc, name)(ideal, mx)
+        with np.errstate(all="ignore"):
+            np.testing.assert_allclose(ours(F2, w), ref(F2, w), rtol=1e-12, equal_nan=True)
+            one = ours(F2[3], w)
+            assert one.shape == (1,)
+            np.testing.assert_allclose(one, ref(F2[3:4], w), rtol=1e-12, equal_nan=True)
+
+
+def test_scalarisation_device_spec_ids_match_oracle():
+    for cls in sc.ALL:
+        sid, params = cls([0, 0], [1, 1]).device_spec()
+        ocls = osc.BY_NAME[cls.__name__]
+        assert sid == ocls.ID
+        assert params == [float(p) for p in ocls([0, 0], [1, 1]).params()]
+
+
+def test_scalarisation_set_bounds():
+    s = sc.Tchebicheff()
+    s.set_bounds([0, 0], [700, 12])
+    assert s(np.array([70.0, 6.0]), np.array([0.5, 0.5]))[0] == pytest.approx(0.25)
+
+
+# ----------------------------------------------------------------------------- Pareto geometry
+def test_calc_pf_golden(golden_dir):
+    z = np.load(os.path.join(golden_dir, "calc_pf.npz"))
+    for t in range(3):
+        np.testing.assert_array_equal(pareto.calc_pf(z[f"Y{t}"]), z[f"pf{t}"])
+
+
+def test_cells_golden(golden_dir):
+    z = np.load(os.path.join(golden_dir, "cells_hvpoi.npz"))
+    for t in range(4):
+        np.testing.assert_array_equal(pareto.decompose_into_cells(z[f"pf{t}"], z[f"ideal{t}"], z[f"max{t}"]),
+                                      z[f"cells{t}"])
+
+
+def test_cells_random_match_oracle():
+    rng = np.random.default_rng(4)
+    for _ in range(100):
+        pf = opar.calc_pf(rng.uniform(0, 1, (int(rng.integers(1, 30)), 2)))
+        ideal, mx = rng.uniform(-0.5, 0.2, 2), rng.uniform(1, 2, 2)
+        np.testing.assert_array_equal(pareto.decompose_into_cells(pf, ideal, mx),
+                                      opar.decompose_into_cells(pf, ideal, mx))
+
+
+@pytest.mark.parametrize("k", [2, 3, 4])
+def test_hypervolume(k):
+    rng = np.random.default_rng(k)
+    for _ in range(20):
+        pts = rng.uniform(0, 1, (int(rng.integers(1, 25)), k))
+        r = np.full(k, 1.1)
+        hv = pareto.hypervolume(pts, r)
+        if k <= 3:
+            assert hv == pytest.approx(opar.hypervolume(pts, r), rel=1e-12, abs=1e-15)
+        else:   # MC sanity for k = 4
+            u = rng.uniform(0, 1.1, (200000, k))
+            dom = np.zeros(len(u), bool)
+            for p in pts:
+                dom |= np.all(u >= p, axis=1)
+            assert hv == pytest.approx(dom.mean() * 1.1 ** k, abs=0.01)
+
+
+def test_cache_and_stripes():
+    c = pareto.cached_samples(2, 5, seed=0)
+    assert c.shape == (32, 2)
+    assert pareto.cache_stats(c) == pytest.approx(oacq.cache_stats(c))
+    pf = np.array([[0.1, 0.9], [0.5, 0.3], [0.3, 0.5]])
+    np.testing.assert_array_equal(pareto.stripes_2d(pf)[:, 1], [0.3, 0.5, 0.9])
+
+
+# ----------------------------------------------------------------------------- Problem
+class _Elem(ElementwiseProblem):
+    def __init__(self, **kw):
+        super().__init__(n_var=2, n_obj=2, n_ieq_constr=1, xl=np.array([-2, -2]), xu=np.array([2, 2]), **kw)
+
+    def _evaluate(self, x, out, *args, **kwargs):
+        out["F"] = [100 * (x[0] ** 2 + x[1] ** 2), (x[0] - 1) ** 2 + x[1] ** 2]
+
+    def _evaluate_constraints(self, x, out, *args, **kwargs):
+        out["G"] = [x[0] + x[1] - 1]
+
+
+class _Vec(Problem):
+    def __init__(self):
+        super().__init__(n_var=2, n_obj=2, n_ieq_constr=2, xl=0, xu=np.array([5.0, 3.0]))
+
+    def _evaluate(self, x, out, *args, **kwargs):
+        out["F"] = [4 * x[:, 0] ** 2 + 4 * x[:, 1] ** 2, (x[:, 0] - 5) ** 2 + (x[:, 1] - 5) ** 2]
+
+    def _evaluate_constraints(self, x, out, *args, **kwargs):
+        out["G"] = [(x[:, 0] - 5) ** 2 + x[:, 1] ** 2 - 25, -((x[:, 0] - 8) ** 2 + (x[:, 1] + 3) ** 2 - 7.7)]
+
+
+def test_problem_elementwise_shapes():
+    p = _Elem()
+    assert p.evaluate(np.array([0.5, 0.5])).shape == (2,)
+    assert p.evaluate(np.array([[0.5, 0.5], [1, 1]])).shape == (2, 2)
+    np.testing.assert_allclose(p.evaluate(np.array([1.0, 0.0])), [100.0, 0.0])
+    assert p.evaluate_constraints(np.array([1.0, 1.0])).shape == (1,)
+    assert p.xl.dtype == float and p.n_constr == 1 and p.has_bounds()
+
+
+def test_problem_vectorised_and_runner():
+    p = _Vec()
+    F = p.evaluate(np.array([[1.0, 1.0], [2.0, 0.5]]))
+    np.testing.assert_allclose(F[0], [8.0, 32.0])
+    assert p.evaluate_constraints(np.array([[1.0, 1.0]])).shape == (1, 2)
+    np.testing.assert_array_equal(p.xl, [0.0, 0.0])
+    import itertools
+    q = _Elem(elementwise_runner=StarmapParallelization(itertools.starmap))
+    assert q.evaluate(np.array([[0.5, 0.5], [1, 1]])).shape == (2, 2)
+    F, = [q.evaluate(np.array([0.0, 0.0]), return_values_of=["F"])]
+    assert F.shape == (2,)
+    d = q.evaluate(np.array([0.0, 0.0]), return_as_dictionary=True)
+    assert set(d) == {"F"}
+
+
+def test_problem_shape_error():
+    class Bad(Problem):
+        def __init__(self):
+            super().__init__(n_var=2, n_obj=3, xl=0, xu=1)
+
+        def _evaluate(self, x, out, *args, **kwargs):
+            out["F"] = np.zeros((len(x), 2))
+    with pytest.raises(Exception, match="Problem Error"):
+        Bad().evaluate(np.zeros((4, 2)))
+
+
+# ----------------------------------------------------------------------------- reference directions
+def test_das_dennis():
+    a = das_dennis(2, 100)
+    assert a.shape == (101, 2) and np.allclose(a.sum(1), 1)
+    b = das_dennis(3, 12)
+    assert b.shape == (91, 3) and np.allclose(b.sum(1), 1) and (b >= 0).all()
+    assert len({tuple(r) for r in np.round(b * 12).astype(int)}) == 91
+
+
+# ----------------------------------------------------------------------------- GP fit (host)
+def test_gpstate_matches_oracle_factors():
+    rng = np.random.default_rng(0)
+    X = rng.uniform(0, 1, (60, 3))
+    y = np.sin(4 * X).sum(1)
+    st = GPState(X, y, [0.3, 0.5, 0.9], 1.3)
+    g = ogp.ExactGP(X, y, [0.3, 0.5, 0.9], 1.3)
+    np.testing.assert_allclose(st.L, g.L, rtol=1e-12, atol=1e-14)
+    np.testing.assert_allclose(st.alpha, g.alpha, rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(st.Linv @ st.L, np.eye(60), atol=1e-8)
+
+
+def test_gp_fit_gradient_and_improvement():
+    rng = np.random.default_rng(1)
+    X = rng.uniform(0, 1, (30, 2))
+    y = np.sin(5 * X[:, 0]) + X[:, 1] ** 2
+    m = GPRegression(X, y[:, None], Matern52(2, ARD=True))
+    m.Gaussian_noise.variance.fix(0)
+    th = m._get_free() + np.array([0.3, -0.2, 0.1])
+    f, g = m._neg_lml_and_grad(th)
+    eps = 1e-6
+    for i in range(len(th)):
+        e = np.zeros_like(th)
+        e[i] = eps
+        fd = (m._neg_lml_and_grad(th + e)[0] - m._neg_lml_and_grad(th - e)[0]) / (2 * eps)
+        assert g[i] == pytest.approx(fd, rel=1e-4, abs=1e-5)
+    m._set_free(np.zeros(3))
+    before = m.log_likelihood()
+    m.optimize(max_f_eval=200)
+    assert m.log_likelihood() >= before

@@ -1,0 +1,84 @@
+"""Multi-rank arg-max exchange on CPU (gloo, world_size 2 and 3): the sharded result must equal
+the single-process arg-max over the whole batch."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from optimobo_amd.parallel import global_argmax, reduce_pairs, shard_range
+from oracle import acquisition as oacq
+
+
+def test_shard_range_covers_exactly():
+    for n in [0, 1, 7, 64, 1000, (1 << 20) + 3]:
+        for w in [1, 2, 3, 8]:
+            spans = [shard_range(n, w, r) for r in range(w)]
+            assert spans[0][0] == 0
+            for (s0, c0), (s1, _) in zip(spans, spans[1:]):
+                assert s0 + c0 == s1
+            assert sum(c for _, c in spans) == n
+            assert max(c for _, c in spans) - min(c for _, c in spans) <= 1
+
+
+def test_reduce_pairs_rules():
+    P = torch.tensor([[1.0, 5.0], [3.0, 9.0], [3.0, 2.0], [float("-inf"), -1.0]], dtype=torch.float64)
+    assert reduce_pairs(P).tolist() == [3.0, 2.0]
+    none = torch.tensor([[float("-inf"), -1.0], [float("-inf"), -1.0]], dtype=torch.float64)
+    assert reduce_pairs(none).tolist() == [float("-inf"), -1.0]
+
+
+def _local_pair(vals, start):
+    # the device kernel's rule on this rank's shard (NaN / −inf never win, lowest index on ties)
+    v, i = oacq.argmax(vals, offset=start)
+    return torch.tensor([v, float(i)], dtype=torch.float64)
+
+
+def _worker(rank, world, port, vals, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        start, count = shard_range(len(vals), world, rank)
+        g = global_argmax(_local_pair(vals[start:start + count], start))
+        q.put((rank, g.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_global_argmax_matches_single_process(world):
+    rng = np.random.default_rng(world)
+    cases = []
+    v = rng.standard_normal(1001)
+    cases.append(v)
+    t = v.copy()
+    t[100] = t[900] = t.max() + 1          # tie across shards → lowest global index
+    cases.append(t)
+    n = v.copy()
+    n[:600] = np.nan                        # a whole shard of NaN
+    cases.append(n)
+    cases.append(np.full(10, np.nan))       # nothing valid anywhere
+    ctx = mp.get_context("spawn")
+    for vals in cases:
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_worker, args=(r, world, port, vals, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+        got = [q.get(timeout=120) for _ in range(world)]
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+        ev, ei = oacq.argmax(vals)
+        for _, (gv, gi) in got:
+            assert (gv, int(gi)) == (ev, ei)

@@ -33,17 +33,43 @@ def zdt1(X):
     return np.column_stack([f1, g * (1 - np.sqrt(f1 / g))])
 
 
+def dtlz2(X, k=3):
+    """DTLZ2 with k objectives (builder-defined 3-objective workload of BASELINE config 4)."""
+    g = np.sum((X[:, k - 1:] - 0.5) ** 2, axis=1)
+    th = X[:, :k - 1] * np.pi / 2
+    F = np.empty((len(X), k))
+    for i in range(k):
+        f = 1 + g
+        for j in range(k - 1 - i):
+            f = f * np.cos(th[:, j])
+        if i > 0:
+            f = f * np.sin(th[:, k - 1 - i])
+        F[:, i] = f
+    return F
+
+
 def posterior_flops_per_candidate(n, d):
     """n(n+1) triangular L⁻¹k* + 2n ‖·‖² + 2n αᵀk* + n(2d+2) distance + ~10n Matern."""
     return n * (n + 1) + 2 * n + 2 * n + n * (2 * d + 2) + 10 * n
 
 
-def setup_problem(n, d, seed=0):
+# BASELINE.json configs 2-5 (config 1 is the CPU-only README run).  Per-GPU candidate counts:
+# configs 4 and 5 quote their totals over 8 GPUs, so one GPU scores 1/8 of them (weak scaling).
+CONFIGS = {
+    2: dict(problem="zdt1", n=128, d=6, log2=16, acq="ehvi2d"),
+    3: dict(problem="zdt1", n=512, d=6, log2=20, acq="ehvi2d"),
+    4: dict(problem="dtlz2", n=256, d=6, log2=17, acq="ehvi3d"),
+    5: dict(problem="zdt1", n=1024, d=30, log2=19, acq="ei_tch"),
+}
+METRIC = "EHVI candidate evals/sec at n_train=512, 2-obj; 1/2/4/8-GPU scaling"
+
+
+def setup_problem(n, d, seed=0, problem="zdt1"):
     rng = np.random.default_rng(seed)
     X = rng.uniform(0.0, 1.0, (n, d))
-    Y = zdt1(X)
+    Y = zdt1(X) if problem == "zdt1" else dtlz2(X)
     ls = np.random.default_rng(seed + 1).uniform(0.2, 2.0, d)
-    variances = [float(np.var(Y[:, 0])), float(np.var(Y[:, 1]))]
+    variances = [float(np.var(Y[:, o])) for o in range(Y.shape[1])]
     return X, Y, ls, variances
 
 
@@ -55,7 +81,7 @@ def candidates(d, start, count):
     return s.random(count)
 
 
-def cpu_baseline(X, Y, ls, variances, pf, r, cache, Xc, seconds):
+def cpu_baseline(X, Y, ls, variances, pf, r, cache, Xc, seconds):  # noqa: C901
     """The oracle (numpy fp64, batched, BLAS-threaded) on a bounded sample of the same workload."""
     from oracle import acquisition as oacq
     from oracle import gp as ogp
@@ -103,14 +129,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n-train", type=int, default=512)
-    ap.add_argument("--n-var", type=int, default=6)
-    ap.add_argument("--log2-cand", type=int, default=20, help="candidates per GPU = 2^this")
+    ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS), help="BASELINE.json config")
+    ap.add_argument("--log2-cand", type=int, default=None, help="candidates per GPU = 2^this (default: config)")
     ap.add_argument("--mode", default="reference", choices=["reference", "textbook"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kblock", action="store_true")
     args = ap.parse_args()
+    cfg = CONFIGS[args.config]
 
     import torch
     import torch.distributed as dist
@@ -118,45 +144,74 @@ def main():
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # OMB_DIST_BACKEND=gloo rehearses the multi-rank path on a box with fewer GPUs than ranks
+    # (ranks then share GPUs round-robin); the driver's multi-GPU runs use nccl (= RCCL).
+    backend = os.environ.get("OMB_DIST_BACKEND", "nccl")
+    gpu = local_rank % max(1, torch.cuda.device_count()) if backend == "gloo" else local_rank
     if world_size > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group(backend="nccl", init_method="env://")
-    device = torch.device("cuda", local_rank)
+        torch.cuda.set_device(gpu)
+        dist.init_process_group(backend=backend, init_method="env://")
+    device = torch.device("cuda", gpu)
+    local_rank = gpu
 
     from optimobo_amd import pareto
+    from optimobo_amd import scalarisations as sc
     from optimobo_amd.device import AcqContext
     from optimobo_amd.gp import GPState
     from optimobo_amd.parallel import global_argmax
 
-    n, d = args.n_train, args.n_var
-    N = 1 << args.log2_cand
-    X, Y, ls, variances = setup_problem(n, d)
+    n, d, acq_kind = cfg["n"], cfg["d"], cfg["acq"]
+    N = 1 << (args.log2_cand if args.log2_cand is not None else cfg["log2"])
+    X, Y, ls, variances = setup_problem(n, d, problem=cfg["problem"])
+    k_obj = Y.shape[1]
     pf = pareto.calc_pf(Y)
-    pf_sorted = pareto.stripes_2d(pf)
     r = Y.max(axis=0) + 0.1 * (Y.max(axis=0) - Y.min(axis=0))
-    cache = pareto.cached_samples(2, 5, seed=0)
-    s00, s01 = pareto.cache_stats(cache)
+    cache = pareto.cached_samples(k_obj, 5, seed=0)
 
     ctx = AcqContext(local_rank)
-    for o in range(2):
-        ctx.set_gp_state(o, GPState(X, Y[:, o], ls, variances[o]))
+    if acq_kind == "ei_tch":
+        # ParEGO-style mono surrogate: Tchebicheff-aggregate the objectives (parego.py:212-219)
+        tch = sc.Tchebicheff(Y.min(axis=0), Y.max(axis=0))
+        yagg = tch(Y, np.array([0.5, 0.5]))
+        states = [GPState(X, yagg, ls, float(np.var(yagg)))]
+        best_y = float(yagg.min())
+    else:
+        states = [GPState(X, Y[:, o], ls, variances[o]) for o in range(k_obj)]
+    n_obj = len(states)
+    for o, st in enumerate(states):
+        ctx.set_gp_state(o, st)
+
     start = rank * N
     Xc_host = candidates(d, start, N)
     Xc = torch.as_tensor(Xc_host, device=device)
-    pf_dev = torch.as_tensor(pf_sorted, device=device)
-    mu = torch.empty((2, N), dtype=torch.float64, device=device)
+    mu = torch.empty((n_obj, N), dtype=torch.float64, device=device)
     var = torch.empty_like(mu)
     acq = torch.empty(N, dtype=torch.float64, device=device)
+    raised = torch.empty(N, dtype=torch.int32, device=device)
     pair = torch.empty(2, dtype=torch.float64, device=device)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if acq_kind == "ehvi2d":
+        s00, s01 = pareto.cache_stats(cache)
+        pf_dev = torch.as_tensor(pareto.stripes_2d(pf), device=device)
+    elif acq_kind == "ehvi3d":
+        hv_pf = pareto.hypervolume(pf, r)
+        cache_dev = torch.as_tensor(cache, device=device)
+
+    def acquisition():
+        if acq_kind == "ehvi2d":
+            ctx.ehvi2d(mu, var, pf_dev, r, s00, s01, mode=args.mode, out=acq)
+        elif acq_kind == "ehvi3d":
+            ctx.ehvi3d_mc(mu, var, cache_dev, r, hv_pf, out=acq, raised=raised)
+        else:
+            ctx.ei(mu[0], var[0], best_y, 1e-6, out=acq)
 
     def step(i=None):
         if i is not None:
             ev[i][0].record()
-        ctx.posterior(Xc, 2, out=(mu, var))
+        ctx.posterior(Xc, n_obj, out=(mu, var))
         if i is not None:
             ev[i][1].record()
-        ctx.ehvi2d(mu, var, pf_dev, r, s00, s01, mode=args.mode, out=acq)
+        acquisition()
         ctx.argmax_dev(acq, offset=start, out=pair)
         return global_argmax(pair)
 
@@ -175,7 +230,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world_size > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     post_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
@@ -198,24 +253,26 @@ def main():
         kb_bytes = 8.0 * (n + d) * N + 8.0 * n * (d + 1)      # 8(n+d) per candidate + model state
         kblock = {"bound": "hbm", "achieved": kb_bytes / (kb_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                   "frac": kb_bytes / (kb_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "ms": kb_ms,
-                  "note": "omb_kernel_block writes K (n, N) fp64 to HBM (4 GiB at config 3)"}
+                  "note": f"omb_kernel_block writes K ({n}, {N}) fp64 to HBM"}
         del K
 
-    flops = 2 * posterior_flops_per_candidate(n, d) * N
+    flops = n_obj * posterior_flops_per_candidate(n, d) * N
     achieved = flops / (post_ms * 1e-3) / 1e12
     roofline = {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": load_traffic(n, N),
-                "kernel": "posterior_kernel<4,4,6,Matern52> (omb_posterior, both objectives)",
+                "kernel": f"posterior_kernel (omb_posterior, {n_obj} objective(s), n_train={n}, n_var={d})",
                 "ms_per_launch": post_ms}
 
     cpu = None
-    if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world_size == 1 and not args.no_cpu_baseline and acq_kind == "ehvi2d":
         cpu = cpu_baseline(X, Y, ls, variances, pf, r, cache, Xc_host, args.cpu_seconds)
 
     if rank == 0:
         total = N * world_size * args.steps
+        label = {"ehvi2d": f"2-obj EHVI ({args.mode} mode)", "ehvi3d": "3-obj EHVI (reference Monte-Carlo form)",
+                 "ei_tch": "ParEGO Tchebicheff EI (mono surrogate)"}[acq_kind]
         out = {
-            "metric": "EHVI candidate evals/sec at n_train=512, 2-obj; 1/2/4/8-GPU scaling",
+            "metric": METRIC if args.config == 3 else f"{label} candidate evals/sec (BASELINE config {args.config})",
             "value": total / elapsed,
             "unit": "candidates/s",
             "n_gpus": world_size,
@@ -227,9 +284,9 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": f"2-obj EHVI ({args.mode} mode), ZDT1 surrogate, n_train={n}, n_var={d}, "
-                                   f"2^{args.log2_cand} Sobol candidates per GPU (BASELINE config 3)",
-                       "n_train": n, "n_var": d, "n_obj": 2, "candidates_per_gpu": N,
+            "config": {"workload": f"{label}, {cfg['problem'].upper()} surrogate, n_train={n}, n_var={d}, "
+                                   f"2^{int(np.log2(N))} Sobol candidates per GPU (BASELINE config {args.config})",
+                       "n_train": n, "n_var": d, "n_obj": k_obj, "candidates_per_gpu": N,
                        "global_batch": N * world_size, "parallelism": f"dp{world_size}"},
             "roofline": roofline,
             "roofline_kblock": kblock,

@@ -126,24 +126,32 @@ __global__ __launch_bounds__(256) void kernel_block_kernel(GPDev g, int d, const
 }
 
 // ----------------------------------------------------------------------------- posterior
-template <int RT, int CT, int DP, int KIND>
-__global__ __launch_bounds__(kBlockThreads, 2) void posterior_kernel(GPArgs args, const double* __restrict__ Xc,
-                                                                      int64_t N, double* __restrict__ mu_out,
-                                                                      double* __restrict__ var_out) {
+// ABL (ablation, tools/ablate only; the library instantiates ABL = 0): bit 1 replaces the Matern
+// transform by the raw dot product, bit 2 skips the MFMA phase, bit 4 feeds a constant A
+// operand instead of loading L⁻¹, bit 8 drops the per-chunk barrier.
+// NW = waves per workgroup (8 or 16): waves w, w+4, w+8, w+12 share a SIMD.
+template <int RT, int CT, int DP, int KIND, int NW = 8, int ABL = 0>
+__global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args, const double* __restrict__ Xc,
+                                                                     int64_t N, double* __restrict__ mu_out,
+                                                                     double* __restrict__ var_out) {
+  constexpr int NT = 64 * NW;                 // threads per workgroup
+  constexpr int G = NW / 4;                   // waves sharing one SIMD
   constexpr int BN = 16 * CT;                 // candidates per workgroup
   constexpr int KS = kChunkRows / 4;          // MFMA k-steps per chunk (16)
   constexpr int CHUNK = kChunkRows * BN;      // doubles per LDS buffer
-  constexpr int EPT = CHUNK / kBlockThreads;  // generated K* elements per thread per chunk
-  static_assert(kBlockThreads % BN == 0, "BN must divide the block");
+  constexpr int EPT = CHUNK / NT;             // generated K* elements per thread per chunk
+  static_assert(NT % BN == 0 && CHUNK % NT == 0, "BN must divide the block");
+  static_assert(2 * CHUNK >= NW * BN + NT, "epilogue scratch must fit in the K* buffers");
   __shared__ double kbuf[2 * CHUNK];
 
   const int obj = blockIdx.y;
   const GPDev g = args.gp[obj];
   const int d = args.d;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t c0 = (int64_t)blockIdx.x * BN;
 
-  // ---- this thread's generation candidate (fixed across chunks since BN | 512)
+  // ---- this thread's generation candidate (fixed across chunks since BN | NT)
   const int cg = tid % BN;
   const int64_t ci = min(c0 + cg, N - 1);
   double b[DP];
@@ -155,15 +163,17 @@ __global__ __launch_bounds__(kBlockThreads, 2) void posterior_kernel(GPArgs args
   }
   const int gen_ct = cg >> 4, gen_cc = cg & 15;
 
-  // ---- row-tile slots of this wave (SIMD-pair balanced, see header)
-  const int pair = wave & 3, half = wave >> 2;
+  // ---- row-tile slots of this wave (SIMD balanced, see header): SIMD group s = wave & 3 owns
+  // tile 4q + ((s + q) & 3) of every quad q; the G waves of the group take quads in snake order
+  // (q mod 2G = 0,1,..,G-1,G-1,..,0), so wave h's j-th quad is 2G(j>>1) + (j odd ? 2G-1-h : h).
+  const int simd = wave & 3, h = wave >> 2;
   const int Q = (g.R + 3) >> 2;  // chunks of 64 rows
   int slot_r[RT], slot_q[RT];
   const double* slot_A[RT];
 #pragma unroll
   for (int j = 0; j < RT; ++j) {
-    int q = 4 * (j >> 1) + (half ? (1 + (j & 1)) : 3 * (j & 1));
-    int r = 4 * q + ((pair + q) & 3);
+    int q = 2 * G * (j >> 1) + ((j & 1) ? (2 * G - 1 - h) : h);
+    int r = 4 * q + ((simd + q) & 3);
     bool ok = r < g.R;
     slot_q[j] = ok ? q : -1;
     slot_r[j] = ok ? r : 0;
@@ -180,7 +190,7 @@ __global__ __launch_bounds__(kBlockThreads, 2) void posterior_kernel(GPArgs args
   auto generate = [&](int kc, double* buf) {
 #pragma unroll
     for (int i = 0; i < EPT; ++i) {
-      const int e = tid + kBlockThreads * i;
+      const int e = tid + NT * i;
       const int kl = e / BN;
       const int k = kc * kChunkRows + kl;
       double val = 0.0;
@@ -189,7 +199,10 @@ __global__ __launch_bounds__(kBlockThreads, 2) void posterior_kernel(GPArgs args
         double dot = 0.0;
 #pragma unroll
         for (int j = 0; j < DP; ++j) dot = fma(xr[j], b[j], dot);
-        val = kernel_of_r2<KIND>(fma(-2.0, dot, g.xsq[k] + csq), g.variance);
+        if constexpr (ABL & 1)
+          val = dot;
+        else
+          val = kernel_of_r2<KIND>(fma(-2.0, dot, g.xsq[k] + csq), g.variance);
         mu_part = fma(g.alpha[k], val, mu_part);
       }
       buf[((kl >> 2) * CT + gen_ct) * 64 + (kl & 3) * 16 + gen_cc] = val;
@@ -197,6 +210,7 @@ __global__ __launch_bounds__(kBlockThreads, 2) void posterior_kernel(GPArgs args
   };
 
   auto multiply = [&](int kc, const double* buf) {
+    if constexpr (ABL & 2) return;
     // k-steps of each slot inside this chunk: 16 (below the diagonal quad), 4(r mod 4 + 1)
     // (diagonal quad), 0 (finished or empty slot).
     int nS[RT];
@@ -204,15 +218,36 @@ __global__ __launch_bounds__(kBlockThreads, 2) void posterior_kernel(GPArgs args
     for (int j = 0; j < RT; ++j)
       nS[j] = (slot_q[j] > kc) ? KS : (slot_q[j] == kc ? 4 * ((slot_r[j] & 3) + 1) : 0);
     const int P0 = kc * (KS / 2);
+    // With 2 waves per SIMD the next k-step pair of A is prefetched into registers; with 4 the
+    // other waves hide the L2 latency and the registers are worth more as occupancy.
+    constexpr bool kPrefetchA = (NW == 8);
     d2 a_cur[RT], a_nxt[RT];
 #pragma unroll
-    for (int j = 0; j < RT; ++j) a_cur[j] = *reinterpret_cast<const d2*>(slot_A[j] + 128 * min(P0, 2 * slot_r[j] + 1));
+    for (int j = 0; j < RT; ++j) {
+      if constexpr (ABL & 4)
+        a_cur[j] = d2{1e-3 * lane, 2e-3 * j};
+      else
+        a_cur[j] = *reinterpret_cast<const d2*>(slot_A[j] + 128 * min(P0, 2 * slot_r[j] + 1));
+    }
 #pragma unroll
     for (int sp = 0; sp < KS / 2; ++sp) {
-      if (sp + 1 < KS / 2) {
+      if (!kPrefetchA && sp > 0) {
 #pragma unroll
-        for (int j = 0; j < RT; ++j)
-          a_nxt[j] = *reinterpret_cast<const d2*>(slot_A[j] + 128 * min(P0 + sp + 1, 2 * slot_r[j] + 1));
+        for (int j = 0; j < RT; ++j) {
+          if constexpr (ABL & 4)
+            a_cur[j] = d2{a_cur[j].y, a_cur[j].x};
+          else
+            a_cur[j] = *reinterpret_cast<const d2*>(slot_A[j] + 128 * min(P0 + sp, 2 * slot_r[j] + 1));
+        }
+      }
+      if (kPrefetchA && sp + 1 < KS / 2) {
+#pragma unroll
+        for (int j = 0; j < RT; ++j) {
+          if constexpr (ABL & 4)
+            a_nxt[j] = d2{a_cur[j].y, a_cur[j].x};
+          else
+            a_nxt[j] = *reinterpret_cast<const d2*>(slot_A[j] + 128 * min(P0 + sp + 1, 2 * slot_r[j] + 1));
+        }
       }
       double b0[CT], b1[CT];
 #pragma unroll
@@ -230,7 +265,7 @@ __global__ __launch_bounds__(kBlockThreads, 2) void posterior_kernel(GPArgs args
           }
         }
       }
-      if (sp + 1 < KS / 2) {
+      if (kPrefetchA && sp + 1 < KS / 2) {
 #pragma unroll
         for (int j = 0; j < RT; ++j) a_cur[j] = a_nxt[j];
       }
@@ -240,9 +275,14 @@ __global__ __launch_bounds__(kBlockThreads, 2) void posterior_kernel(GPArgs args
   generate(0, kbuf);
   __syncthreads();
   for (int kc = 0; kc < Q; ++kc) {
-    if (kc + 1 < Q) generate(kc + 1, kbuf + ((kc + 1) & 1) * CHUNK);
-    multiply(kc, kbuf + (kc & 1) * CHUNK);
-    __syncthreads();
+    if constexpr (NW == 8) {
+      if (kc + 1 < Q) generate(kc + 1, kbuf + ((kc + 1) & 1) * CHUNK);
+      multiply(kc, kbuf + (kc & 1) * CHUNK);
+    } else {   // 4 waves per SIMD interleave across waves; keep each wave's live range short
+      multiply(kc, kbuf + (kc & 1) * CHUNK);
+      if (kc + 1 < Q) generate(kc + 1, kbuf + ((kc + 1) & 1) * CHUNK);
+    }
+    if constexpr (!(ABL & 8)) __syncthreads();
   }
 
   // ---- σ²: Σ over rows of V² — registers, then lanes {l, l^16, l^32, l^48}, then waves.
@@ -258,8 +298,8 @@ __global__ __launch_bounds__(kBlockThreads, 2) void posterior_kernel(GPArgs args
     s += __shfl_xor(s, 32);
     part[ct] = s;
   }
-  double* red = kbuf;                 // 8 waves × BN
-  double* redmu = kbuf + 8 * BN;      // 512 partial μ
+  double* red = kbuf;                 // NW waves × BN
+  double* redmu = kbuf + NW * BN;     // NT partial μ
   if (lane < 16) {
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) red[wave * BN + ct * 16 + lane] = part[ct];
@@ -269,9 +309,9 @@ __global__ __launch_bounds__(kBlockThreads, 2) void posterior_kernel(GPArgs args
   if (tid < BN) {
     double s = 0.0;
 #pragma unroll
-    for (int w = 0; w < 8; ++w) s += red[w * BN + tid];
+    for (int w = 0; w < NW; ++w) s += red[w * BN + tid];
     double m = 0.0;
-    for (int t = tid; t < kBlockThreads; t += BN) m += redmu[t];
+    for (int t = tid; t < NT; t += BN) m += redmu[t];
     const int64_t c = c0 + tid;
     if (c < N) {
       mu_out[(int64_t)obj * N + c] = m;

@@ -45,6 +45,9 @@ def global_argmax(local_pair, group=None):
     w, _ = world()
     if w == 1:
         return local_pair
-    gathered = [torch.empty_like(local_pair) for _ in range(w)]
-    dist.all_gather(gathered, local_pair.contiguous(), group=group)
-    return reduce_pairs(torch.stack(gathered))
+    pair = local_pair.contiguous()
+    if dist.get_backend(group) == "gloo" and pair.is_cuda:
+        pair = pair.cpu()            # gloo rehearsal of the multi-rank path (tests, 1-GPU boxes)
+    gathered = [torch.empty_like(pair) for _ in range(w)]
+    dist.all_gather(gathered, pair, group=group)
+    return reduce_pairs(torch.stack(gathered)).to(local_pair.device)

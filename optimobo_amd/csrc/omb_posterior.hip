@@ -128,7 +128,7 @@ __global__ __launch_bounds__(256) void kernel_block_kernel(GPDev g, int d, const
 // ----------------------------------------------------------------------------- posterior
 // ABL (ablation, tools/ablate only; the library instantiates ABL = 0): bit 1 replaces the Matern
 // transform by the raw dot product, bit 2 skips the MFMA phase, bit 4 feeds a constant A
-// operand instead of loading L⁻¹, bit 8 drops the per-chunk barrier.
+// operand instead of loading L⁻¹, bit 8 drops the per-chunk barrier, bit 16 uses libm exp/sqrt.
 // NW = waves per workgroup (8 or 16): waves w, w+4, w+8, w+12 share a SIMD.
 template <int RT, int CT, int DP, int KIND, int NW = 8, int ABL = 0>
 __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args, const double* __restrict__ Xc,
@@ -202,7 +202,7 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
         if constexpr (ABL & 1)
           val = dot;
         else
-          val = kernel_of_r2<KIND>(fma(-2.0, dot, g.xsq[k] + csq), g.variance);
+          val = kernel_of_r2<KIND, !(ABL & 16)>(fma(-2.0, dot, g.xsq[k] + csq), g.variance);
         mu_part = fma(g.alpha[k], val, mu_part);
       }
       buf[((kl >> 2) * CT + gen_ct) * 64 + (kl & 3) * 16 + gen_cc] = val;

@@ -59,10 +59,13 @@ int main(int argc, char** argv) {
   a.d = d;
   a.DP = DP;
   const char* names[] = {"8w full", "8w no-matern(1)", "8w no-mfma(2)", "8w constA(4)", "8w nobarrier(8)",
-                         "16w full", "16w no-matern(1)", "16w no-mfma(2)", "16w constA(4)", "16w nobarrier(8)"};
-  const int NV = 10;
+                         "16w full", "16w no-matern(1)", "16w no-mfma(2)", "16w constA(4)", "16w nobarrier(8)",
+                         "8w libm-math(16)", "16w libm-math(16)"};
+  const int NV = 12;
   float t[NV] = {0};
   for (int round = 0; round < 3; ++round) {
+    t[10] += run<4, 8, 16>(a, Xc, N, mu, var, 5);
+    t[11] += run<2, 16, 16>(a, Xc, N, mu, var, 5);
     t[0] += run<4, 8, 0>(a, Xc, N, mu, var, 5);
     t[1] += run<4, 8, 1>(a, Xc, N, mu, var, 5);
     t[2] += run<4, 8, 2>(a, Xc, N, mu, var, 5);

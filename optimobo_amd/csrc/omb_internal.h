@@ -11,6 +11,8 @@ namespace omb {
 // Rows of the training set handled per streamed K* chunk (4 row tiles of 16).
 constexpr int kChunkRows = 64;
 constexpr int kBlockThreads = 512;
+// Training rows per workgroup of the standalone K-block kernel.
+constexpr int kKBlockRows = 256;
 
 // Device-side state of one fitted GP (objective), built by omb_set_gp.
 struct GPDev {

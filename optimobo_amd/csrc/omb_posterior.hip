@@ -85,11 +85,13 @@ hipError_t launch_pack_gp(hipStream_t stream, int n, int d, int DP, const double
 
 // ----------------------------------------------------------------------------- K block
 // Standalone K(X_train, X*) (n, N) row-major — the HBM-bound kernel of the north star.
-// Each thread owns two adjacent candidates (16-byte stores), each block 64 training rows.
+// Each thread owns two adjacent candidates (16-byte stores), each block 256 training rows;
+// K is written with non-temporal stores (written once, never re-read by this kernel):
+// tools/ablate/ablate_kblock measured 3.47 → 4.20 TB/s for 64-row plain → 256-row nt.
 template <int DP, int KIND>
 __global__ __launch_bounds__(256) void kernel_block_kernel(GPDev g, int d, const double* __restrict__ Xc,
                                                            int64_t N, double* __restrict__ K) {
-  constexpr int kRows = 64;
+  constexpr int kRows = kKBlockRows;
   const int64_t c = 2 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
   if (c >= N) return;
   const bool two = (c + 1) < N;
@@ -117,10 +119,10 @@ __global__ __launch_bounds__(256) void kernel_block_kernel(GPDev g, int d, const
     double v1 = kernel_of_r2<KIND>(fma(-2.0, dot1, xk + s1), g.variance);
     double* dst = K + (int64_t)k * N + c;
     if (two && ((N & 1) == 0)) {
-      *reinterpret_cast<d2*>(dst) = d2{v0, v1};
+      __builtin_nontemporal_store(d2{v0, v1}, reinterpret_cast<d2*>(dst));
     } else {
-      dst[0] = v0;
-      if (two) dst[1] = v1;
+      __builtin_nontemporal_store(v0, dst);
+      if (two) __builtin_nontemporal_store(v1, dst + 1);
     }
   }
 }
@@ -128,7 +130,9 @@ __global__ __launch_bounds__(256) void kernel_block_kernel(GPDev g, int d, const
 // ----------------------------------------------------------------------------- posterior
 // ABL (ablation, tools/ablate only; the library instantiates ABL = 0): bit 1 replaces the Matern
 // transform by the raw dot product, bit 2 skips the MFMA phase, bit 4 feeds a constant A
-// operand instead of loading L⁻¹, bit 8 drops the per-chunk barrier, bit 16 uses libm exp/sqrt.
+// operand instead of loading L⁻¹, bit 8 drops the per-chunk barrier (barrier mode only), bit 16
+// uses libm exp/sqrt, bit 32 selects the 2-buffer / block-barrier pipeline instead of the
+// counter-synchronised 3-buffer ring (tools/ablate: 12.03 → 11.23 ms at n = 512, N = 2^20).
 // NW = waves per workgroup (8 or 16): waves w, w+4, w+8, w+12 share a SIMD.
 template <int RT, int CT, int DP, int KIND, int NW = 8, int ABL = 0>
 __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args, const double* __restrict__ Xc,
@@ -140,9 +144,13 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
   constexpr int KS = kChunkRows / 4;          // MFMA k-steps per chunk (16)
   constexpr int CHUNK = kChunkRows * BN;      // doubles per LDS buffer
   constexpr int EPT = CHUNK / NT;             // generated K* elements per thread per chunk
+  constexpr bool kCounters = (ABL & 32) == 0;   // counter-synchronised 3-buffer ring (default)
+  constexpr int NBUF = kCounters ? 3 : 2;
+  constexpr int kMaxChunks = OMB_MAX_TRAIN / kChunkRows;
+  constexpr int kSpinLimit = 1 << 22;
   static_assert(NT % BN == 0 && CHUNK % NT == 0, "BN must divide the block");
   static_assert(2 * CHUNK >= NW * BN + NT, "epilogue scratch must fit in the K* buffers");
-  __shared__ double kbuf[2 * CHUNK];
+  __shared__ double kbuf[NBUF * CHUNK + (kCounters ? kMaxChunks : 0)];
 
   const int obj = blockIdx.y;
   const GPDev g = args.gp[obj];
@@ -190,8 +198,9 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
   auto generate = [&](int kc, double* buf) {
 #pragma unroll
     for (int i = 0; i < EPT; ++i) {
-      const int e = tid + NT * i;
-      const int kl = e / BN;
+      // row of the chunk this lane generates; with BN = 64 a wave covers exactly one row, so the
+      // row is wave-uniform and Xs / xsq / α come through scalar loads
+      const int kl = (BN == 64) ? wave + NW * i : (tid + NT * i) / BN;
       const int k = kc * kChunkRows + kl;
       double val = 0.0;
       if (k < g.n) {
@@ -272,17 +281,60 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
     }
   };
 
-  generate(0, kbuf);
-  __syncthreads();
-  for (int kc = 0; kc < Q; ++kc) {
-    if constexpr (NW == 8) {
-      if (kc + 1 < Q) generate(kc + 1, kbuf + ((kc + 1) & 1) * CHUNK);
-      multiply(kc, kbuf + (kc & 1) * CHUNK);
-    } else {   // 4 waves per SIMD interleave across waves; keep each wave's live range short
-      multiply(kc, kbuf + (kc & 1) * CHUNK);
-      if (kc + 1 < Q) generate(kc + 1, kbuf + ((kc + 1) & 1) * CHUNK);
+  if constexpr (kCounters) {
+    // Three-buffer ring with per-chunk LDS counters instead of a block barrier per chunk:
+    // ready[c] counts the waves whose share of K* chunk c is in LDS, done[c] the waves that have
+    // finished multiplying chunk c.  A wave multiplies chunk c once ready[c] == NW and refills
+    // ring slot (c+2)%3 once done[c-1] == NW, so fast waves run up to a chunk ahead of slow
+    // ones.  Every wait refers to an earlier stage of every other wave (no cycle); the spins are
+    // bounded anyway (kSpinLimit) so a broken invariant cannot hang the GPU.
+    int* ready = reinterpret_cast<int*>(kbuf + NBUF * CHUNK);
+    int* done = ready + kMaxChunks;
+    if (tid < 2 * kMaxChunks) ready[tid] = 0;
+    __syncthreads();
+    auto signal = [&](int* ctr) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    auto wait_all = [&](int* ctr) {
+      if (lane == 0) {
+        for (int spin = 0; spin < kSpinLimit; ++spin) {
+          if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= NW) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    };
+    generate(0, kbuf);
+    signal(&ready[0]);
+    if (Q > 1) {
+      generate(1, kbuf + CHUNK);
+      signal(&ready[1]);
     }
-    if constexpr (!(ABL & 8)) __syncthreads();
+    for (int kc = 0; kc < Q; ++kc) {
+      wait_all(&ready[kc]);
+      multiply(kc, kbuf + (kc % 3) * CHUNK);
+      signal(&done[kc]);
+      if (kc + 2 < Q) {
+        if (kc >= 1) wait_all(&done[kc - 1]);
+        generate(kc + 2, kbuf + ((kc + 2) % 3) * CHUNK);
+        signal(&ready[kc + 2]);
+      }
+    }
+    __syncthreads();
+  } else {
+    generate(0, kbuf);
+    __syncthreads();
+    for (int kc = 0; kc < Q; ++kc) {
+      if constexpr (NW == 8) {
+        if (kc + 1 < Q) generate(kc + 1, kbuf + ((kc + 1) & 1) * CHUNK);
+        multiply(kc, kbuf + (kc & 1) * CHUNK);
+      } else {   // 4 waves per SIMD interleave across waves; keep each wave's live range short
+        multiply(kc, kbuf + (kc & 1) * CHUNK);
+        if (kc + 1 < Q) generate(kc + 1, kbuf + ((kc + 1) & 1) * CHUNK);
+      }
+      if constexpr (!(ABL & 8)) __syncthreads();
+    }
   }
 
   // ---- σ²: Σ over rows of V² — registers, then lanes {l, l^16, l^32, l^48}, then waves.
@@ -320,6 +372,135 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
   }
 }
 
+// ----------------------------------------------------------------------------- two-phase posterior
+// For n_pad·BN ≤ 16384 (n ≤ 512 at BN = 32, n ≤ 256 at BN = 64): phase 1 generates K* for ALL
+// training rows of the block's candidates into one 128 KiB LDS tile (fragment order, as above);
+// after a single barrier, phase 2 runs every wave's whole triangular row-tile work with no
+// further synchronisation.  FP64 VALU (generation) and FP64 MFMA share one pipe on gfx950
+// (tools/microbench), so overlapping the two phases buys nothing — removing the per-chunk
+// barriers does.  Same SIMD-balanced row-tile assignment as posterior_kernel.
+constexpr int kTwoPhaseLds = 16384;   // doubles (128 KiB)
+
+template <int RT, int CT, int DP, int KIND, int NW = 16, int ABL = 0>
+__global__ __launch_bounds__(64 * NW, NW / 4) void posterior2p_kernel(GPArgs args, const double* __restrict__ Xc,
+                                                                       int64_t N, double* __restrict__ mu_out,
+                                                                       double* __restrict__ var_out) {
+  constexpr int NT = 64 * NW;
+  constexpr int G = NW / 4;
+  constexpr int BN = 16 * CT;
+  constexpr int RPI = NT / BN;                // K* rows generated per pass of the block
+  static_assert(NT % BN == 0, "BN must divide the block");
+  static_assert(kTwoPhaseLds >= NW * BN + NT, "epilogue scratch must fit");
+  __shared__ double kbuf[kTwoPhaseLds];
+
+  const int obj = blockIdx.y;
+  const GPDev g = args.gp[obj];
+  const int d = args.d;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t c0 = (int64_t)blockIdx.x * BN;
+  const int Q = (g.R + 3) >> 2;
+  const int n_pad = kChunkRows * Q;
+
+  // ---- phase 1: K* (n_pad × BN) into LDS, μ partials in registers
+  const int cg = tid % BN;
+  const int64_t ci = min(c0 + cg, N - 1);
+  double b[DP];
+  double csq = 0.0;
+#pragma unroll
+  for (int j = 0; j < DP; ++j) {
+    b[j] = (j < d) ? Xc[ci * d + j] / g.ls[j] : 0.0;
+    csq += b[j] * b[j];
+  }
+  const int gen_ct = cg >> 4, gen_cc = cg & 15;
+  const int row_in_pass = (BN == 64) ? wave : tid / BN;
+  double mu_part = 0.0;
+  for (int k0 = 0; k0 < n_pad; k0 += RPI) {
+    const int k = k0 + row_in_pass;
+    double val = 0.0;
+    if (k < g.n) {
+      const double* xr = g.Xs + (int64_t)k * DP;
+      double dot = 0.0;
+#pragma unroll
+      for (int j = 0; j < DP; ++j) dot = fma(xr[j], b[j], dot);
+      if constexpr (ABL & 1)
+        val = dot;
+      else
+        val = kernel_of_r2<KIND, !(ABL & 16)>(fma(-2.0, dot, g.xsq[k] + csq), g.variance);
+      mu_part = fma(g.alpha[k], val, mu_part);
+    }
+    if (k < n_pad) kbuf[((k >> 2) * CT + gen_ct) * 64 + (k & 3) * 16 + gen_cc] = val;
+  }
+  __syncthreads();
+
+  // ---- phase 2: V = L⁻¹ K* on FP64 MFMA, one slot (16-row tile) after the other
+  const int simd = wave & 3, h = wave >> 2;
+  d4 acc[RT][CT];
+#pragma unroll
+  for (int j = 0; j < RT; ++j) {
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) acc[j][ct] = d4{0.0, 0.0, 0.0, 0.0};
+    if constexpr (ABL & 2) continue;
+    const int q = 2 * G * (j >> 1) + ((j & 1) ? (2 * G - 1 - h) : h);
+    const int r = 4 * q + ((simd + q) & 3);
+    if (r >= g.R) continue;
+    const double* A = g.Lp + 128ll * r * (r + 1) + 2 * lane;
+    const int npairs = 2 * (r + 1);
+    d2 a_cur = (ABL & 4) ? d2{1e-3 * lane, 2e-3} : *reinterpret_cast<const d2*>(A);
+    for (int P = 0; P < npairs; ++P) {
+      d2 a_nxt = a_cur;
+      if (P + 1 < npairs) {
+        if constexpr (ABL & 4)
+          a_nxt = d2{a_cur.y, a_cur.x};
+        else
+          a_nxt = *reinterpret_cast<const d2*>(A + 128 * (P + 1));
+      }
+      const double* bp = kbuf + (2 * P) * CT * 64 + lane;
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        acc[j][ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(a_cur.x, bp[ct * 64], acc[j][ct], 0, 0, 0);
+        acc[j][ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(a_cur.y, bp[(CT + ct) * 64], acc[j][ct], 0, 0, 0);
+      }
+      a_cur = a_nxt;
+    }
+  }
+  __syncthreads();   // every wave is done reading K* before the epilogue reuses the LDS
+
+  // ---- epilogue (as posterior_kernel)
+  double part[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < RT; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) s = fma(acc[j][ct][i], acc[j][ct][i], s);
+    s += __shfl_xor(s, 16);
+    s += __shfl_xor(s, 32);
+    part[ct] = s;
+  }
+  double* red = kbuf;
+  double* redmu = kbuf + NW * BN;
+  if (lane < 16) {
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) red[wave * BN + ct * 16 + lane] = part[ct];
+  }
+  redmu[tid] = mu_part;
+  __syncthreads();
+  if (tid < BN) {
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) s += red[w * BN + tid];
+    double m = 0.0;
+    for (int t = tid; t < NT; t += BN) m += redmu[t];
+    const int64_t c = c0 + tid;
+    if (c < N) {
+      mu_out[(int64_t)obj * N + c] = m;
+      var_out[(int64_t)obj * N + c] = g.variance - s;
+    }
+  }
+}
+
 // ----------------------------------------------------------------------------- dispatch
 template <int DP, int KIND>
 static hipError_t launch_posterior_dp(hipStream_t stream, const GPArgs& args, int n_obj, int max_R,
@@ -328,10 +509,11 @@ static hipError_t launch_posterior_dp(hipStream_t stream, const GPArgs& args, in
   const int RTneed = (Q + 1) / 2;
   if (RTneed <= 1) {
     dim3 grid((unsigned)((N + 63) / 64), n_obj);
-    hipLaunchKernelGGL((posterior_kernel<1, 4, DP, KIND>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var);
+    // n ≤ 256: two 64-KiB workgroups per CU beat the 96-KiB counter ring
+    hipLaunchKernelGGL((posterior_kernel<1, 4, DP, KIND, 8, 32>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var);
   } else if (RTneed <= 2) {
     dim3 grid((unsigned)((N + 63) / 64), n_obj);
-    hipLaunchKernelGGL((posterior_kernel<2, 4, DP, KIND>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var);
+    hipLaunchKernelGGL((posterior_kernel<2, 4, DP, KIND, 8, 32>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var);
   } else if (RTneed <= 4) {
     dim3 grid((unsigned)((N + 63) / 64), n_obj);
     hipLaunchKernelGGL((posterior_kernel<4, 4, DP, KIND>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var);
@@ -368,7 +550,7 @@ template <int KIND>
 static hipError_t launch_kblock_kind(hipStream_t stream, const GPArgs& args, int obj, const double* Xc, int64_t N,
                                      double* K) {
   const GPDev& g = args.gp[obj];
-  dim3 grid((unsigned)((N + 511) / 512), (unsigned)((g.n + 63) / 64));
+  dim3 grid((unsigned)((N + 511) / 512), (unsigned)((g.n + kKBlockRows - 1) / kKBlockRows));
   switch (args.DP) {
 #define OMB_KB(DPV) \
   case DPV: hipLaunchKernelGGL((kernel_block_kernel<DPV, KIND>), grid, dim3(256), 0, stream, g, args.d, Xc, N, K); break;

@@ -28,6 +28,23 @@ float run(const GPArgs& a, const double* Xc, int64_t N, double* mu, double* var,
   return ms / reps;
 }
 
+template <int RT, int CT, int NW, int ABL>
+float run2p(const GPArgs& a, const double* Xc, int64_t N, double* mu, double* var, int reps) {
+  dim3 grid((unsigned)((N + 16 * CT - 1) / (16 * CT)), 2);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  hipLaunchKernelGGL((posterior2p_kernel<RT, CT, 6, 0, NW, ABL>), grid, dim3(64 * NW), 0, 0, a, Xc, N, mu, var);
+  CK(hipEventRecord(e0));
+  for (int i = 0; i < reps; ++i)
+    hipLaunchKernelGGL((posterior2p_kernel<RT, CT, 6, 0, NW, ABL>), grid, dim3(64 * NW), 0, 0, a, Xc, N, mu, var);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  return ms / reps;
+}
+
 int main(int argc, char** argv) {
   int n = argc > 1 ? atoi(argv[1]) : 512;
   int64_t N = argc > 2 ? atoll(argv[2]) : (1 << 20);
@@ -60,10 +77,19 @@ int main(int argc, char** argv) {
   a.DP = DP;
   const char* names[] = {"8w full", "8w no-matern(1)", "8w no-mfma(2)", "8w constA(4)", "8w nobarrier(8)",
                          "16w full", "16w no-matern(1)", "16w no-mfma(2)", "16w constA(4)", "16w nobarrier(8)",
-                         "8w libm-math(16)", "16w libm-math(16)"};
-  const int NV = 12;
+                         "8w libm-math(16)", "16w libm-math(16)",
+                         "2p 16w bn32", "2p 16w bn32 no-mfma", "2p 16w bn32 constA", "2p 8w bn32",
+                         "8w barrier(32)", "16w barrier(32)", "8w counters+constA(4)"};
+  const int NV = 19;
   float t[NV] = {0};
   for (int round = 0; round < 3; ++round) {
+    t[16] += run<4, 8, 32>(a, Xc, N, mu, var, 5);
+    t[17] += run<2, 16, 32>(a, Xc, N, mu, var, 5);
+    t[18] += run<4, 8, 4>(a, Xc, N, mu, var, 5);
+    t[12] += run2p<2, 2, 16, 0>(a, Xc, N, mu, var, 5);
+    t[13] += run2p<2, 2, 16, 2>(a, Xc, N, mu, var, 5);
+    t[14] += run2p<2, 2, 16, 4>(a, Xc, N, mu, var, 5);
+    t[15] += run2p<4, 2, 8, 0>(a, Xc, N, mu, var, 5);
     t[10] += run<4, 8, 16>(a, Xc, N, mu, var, 5);
     t[11] += run<2, 16, 16>(a, Xc, N, mu, var, 5);
     t[0] += run<4, 8, 0>(a, Xc, N, mu, var, 5);

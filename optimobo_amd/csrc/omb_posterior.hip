@@ -150,7 +150,11 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
   constexpr int kSpinLimit = 1 << 22;
   static_assert(NT % BN == 0 && CHUNK % NT == 0, "BN must divide the block");
   static_assert(2 * CHUNK >= NW * BN + NT, "epilogue scratch must fit in the K* buffers");
-  __shared__ double kbuf[NBUF * CHUNK + (kCounters ? kMaxChunks : 0)];
+  // Candidate coordinates (x*/ℓ) live in registers for n_var ≤ 8; wider ones are staged in LDS
+  // as [j][c] (lanes read consecutive doubles) so the 256-VGPR budget stays with the MFMA tiles.
+  constexpr bool kCandLds = DP > 8 || RT >= 8;
+  constexpr int kCtrDoubles = kCounters ? kMaxChunks : 0;
+  __shared__ double kbuf[NBUF * CHUNK + kCtrDoubles + (kCandLds ? DP * BN : 0)];
 
   const int obj = blockIdx.y;
   const GPDev g = args.gp[obj];
@@ -161,13 +165,25 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
 
   // ---- this thread's generation candidate (fixed across chunks since BN | NT)
   const int cg = tid % BN;
-  const int64_t ci = min(c0 + cg, N - 1);
-  double b[DP];
+  double b[kCandLds ? 1 : DP];
+  double* cand = kbuf + NBUF * CHUNK + kCtrDoubles;
   double csq = 0.0;
+  if constexpr (kCandLds) {
+    for (int e = tid; e < DP * BN; e += NT) {
+      const int j = e / BN, c = e % BN;
+      const int64_t cc = min(c0 + c, N - 1);
+      cand[e] = (j < d) ? Xc[cc * d + j] / g.ls[j] : 0.0;
+    }
+    __syncthreads();
 #pragma unroll
-  for (int j = 0; j < DP; ++j) {
-    b[j] = (j < d) ? Xc[ci * d + j] / g.ls[j] : 0.0;
-    csq += b[j] * b[j];
+    for (int j = 0; j < DP; ++j) csq += cand[j * BN + cg] * cand[j * BN + cg];
+  } else {
+    const int64_t ci = min(c0 + cg, N - 1);
+#pragma unroll
+    for (int j = 0; j < DP; ++j) {
+      b[j] = (j < d) ? Xc[ci * d + j] / g.ls[j] : 0.0;
+      csq += b[j] * b[j];
+    }
   }
   const int gen_ct = cg >> 4, gen_cc = cg & 15;
 
@@ -207,7 +223,7 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
         const double* xr = g.Xs + (int64_t)k * DP;
         double dot = 0.0;
 #pragma unroll
-        for (int j = 0; j < DP; ++j) dot = fma(xr[j], b[j], dot);
+        for (int j = 0; j < DP; ++j) dot = fma(xr[j], kCandLds ? cand[j * BN + cg] : b[j], dot);
         if constexpr (ABL & 1)
           val = dot;
         else
@@ -227,37 +243,26 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
     for (int j = 0; j < RT; ++j)
       nS[j] = (slot_q[j] > kc) ? KS : (slot_q[j] == kc ? 4 * ((slot_r[j] & 3) + 1) : 0);
     const int P0 = kc * (KS / 2);
-    // With 2 waves per SIMD the next k-step pair of A is prefetched into registers; with 4 the
-    // other waves hide the L2 latency and the registers are worth more as occupancy.
-    constexpr bool kPrefetchA = (NW == 8);
-    d2 a_cur[RT], a_nxt[RT];
+    // A (L⁻¹) k-step pairs are loaded PD pairs ahead of their MFMAs into a register ring (the sp
+    // loop is fully unrolled, so ring indices are static).  With 2 waves per SIMD the ring hides
+    // the L2 latency; with 4 the other waves do and the registers are worth more as occupancy.
+    constexpr int PD = (NW == 8) ? ((ABL & 64) ? 2 : 1) : 0;   // PD 2 measured no faster (11.19 vs 11.16 ms)
+    d2 a_ring[PD + 1][RT];
+    auto load_a = [&](int sp, d2* dst) {
 #pragma unroll
-    for (int j = 0; j < RT; ++j) {
-      if constexpr (ABL & 4)
-        a_cur[j] = d2{1e-3 * lane, 2e-3 * j};
-      else
-        a_cur[j] = *reinterpret_cast<const d2*>(slot_A[j] + 128 * min(P0, 2 * slot_r[j] + 1));
-    }
+      for (int j = 0; j < RT; ++j) {
+        if constexpr (ABL & 4)
+          dst[j] = d2{1e-3 * lane + sp, 2e-3 * j};
+        else
+          dst[j] = *reinterpret_cast<const d2*>(slot_A[j] + 128 * min(P0 + sp, 2 * slot_r[j] + 1));
+      }
+    };
+#pragma unroll
+    for (int p = 0; p < PD; ++p) load_a(p, a_ring[p]);
 #pragma unroll
     for (int sp = 0; sp < KS / 2; ++sp) {
-      if (!kPrefetchA && sp > 0) {
-#pragma unroll
-        for (int j = 0; j < RT; ++j) {
-          if constexpr (ABL & 4)
-            a_cur[j] = d2{a_cur[j].y, a_cur[j].x};
-          else
-            a_cur[j] = *reinterpret_cast<const d2*>(slot_A[j] + 128 * min(P0 + sp, 2 * slot_r[j] + 1));
-        }
-      }
-      if (kPrefetchA && sp + 1 < KS / 2) {
-#pragma unroll
-        for (int j = 0; j < RT; ++j) {
-          if constexpr (ABL & 4)
-            a_nxt[j] = d2{a_cur[j].y, a_cur[j].x};
-          else
-            a_nxt[j] = *reinterpret_cast<const d2*>(slot_A[j] + 128 * min(P0 + sp + 1, 2 * slot_r[j] + 1));
-        }
-      }
+      if (sp + PD < KS / 2) load_a(sp + PD, a_ring[(sp + PD) % (PD + 1)]);
+      const d2* a_cur = a_ring[sp % (PD + 1)];
       double b0[CT], b1[CT];
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
@@ -273,10 +278,6 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
             acc[j][ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(a_cur[j].y, b1[ct], acc[j][ct], 0, 0, 0);
           }
         }
-      }
-      if (kPrefetchA && sp + 1 < KS / 2) {
-#pragma unroll
-        for (int j = 0; j < RT; ++j) a_cur[j] = a_nxt[j];
       }
     }
   };

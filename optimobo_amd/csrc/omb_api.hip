@@ -56,6 +56,10 @@ int hip_fail(omb_ctx* ctx, hipError_t e, const char* where) {
     if (e_ != hipSuccess) return hip_fail(ctx, e_, #call);   \
   } while (0)
 
+// Acquisition kernels stage their per-iteration geometry in ≤ 64 KiB of dynamic LDS.
+constexpr int kMaxLdsDoubles = 8192;
+constexpr int kMaxStripes = (kMaxLdsDoubles - 1) / 2;
+
 int pad_dim(int d) {
   const int opts[] = {2, 4, 6, 8, 16, 32};
   for (int o : opts)
@@ -89,8 +93,8 @@ int gather_gp(omb_ctx* ctx, int n_obj, GPArgs* args, int* max_R) {
 }
 
 int check_moments(omb_ctx* ctx, const double* mu, const double* var, int64_t ld, int64_t N, int k, const double* out) {
-  if (!mu || !var || !out) return fail(ctx, OMB_EINVAL, "null device pointer");
   if (N < 0) return fail(ctx, OMB_EINVAL, "N=%lld < 0", (long long)N);
+  if (N > 0 && (!mu || !var || !out)) return fail(ctx, OMB_EINVAL, "null device pointer");
   if (k > 1 && ld < N) return fail(ctx, OMB_EINVAL, "ld=%lld < N=%lld", (long long)ld, (long long)N);
   return OMB_OK;
 }
@@ -216,7 +220,7 @@ int omb_kernel_block(omb_ctx* ctx, int obj, const double* Xc_dev, int64_t N, dou
   int rc = enter(ctx);
   if (rc) return rc;
   if (obj < 0 || obj >= OMB_MAX_OBJ || !ctx->obj[obj].set) return fail(ctx, OMB_ESTATE, "objective %d not set", obj);
-  if (!Xc_dev || !K_dev || N < 0) return fail(ctx, OMB_EINVAL, "bad candidate/output arguments");
+  if (N < 0 || (N > 0 && (!Xc_dev || !K_dev))) return fail(ctx, OMB_EINVAL, "bad candidate/output arguments");
   if (N == 0) return OMB_OK;
   GPArgs args;
   memset(&args, 0, sizeof(args));
@@ -231,7 +235,8 @@ int omb_kernel_block(omb_ctx* ctx, int obj, const double* Xc_dev, int64_t N, dou
 int omb_posterior(omb_ctx* ctx, int n_obj, const double* Xc_dev, int64_t N, double* mu_dev, double* var_dev) {
   int rc = enter(ctx);
   if (rc) return rc;
-  if (!Xc_dev || !mu_dev || !var_dev || N < 0) return fail(ctx, OMB_EINVAL, "bad candidate/output arguments");
+  if (N < 0 || (N > 0 && (!Xc_dev || !mu_dev || !var_dev)))
+    return fail(ctx, OMB_EINVAL, "bad candidate/output arguments");
   GPArgs args;
   int max_R = 0;
   rc = gather_gp(ctx, n_obj, &args, &max_R);
@@ -249,7 +254,8 @@ int omb_ehvi2d(omb_ctx* ctx, const double* mu_dev, const double* var_dev, int64_
   int rc = enter(ctx);
   if (rc) return rc;
   if ((rc = check_moments(ctx, mu_dev, var_dev, ld, N, 2, out_dev))) return rc;
-  if (!pf_sorted_dev || P < 1 || P > 4096) return fail(ctx, OMB_EINVAL, "Pareto front size P=%d outside [1, 4096]", P);
+  // stripes y1[0..P], y2[1..P] are staged in ≤ 64 KiB of LDS
+  if (!pf_sorted_dev || P < 1 || P > kMaxStripes) return fail(ctx, OMB_EUNSUP, "Pareto front size P=%d outside [1, %d]", P, kMaxStripes);
   if (!r_host) return fail(ctx, OMB_EINVAL, "null reference point");
   if (mode != OMB_EHVI_REFERENCE && mode != OMB_EHVI_TEXTBOOK && mode != OMB_EHVI_SIGMA) return fail(ctx, OMB_EINVAL, "unknown EHVI mode %d", mode);
   if (N == 0) return OMB_OK;
@@ -265,7 +271,8 @@ int omb_ehvi3d_mc(omb_ctx* ctx, const double* mu_dev, const double* var_dev, int
   int rc = enter(ctx);
   if (rc) return rc;
   if ((rc = check_moments(ctx, mu_dev, var_dev, ld, N, 3, out_dev))) return rc;
-  if (!cache_dev || M < 1 || M > 4096) return fail(ctx, OMB_EINVAL, "cache size M=%d outside [1, 4096]", M);
+  if (!cache_dev || M < 1 || 3 * M > kMaxLdsDoubles)
+    return fail(ctx, OMB_EUNSUP, "cache size M=%d outside [1, %d]", M, kMaxLdsDoubles / 3);
   if (!r_host) return fail(ctx, OMB_EINVAL, "null reference point");
   if (N == 0) return OMB_OK;
   hipError_t e = launch_ehvi3d_mc(ctx->stream, mu_dev, var_dev, ld, N, cache_dev, M, r_host, hv_pf, out_dev, raised_dev);
@@ -278,7 +285,8 @@ int omb_hvpoi(omb_ctx* ctx, const double* mu_dev, const double* var_dev, int64_t
   int rc = enter(ctx);
   if (rc) return rc;
   if ((rc = check_moments(ctx, mu_dev, var_dev, ld, N, 2, out_dev))) return rc;
-  if (!cells_dev || C < 1 || C > 4096) return fail(ctx, OMB_EINVAL, "cell count C=%d outside [1, 4096]", C);
+  if (!cells_dev || C < 1 || 4 * C > kMaxLdsDoubles)
+    return fail(ctx, OMB_EUNSUP, "cell count C=%d outside [1, %d]", C, kMaxLdsDoubles / 4);
   if (N == 0) return OMB_OK;
   hipError_t e = launch_hvpoi(ctx->stream, mu_dev, var_dev, ld, N, cells_dev, C, out_dev);
   if (e != hipSuccess) return hip_fail(ctx, e, "hvpoi");
@@ -292,7 +300,8 @@ int omb_expdec(omb_ctx* ctx, int k, const double* mu_dev, const double* var_dev,
   if (rc) return rc;
   if (k < 1 || k > OMB_MAX_OBJ) return fail(ctx, OMB_EINVAL, "k=%d outside [1, %d]", k, OMB_MAX_OBJ);
   if ((rc = check_moments(ctx, mu_dev, var_dev, ld, N, k, out_dev))) return rc;
-  if (!cache_dev || M < 1 || M > 4096) return fail(ctx, OMB_EINVAL, "cache size M=%d outside [1, 4096]", M);
+  if (!cache_dev || M < 1 || k * M > kMaxLdsDoubles)
+    return fail(ctx, OMB_EUNSUP, "cache size M=%d x k=%d exceeds %d doubles of LDS", M, k, kMaxLdsDoubles);
   if (scal_id < OMB_SCAL_WS || scal_id > OMB_SCAL_APD) return fail(ctx, OMB_EINVAL, "unknown scalarisation %d", scal_id);
   if (!weights_host || !ideal_host || !max_host) return fail(ctx, OMB_EINVAL, "null weights/ideal/max");
   ScalParams sp;
@@ -342,7 +351,7 @@ int omb_ei(omb_ctx* ctx, const double* mu_dev, const double* var_dev, int64_t N,
 int omb_argmax_dev(omb_ctx* ctx, const double* vals_dev, int64_t N, int64_t offset, double* result_dev) {
   int rc = enter(ctx);
   if (rc) return rc;
-  if (!vals_dev || !result_dev || N < 0) return fail(ctx, OMB_EINVAL, "bad arg-max arguments");
+  if (!result_dev || N < 0 || (N > 0 && !vals_dev)) return fail(ctx, OMB_EINVAL, "bad arg-max arguments");
   hipError_t e = launch_argmax(ctx->stream, vals_dev, N, offset, ctx->partials, result_dev);
   if (e != hipSuccess) return hip_fail(ctx, e, "argmax");
   return OMB_OK;

@@ -1,0 +1,110 @@
+"""GPU edge cases through the C-ABI: error codes, empty/tiny batches, maximum geometry sizes,
+NaN propagation, degenerate training sets."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from oracle import acquisition as oacq  # noqa: E402
+from oracle import gp as ogp  # noqa: E402
+
+
+@pytest.fixture()
+def ctx():
+    from optimobo_amd.device import AcqContext
+    c = AcqContext(0)
+    yield c
+    c.close()
+
+
+def dev(x):
+    return torch.as_tensor(np.ascontiguousarray(x, dtype=np.float64), device="cuda:0")
+
+
+def _gp(ctx, obj, X, y, ls, var=1.0):
+    from optimobo_amd.gp import GPState
+    ctx.set_gp_state(obj, GPState(X, y, ls, var))
+
+
+def test_error_codes(ctx):
+    from optimobo_amd import _lib
+    with pytest.raises(_lib.OMBError) as e:
+        ctx.posterior(dev(np.zeros((4, 2))), n_obj=1)
+    assert e.value.code == _lib.OMB_ESTATE
+    rng = np.random.default_rng(0)
+    _gp(ctx, 0, rng.uniform(0, 1, (10, 2)), rng.uniform(0, 1, 10), [0.5, 0.5])
+    _gp(ctx, 1, rng.uniform(0, 1, (10, 3)), rng.uniform(0, 1, 10), [0.5, 0.5, 0.5])
+    with pytest.raises(_lib.OMBError) as e:
+        ctx.posterior(dev(np.zeros((4, 2))), n_obj=2)
+    assert e.value.code == _lib.OMB_EINVAL
+    with pytest.raises(_lib.OMBError) as e:
+        ctx.set_gp(2, np.zeros((1025, 2)), [1, 1], 1.0, np.zeros(1025), np.eye(1025))
+    assert e.value.code == _lib.OMB_EUNSUP
+    with pytest.raises(_lib.OMBError) as e:
+        ctx.set_gp(2, np.zeros((4, 33)), np.ones(33), 1.0, np.zeros(4), np.eye(4))
+    assert e.value.code == _lib.OMB_EUNSUP
+    with pytest.raises(_lib.OMBError):
+        ctx.set_gp(2, np.zeros((4, 2)), [1.0, -1.0], 1.0, np.zeros(4), np.eye(4))   # ℓ ≤ 0
+
+
+def test_empty_and_single_candidate(ctx):
+    rng = np.random.default_rng(1)
+    X = rng.uniform(0, 1, (30, 3))
+    y = X.sum(1)
+    _gp(ctx, 0, X, y, [0.4, 0.6, 0.9], 2.0)
+    mu, var = ctx.posterior(dev(np.zeros((0, 3))), n_obj=1)
+    assert mu.shape == (1, 0)
+    x1 = rng.uniform(0, 1, (1, 3))
+    mu, var = ctx.posterior(dev(x1), n_obj=1)
+    m, v = ogp.ExactGP(X, y, [0.4, 0.6, 0.9], 2.0).predict(x1)
+    assert mu.item() == pytest.approx(m.item(), rel=1e-9, abs=1e-12)
+    assert var.item() == pytest.approx(v.item(), rel=1e-7, abs=1e-12)
+    assert ctx.argmax(dev(np.zeros(0))) == (-np.inf, -1)
+
+
+def test_max_geometry_sizes(ctx):
+    from optimobo_amd import _lib
+    rng = np.random.default_rng(2)
+    x = np.sort(rng.uniform(0, 1, 4095))
+    pf = np.column_stack([x, 1 - np.sqrt(x)])
+    pf_sorted = pf[np.argsort(pf[:, 1])]
+    mu = rng.uniform(0, 1, (2, 64))
+    var = 10 ** rng.uniform(-4, -1, (2, 64))
+    r = np.array([1.1, 1.1])
+    out = ctx.ehvi2d(dev(mu), dev(var), pf_sorted, r, 1.0, 0.1, mode="textbook").cpu().numpy()
+    ref = oacq.ehvi2d(mu, var, pf, r, None, mode="textbook")
+    np.testing.assert_allclose(out, ref, rtol=1e-9, atol=1e-13)
+    with pytest.raises(_lib.OMBError) as e:
+        ctx.ehvi2d(dev(mu), dev(var), np.vstack([pf_sorted, [[2.0, 2.0]]]), r, 1.0, 0.1)
+    assert e.value.code == _lib.OMB_EUNSUP
+    cache = rng.standard_normal((4096, 2))
+    out = ctx.expdec(dev(mu), dev(var), cache, 1, [], [0.5, 0.5], [0, 0], [1, 1], 0.3).cpu().numpy()
+    from oracle import scalarisations as osc
+    ref = oacq.expected_decomposition(mu, var, cache, osc.Tchebicheff([0, 0], [1, 1]), np.array([0.5, 0.5]), 0.3)
+    np.testing.assert_allclose(out, ref, rtol=1e-9, atol=1e-13)
+    with pytest.raises(_lib.OMBError):
+        ctx.expdec(dev(mu), dev(var), rng.standard_normal((4097, 2)), 1, [], [0.5, 0.5], [0, 0], [1, 1], 0.3)
+
+
+def test_nan_moments_never_win(ctx):
+    mu = np.array([[0.2, np.nan, 0.4], [0.3, 0.1, np.nan]])
+    var = np.full((2, 3), 0.01)
+    pf = np.array([[0.5, 0.5]])
+    out = ctx.ehvi2d(dev(mu), dev(var), pf, [1.0, 1.0], 1.0, 0.1, mode="textbook").cpu().numpy()
+    assert np.isfinite(out[0]) and np.isnan(out[1]) and np.isnan(out[2])
+    assert ctx.argmax(dev(out)) == (out[0], 0)
+
+
+def test_duplicate_training_points(ctx):
+    """Repeated rows make K singular; GPy's 1e-8 jitter (and jitchol) keeps the fit finite."""
+    rng = np.random.default_rng(3)
+    X = rng.uniform(0, 1, (40, 2))
+    X[20:] = X[:20]
+    y = np.sin(3 * X[:, 0]) + X[:, 1]
+    _gp(ctx, 0, X, y, [0.3, 0.3], 1.0)
+    Xc = rng.uniform(0, 1, (500, 2))
+    mu, var = ctx.posterior(dev(Xc), n_obj=1)
+    m, v = ogp.ExactGP(X, y, [0.3, 0.3], 1.0).predict(Xc)
+    np.testing.assert_allclose(mu[0].cpu().numpy(), m[:, 0], rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(var[0].cpu().numpy(), v[:, 0], rtol=1e-6, atol=1e-9)

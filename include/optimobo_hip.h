@@ -115,6 +115,16 @@ int omb_ehvi3d_mc(omb_ctx* ctx, const double* mu_dev, const double* var_dev, int
                   const double* cache_dev, int M, const double* r_host, double hv_pf, double* out_dev,
                   int32_t* raised_dev);
 
+/* Exact ("textbook") EHVI for k = 2 or 3 objectives — the exact value the Monte-Carlo
+ * EHVI_3D (util_functions.py:170-214) estimates — from a disjoint box decomposition of the
+ * non-dominated region (optimobo_amd.pareto.box_decomposition):
+ *   coords_dev (k, C) f64: per objective a sorted grid [-inf, front values..., r_j] (padded)
+ *   boxes_dev  (B, 2k) uint16: [lo_0, hi_0, lo_1, hi_1, ...] grid indices of each box
+ *   EHVI = Σ_b Π_j E[(hi_j − max(Y_j, lo_j))⁺],  Y_j ~ N(μ_j, σ²_j) independent.
+ * One wavefront per candidate; k·C ≤ 2048. */
+int omb_ehvi_boxes(omb_ctx* ctx, int k, const double* mu_dev, const double* var_dev, int64_t ld, int64_t N,
+                   const double* coords_dev, int C, const uint16_t* boxes_dev, int B, double* out_dev);
+
 /* Hypervolume-based PoI of EMO (emo.py:176-228): cells_dev (C, 2, 2) [upper, lower]. */
 int omb_hvpoi(omb_ctx* ctx, const double* mu_dev, const double* var_dev, int64_t ld, int64_t N,
               const double* cells_dev, int C, double* out_dev);

@@ -38,6 +38,7 @@ SIGNATURES = {
     "omb_posterior": (_i, [_p, _i, _p, _i64, _p, _p]),
     "omb_ehvi2d": (_i, [_p, _p, _p, _i64, _i64, _p, _i, _dp, _d, _d, _i, _p]),
     "omb_ehvi3d_mc": (_i, [_p, _p, _p, _i64, _i64, _p, _i, _dp, _d, _p, _p]),
+    "omb_ehvi_boxes": (_i, [_p, _i, _p, _p, _i64, _i64, _p, _i, _p, _i, _p]),
     "omb_hvpoi": (_i, [_p, _p, _p, _i64, _i64, _p, _i, _p]),
     "omb_expdec": (_i, [_p, _i, _p, _p, _i64, _i64, _p, _i, _i, _dp, _dp, _dp, _dp, _d, _p]),
     "omb_ei": (_i, [_p, _p, _p, _i64, _d, _d, _p]),

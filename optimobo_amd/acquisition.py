@@ -68,6 +68,12 @@ class AcquisitionEngine:
         sig = self._dev(np.asarray(sigma, np.float64).reshape(2, -1))
         return self.ctx.ehvi2d(mu, sig, pareto.stripes_2d(PF), np.asarray(r, np.float64), 1.0, 1.0, mode="sigma")
 
+    def ehvi_exact(self, Xc, max_point, PF):
+        """Exact EHVI (2 or 3 objectives) over the box decomposition — "textbook" mode."""
+        mu, var = self.posterior(Xc)
+        coords, _, boxes = pareto.box_decomposition(PF, max_point)
+        return self.ctx.ehvi_boxes(mu, var, coords, boxes)
+
     def ehvi3d(self, Xc, max_point, PF, cache):
         mu, var = self.posterior(Xc)
         hv = pareto.hypervolume(PF, max_point)

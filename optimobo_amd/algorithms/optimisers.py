@@ -25,7 +25,13 @@ class MultiSurrogateOptimiser(BODriver):
         """optimisers.py:91-119 on the device: returns (x, −EHVI(x))."""
         from ..acquisition import engine_for
         eng = engine_for(models, self.device)
-        if function == "EHVI_3D" or self.n_obj == 3:
+        if (function == "EHVI_3D" or self.n_obj == 3) and self.mode == "textbook":
+            coords, _, boxes = pareto.box_decomposition(pf, max_point)
+
+            def acq(Xc):                      # exact EHVI in place of the MC estimate
+                mu, var = eng.posterior(Xc)
+                return eng.ctx.ehvi_boxes(mu, var, coords, boxes)
+        elif function == "EHVI_3D" or self.n_obj == 3:
             hv = pareto.hypervolume(pf, max_point)
 
             def acq(Xc):

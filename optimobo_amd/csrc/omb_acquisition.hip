@@ -129,6 +129,96 @@ hipError_t launch_ehvi3d_mc(hipStream_t stream, const double* mu, const double* 
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------ exact EHVI over boxes
+// "textbook" EHVI for k = 2, 3 objectives from a disjoint box decomposition of the non-dominated
+// region (optimobo_amd.pareto.box_decomposition; replaces the Monte-Carlo EHVI_3D of
+// util_functions.py:170-214 by its exact value):
+//   EHVI = Σ_b Π_j G(lo_bj, hi_bj),  G(l, u) = (u−l)Φ(α) + (u−μ)(Φ(β)−Φ(α)) + σ(φ(β)−φ(α)),
+//   α = (l−μ)/σ, β = (u−μ)/σ, σ_j = sqrt(σ²_j) per objective.
+// One wavefront per candidate: its lanes tabulate Φ and φ at every grid coordinate (k·C values,
+// a per-wave LDS table), then stride over the box list (staged once per workgroup in LDS when it
+// fits) and reduce the box sum across the wave.  −∞ grid values arrive as −1e300 so
+// (u − l)·Φ(α) is an exact 0 with no inf·0.
+constexpr int kBoxWaves = 4;
+
+template <int K, bool BOXES_LDS>
+__global__ __launch_bounds__(64 * kBoxWaves) void ehvi_boxes_kernel(const double* __restrict__ mu,
+                                                                    const double* __restrict__ var, int64_t ld,
+                                                                    int64_t N, const double* __restrict__ coords,
+                                                                    int C, const uint16_t* __restrict__ boxes, int B,
+                                                                    double* __restrict__ out) {
+  extern __shared__ double sm[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  double* grid = sm;                                    // K·C coordinates (−∞ → −1e300)
+  double* tabP = grid + K * C + wave * 2 * K * C;      // this wave's Φ table
+  double* tabp = tabP + K * C;                          // this wave's φ table
+  uint16_t* lbox = reinterpret_cast<uint16_t*>(sm + K * C + kBoxWaves * 2 * K * C);
+  for (int i = threadIdx.x; i < K * C; i += blockDim.x) grid[i] = fmax(coords[i], -1e300);
+  if constexpr (BOXES_LDS) {
+    for (int i = threadIdx.x; i < 2 * K * B; i += blockDim.x) lbox[i] = boxes[i];
+  }
+  __syncthreads();
+  const uint16_t* bx = BOXES_LDS ? lbox : boxes;
+  for (int64_t c = (int64_t)blockIdx.x * kBoxWaves + wave; c < N; c += (int64_t)gridDim.x * kBoxWaves) {
+    double m[K], s[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      m[j] = mu[j * ld + c];
+      s[j] = sqrt(var[j * ld + c]);
+    }
+    for (int i = lane; i < K * C; i += 64) {
+      const int j = i / C;
+      double mj = m[0], sj = s[0];
+#pragma unroll
+      for (int q = 1; q < K; ++q)
+        if (j == q) {
+          mj = m[q];
+          sj = s[q];
+        }
+      const double t = (grid[i] - mj) / sj;
+      tabP[i] = ndtr(t);
+      tabp[i] = npdf(t);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    double acc = 0.0;
+    for (int b = lane; b < B; b += 64) {
+      double prod = 1.0;
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const int il = j * C + bx[2 * K * b + 2 * j], ih = j * C + bx[2 * K * b + 2 * j + 1];
+        const double l = grid[il], u = grid[ih];
+        const double Pl = tabP[il], Pu = tabP[ih];
+        prod *= (u - l) * Pl + (u - m[j]) * (Pu - Pl) + s[j] * (tabp[ih] - tabp[il]);
+      }
+      acc += prod;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+    if (lane == 0) out[c] = acc;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // table reads done before the next candidate
+  }
+}
+
+hipError_t launch_ehvi_boxes(hipStream_t stream, int k, const double* mu, const double* var, int64_t ld, int64_t N,
+                             const double* coords, int C, const uint16_t* boxes, int B, double* out) {
+  const size_t table = sizeof(double) * (size_t)k * C * (1 + 2 * kBoxWaves);
+  const size_t box_bytes = sizeof(uint16_t) * 2 * (size_t)k * B;
+  const bool in_lds = table + box_bytes <= 64 * 1024;
+  const size_t shm = table + (in_lds ? box_bytes : 0);
+  int64_t nb = (N + kBoxWaves - 1) / kBoxWaves;
+  const unsigned grid = (unsigned)(nb > 16384 ? 16384 : (nb < 1 ? 1 : nb));
+  dim3 g(grid), b(64 * kBoxWaves);
+  if (k == 2) {
+    if (in_lds) hipLaunchKernelGGL((ehvi_boxes_kernel<2, true>), g, b, shm, stream, mu, var, ld, N, coords, C, boxes, B, out);
+    else hipLaunchKernelGGL((ehvi_boxes_kernel<2, false>), g, b, shm, stream, mu, var, ld, N, coords, C, boxes, B, out);
+  } else {
+    if (in_lds) hipLaunchKernelGGL((ehvi_boxes_kernel<3, true>), g, b, shm, stream, mu, var, ld, N, coords, C, boxes, B, out);
+    else hipLaunchKernelGGL((ehvi_boxes_kernel<3, false>), g, b, shm, stream, mu, var, ld, N, coords, C, boxes, B, out);
+  }
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------------------------ HV-PoI
 // emo.py:192-228 with vol5 (:176-189):  s = sqrt(σ² + 1e-5);
 //   PoI = Σ_c Π_k [Φ((u_k−μ_k)/s_k) − Φ((l_k−μ_k)/s_k)],  I = Σ_c [u > μ]·Π_k(u_k − max(l_k, μ_k)).

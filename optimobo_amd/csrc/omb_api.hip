@@ -280,6 +280,22 @@ int omb_ehvi3d_mc(omb_ctx* ctx, const double* mu_dev, const double* var_dev, int
   return OMB_OK;
 }
 
+int omb_ehvi_boxes(omb_ctx* ctx, int k, const double* mu_dev, const double* var_dev, int64_t ld, int64_t N,
+                   const double* coords_dev, int C, const uint16_t* boxes_dev, int B, double* out_dev) {
+  int rc = enter(ctx);
+  if (rc) return rc;
+  if (k != 2 && k != 3) return fail(ctx, OMB_EUNSUP, "exact EHVI needs k = 2 or 3 objectives (k=%d)", k);
+  if ((rc = check_moments(ctx, mu_dev, var_dev, ld, N, k, out_dev))) return rc;
+  // grid + 4 per-wave Φ/φ tables must fit the 64 KiB of dynamic LDS
+  if (!coords_dev || C < 2 || (size_t)k * C * 9 > (size_t)kMaxLdsDoubles)
+    return fail(ctx, OMB_EUNSUP, "grid size C=%d outside [2, %d] for k=%d", C, kMaxLdsDoubles / (9 * k), k);
+  if (!boxes_dev || B < 1) return fail(ctx, OMB_EINVAL, "empty box list");
+  if (N == 0) return OMB_OK;
+  hipError_t e = launch_ehvi_boxes(ctx->stream, k, mu_dev, var_dev, ld, N, coords_dev, C, boxes_dev, B, out_dev);
+  if (e != hipSuccess) return hip_fail(ctx, e, "ehvi_boxes");
+  return OMB_OK;
+}
+
 int omb_hvpoi(omb_ctx* ctx, const double* mu_dev, const double* var_dev, int64_t ld, int64_t N,
               const double* cells_dev, int C, double* out_dev) {
   int rc = enter(ctx);

@@ -54,6 +54,9 @@ hipError_t launch_ehvi3d_mc(hipStream_t stream, const double* mu, const double* 
                             const double* cache, int M, const double* r, double hv_pf, double* out,
                             int32_t* raised);
 
+hipError_t launch_ehvi_boxes(hipStream_t stream, int k, const double* mu, const double* var, int64_t ld, int64_t N,
+                             const double* coords, int C, const uint16_t* boxes, int B, double* out);
+
 hipError_t launch_hvpoi(hipStream_t stream, const double* mu, const double* var, int64_t ld, int64_t N,
                         const double* cells, int C, double* out);
 

@@ -133,6 +133,21 @@ class AcqContext:
                                            _lib.darr(r), float(hv_pf), _ptr(out), _ptr(raised)), "omb_ehvi3d_mc")
         return out, raised
 
+    def ehvi_boxes(self, mu, var, coords, boxes, out=None):
+        """Exact EHVI over a box decomposition (optimobo_amd.pareto.box_decomposition)."""
+        k, N = mu.shape
+        coords = _dev_f64(coords, self.device)
+        if not isinstance(boxes, torch.Tensor):
+            # uint16 indices < 32768 travel as int16 (torch has no uint16 on every build)
+            b = np.ascontiguousarray(boxes, dtype=np.uint16)
+            boxes = torch.as_tensor(b.view(np.int16), device=self.device)
+        out = out if out is not None else torch.empty(N, dtype=torch.float64, device=self.device)
+        self._stream()
+        self._check(self.lib.omb_ehvi_boxes(self._h, k, _ptr(mu), _ptr(var), mu.stride(0), N, _ptr(coords),
+                                            coords.shape[1], _ptr(boxes), boxes.shape[0], _ptr(out)),
+                    "omb_ehvi_boxes")
+        return out
+
     def hvpoi(self, mu, var, cells, out=None):
         N = mu.shape[1]
         cells = _dev_f64(cells, self.device)

@@ -90,6 +90,56 @@ def hypervolume(points, ref):
     return float(total)
 
 
+def box_decomposition(pf, ref):
+    """Disjoint boxes covering the part of (−∞, ref] the front does not dominate (k = 2, 3).
+
+    Input of omb_ehvi_boxes (the exact "textbook" EHVI): HVI(y) = Σ_b Π_j (hi_bj − max(y_j, lo_bj))⁺.
+    Returns (coords (k, C) f64 — per objective the sorted grid [−∞, front values…, ref_j] padded
+    with ref_j —, ncoord (k,) int32, boxes (B, 2k) uint16 = [lo_idx_0, hi_idx_0, lo_idx_1, …]).
+    3-D: one slab per distinct f3 level; inside a slab the 2-D staircase of the points below it.
+    """
+    pf = np.asarray(pf, np.float64)
+    ref = np.asarray(ref, np.float64)
+    k = ref.size
+    if k not in (2, 3):
+        raise NotImplementedError("box_decomposition: 2 or 3 objectives")
+    pts = pf[np.all(pf < ref, axis=1)] if pf.size else np.zeros((0, k))
+    pts = calc_pf(pts) if len(pts) > 1 else pts
+    grids = [np.concatenate(([-np.inf], np.unique(pts[:, j]), [ref[j]])) for j in range(k)]
+
+    def staircase(P2):
+        """(x_lo, x_hi, y_hi) of the 2-D non-dominated stripes below ref[:2]."""
+        if len(P2) == 0:
+            return [(-np.inf, ref[0], ref[1])]
+        F = calc_pf(P2)
+        F = F[np.argsort(F[:, 0], kind="stable")]
+        xb = np.concatenate(([-np.inf], F[:, 0], [ref[0]]))
+        yt = np.concatenate(([ref[1]], F[:, 1]))
+        return [(xb[i], xb[i + 1], yt[i]) for i in range(len(F) + 1) if xb[i + 1] > xb[i]]
+
+    rows = []
+    if k == 2:
+        for xl, xh, yh in staircase(pts):
+            rows.append((xl, xh, -np.inf, yh))
+    else:
+        z_levels = grids[2]                      # −∞, distinct f3 values, ref_3
+        for a in range(len(z_levels) - 1):
+            below = pts[pts[:, 2] <= z_levels[a], :2]
+            for xl, xh, yh in staircase(below):
+                rows.append((xl, xh, -np.inf, yh, z_levels[a], z_levels[a + 1]))
+    vals = np.asarray(rows, np.float64).reshape(-1, 2 * k)
+    idx = np.empty(vals.shape, np.int64)
+    for j in range(k):
+        for s in (0, 1):
+            idx[:, 2 * j + s] = np.searchsorted(grids[j], vals[:, 2 * j + s])
+    C = max(len(g) for g in grids)
+    coords = np.stack([np.concatenate((g, np.full(C - len(g), g[-1]))) for g in grids])
+    if C > 65535:
+        raise ValueError("box_decomposition: front too large for 16-bit grid indices")
+    return (np.ascontiguousarray(coords), np.array([len(g) for g in grids], np.int32),
+            np.ascontiguousarray(idx.astype(np.uint16)))
+
+
 def cached_samples(k, sample_exponent, seed=None):
     s = qmc.Sobol(d=k, scramble=True, seed=seed).random_base2(m=sample_exponent)
     return np.ascontiguousarray(np.column_stack([norm.ppf(s[:, i]) for i in range(k)]))

@@ -97,12 +97,17 @@ def EHVI(X, models, max_point, PF, cache, mode="reference"):
     return out[:1] if single else out
 
 
-def EHVI_3D(X, models, max_point, PF, cache):
-    """util_functions.py:170-214 (Monte-Carlo form).  One x: float, ValueError where pygmo raises.
+def EHVI_3D(X, models, max_point, PF, cache, mode="reference"):
+    """util_functions.py:170-214.  One x: float, ValueError where pygmo raises.
 
-    Batch: (values (N,), raised (N,) bool) — NaN where the reference would raise.
+    mode "reference": the reference's Monte-Carlo form; batch → (values (N,), raised (N,) bool),
+    NaN where the reference would raise.  mode "textbook": the exact EHVI over a box
+    decomposition (no MC error, never raises); batch → (N,).
     """
     Xb, single = _batch(X)
+    if mode == "textbook":
+        out = engine_for(models).ehvi_exact(Xb, max_point, PF).cpu().numpy()
+        return float(out[0]) if single else out
     vals, raised = engine_for(models).ehvi3d(Xb, max_point, PF, cache)
     vals, raised = vals.cpu().numpy(), raised.cpu().numpy().astype(bool)
     if single:

@@ -199,3 +199,29 @@ def argmax(values, offset=0):
 __all__ = ["norm_cdf", "norm_pdf", "psi_cal", "cache_stats", "change", "sample_cov2", "stripes_2d",
            "ehvi2d_aux", "ehvi2d", "ehvi3d_reference", "hvpoi", "expected_decomposition", "ei",
            "argmax", "scal_mod"]
+
+
+def ehvi_exact_boxes(mu, var, lo, hi):
+    """Exact EHVI for independent Gaussian objectives over a disjoint box decomposition of the
+    non-dominated region (oracle.pareto.nondominated_boxes): Σ_b Π_j G(lo_bj, hi_bj; μ_j, σ_j),
+    G(l, u) = E[(u − max(Y, l))⁺] = (u − l)Φ(α) + (u − μ)(Φ(β) − Φ(α)) + σ(φ(β) − φ(α)),
+    α = (l − μ)/σ, β = (u − μ)/σ (l = −∞ → Φ(α) = φ(α) = 0).  "textbook" EHVI-3D mode.
+    """
+    mu = np.asarray(mu, np.float64)          # (k, N)
+    sd = np.sqrt(np.asarray(var, np.float64))
+    total = np.zeros(mu.shape[1])
+    for b in range(len(lo)):
+        prod = np.ones(mu.shape[1])
+        for j in range(mu.shape[0]):
+            l, u = lo[b, j], hi[b, j]
+            be = (u - mu[j]) / sd[j]
+            if np.isfinite(l):
+                al = (l - mu[j]) / sd[j]
+                Pa, pa = norm_cdf(al), norm_pdf(al)
+                first = (u - l) * Pa
+            else:
+                Pa = pa = 0.0
+                first = 0.0
+            prod = prod * (first + (u - mu[j]) * (norm_cdf(be) - Pa) + sd[j] * (norm_pdf(be) - pa))
+        total += prod
+    return total

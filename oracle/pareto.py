@@ -90,3 +90,50 @@ def _hv2d(pts, r):
             total += (r[0] - x) * (best_f2 - y)
             best_f2 = y
     return total
+
+
+def nondominated_boxes(pf, r):
+    """Disjoint boxes [lo, hi) covering the region below ``r`` that ``pf`` does NOT dominate
+    (k = 2 or 3), so that HVI(y) = Σ_b Π_j (hi_j − max(y_j, lo_j))⁺ exactly.
+
+    Not a reference function: it is the textbook decomposition behind the exact EHVI that
+    "textbook" mode computes in place of the Monte-Carlo EHVI_3D (util_functions.py:170-214).
+    2-D: the staircase stripes of EHVI_2D_aux (util_functions.py:93-125) as boxes.
+    3-D: slabs between consecutive f3 levels, each the 2-D staircase of the points below it.
+    Lower bounds may be −inf.  Returns (lo (B, k), hi (B, k)).
+    """
+    pf = np.asarray(pf, np.float64)
+    r = np.asarray(r, np.float64)
+    pf = calc_pf(pf[np.all(pf < r, axis=1)]) if len(pf) else pf.reshape(0, len(r))
+    k = len(r)
+
+    def stairs(P2, r2):
+        # x-sorted 2-D front → boxes [lo, hi) in (x, y)
+        out_lo, out_hi = [], []
+        if len(P2) == 0:
+            return [(-np.inf, -np.inf)], [(r2[0], r2[1])]
+        Q = calc_pf(P2)
+        Q = Q[np.lexsort((Q[:, 1], Q[:, 0]))]
+        xs = [-np.inf] + list(Q[:, 0]) + [r2[0]]
+        ys = [r2[1]] + list(Q[:, 1])
+        for i in range(len(Q) + 1):
+            if xs[i + 1] > xs[i]:
+                out_lo.append((xs[i], -np.inf))
+                out_hi.append((xs[i + 1], ys[i]))
+        return out_lo, out_hi
+
+    if k == 2:
+        lo, hi = stairs(pf, r)
+        return np.array(lo), np.array(hi)
+    if k != 3:
+        raise NotImplementedError("nondominated_boxes: k must be 2 or 3")
+    levels = np.unique(pf[:, 2]) if len(pf) else np.array([])
+    zs = np.concatenate(([-np.inf], levels, [r[2]]))
+    LO, HI = [], []
+    for a in range(len(zs) - 1):
+        below = pf[pf[:, 2] <= zs[a]][:, :2] if a > 0 else np.zeros((0, 2))
+        lo2, hi2 = stairs(below, r[:2])
+        for (l0, l1), (h0, h1) in zip(lo2, hi2):
+            LO.append((l0, l1, zs[a]))
+            HI.append((h0, h1, zs[a + 1]))
+    return np.array(LO), np.array(HI)

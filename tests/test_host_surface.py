@@ -89,6 +89,22 @@ def test_hypervolume(k):
             assert hv == pytest.approx(dom.mean() * 1.1 ** k, abs=0.01)
 
 
+@pytest.mark.parametrize("k", [2, 3])
+def test_box_decomposition_matches_oracle_hvi(k):
+    rng = np.random.default_rng(20 + k)
+    for _ in range(20):
+        pf = opar.calc_pf(rng.uniform(0, 1, (int(rng.integers(1, 30)), k)))
+        r = np.full(k, 1.1)
+        coords, ncoord, boxes = pareto.box_decomposition(pf, r)
+        assert boxes.dtype == np.uint16 and coords.shape == (k, ncoord.max())
+        lo = np.stack([coords[j][boxes[:, 2 * j]] for j in range(k)], 1)
+        hi = np.stack([coords[j][boxes[:, 2 * j + 1]] for j in range(k)], 1)
+        hv0 = opar.hypervolume(pf, r)
+        for y in rng.uniform(-0.2, 1.2, (10, k)):
+            hvi = np.prod(np.clip(hi - np.maximum(y, lo), 0, None), axis=1).sum()
+            assert hvi == pytest.approx(opar.hypervolume(np.vstack([pf, y]), r) - hv0, rel=1e-10, abs=1e-12)
+
+
 def test_cache_and_stripes():
     c = pareto.cached_samples(2, 5, seed=0)
     assert c.shape == (32, 2)

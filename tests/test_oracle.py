@@ -134,3 +134,39 @@ def test_argmax_rule():
 
 def test_fixture_files_present(golden_dir):
     assert len(glob.glob(os.path.join(golden_dir, "*.npz"))) >= 12
+
+
+def test_boxes_reproduce_hvi_and_2d_ehvi():
+    rng = np.random.default_rng(8)
+    for k in (2, 3):
+        pf = pareto.calc_pf(rng.uniform(0, 1, (25, k)))
+        r = np.full(k, 1.2)
+        lo, hi = pareto.nondominated_boxes(pf, r)
+        hv0 = pareto.hypervolume(pf, r)
+        for y in rng.uniform(-0.2, 1.2, (30, k)):
+            hvi = np.prod(np.clip(hi - np.maximum(y, lo), 0, None), axis=1).sum()
+            assert hvi == pytest.approx(pareto.hypervolume(np.vstack([pf, y]), r) - hv0, rel=1e-10, abs=1e-12)
+    # k = 2: the box form of the exact EHVI equals the textbook EHVI_2D_aux
+    x = np.sort(rng.uniform(0.05, 0.95, 9))
+    pf = np.column_stack([x, 1 - np.sqrt(x)])
+    r = np.array([1.1, 1.05])
+    mu = rng.uniform(0, 1, (2, 50))
+    var = 10 ** rng.uniform(-4, -1, (2, 50))
+    lo, hi = pareto.nondominated_boxes(pf, r)
+    np.testing.assert_allclose(acq.ehvi_exact_boxes(mu, var, lo, hi),
+                               acq.ehvi2d(mu, var, pf, r, None, mode="textbook"), rtol=1e-10, atol=1e-14)
+
+
+def test_exact_ehvi3d_matches_monte_carlo():
+    rng = np.random.default_rng(9)
+    pts = rng.uniform(0, 1, (60, 3))
+    pts /= np.linalg.norm(pts, axis=1, keepdims=True)
+    pf = pareto.calc_pf(pts)[:10]
+    r = np.full(3, 1.3)
+    lo, hi = pareto.nondominated_boxes(pf, r)
+    mu = np.array([[0.5], [0.6], [0.4]])
+    sd = np.array([0.2, 0.15, 0.25])
+    ex = acq.ehvi_exact_boxes(mu, sd[:, None] ** 2, lo, hi)[0]
+    y = rng.standard_normal((40000, 3)) * sd + mu[:, 0]
+    hvi = np.prod(np.clip(hi[None] - np.maximum(y[:, None, :], lo[None]), 0, None), axis=2).sum(1)
+    assert abs(ex - hvi.mean()) < 4 * hvi.std() / np.sqrt(len(hvi))

@@ -2,9 +2,11 @@
 """Benchmark: EHVI candidate evaluations per second (BASELINE.json metric, config 3).
 
 One step = the whole acquisition hot path over one resident batch of candidates on every
-GPU: fused GP posterior for both objectives (omb_posterior) → reference-mode EHVI-2D
-(omb_ehvi2d) → device arg-max (omb_argmax_dev) → cross-rank arg-max exchange (RCCL
-all-gather of 16 B).  Workload per GPU: ZDT1 (n_var=6) surrogate with n_train=512 and
+GPU, one C call (omb_eval_argmax, the fused chain): GP posterior for both objectives →
+reference-mode EHVI-2D → device arg-max; then the cross-rank arg-max exchange (RCCL
+all-gather of 16 B).  `--chain separate` issues the three entry points one by one
+(omb_posterior, omb_ehvi2d, omb_argmax_dev); `--chain sobol` also generates the candidates
+on the device inside the step (omb_eval_argmax_sobol, what the maximiser runs).  Workload per GPU: ZDT1 (n_var=6) surrogate with n_train=512 and
 N = 2^20 unscrambled-Sobol candidates; rank g scores Sobol indices [g·N, (g+1)·N) (weak scaling).
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W]
@@ -135,6 +137,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kblock", action="store_true")
+    ap.add_argument("--chain", default="fused", choices=["fused", "separate", "sobol"])
+    ap.add_argument("--stage-timing", action="store_true", help="events around every stage (adds ~5 us/stage)")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
 
@@ -197,6 +201,17 @@ def main():
         hv_pf = pareto.hypervolume(pf, r)
         cache_dev = torch.as_tensor(cache, device=device)
 
+    # the plan of the fused chain: the same acquisition as acquisition() below
+    if acq_kind == "ehvi2d":
+        ctx.plan_ehvi2d(pareto.stripes_2d(pf), r, s00, s01, mode=args.mode)
+    elif acq_kind == "ehvi3d":
+        ctx.plan_ehvi3d_mc(cache, r, hv_pf)
+    else:
+        ctx.plan_ei(best_y, 1e-6)
+    if args.chain == "sobol":
+        # unscrambled Sobol over [0, 1]^d: the same points as `candidates` above
+        ctx.set_sobol(d, np.zeros(d), np.ones(d), scramble=False)
+
     def acquisition():
         if acq_kind == "ehvi2d":
             ctx.ehvi2d(mu, var, pf_dev, r, s00, s01, mode=args.mode, out=acq)
@@ -206,13 +221,18 @@ def main():
             ctx.ei(mu[0], var[0], best_y, 1e-6, out=acq)
 
     def step(i=None):
-        if i is not None:
-            ev[i][0].record()
-        ctx.posterior(Xc, n_obj, out=(mu, var))
-        if i is not None:
-            ev[i][1].record()
-        acquisition()
-        ctx.argmax_dev(acq, offset=start, out=pair)
+        if args.chain == "fused":
+            ctx.eval_argmax(Xc, offset=start, out=pair)
+        elif args.chain == "sobol":
+            ctx.eval_argmax_sobol(start, N, out=pair)
+        else:
+            if i is not None:
+                ev[i][0].record()
+            ctx.posterior(Xc, n_obj, out=(mu, var))
+            if i is not None:
+                ev[i][1].record()
+            acquisition()
+            ctx.argmax_dev(acq, offset=start, out=pair)
         return global_argmax(pair)
 
     for _ in range(args.warmup):
@@ -222,6 +242,9 @@ def main():
     if world_size > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    if args.chain != "separate":
+        # HIP events on the chain's stream: around the posterior (level 1) or every stage (2)
+        ctx.timing(2 if args.stage_timing else 1)
     t0 = time.perf_counter()
     for i in range(args.steps):
         best = step(i)
@@ -229,11 +252,19 @@ def main():
     if world_size > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    stage_ms = None
+    if args.chain != "separate":
+        stage_sum, chains = ctx.timing_read()
+        ctx.timing(0)
+        stage_ms = {k: v / chains for k, v in stage_sum.items() if args.stage_timing or k == "posterior"}
     if world_size > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    post_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if stage_ms is not None:
+        post_ms = stage_ms["posterior"]
+    else:
+        post_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     best = best.cpu().numpy()
 
     # standalone K(X, X*) block: the HBM-bound kernel of the north star
@@ -291,6 +322,8 @@ def main():
             "roofline": roofline,
             "roofline_kblock": kblock,
             "cpu_baseline": cpu,
+            "chain": args.chain,
+            "stage_ms": stage_ms,
             "best": {"value": float(best[0]), "index": int(best[1])},
         }
         print(json.dumps(out))

@@ -11,9 +11,10 @@
  *   - Every array argument named *_dev is a DEVICE pointer owned by the caller (e.g. a torch
  *     tensor's data_ptr()); fp64, C-contiguous.  Small fixed-size vectors (reference point,
  *     weights, bounds, scalarisation parameters) are HOST pointers read during the call.
- *   - Calls are asynchronous on the context's stream (omb_set_stream), except omb_argmax
- *     and omb_synchronize, which synchronise.  No call allocates device memory except
- *     omb_create and omb_set_gp.
+ *   - Calls are asynchronous on the context's stream (omb_set_stream), except omb_argmax,
+ *     omb_synchronize and omb_timing_read, which synchronise.  Device memory is allocated by
+ *     omb_create, omb_set_gp, the omb_plan_* calls (geometry) and the fused-chain calls
+ *     (workspace, grown on demand); a grow synchronises the stream first.
  *   - Return 0 (OMB_OK) on success or a negative OMB_E* code; omb_last_error() describes the
  *     last failure.  No C++ exception crosses the ABI.
  *   - One context per device; a context is not thread-safe; different contexts are
@@ -121,7 +122,7 @@ int omb_ehvi3d_mc(omb_ctx* ctx, const double* mu_dev, const double* var_dev, int
  *   coords_dev (k, C) f64: per objective a sorted grid [-inf, front values..., r_j] (padded)
  *   boxes_dev  (B, 2k) uint16: [lo_0, hi_0, lo_1, hi_1, ...] grid indices of each box
  *   EHVI = Σ_b Π_j E[(hi_j − max(Y_j, lo_j))⁺],  Y_j ~ N(μ_j, σ²_j) independent.
- * One wavefront per candidate; k·C ≤ 2048. */
+ * One wavefront per candidate; 9·k·C ≤ 8192 (grid and per-wave Φ/φ tables in LDS). */
 int omb_ehvi_boxes(omb_ctx* ctx, int k, const double* mu_dev, const double* var_dev, int64_t ld, int64_t N,
                    const double* coords_dev, int C, const uint16_t* boxes_dev, int B, double* out_dev);
 
@@ -149,6 +150,60 @@ int omb_argmax_dev(omb_ctx* ctx, const double* vals_dev, int64_t N, int64_t offs
 /* Same, synchronising and returning to host. */
 int omb_argmax(omb_ctx* ctx, const double* vals_dev, int64_t N, int64_t offset, double* best_val,
                int64_t* best_idx);
+
+/* ---------------------------------------------------------------------------------------
+ * Fused chain.  One BO iteration of the reference calls
+ *   differential_evolution(lambda x: -acq(x, models, ...), bounds)      (optimisers.py:87,118)
+ * where acq is fixed for the iteration.  Here the acquisition and its per-iteration geometry
+ * are uploaded once as a *plan* (HOST pointers, copied into context-owned device memory; the
+ * call synchronises the stream first), then each candidate batch is one call that runs
+ * posterior (objectives 0..k-1) → acquisition → arg-max on the stream, with the moments in a
+ * context-owned workspace (grown on demand).  Setting a plan replaces the previous one; a
+ * failed plan call leaves no plan (OMB_ESTATE from the eval calls).
+ * ------------------------------------------------------------------------------------- */
+/* util_functions.EHVI / EHVI_2D_aux (k = 2): as omb_ehvi2d, pf_sorted_host (P, 2). */
+int omb_plan_ehvi2d(omb_ctx* ctx, const double* pf_sorted_host, int P, const double* r_host, double s00,
+                    double s01, int mode);
+/* util_functions.EHVI_3D reference Monte-Carlo form (k = 3): as omb_ehvi3d_mc, cache_host (M, 3). */
+int omb_plan_ehvi3d_mc(omb_ctx* ctx, const double* cache_host, int M, const double* r_host, double hv_pf);
+/* Exact EHVI (k = 2, 3): as omb_ehvi_boxes, coords_host (k, C), boxes_host (B, 2k). */
+int omb_plan_ehvi_boxes(omb_ctx* ctx, int k, const double* coords_host, int C, const uint16_t* boxes_host, int B);
+/* EMO hypervolume-based PoI (k = 2): as omb_hvpoi, cells_host (C, 2, 2). */
+int omb_plan_hvpoi(omb_ctx* ctx, const double* cells_host, int C);
+/* expected_decomposition (k objectives): as omb_expdec, cache_host (M, k). */
+int omb_plan_expdec(omb_ctx* ctx, int k, const double* cache_host, int M, int scal_id, const double* params_host,
+                    const double* weights_host, const double* ideal_host, const double* max_host, double agg_min);
+/* Expected improvement of objective 0 (k = 1): as omb_ei. */
+int omb_plan_ei(omb_ctx* ctx, double best, double var_eps);
+
+/* Scrambled Sobol' candidates generated on the device (replaces the host-side sampling that
+ * feeds the maximiser; same sequence as scipy.stats.qmc.Sobol, which the reference uses for
+ * its MC cache at optimisers.py:121-141).  sv_host (d, bits) and shift_host (d) are the
+ * engine's scrambled direction numbers and digital shift (scipy: Sobol._sv, Sobol._shift);
+ * point i of the engine, mapped to the box, is
+ *   x_ij = lo_j + u_ij (hi_j − lo_j),  u_ij = (shift_j ⊕ ⨁_{b ∈ gray(i)} sv_jb) · 2^-bits,
+ * bit-identical to numpy's `lo + U * (hi - lo)` on scipy's U.  bits ≤ 32, d ≤ OMB_MAX_DIM. */
+int omb_set_sobol(omb_ctx* ctx, int d, int bits, const uint32_t* sv_host, const uint32_t* shift_host,
+                  const double* lo_host, const double* hi_host);
+/* Points start .. start+N-1 → X_dev (N, d). */
+int omb_sobol(omb_ctx* ctx, int64_t start, int64_t N, double* X_dev);
+
+/* Acquisition values of the plan at candidates Xc_dev (N, d) → vals_dev (N). */
+int omb_eval(omb_ctx* ctx, const double* Xc_dev, int64_t N, double* vals_dev);
+/* posterior → plan → arg-max: result_dev = {best value, best index + offset} (see omb_argmax_dev). */
+int omb_eval_argmax(omb_ctx* ctx, const double* Xc_dev, int64_t N, int64_t offset, double* result_dev);
+/* Same over the Sobol' points start .. start+N-1 generated into the workspace; the index in
+ * result_dev is the Sobol index (offset = start). */
+int omb_eval_argmax_sobol(omb_ctx* ctx, int64_t start, int64_t N, double* result_dev);
+
+/* Device timing of the fused chain (HIP events on the context's stream), up to 4096 chains.
+ * omb_timing(ctx, level): 0 off; 1 the posterior stage only (2 events per chain); 2 every
+ * stage (5 events; each record costs a few µs of GPU time).  omb_timing_read synchronises
+ * and returns the summed milliseconds of {Sobol generation, posterior, acquisition, arg-max}
+ * (0 for stages not recorded) over the chains recorded since the last read, and their count.
+ * Changing the level discards unread records. */
+int omb_timing(omb_ctx* ctx, int enable);
+int omb_timing_read(omb_ctx* ctx, double* stage_ms /* [4] */, int64_t* chains);
 
 #ifdef __cplusplus
 }

@@ -44,6 +44,20 @@ SIGNATURES = {
     "omb_ei": (_i, [_p, _p, _p, _i64, _d, _d, _p]),
     "omb_argmax_dev": (_i, [_p, _p, _i64, _i64, _p]),
     "omb_argmax": (_i, [_p, _p, _i64, _i64, _dp, ctypes.POINTER(_i64)]),
+    # fused chain (host pointers for plan geometry)
+    "omb_plan_ehvi2d": (_i, [_p, _p, _i, _dp, _d, _d, _i]),
+    "omb_plan_ehvi3d_mc": (_i, [_p, _p, _i, _dp, _d]),
+    "omb_plan_ehvi_boxes": (_i, [_p, _i, _p, _i, _p, _i]),
+    "omb_plan_hvpoi": (_i, [_p, _p, _i]),
+    "omb_plan_expdec": (_i, [_p, _i, _p, _i, _i, _dp, _dp, _dp, _dp, _d]),
+    "omb_plan_ei": (_i, [_p, _d, _d]),
+    "omb_set_sobol": (_i, [_p, _i, _i, _p, _p, _dp, _dp]),
+    "omb_sobol": (_i, [_p, _i64, _i64, _p]),
+    "omb_eval": (_i, [_p, _p, _i64, _p]),
+    "omb_eval_argmax": (_i, [_p, _p, _i64, _i64, _p]),
+    "omb_eval_argmax_sobol": (_i, [_p, _i64, _i64, _p]),
+    "omb_timing": (_i, [_p, _i]),
+    "omb_timing_read": (_i, [_p, _dp, ctypes.POINTER(_i64)]),
 }
 
 
@@ -73,6 +87,11 @@ def load():
         raise ImportError("liboptimobo_hip.so ABI version mismatch")
     _LIB = lib
     return lib
+
+
+def host_ptr(arr):
+    """Pointer to a C-contiguous numpy array that the call reads synchronously (plan geometry)."""
+    return ctypes.c_void_p(arr.ctypes.data)
 
 
 def darr(values):

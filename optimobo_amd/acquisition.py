@@ -3,14 +3,13 @@
 The reference maximises every acquisition with ``scipy.optimize.differential_evolution``,
 calling ``acq(x)`` one candidate at a time (optimisers.py:87,118,366; emo.py:240).  Here one
 BO iteration uploads the fitted surrogates once, scores a large quasi-random candidate batch
-on the GPU (posterior → acquisition) and reduces it with the device arg-max.  With
+on the GPU (Sobol generation → posterior → acquisition) and reduces it with the device arg-max.  With
 torch.distributed initialised, every rank scores its own contiguous shard of the Sobol
 sequence and the ranks exchange one {value, index} pair (optimobo_amd.parallel); the winning
 point is regenerated from its Sobol index on every rank, so no coordinates are broadcast.
 """
 import numpy as np
 import torch
-from scipy.stats import qmc
 
 from . import pareto
 from .device import AcqContext
@@ -94,14 +93,43 @@ class AcquisitionEngine:
         mu, var = self.posterior(Xc)
         return self.ctx.ei(mu[0], var[0], float(best), float(var_eps))
 
+    # ------------------------------------------------------------------ plans (fused chain)
+    # One plan per BO iteration; each candidate batch is then a single omb_eval_argmax_sobol
+    # (Sobol generation → posterior → acquisition → arg-max on the device).
+    def plan_ehvi(self, max_point, PF, cache, mode="reference"):
+        s00, s01 = pareto.cache_stats(np.asarray(cache, np.float64))
+        self.ctx.plan_ehvi2d(pareto.stripes_2d(PF), np.asarray(max_point, np.float64), s00, s01, mode=mode)
+
+    def plan_ehvi_exact(self, max_point, PF):
+        coords, _, boxes = pareto.box_decomposition(PF, max_point)
+        self.ctx.plan_ehvi_boxes(coords, boxes)
+
+    def plan_ehvi3d(self, max_point, PF, cache):
+        self.ctx.plan_ehvi3d_mc(np.asarray(cache, np.float64), np.asarray(max_point, np.float64),
+                                pareto.hypervolume(PF, max_point))
+
+    def plan_expected_decomposition(self, weights, agg_func, agg_min, cache):
+        sid, params = agg_func.device_spec()
+        self.ctx.plan_expdec(np.asarray(cache, np.float64), sid, params, np.asarray(weights, np.float64),
+                             np.asarray(agg_func.ideal_point, np.float64), np.asarray(agg_func.max_point, np.float64),
+                             float(agg_min))
+
+    def plan_hvpoi(self, cells):
+        self.ctx.plan_hvpoi(np.ascontiguousarray(cells, dtype=np.float64))
+
+    def plan_ei(self, best, var_eps=0.0):
+        self.ctx.plan_ei(float(best), float(var_eps))
+
     # ------------------------------------------------------------------ maximiser
     def maximise(self, acq_fn, lower, upper, n_candidates=1 << 16, seed=0, refine_rounds=2, shrink=0.1):
-        """Arg-max of ``acq_fn(Xc_tensor) -> (N,) tensor`` over [lower, upper]^d.
+        """Arg-max of the acquisition over [lower, upper]^d.
 
-        Round 0 scores the first ``n_candidates`` points of a scrambled Sobol sequence (seeded, so
-        every rank sees the same sequence and owns one contiguous shard).  Each refinement round
-        re-centres a box ``shrink`` times smaller on the incumbent and keeps it if it improves —
-        a batched stand-in for DE's final polish.  Returns (x_best (d,), value).
+        ``acq_fn`` is None for the current plan (fused chain, one C call per batch) or a callable
+        ``acq_fn(Xc_tensor (N, d)) -> (N,) tensor``.  Round 0 scores the first ``n_candidates``
+        points of a scrambled Sobol sequence generated on the device (seeded, so every rank sees
+        the same sequence and owns one contiguous shard).  Each refinement round re-centres a box
+        ``shrink`` times smaller on the incumbent and keeps it if it improves — a batched
+        stand-in for DE's final polish.  Returns (x_best (d,), value).
         """
         lower = np.asarray(lower, np.float64)
         upper = np.asarray(upper, np.float64)
@@ -111,23 +139,15 @@ class AcquisitionEngine:
         lo, hi = lower, upper
         for rnd in range(refine_rounds + 1):
             start, count = shard_range(n_candidates, W, rank)
-            sob = qmc.Sobol(d=d, scramble=True, seed=seed + rnd)
-            if start:
-                sob.fast_forward(start)
-            U = sob.random(max(count, 1))[:count]
-            Xc = self._dev(lo + U * (hi - lo)) if count else torch.empty((0, d), dtype=torch.float64,
-                                                                           device=self.device)
-            vals = acq_fn(Xc) if count else torch.empty(0, dtype=torch.float64, device=self.device)
-            pair = self.ctx.argmax_dev(vals, offset=start) if count else torch.tensor([-np.inf, -1.0],
-                                                                                     dtype=torch.float64,
-                                                                                     device=self.device)
+            self.ctx.set_sobol(d, lo, hi, seed=seed + rnd)
+            if acq_fn is None:
+                pair = self.ctx.eval_argmax_sobol(start, count)
+            else:
+                vals = acq_fn(self.ctx.sobol(start, count))
+                pair = self.ctx.argmax_dev(vals, offset=start)
             g = global_argmax(pair).cpu().numpy()
             if g[1] >= 0 and g[0] > best_v:
-                idx = int(g[1])
-                s2 = qmc.Sobol(d=d, scramble=True, seed=seed + rnd)
-                if idx:
-                    s2.fast_forward(idx)
-                best_x = lo + s2.random(1)[0] * (hi - lo)
+                best_x = self.ctx.sobol(int(g[1]), 1).cpu().numpy()[0]   # the winner, regenerated
                 best_v = float(g[0])
             if best_x is None:
                 break
@@ -135,7 +155,8 @@ class AcquisitionEngine:
             lo = np.maximum(lower, best_x - half)
             hi = np.minimum(upper, best_x + half)
         if best_x is None:   # every candidate was NaN/−inf: fall back to the first Sobol point
-            best_x = lower + qmc.Sobol(d=d, scramble=True, seed=seed).random(1)[0] * (upper - lower)
+            self.ctx.set_sobol(d, lower, upper, seed=seed)
+            best_x = self.ctx.sobol(0, 1).cpu().numpy()[0]
         return best_x, best_v
 
 

@@ -68,6 +68,7 @@ class BODriver:
         return model
 
     def _maximise(self, models, acq_fn):
+        """acq_fn None: the plan set on the engine (fused chain); else a batched callable."""
         eng = engine_for(models, self.device)
         seed = (self.seed if self.seed is not None else np.random.randint(0, 2 ** 31 - 1)) + 7919 * self._iteration
         self._iteration += 1

@@ -37,12 +37,8 @@ class EMO(BODriver):
     def get_proposed(self, function, P, cells, models):
         """emo.py:231-241: maximise HV-PoI with the device arg-max."""
         from ..acquisition import engine_for
-        eng = engine_for(models, self.device)
-        c = np.ascontiguousarray(cells, dtype=np.float64)
-
-        def acq(Xc):
-            return eng.hvpoi(Xc, c)
-        x, v = self._maximise(models, acq)
+        engine_for(models, self.device).plan_hvpoi(cells)
+        x, v = self._maximise(models, None)
         return x, -v
 
     def solve(self, budget=100, n_init_samples=5):

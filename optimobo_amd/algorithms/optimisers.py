@@ -26,37 +26,20 @@ class MultiSurrogateOptimiser(BODriver):
         from ..acquisition import engine_for
         eng = engine_for(models, self.device)
         if (function == "EHVI_3D" or self.n_obj == 3) and self.mode == "textbook":
-            coords, _, boxes = pareto.box_decomposition(pf, max_point)
-
-            def acq(Xc):                      # exact EHVI in place of the MC estimate
-                mu, var = eng.posterior(Xc)
-                return eng.ctx.ehvi_boxes(mu, var, coords, boxes)
+            eng.plan_ehvi_exact(max_point, pf)          # exact EHVI in place of the MC estimate
         elif function == "EHVI_3D" or self.n_obj == 3:
-            hv = pareto.hypervolume(pf, max_point)
-
-            def acq(Xc):
-                mu, var = eng.posterior(Xc)
-                vals, _ = eng.ctx.ehvi3d_mc(mu, var, cache, np.asarray(max_point, np.float64), hv)
-                return vals
+            eng.plan_ehvi3d(max_point, pf, cache)
         else:
-            s00, s01 = pareto.cache_stats(cache)
-            stripes = pareto.stripes_2d(pf)
-            r = np.asarray(max_point, np.float64)
-
-            def acq(Xc):
-                mu, var = eng.posterior(Xc)
-                return eng.ctx.ehvi2d(mu, var, stripes, r, s00, s01, mode=self.mode)
-        x, v = self._maximise(models, acq)
+            eng.plan_ehvi(max_point, pf, cache, mode=self.mode)
+        x, v = self._maximise(models, None)
         return x, -v
 
     def _get_proposed_scalarisation(self, function, models, min_val, scalar_func, ref_dir, cache):
         """optimisers.py:62-88 on the device: returns (x, −value, ref_dir)."""
         from ..acquisition import engine_for
         eng = engine_for(models, self.device)
-
-        def acq(Xc):
-            return eng.expected_decomposition(Xc, ref_dir, scalar_func, min_val, cache)
-        x, v = self._maximise(models, acq)
+        eng.plan_expected_decomposition(ref_dir, scalar_func, min_val, cache)
+        x, v = self._maximise(models, None)
         return x, -v, ref_dir
 
     def solve(self, budget=100, n_init_samples=5, sample_exponent=5, acquisition_func=None):
@@ -97,10 +80,8 @@ class MonoSurrogateOptimiser(BODriver):
     def _get_proposed(self, function, models, current_best):
         from ..acquisition import engine_for
         eng = engine_for([models], self.device)
-
-        def acq(Xc):
-            return eng.ei(Xc, current_best, 0.0)
-        x, v = self._maximise([models], acq)
+        eng.plan_ei(current_best, 0.0)
+        x, v = self._maximise([models], None)
         return x, -v
 
     def _normalize_data(self, data):

@@ -22,10 +22,8 @@ class ParEGO(BODriver):
     def _get_proposed(self, model, current_best):
         from ..acquisition import engine_for
         eng = engine_for([model], self.device)
-
-        def acq(Xc):
-            return eng.ei(Xc, current_best, 1e-6)
-        return self._maximise([model], acq)
+        eng.plan_ei(current_best, 1e-6)
+        return self._maximise([model], None)
 
     def solve(self, aggregation_func, budget=100, n_init_samples=5):
         problem = self.test_problem

@@ -7,6 +7,7 @@
 
 #include <new>
 #include <string>
+#include <vector>
 
 #include "omb_internal.h"
 
@@ -21,6 +22,20 @@ struct ObjState {
   GPDev dev{};
 };
 
+// Acquisition of the fused chain (omb_plan_*), with its geometry resident in ctx->geo.
+enum PlanKind { PLAN_NONE = 0, PLAN_EHVI2D, PLAN_EHVI3D_MC, PLAN_EHVI_BOXES, PLAN_HVPOI, PLAN_EXPDEC, PLAN_EI };
+
+struct Plan {
+  int kind = PLAN_NONE;
+  int k = 0;                    // objectives the acquisition reads (posterior of 0..k-1)
+  int P = 0, M = 0, C = 0, B = 0, mode = 0;
+  double r[OMB_MAX_OBJ] = {};
+  double s00 = 0, s01 = 0, hv = 0, best = 0, var_eps = 0;
+  ScalParams sp{};
+  const double* geo = nullptr;  // pf / cache / coords / cells on the device
+  const uint16_t* boxes = nullptr;
+};
+
 struct omb_ctx {
   int device = 0;
   hipStream_t own_stream = nullptr;
@@ -30,6 +45,20 @@ struct omb_ctx {
   double* partials = nullptr;  // argmax pass-1 output
   double* result_dev = nullptr;
   double* result_host = nullptr;  // pinned
+  // fused chain
+  Plan plan;
+  void* geo = nullptr;    // device: plan geometry
+  size_t geo_cap = 0;
+  void* stage = nullptr;  // pinned host staging of uploads
+  size_t stage_cap = 0;
+  void* work = nullptr;   // device: mu | var | vals | raised | X of the fused chain
+  size_t work_cap = 0;
+  void* sob = nullptr;    // device: packed Sobol state (fixed capacity)
+  int sob_d = 0, sob_bits = 0;
+  // timing of the fused chain: 5 events per chain (level 2) or 2 around the posterior (level 1)
+  int timing = 0;
+  std::vector<hipEvent_t> ev;
+  size_t ev_used = 0;
 };
 
 namespace {
@@ -99,6 +128,206 @@ int check_moments(omb_ctx* ctx, const double* mu, const double* var, int64_t ld,
   return OMB_OK;
 }
 
+// ---- geometry validation shared by the per-kernel entry points and the plans
+int check_ehvi2d(omb_ctx* ctx, int P, const double* r, int mode) {
+  // stripes y1[0..P], y2[1..P] are staged in ≤ 64 KiB of LDS
+  if (P < 1 || P > kMaxStripes) return fail(ctx, OMB_EUNSUP, "Pareto front size P=%d outside [1, %d]", P, kMaxStripes);
+  if (!r) return fail(ctx, OMB_EINVAL, "null reference point");
+  if (mode != OMB_EHVI_REFERENCE && mode != OMB_EHVI_TEXTBOOK && mode != OMB_EHVI_SIGMA)
+    return fail(ctx, OMB_EINVAL, "unknown EHVI mode %d", mode);
+  return OMB_OK;
+}
+
+int check_ehvi3d(omb_ctx* ctx, int M, const double* r) {
+  if (M < 1 || 3 * M > kMaxLdsDoubles) return fail(ctx, OMB_EUNSUP, "cache size M=%d outside [1, %d]", M, kMaxLdsDoubles / 3);
+  if (!r) return fail(ctx, OMB_EINVAL, "null reference point");
+  return OMB_OK;
+}
+
+int check_boxes(omb_ctx* ctx, int k, int C, int B) {
+  if (k != 2 && k != 3) return fail(ctx, OMB_EUNSUP, "exact EHVI needs k = 2 or 3 objectives (k=%d)", k);
+  // grid + 4 per-wave Φ/φ tables must fit the 64 KiB of dynamic LDS
+  if (C < 2 || (size_t)k * C * 9 > (size_t)kMaxLdsDoubles)
+    return fail(ctx, OMB_EUNSUP, "grid size C=%d outside [2, %d] for k=%d", C, kMaxLdsDoubles / (9 * k), k);
+  if (B < 1) return fail(ctx, OMB_EINVAL, "empty box list");
+  return OMB_OK;
+}
+
+int check_hvpoi(omb_ctx* ctx, int C) {
+  if (C < 1 || 4 * C > kMaxLdsDoubles) return fail(ctx, OMB_EUNSUP, "cell count C=%d outside [1, %d]", C, kMaxLdsDoubles / 4);
+  return OMB_OK;
+}
+
+// Validates an expected_decomposition request and fills its ScalParams.
+int build_scal(omb_ctx* ctx, int k, int M, int scal_id, const double* params_host, const double* weights_host,
+               const double* ideal_host, const double* max_host, double agg_min, ScalParams* out) {
+  if (k < 1 || k > OMB_MAX_OBJ) return fail(ctx, OMB_EINVAL, "k=%d outside [1, %d]", k, OMB_MAX_OBJ);
+  if (M < 1 || k * M > kMaxLdsDoubles)
+    return fail(ctx, OMB_EUNSUP, "cache size M=%d x k=%d exceeds %d doubles of LDS", M, k, kMaxLdsDoubles);
+  if (scal_id < OMB_SCAL_WS || scal_id > OMB_SCAL_APD) return fail(ctx, OMB_EINVAL, "unknown scalarisation %d", scal_id);
+  if (!weights_host || !ideal_host || !max_host) return fail(ctx, OMB_EINVAL, "null weights/ideal/max");
+  ScalParams& sp = *out;
+  memset(&sp, 0, sizeof(sp));
+  sp.id = scal_id;
+  sp.k = k;
+  sp.agg_min = agg_min;
+  double wq = 0.0, rsum = 0.0;
+  for (int i = 0; i < k; ++i) {
+    sp.w[i] = weights_host[i];
+    sp.ideal[i] = ideal_host[i];
+    sp.range[i] = max_host[i] - ideal_host[i];
+    wq += sp.w[i] * sp.w[i];
+    rsum += sp.range[i];
+  }
+  sp.wnorm = sqrt(wq);
+  const int np = (scal_id == OMB_SCAL_QPBI || scal_id == OMB_SCAL_APD) ? 3
+                 : (scal_id == OMB_SCAL_WS || scal_id == OMB_SCAL_TCH || scal_id == OMB_SCAL_WPR) ? 0 : 1;
+  if (np > 0 && !params_host) return fail(ctx, OMB_EINVAL, "scalarisation %d needs %d parameter(s)", scal_id, np);
+  for (int i = 0; i < np; ++i) sp.p[i] = params_host[i];
+  if (scal_id == OMB_SCAL_APD && sp.wnorm == 0.0) {
+    // scalarisations.py:392-393 substitutes 1e-5 weights (the reference then fails for k > 1).
+    for (int i = 0; i < k; ++i) sp.w[i] = 1e-5;
+    sp.wnorm = sqrt(k * 1e-10);
+  }
+  if (scal_id == OMB_SCAL_QPBI) {
+    // scalarisations.py:347: alpha * (1/H * 1/k * Σ(max − ideal))
+    sp.d_star = sp.p[1] * ((1.0 / sp.p[2]) * (1.0 / (double)k) * rsum);
+  }
+  return OMB_OK;
+}
+
+// ---- ctx-owned buffers
+int grow_dev(omb_ctx* ctx, void** buf, size_t* cap, size_t bytes, const char* what) {
+  if (bytes <= *cap) return OMB_OK;
+  OMB_HIP(ctx, hipStreamSynchronize(ctx->stream));  // queued kernels may still read the old buffer
+  if (*buf) (void)hipFree(*buf);
+  *buf = nullptr;
+  *cap = 0;
+  if (hipMalloc(buf, bytes) != hipSuccess) return fail(ctx, OMB_ENOMEM, "hipMalloc(%zu) for %s", bytes, what);
+  *cap = bytes;
+  return OMB_OK;
+}
+
+// Pinned staging for a host→device upload of `bytes`; the previous upload is complete on return.
+int stage_begin(omb_ctx* ctx, size_t bytes, void** host) {
+  OMB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (bytes > ctx->stage_cap) {
+    if (ctx->stage) (void)hipHostFree(ctx->stage);
+    ctx->stage = nullptr;
+    ctx->stage_cap = 0;
+    if (hipHostMalloc(&ctx->stage, bytes, hipHostMallocDefault) != hipSuccess)
+      return fail(ctx, OMB_ENOMEM, "hipHostMalloc(%zu) for staging", bytes);
+    ctx->stage_cap = bytes;
+  }
+  *host = ctx->stage;
+  return OMB_OK;
+}
+
+// Uploads the staged bytes as the plan geometry.
+int stage_to_geo(omb_ctx* ctx, size_t bytes) {
+  int rc = grow_dev(ctx, &ctx->geo, &ctx->geo_cap, bytes, "plan geometry");
+  if (rc) return rc;
+  OMB_HIP(ctx, hipMemcpyAsync(ctx->geo, ctx->stage, bytes, hipMemcpyHostToDevice, ctx->stream));
+  return OMB_OK;
+}
+
+int plan_begin(omb_ctx* ctx, size_t bytes, void** host) {
+  int rc = enter(ctx);
+  if (rc) return rc;
+  ctx->plan = Plan();  // an invalid request leaves no plan behind
+  return bytes ? stage_begin(ctx, bytes, host) : OMB_OK;
+}
+
+// The fused chain: [Sobol →] posterior(0..k-1) → planned acquisition → [arg-max].
+int run_chain(omb_ctx* ctx, const double* Xc, bool sobol, int64_t start, int64_t N, int64_t offset, double* vals_out,
+              double* result_dev) {
+  int rc = enter(ctx);
+  if (rc) return rc;
+  const Plan& pl = ctx->plan;
+  if (pl.kind == PLAN_NONE) return fail(ctx, OMB_ESTATE, "no acquisition plan (call an omb_plan_* function)");
+  if (N < 0) return fail(ctx, OMB_EINVAL, "N=%lld < 0", (long long)N);
+  GPArgs args;
+  int max_R = 0;
+  if ((rc = gather_gp(ctx, pl.k, &args, &max_R))) return rc;
+  if (sobol) {
+    if (ctx->sob_d == 0) return fail(ctx, OMB_ESTATE, "no Sobol state (call omb_set_sobol)");
+    if (ctx->sob_d != args.d) return fail(ctx, OMB_EINVAL, "Sobol dimension %d != n_var %d", ctx->sob_d, args.d);
+    if (start < 0 || start + N > (int64_t)(1ull << ctx->sob_bits))
+      return fail(ctx, OMB_EINVAL, "Sobol indices [%lld, %lld) outside [0, 2^%d)", (long long)start,
+                  (long long)(start + N), ctx->sob_bits);
+  } else if (N > 0 && !Xc) {
+    return fail(ctx, OMB_EINVAL, "null candidate pointer");
+  }
+  if ((N + 31) / 32 > 0x7fffffffLL) return fail(ctx, OMB_EUNSUP, "N=%lld too large", (long long)N);
+  const int k = pl.k;
+  const size_t nd = (size_t)N;
+  const size_t doubles = 2 * (size_t)k * nd + nd + (nd + 1) / 2 + (sobol ? nd * args.d : 0);
+  if ((rc = grow_dev(ctx, &ctx->work, &ctx->work_cap, (doubles ? doubles : 1) * sizeof(double), "chain workspace")))
+    return rc;
+  double* mu = static_cast<double*>(ctx->work);
+  double* var = mu + (size_t)k * nd;
+  double* vals = vals_out ? vals_out : var + (size_t)k * nd;
+  int32_t* raised = reinterpret_cast<int32_t*>(var + (size_t)k * nd + nd);
+  double* Xs = var + (size_t)k * nd + nd + (nd + 1) / 2;
+
+  hipEvent_t* ev = nullptr;
+  if (ctx->timing) {
+    if (ctx->ev_used + 5 > ctx->ev.size() && ctx->ev.size() < 5 * 4096) {
+      for (int i = 0; i < 5 * 64; ++i) {
+        hipEvent_t e;
+        OMB_HIP(ctx, hipEventCreate(&e));
+        ctx->ev.push_back(e);
+      }
+    }
+    if (ctx->ev_used + 5 <= ctx->ev.size()) {
+      ev = ctx->ev.data() + ctx->ev_used;
+      ctx->ev_used += 5;
+    }
+  }
+  // Each event record costs a few µs of GPU time, so level 1 records only around the posterior.
+  const int level = ctx->timing;
+  auto mark = [&](int i) -> hipError_t {
+    if (!ev) return hipSuccess;
+    if (level == 1 && i != 1 && i != 2) return hipSuccess;
+    return hipEventRecord(ev[i], ctx->stream);
+  };
+  hipError_t e = mark(0);
+  if (e == hipSuccess && sobol && N > 0) e = launch_sobol(ctx->stream, ctx->sob, ctx->sob_d, ctx->sob_bits, start, N, Xs);
+  if (sobol) Xc = Xs;
+  if (e == hipSuccess) e = mark(1);
+  if (e == hipSuccess && N > 0) e = launch_posterior(ctx->stream, args, k, max_R, Xc, N, mu, var);
+  if (e == hipSuccess) e = mark(2);
+  if (e == hipSuccess && N > 0) {
+    switch (pl.kind) {
+      case PLAN_EHVI2D:
+        e = launch_ehvi2d(ctx->stream, mu, var, N, N, pl.geo, pl.P, pl.r[0], pl.r[1], pl.s00, pl.s01, pl.mode, vals);
+        break;
+      case PLAN_EHVI3D_MC:
+        e = launch_ehvi3d_mc(ctx->stream, mu, var, N, N, pl.geo, pl.M, pl.r, pl.hv, vals, raised);
+        break;
+      case PLAN_EHVI_BOXES:
+        e = launch_ehvi_boxes(ctx->stream, k, mu, var, N, N, pl.geo, pl.C, pl.boxes, pl.B, vals);
+        break;
+      case PLAN_HVPOI:
+        e = launch_hvpoi(ctx->stream, mu, var, N, N, pl.geo, pl.C, vals);
+        break;
+      case PLAN_EXPDEC:
+        e = launch_expdec(ctx->stream, pl.sp, mu, var, N, N, pl.geo, pl.M, vals);
+        break;
+      case PLAN_EI:
+        e = launch_ei(ctx->stream, mu, var, N, pl.best, pl.var_eps, vals);
+        break;
+      default:
+        return fail(ctx, OMB_ESTATE, "corrupt plan");
+    }
+  }
+  if (e == hipSuccess) e = mark(3);
+  if (e == hipSuccess && result_dev) e = launch_argmax(ctx->stream, vals, N, offset, ctx->partials, result_dev);
+  if (e == hipSuccess) e = mark(4);
+  if (e != hipSuccess) return hip_fail(ctx, e, "fused chain");
+  return OMB_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -117,7 +346,8 @@ int omb_create(int device, omb_ctx** out) {
       hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(&ctx->partials, sizeof(double) * 2 * kArgmaxMaxBlocks) != hipSuccess ||
       hipMalloc(&ctx->result_dev, sizeof(double) * 2) != hipSuccess ||
-      hipHostMalloc(&ctx->result_host, sizeof(double) * 2, hipHostMallocDefault) != hipSuccess) {
+      hipHostMalloc(&ctx->result_host, sizeof(double) * 2, hipHostMallocDefault) != hipSuccess ||
+      hipMalloc(&ctx->sob, sobol_state_bytes(OMB_MAX_DIM, 32)) != hipSuccess) {
     omb_destroy(ctx);
     return OMB_ENOMEM;
   }
@@ -135,6 +365,11 @@ int omb_destroy(omb_ctx* ctx) {
   if (ctx->partials) (void)hipFree(ctx->partials);
   if (ctx->result_dev) (void)hipFree(ctx->result_dev);
   if (ctx->result_host) (void)hipHostFree(ctx->result_host);
+  if (ctx->geo) (void)hipFree(ctx->geo);
+  if (ctx->stage) (void)hipHostFree(ctx->stage);
+  if (ctx->work) (void)hipFree(ctx->work);
+  if (ctx->sob) (void)hipFree(ctx->sob);
+  for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;
   return OMB_OK;
@@ -254,10 +489,8 @@ int omb_ehvi2d(omb_ctx* ctx, const double* mu_dev, const double* var_dev, int64_
   int rc = enter(ctx);
   if (rc) return rc;
   if ((rc = check_moments(ctx, mu_dev, var_dev, ld, N, 2, out_dev))) return rc;
-  // stripes y1[0..P], y2[1..P] are staged in ≤ 64 KiB of LDS
-  if (!pf_sorted_dev || P < 1 || P > kMaxStripes) return fail(ctx, OMB_EUNSUP, "Pareto front size P=%d outside [1, %d]", P, kMaxStripes);
-  if (!r_host) return fail(ctx, OMB_EINVAL, "null reference point");
-  if (mode != OMB_EHVI_REFERENCE && mode != OMB_EHVI_TEXTBOOK && mode != OMB_EHVI_SIGMA) return fail(ctx, OMB_EINVAL, "unknown EHVI mode %d", mode);
+  if (!pf_sorted_dev) return fail(ctx, OMB_EINVAL, "null Pareto front");
+  if ((rc = check_ehvi2d(ctx, P, r_host, mode))) return rc;
   if (N == 0) return OMB_OK;
   hipError_t e = launch_ehvi2d(ctx->stream, mu_dev, var_dev, ld, N, pf_sorted_dev, P, r_host[0], r_host[1], s00, s01,
                                mode, out_dev);
@@ -271,9 +504,8 @@ int omb_ehvi3d_mc(omb_ctx* ctx, const double* mu_dev, const double* var_dev, int
   int rc = enter(ctx);
   if (rc) return rc;
   if ((rc = check_moments(ctx, mu_dev, var_dev, ld, N, 3, out_dev))) return rc;
-  if (!cache_dev || M < 1 || 3 * M > kMaxLdsDoubles)
-    return fail(ctx, OMB_EUNSUP, "cache size M=%d outside [1, %d]", M, kMaxLdsDoubles / 3);
-  if (!r_host) return fail(ctx, OMB_EINVAL, "null reference point");
+  if (!cache_dev) return fail(ctx, OMB_EINVAL, "null cache");
+  if ((rc = check_ehvi3d(ctx, M, r_host))) return rc;
   if (N == 0) return OMB_OK;
   hipError_t e = launch_ehvi3d_mc(ctx->stream, mu_dev, var_dev, ld, N, cache_dev, M, r_host, hv_pf, out_dev, raised_dev);
   if (e != hipSuccess) return hip_fail(ctx, e, "ehvi3d_mc");
@@ -284,12 +516,9 @@ int omb_ehvi_boxes(omb_ctx* ctx, int k, const double* mu_dev, const double* var_
                    const double* coords_dev, int C, const uint16_t* boxes_dev, int B, double* out_dev) {
   int rc = enter(ctx);
   if (rc) return rc;
-  if (k != 2 && k != 3) return fail(ctx, OMB_EUNSUP, "exact EHVI needs k = 2 or 3 objectives (k=%d)", k);
+  if ((rc = check_boxes(ctx, k, C, B))) return rc;
   if ((rc = check_moments(ctx, mu_dev, var_dev, ld, N, k, out_dev))) return rc;
-  // grid + 4 per-wave Φ/φ tables must fit the 64 KiB of dynamic LDS
-  if (!coords_dev || C < 2 || (size_t)k * C * 9 > (size_t)kMaxLdsDoubles)
-    return fail(ctx, OMB_EUNSUP, "grid size C=%d outside [2, %d] for k=%d", C, kMaxLdsDoubles / (9 * k), k);
-  if (!boxes_dev || B < 1) return fail(ctx, OMB_EINVAL, "empty box list");
+  if (!coords_dev || !boxes_dev) return fail(ctx, OMB_EINVAL, "null grid/box list");
   if (N == 0) return OMB_OK;
   hipError_t e = launch_ehvi_boxes(ctx->stream, k, mu_dev, var_dev, ld, N, coords_dev, C, boxes_dev, B, out_dev);
   if (e != hipSuccess) return hip_fail(ctx, e, "ehvi_boxes");
@@ -301,8 +530,8 @@ int omb_hvpoi(omb_ctx* ctx, const double* mu_dev, const double* var_dev, int64_t
   int rc = enter(ctx);
   if (rc) return rc;
   if ((rc = check_moments(ctx, mu_dev, var_dev, ld, N, 2, out_dev))) return rc;
-  if (!cells_dev || C < 1 || 4 * C > kMaxLdsDoubles)
-    return fail(ctx, OMB_EUNSUP, "cell count C=%d outside [1, %d]", C, kMaxLdsDoubles / 4);
+  if (!cells_dev) return fail(ctx, OMB_EINVAL, "null cells");
+  if ((rc = check_hvpoi(ctx, C))) return rc;
   if (N == 0) return OMB_OK;
   hipError_t e = launch_hvpoi(ctx->stream, mu_dev, var_dev, ld, N, cells_dev, C, out_dev);
   if (e != hipSuccess) return hip_fail(ctx, e, "hvpoi");
@@ -314,39 +543,10 @@ int omb_expdec(omb_ctx* ctx, int k, const double* mu_dev, const double* var_dev,
                const double* ideal_host, const double* max_host, double agg_min, double* out_dev) {
   int rc = enter(ctx);
   if (rc) return rc;
-  if (k < 1 || k > OMB_MAX_OBJ) return fail(ctx, OMB_EINVAL, "k=%d outside [1, %d]", k, OMB_MAX_OBJ);
-  if ((rc = check_moments(ctx, mu_dev, var_dev, ld, N, k, out_dev))) return rc;
-  if (!cache_dev || M < 1 || k * M > kMaxLdsDoubles)
-    return fail(ctx, OMB_EUNSUP, "cache size M=%d x k=%d exceeds %d doubles of LDS", M, k, kMaxLdsDoubles);
-  if (scal_id < OMB_SCAL_WS || scal_id > OMB_SCAL_APD) return fail(ctx, OMB_EINVAL, "unknown scalarisation %d", scal_id);
-  if (!weights_host || !ideal_host || !max_host) return fail(ctx, OMB_EINVAL, "null weights/ideal/max");
   ScalParams sp;
-  memset(&sp, 0, sizeof(sp));
-  sp.id = scal_id;
-  sp.k = k;
-  sp.agg_min = agg_min;
-  double wq = 0.0, rsum = 0.0;
-  for (int i = 0; i < k; ++i) {
-    sp.w[i] = weights_host[i];
-    sp.ideal[i] = ideal_host[i];
-    sp.range[i] = max_host[i] - ideal_host[i];
-    wq += sp.w[i] * sp.w[i];
-    rsum += sp.range[i];
-  }
-  sp.wnorm = sqrt(wq);
-  const int np = (scal_id == OMB_SCAL_QPBI || scal_id == OMB_SCAL_APD) ? 3
-                 : (scal_id == OMB_SCAL_WS || scal_id == OMB_SCAL_TCH || scal_id == OMB_SCAL_WPR) ? 0 : 1;
-  if (np > 0 && !params_host) return fail(ctx, OMB_EINVAL, "scalarisation %d needs %d parameter(s)", scal_id, np);
-  for (int i = 0; i < np; ++i) sp.p[i] = params_host[i];
-  if (scal_id == OMB_SCAL_APD && sp.wnorm == 0.0) {
-    // scalarisations.py:392-393 substitutes 1e-5 weights (the reference then fails for k > 1).
-    for (int i = 0; i < k; ++i) sp.w[i] = 1e-5;
-    sp.wnorm = sqrt(k * 1e-10);
-  }
-  if (scal_id == OMB_SCAL_QPBI) {
-    // scalarisations.py:347: alpha * (1/H * 1/k * Σ(max − ideal))
-    sp.d_star = sp.p[1] * ((1.0 / sp.p[2]) * (1.0 / (double)k) * rsum);
-  }
+  if ((rc = build_scal(ctx, k, M, scal_id, params_host, weights_host, ideal_host, max_host, agg_min, &sp))) return rc;
+  if ((rc = check_moments(ctx, mu_dev, var_dev, ld, N, k, out_dev))) return rc;
+  if (!cache_dev) return fail(ctx, OMB_EINVAL, "null cache");
   if (N == 0) return OMB_OK;
   hipError_t e = launch_expdec(ctx->stream, sp, mu_dev, var_dev, ld, N, cache_dev, M, out_dev);
   if (e != hipSuccess) return hip_fail(ctx, e, "expdec");
@@ -380,6 +580,216 @@ int omb_argmax(omb_ctx* ctx, const double* vals_dev, int64_t N, int64_t offset, 
   OMB_HIP(ctx, hipStreamSynchronize(ctx->stream));
   if (best_val) *best_val = ctx->result_host[0];
   if (best_idx) *best_idx = (int64_t)ctx->result_host[1];
+  return OMB_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// Fused chain: per-iteration plans, device Sobol' generation, one-call batch evaluation.
+
+int omb_plan_ehvi2d(omb_ctx* ctx, const double* pf_sorted_host, int P, const double* r_host, double s00, double s01,
+                    int mode) {
+  void* h = nullptr;
+  int rc = enter(ctx);
+  if (rc) return rc;
+  ctx->plan = Plan();
+  if ((rc = check_ehvi2d(ctx, P, r_host, mode))) return rc;
+  if (!pf_sorted_host) return fail(ctx, OMB_EINVAL, "null Pareto front");
+  const size_t bytes = sizeof(double) * 2 * (size_t)P;
+  if ((rc = plan_begin(ctx, bytes, &h))) return rc;
+  memcpy(h, pf_sorted_host, bytes);
+  if ((rc = stage_to_geo(ctx, bytes))) return rc;
+  Plan pl;
+  pl.kind = PLAN_EHVI2D;
+  pl.k = 2;
+  pl.P = P;
+  pl.mode = mode;
+  pl.r[0] = r_host[0];
+  pl.r[1] = r_host[1];
+  pl.s00 = s00;
+  pl.s01 = s01;
+  pl.geo = static_cast<const double*>(ctx->geo);
+  ctx->plan = pl;
+  return OMB_OK;
+}
+
+int omb_plan_ehvi3d_mc(omb_ctx* ctx, const double* cache_host, int M, const double* r_host, double hv_pf) {
+  void* h = nullptr;
+  int rc = enter(ctx);
+  if (rc) return rc;
+  ctx->plan = Plan();
+  if ((rc = check_ehvi3d(ctx, M, r_host))) return rc;
+  if (!cache_host) return fail(ctx, OMB_EINVAL, "null cache");
+  const size_t bytes = sizeof(double) * 3 * (size_t)M;
+  if ((rc = plan_begin(ctx, bytes, &h))) return rc;
+  memcpy(h, cache_host, bytes);
+  if ((rc = stage_to_geo(ctx, bytes))) return rc;
+  Plan pl;
+  pl.kind = PLAN_EHVI3D_MC;
+  pl.k = 3;
+  pl.M = M;
+  for (int j = 0; j < 3; ++j) pl.r[j] = r_host[j];
+  pl.hv = hv_pf;
+  pl.geo = static_cast<const double*>(ctx->geo);
+  ctx->plan = pl;
+  return OMB_OK;
+}
+
+int omb_plan_ehvi_boxes(omb_ctx* ctx, int k, const double* coords_host, int C, const uint16_t* boxes_host, int B) {
+  void* h = nullptr;
+  int rc = enter(ctx);
+  if (rc) return rc;
+  ctx->plan = Plan();
+  if ((rc = check_boxes(ctx, k, C, B))) return rc;
+  if (!coords_host || !boxes_host) return fail(ctx, OMB_EINVAL, "null grid/box list");
+  const size_t cbytes = sizeof(double) * (size_t)k * C;
+  const size_t bbytes = sizeof(uint16_t) * 2 * (size_t)k * B;
+  if ((rc = plan_begin(ctx, cbytes + bbytes, &h))) return rc;
+  memcpy(h, coords_host, cbytes);
+  memcpy(static_cast<char*>(h) + cbytes, boxes_host, bbytes);
+  if ((rc = stage_to_geo(ctx, cbytes + bbytes))) return rc;
+  Plan pl;
+  pl.kind = PLAN_EHVI_BOXES;
+  pl.k = k;
+  pl.C = C;
+  pl.B = B;
+  pl.geo = static_cast<const double*>(ctx->geo);
+  pl.boxes = reinterpret_cast<const uint16_t*>(static_cast<const char*>(ctx->geo) + cbytes);
+  ctx->plan = pl;
+  return OMB_OK;
+}
+
+int omb_plan_hvpoi(omb_ctx* ctx, const double* cells_host, int C) {
+  void* h = nullptr;
+  int rc = enter(ctx);
+  if (rc) return rc;
+  ctx->plan = Plan();
+  if ((rc = check_hvpoi(ctx, C))) return rc;
+  if (!cells_host) return fail(ctx, OMB_EINVAL, "null cells");
+  const size_t bytes = sizeof(double) * 4 * (size_t)C;
+  if ((rc = plan_begin(ctx, bytes, &h))) return rc;
+  memcpy(h, cells_host, bytes);
+  if ((rc = stage_to_geo(ctx, bytes))) return rc;
+  Plan pl;
+  pl.kind = PLAN_HVPOI;
+  pl.k = 2;
+  pl.C = C;
+  pl.geo = static_cast<const double*>(ctx->geo);
+  ctx->plan = pl;
+  return OMB_OK;
+}
+
+int omb_plan_expdec(omb_ctx* ctx, int k, const double* cache_host, int M, int scal_id, const double* params_host,
+                    const double* weights_host, const double* ideal_host, const double* max_host, double agg_min) {
+  void* h = nullptr;
+  int rc = enter(ctx);
+  if (rc) return rc;
+  ctx->plan = Plan();
+  ScalParams sp;
+  if ((rc = build_scal(ctx, k, M, scal_id, params_host, weights_host, ideal_host, max_host, agg_min, &sp))) return rc;
+  if (!cache_host) return fail(ctx, OMB_EINVAL, "null cache");
+  const size_t bytes = sizeof(double) * (size_t)k * M;
+  if ((rc = plan_begin(ctx, bytes, &h))) return rc;
+  memcpy(h, cache_host, bytes);
+  if ((rc = stage_to_geo(ctx, bytes))) return rc;
+  Plan pl;
+  pl.kind = PLAN_EXPDEC;
+  pl.k = k;
+  pl.M = M;
+  pl.sp = sp;
+  pl.geo = static_cast<const double*>(ctx->geo);
+  ctx->plan = pl;
+  return OMB_OK;
+}
+
+int omb_plan_ei(omb_ctx* ctx, double best, double var_eps) {
+  int rc = enter(ctx);
+  if (rc) return rc;
+  ctx->plan = Plan();
+  if (!(var_eps >= 0.0)) return fail(ctx, OMB_EINVAL, "var_eps=%g must be >= 0", var_eps);
+  Plan pl;
+  pl.kind = PLAN_EI;
+  pl.k = 1;
+  pl.best = best;
+  pl.var_eps = var_eps;
+  ctx->plan = pl;
+  return OMB_OK;
+}
+
+int omb_set_sobol(omb_ctx* ctx, int d, int bits, const uint32_t* sv_host, const uint32_t* shift_host,
+                  const double* lo_host, const double* hi_host) {
+  int rc = enter(ctx);
+  if (rc) return rc;
+  ctx->sob_d = 0;
+  if (d < 1 || d > OMB_MAX_DIM) return fail(ctx, OMB_EUNSUP, "Sobol dimension %d outside [1, %d]", d, OMB_MAX_DIM);
+  if (bits < 1 || bits > 32) return fail(ctx, OMB_EUNSUP, "Sobol bits=%d outside [1, 32]", bits);
+  if (!sv_host || !shift_host || !lo_host || !hi_host) return fail(ctx, OMB_EINVAL, "null Sobol state");
+  for (int j = 0; j < d; ++j)
+    if (!(hi_host[j] >= lo_host[j])) return fail(ctx, OMB_EINVAL, "box [%g, %g] of dimension %d is empty", lo_host[j], hi_host[j], j);
+  const size_t bytes = sobol_state_bytes(d, bits);
+  void* h = nullptr;
+  if ((rc = stage_begin(ctx, bytes, &h))) return rc;
+  sobol_pack_state(d, bits, sv_host, shift_host, lo_host, hi_host, h);
+  OMB_HIP(ctx, hipMemcpyAsync(ctx->sob, h, bytes, hipMemcpyHostToDevice, ctx->stream));
+  ctx->sob_d = d;
+  ctx->sob_bits = bits;
+  return OMB_OK;
+}
+
+int omb_sobol(omb_ctx* ctx, int64_t start, int64_t N, double* X_dev) {
+  int rc = enter(ctx);
+  if (rc) return rc;
+  if (ctx->sob_d == 0) return fail(ctx, OMB_ESTATE, "no Sobol state (call omb_set_sobol)");
+  if (N < 0 || (N > 0 && !X_dev)) return fail(ctx, OMB_EINVAL, "bad output arguments");
+  if (start < 0 || start + N > (int64_t)(1ull << ctx->sob_bits))
+    return fail(ctx, OMB_EINVAL, "Sobol indices [%lld, %lld) outside [0, 2^%d)", (long long)start, (long long)(start + N),
+                ctx->sob_bits);
+  hipError_t e = launch_sobol(ctx->stream, ctx->sob, ctx->sob_d, ctx->sob_bits, start, N, X_dev);
+  if (e != hipSuccess) return hip_fail(ctx, e, "sobol");
+  return OMB_OK;
+}
+
+int omb_eval(omb_ctx* ctx, const double* Xc_dev, int64_t N, double* vals_dev) {
+  if (ctx && N > 0 && !vals_dev) return fail(ctx, OMB_EINVAL, "null output");
+  return run_chain(ctx, Xc_dev, false, 0, N, 0, vals_dev, nullptr);
+}
+
+int omb_eval_argmax(omb_ctx* ctx, const double* Xc_dev, int64_t N, int64_t offset, double* result_dev) {
+  if (ctx && !result_dev) return fail(ctx, OMB_EINVAL, "null result");
+  return run_chain(ctx, Xc_dev, false, 0, N, offset, nullptr, result_dev);
+}
+
+int omb_eval_argmax_sobol(omb_ctx* ctx, int64_t start, int64_t N, double* result_dev) {
+  if (ctx && !result_dev) return fail(ctx, OMB_EINVAL, "null result");
+  return run_chain(ctx, nullptr, true, start, N, start, nullptr, result_dev);
+}
+
+int omb_timing(omb_ctx* ctx, int enable) {
+  int rc = enter(ctx);
+  if (rc) return rc;
+  OMB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (enable < 0 || enable > 2) return fail(ctx, OMB_EINVAL, "timing level %d outside [0, 2]", enable);
+  ctx->timing = enable;
+  ctx->ev_used = 0;
+  return OMB_OK;
+}
+
+int omb_timing_read(omb_ctx* ctx, double* stage_ms, int64_t* chains) {
+  int rc = enter(ctx);
+  if (rc) return rc;
+  if (!stage_ms) return fail(ctx, OMB_EINVAL, "null output");
+  OMB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  for (int s = 0; s < 4; ++s) stage_ms[s] = 0.0;
+  const size_t n = ctx->ev_used / 5;
+  for (size_t c = 0; c < n; ++c) {
+    for (int s = 0; s < 4; ++s) {
+      if (ctx->timing == 1 && s != 1) continue;
+      float ms = 0.0f;
+      OMB_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev[5 * c + s], ctx->ev[5 * c + s + 1]));
+      stage_ms[s] += ms;
+    }
+  }
+  if (chains) *chains = (int64_t)n;
+  ctx->ev_used = 0;
   return OMB_OK;
 }
 

@@ -83,6 +83,15 @@ constexpr int kArgmaxMaxBlocks = 1024;
 hipError_t launch_argmax(hipStream_t stream, const double* vals, int64_t N, int64_t offset, double* partials,
                          double* result);
 
+// Scrambled Sobol' generation (omb_sobol.hip).  The packed state holds the direction
+// numbers, shift and box of one engine; sobol_pack_state fills a host buffer of
+// sobol_state_bytes(d, bits) that is then copied to the device.
+size_t sobol_state_bytes(int d, int bits);
+void sobol_pack_state(int d, int bits, const uint32_t* sv, const uint32_t* shift, const double* lo,
+                      const double* hi, void* dst);
+hipError_t launch_sobol(hipStream_t stream, const void* state_dev, int d, int bits, int64_t start, int64_t N,
+                        double* X);
+
 // Packed-L^-1 size in doubles for R row tiles: Σ_{r<R} 4(r+1)·64 = 128·R·(R+1).
 inline int64_t packed_L_size(int R) { return 128ll * R * (R + 1); }
 

@@ -189,3 +189,86 @@ class AcqContext:
         self._check(self.lib.omb_argmax(self._h, _ptr(vals), vals.numel(), int(offset), ctypes.byref(v),
                                         ctypes.byref(i)), "omb_argmax")
         return v.value, i.value
+
+    # ------------------------------------------------------------------ fused chain (plans)
+    def _plan(self, fn, *args):
+        self._stream()
+        self._check(getattr(self.lib, fn)(self._h, *args), fn)
+
+    def plan_ehvi2d(self, pf_sorted, r, s00, s01, mode="reference"):
+        pf = np.ascontiguousarray(pf_sorted, dtype=np.float64).reshape(-1, 2)
+        m = {"reference": _lib.EHVI_REFERENCE, "textbook": _lib.EHVI_TEXTBOOK, "sigma": _lib.EHVI_SIGMA}[mode]
+        self._plan("omb_plan_ehvi2d", _lib.host_ptr(pf), pf.shape[0], _lib.darr(r), float(s00), float(s01), m)
+
+    def plan_ehvi3d_mc(self, cache, r, hv_pf):
+        c = np.ascontiguousarray(cache, dtype=np.float64).reshape(-1, 3)
+        self._plan("omb_plan_ehvi3d_mc", _lib.host_ptr(c), c.shape[0], _lib.darr(r), float(hv_pf))
+
+    def plan_ehvi_boxes(self, coords, boxes):
+        c = np.ascontiguousarray(coords, dtype=np.float64)
+        b = np.ascontiguousarray(boxes, dtype=np.uint16)
+        self._plan("omb_plan_ehvi_boxes", c.shape[0], _lib.host_ptr(c), c.shape[1], _lib.host_ptr(b), b.shape[0])
+
+    def plan_hvpoi(self, cells):
+        c = np.ascontiguousarray(cells, dtype=np.float64).reshape(-1, 2, 2)
+        self._plan("omb_plan_hvpoi", _lib.host_ptr(c), c.shape[0])
+
+    def plan_expdec(self, cache, scal_id, params, weights, ideal, max_point, agg_min):
+        c = np.ascontiguousarray(cache, dtype=np.float64)
+        self._plan("omb_plan_expdec", c.shape[1], _lib.host_ptr(c), c.shape[0], int(scal_id), _lib.darr(params),
+                   _lib.darr(weights), _lib.darr(ideal), _lib.darr(max_point), float(agg_min))
+
+    def plan_ei(self, best, var_eps=0.0):
+        self._plan("omb_plan_ei", float(best), float(var_eps))
+
+    def set_sobol(self, d, lo, hi, seed=None, scramble=True, state=None):
+        """Device Sobol' engine = scipy qmc.Sobol(d, scramble=scramble, seed=seed) over [lo, hi]."""
+        from .sobol import engine_state
+        sv, shift, bits = state if state is not None else engine_state(d, seed, scramble)
+        lo = np.broadcast_to(np.asarray(lo, np.float64), (d,))
+        hi = np.broadcast_to(np.asarray(hi, np.float64), (d,))
+        self._stream()
+        self._check(self.lib.omb_set_sobol(self._h, d, bits, _lib.host_ptr(sv), _lib.host_ptr(shift), _lib.darr(lo),
+                                           _lib.darr(hi)), "omb_set_sobol")
+        self.sobol_dim = d
+
+    def sobol(self, start, N, out=None):
+        out = out if out is not None else torch.empty((N, self.sobol_dim), dtype=torch.float64, device=self.device)
+        self._stream()
+        self._check(self.lib.omb_sobol(self._h, int(start), int(N), _ptr(out)), "omb_sobol")
+        return out
+
+    def eval(self, Xc, out=None):
+        Xc = _dev_f64(Xc, self.device)
+        N = Xc.shape[0]
+        out = out if out is not None else torch.empty(N, dtype=torch.float64, device=self.device)
+        self._stream()
+        self._check(self.lib.omb_eval(self._h, _ptr(Xc), N, _ptr(out)), "omb_eval")
+        return out
+
+    def eval_argmax(self, Xc, offset=0, out=None):
+        Xc = _dev_f64(Xc, self.device)
+        out = out if out is not None else torch.empty(2, dtype=torch.float64, device=self.device)
+        self._stream()
+        self._check(self.lib.omb_eval_argmax(self._h, _ptr(Xc), Xc.shape[0], int(offset), _ptr(out)),
+                    "omb_eval_argmax")
+        return out
+
+    def eval_argmax_sobol(self, start, N, out=None):
+        out = out if out is not None else torch.empty(2, dtype=torch.float64, device=self.device)
+        self._stream()
+        self._check(self.lib.omb_eval_argmax_sobol(self._h, int(start), int(N), _ptr(out)), "omb_eval_argmax_sobol")
+        return out
+
+    def timing(self, level=2):
+        """0 off, 1 posterior only, 2 every stage of the fused chain (see omb_timing)."""
+        self._stream()
+        self._check(self.lib.omb_timing(self._h, int(level)), "omb_timing")
+
+    def timing_read(self):
+        """{stage: summed ms} over the fused chains since the last read, and their count."""
+        ms = (ctypes.c_double * 4)()
+        n = ctypes.c_int64()
+        self._stream()
+        self._check(self.lib.omb_timing_read(self._h, ms, ctypes.byref(n)), "omb_timing_read")
+        return dict(zip(("sobol", "posterior", "acquisition", "argmax"), list(ms))), n.value

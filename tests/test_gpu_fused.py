@@ -1,0 +1,233 @@
+"""GPU: device Sobol' generation (bit-exact vs scipy), and the fused chain
+(omb_plan_* + omb_eval / omb_eval_argmax / omb_eval_argmax_sobol) against the per-kernel
+entry points (bit-exact: same kernels) and the oracle."""
+import numpy as np
+import pytest
+from scipy.stats import qmc
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from oracle import acquisition as oacq  # noqa: E402
+from oracle import gp as ogp  # noqa: E402
+from oracle import pareto as opar  # noqa: E402
+from oracle import scalarisations as osc  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from optimobo_amd.device import AcqContext
+    c = AcqContext(0)
+    yield c
+    c.close()
+
+
+def dev(x):
+    return torch.as_tensor(np.ascontiguousarray(x, dtype=np.float64), device="cuda:0")
+
+
+def host_points(d, seed, scramble, lo, hi, start, N):
+    s = qmc.Sobol(d=d, scramble=scramble, seed=seed)
+    if start:
+        s.fast_forward(start)
+    U = s.random(N)
+    return lo + U * (hi - lo)
+
+
+# ----------------------------------------------------------------------------- Sobol'
+@pytest.mark.parametrize("d,seed,scramble", [(1, 0, True), (2, 5, True), (6, 11, True), (30, 3, True),
+                                             (32, 9, True), (6, None, False)])
+def test_sobol_bit_exact_vs_scipy(ctx, d, seed, scramble):
+    rng = np.random.default_rng(d)
+    lo = rng.uniform(-3, 0, d)
+    hi = lo + rng.uniform(0.1, 5, d)
+    ctx.set_sobol(d, lo, hi, seed=seed, scramble=scramble)
+    for start, N in [(0, 1), (0, 4096), (1, 777), (123457, 1000), ((1 << 22) - 5, 5)]:
+        got = ctx.sobol(start, N).cpu().numpy()
+        want = host_points(d, seed, scramble, lo, hi, start, N)
+        assert np.array_equal(got, want), (start, N)
+
+
+def test_sobol_large_batch_properties(ctx):
+    """2^20 points: first 4096 bit-exact, all inside the box, balanced per dyadic interval."""
+    d = 6
+    lo, hi = np.zeros(d), np.ones(d)
+    ctx.set_sobol(d, lo, hi, seed=1)
+    X = ctx.sobol(0, 1 << 20)
+    assert np.array_equal(X[:4096].cpu().numpy(), host_points(d, 1, True, lo, hi, 0, 4096))
+    assert bool(((X >= 0) & (X < 1)).all())
+    counts = torch.histc(X[:, 0], bins=1024, min=0, max=1)
+    assert int(counts.min()) == int(counts.max()) == 1024      # (0, m, s)-net balance
+
+
+def test_sobol_errors(ctx):
+    from optimobo_amd import _lib
+    ctx.set_sobol(2, [0, 0], [1, 1], seed=0)
+    with pytest.raises(_lib.OMBError) as e:
+        ctx.sobol((1 << 30) - 2, 4)
+    assert e.value.code == _lib.OMB_EINVAL
+    with pytest.raises(_lib.OMBError) as e:
+        ctx.set_sobol(2, [0, 0], [1, -1], seed=0)
+    assert e.value.code == _lib.OMB_EINVAL
+    with pytest.raises(_lib.OMBError) as e:
+        ctx.sobol(0, 4)                          # the failed set cleared the state
+    assert e.value.code == _lib.OMB_ESTATE
+
+
+# ----------------------------------------------------------------------------- fused chain
+def _zdt(X):
+    f1 = X[:, 0]
+    g = 1 + 9.0 / (X.shape[1] - 1) * X[:, 1:].sum(1)
+    return np.column_stack([f1, g * (1 - np.sqrt(f1 / g)), (1 + X[:, 1]) * (1.2 - f1)])
+
+
+@pytest.fixture(scope="module")
+def gp3(ctx):
+    from optimobo_amd.gp import GPState
+    rng = np.random.default_rng(7)
+    X = rng.uniform(0, 1, (70, 4))
+    Y = _zdt(X)
+    ls = np.array([0.3, 0.7, 1.2, 0.9])
+    for o in range(3):
+        ctx.set_gp_state(o, GPState(X, Y[:, o], ls, float(np.var(Y[:, o]))))
+    Xc = rng.uniform(0, 1, (3000, 4))
+    mu, var = [], []
+    for o in range(3):
+        m, v = ogp.ExactGP(X, Y[:, o], ls, float(np.var(Y[:, o]))).predict(Xc)
+        mu.append(m[:, 0])
+        var.append(v[:, 0])
+    return Y, Xc, np.array(mu), np.array(var)
+
+
+def _plans(ctx, Y):
+    """(name, k, set_plan(), separate(mu, var) -> vals tensor, oracle(mu, var) -> vals)."""
+    rng = np.random.default_rng(0)
+    pf2 = opar.calc_pf(Y[:, :2])
+    r2 = Y[:, :2].max(0) + 0.1
+    cache2 = rng.standard_normal((32, 2))
+    s00, s01 = oacq.cache_stats(cache2)
+    from optimobo_amd import pareto
+    stripes = pareto.stripes_2d(pf2)
+    pf3 = opar.calc_pf(Y)
+    r3 = Y.max(0) + 0.2
+    cache3 = rng.standard_normal((32, 3))
+    hv3 = opar.hypervolume(pf3, r3)
+    coords, _, boxes = pareto.box_decomposition(pf3, r3)
+    lo3, hi3 = opar.nondominated_boxes(pf3, r3)
+    cells = opar.decompose_into_cells(pf2, Y[:, :2].min(0), Y[:, :2].max(0))
+    tch = osc.Tchebicheff(Y.min(0), Y.max(0))
+    w3 = np.array([0.2, 0.5, 0.3])
+    out = []
+    for mode in ("reference", "textbook", "sigma"):
+        out.append((f"ehvi2d-{mode}", 2, lambda m=mode: ctx.plan_ehvi2d(stripes, r2, s00, s01, mode=m),
+                    lambda mu, var, m=mode: ctx.ehvi2d(mu, var, stripes, r2, s00, s01, mode=m),
+                    None if mode == "sigma" else
+                    (lambda mu, var, m=mode: oacq.ehvi2d(mu[:2], var[:2], pf2, r2, cache2, mode=m))))
+    out.append(("ehvi3d-mc", 3, lambda: ctx.plan_ehvi3d_mc(cache3, r3, hv3),
+                lambda mu, var: ctx.ehvi3d_mc(mu, var, cache3, r3, hv3)[0],
+                lambda mu, var: np.where(oacq.ehvi3d_reference(mu, var, hv3, r3, cache3)[1], np.nan,
+                                         oacq.ehvi3d_reference(mu, var, hv3, r3, cache3)[0])))
+    out.append(("boxes3", 3, lambda: ctx.plan_ehvi_boxes(coords, boxes),
+                lambda mu, var: ctx.ehvi_boxes(mu, var, coords, boxes),
+                lambda mu, var: oacq.ehvi_exact_boxes(mu, var, lo3, hi3)))
+    out.append(("hvpoi", 2, lambda: ctx.plan_hvpoi(cells), lambda mu, var: ctx.hvpoi(mu, var, cells),
+                lambda mu, var: oacq.hvpoi(mu[:2], var[:2], cells)))
+    out.append(("expdec-tch", 3, lambda: ctx.plan_expdec(cache3, 1, [], w3, Y.min(0), Y.max(0), 0.4),
+                lambda mu, var: ctx.expdec(mu, var, cache3, 1, [], w3, Y.min(0), Y.max(0), 0.4),
+                lambda mu, var: oacq.expected_decomposition(mu, var, cache3, tch, w3, 0.4)))
+    out.append(("ei", 1, lambda: ctx.plan_ei(0.3, 1e-6), lambda mu, var: ctx.ei(mu[0], var[0], 0.3, 1e-6),
+                lambda mu, var: oacq.ei(mu[0], var[0], 0.3, 1e-6)))
+    return out
+
+
+def test_fused_chain_matches_kernels_and_oracle(ctx, gp3):
+    Y, Xc, mu_o, var_o = gp3
+    Xd = dev(Xc)
+    for name, k, plan, separate, oracle in _plans(ctx, Y):
+        plan()
+        fused = ctx.eval(Xd).cpu().numpy()
+        mu, var = ctx.posterior(Xd, k)
+        sep = separate(mu.contiguous(), var.contiguous()).cpu().numpy()
+        np.testing.assert_array_equal(fused, sep, err_msg=name)
+        if oracle is not None:
+            np.testing.assert_allclose(fused, oracle(mu_o[:k], var_o[:k]), rtol=1e-7, atol=1e-11, equal_nan=True,
+                                       err_msg=name)
+        pair = ctx.eval_argmax(Xd, offset=1000).cpu().numpy()
+        v, i = oacq.argmax(sep, offset=1000)
+        assert (pair[0], int(pair[1])) == (v, i), name
+
+
+def test_eval_argmax_sobol_indices(ctx, gp3):
+    Y = gp3[0]
+    name, k, plan, separate, _ = _plans(ctx, Y)[1]          # textbook EHVI-2D
+    plan()
+    lo, hi = np.zeros(4), np.ones(4)
+    ctx.set_sobol(4, lo, hi, seed=42)
+    start, N = 5000, 20000
+    pair = ctx.eval_argmax_sobol(start, N).cpu().numpy()
+    X = dev(host_points(4, 42, True, lo, hi, start, N))
+    vals = ctx.eval(X).cpu().numpy()
+    v, i = oacq.argmax(vals, offset=start)
+    assert (pair[0], int(pair[1])) == (v, i)
+    # the winning index regenerates the winning point
+    assert np.array_equal(ctx.sobol(i, 1).cpu().numpy()[0], host_points(4, 42, True, lo, hi, i, 1)[0])
+
+
+def test_fused_empty_batch_and_errors(ctx, gp3):
+    from optimobo_amd import _lib
+    ctx.plan_ei(0.0)
+    pair = ctx.eval_argmax(dev(np.zeros((0, 4)))).cpu().numpy()
+    assert pair[0] == -np.inf and pair[1] == -1
+    with pytest.raises(_lib.OMBError) as e:
+        ctx.plan_ehvi2d(np.zeros((0, 2)), [1, 1], 1.0, 0.1)      # invalid plan …
+    assert e.value.code == _lib.OMB_EUNSUP
+    with pytest.raises(_lib.OMBError) as e:
+        ctx.eval(dev(np.zeros((3, 4))))                         # … leaves no plan
+    assert e.value.code == _lib.OMB_ESTATE
+    ctx.plan_ei(0.0)
+    ctx.set_sobol(3, np.zeros(3), np.ones(3), seed=0)
+    with pytest.raises(_lib.OMBError) as e:
+        ctx.eval_argmax_sobol(0, 16)                            # Sobol d=3 vs n_var=4
+    assert e.value.code == _lib.OMB_EINVAL
+
+
+def test_stage_timing(ctx, gp3):
+    Y = gp3[0]
+    _plans(ctx, Y)[0][2]()
+    ctx.set_sobol(4, np.zeros(4), np.ones(4), seed=0)
+    ctx.timing(2)
+    for _ in range(3):
+        ctx.eval_argmax_sobol(0, 1 << 14)
+    ms, n = ctx.timing_read()
+    assert n == 3 and ms["posterior"] > 0 and ms["acquisition"] > 0 and ms["sobol"] > 0 and ms["argmax"] > 0
+    ctx.timing(1)
+    for _ in range(2):
+        ctx.eval_argmax_sobol(0, 1 << 14)
+    ms, n = ctx.timing_read()
+    ctx.timing(0)
+    assert n == 2 and ms["posterior"] > 0 and ms["acquisition"] == 0 and ms["sobol"] == 0
+
+
+def test_engine_maximise_plan_equals_callable(gp3):
+    """AcquisitionEngine.maximise: the fused plan path and the callable path agree exactly."""
+    from optimobo_amd.acquisition import AcquisitionEngine
+    from optimobo_amd.gp import GPState
+    rng = np.random.default_rng(9)
+    X = rng.uniform(0, 1, (40, 3))
+    Y = _zdt(X)[:, :2]
+    eng = AcquisitionEngine(0).load_models([GPState(X, Y[:, o], [0.5, 0.8, 1.0], float(np.var(Y[:, o])))
+                                            for o in range(2)])
+    pf = opar.calc_pf(Y)
+    r = Y.max(0) + 0.1
+    cache = rng.standard_normal((32, 2))
+    eng.plan_ehvi(r, pf, cache, mode="textbook")
+    x1, v1 = eng.maximise(None, np.zeros(3), np.ones(3), n_candidates=1 << 13, seed=4)
+    x2, v2 = eng.maximise(lambda Xc: eng.ehvi(Xc, r, pf, cache, mode="textbook"), np.zeros(3), np.ones(3),
+                          n_candidates=1 << 13, seed=4)
+    assert v1 == v2 and np.array_equal(x1, x2)
+    # the result is the best of the scored host points of round 0 or better
+    U = host_points(3, 4, True, np.zeros(3), np.ones(3), 0, 1 << 13)
+    mu, var = eng.posterior(U)
+    from optimobo_amd import pareto
+    v0 = eng.ctx.ehvi2d(mu, var, pareto.stripes_2d(pf), r, *oacq.cache_stats(cache), mode="textbook").max().item()
+    assert v1 >= v0

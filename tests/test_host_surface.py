@@ -113,6 +113,25 @@ def test_cache_and_stripes():
     np.testing.assert_array_equal(pareto.stripes_2d(pf)[:, 1], [0.3, 0.5, 0.9])
 
 
+@pytest.mark.parametrize("d,seed", [(1, 0), (6, 3), (32, 8)])
+def test_sobol_engine_state_closed_form(d, seed):
+    """The closed form omb_sobol evaluates reproduces scipy's Sobol' engine bit for bit."""
+    from scipy.stats import qmc
+
+    from optimobo_amd.sobol import engine_state
+    sv, shift, bits = engine_state(d, seed)
+    assert sv.shape == (d, bits) and sv.dtype == np.uint32 and bits == 30
+    i = np.arange(3000, 5048, dtype=np.uint64)
+    g = i ^ (i >> np.uint64(1))
+    q = np.tile(shift.astype(np.uint64), (len(i), 1))
+    for b in range(bits):
+        hit = ((g >> np.uint64(b)) & np.uint64(1)).astype(bool)
+        q[hit] ^= sv[:, b].astype(np.uint64)
+    s = qmc.Sobol(d=d, scramble=True, seed=seed)
+    s.fast_forward(3000)
+    assert np.array_equal(q * (1.0 / 2 ** bits), s.random(len(i)))
+
+
 # ----------------------------------------------------------------------------- Problem
 class _Elem(ElementwiseProblem):
     def __init__(self, **kw):

@@ -199,11 +199,14 @@ def main():
         pf_dev = torch.as_tensor(pareto.stripes_2d(pf), device=device)
     elif acq_kind == "ehvi3d":
         hv_pf = pareto.hypervolume(pf, r)
+        coords, _, boxes = pareto.box_decomposition(pf, r)
         cache_dev = torch.as_tensor(cache, device=device)
 
     # the plan of the fused chain: the same acquisition as acquisition() below
     if acq_kind == "ehvi2d":
         ctx.plan_ehvi2d(pareto.stripes_2d(pf), r, s00, s01, mode=args.mode)
+    elif acq_kind == "ehvi3d" and args.mode == "textbook":
+        ctx.plan_ehvi_boxes(coords, boxes)       # exact EHVI, box decomposition staged in LDS
     elif acq_kind == "ehvi3d":
         ctx.plan_ehvi3d_mc(cache, r, hv_pf)
     else:
@@ -215,6 +218,8 @@ def main():
     def acquisition():
         if acq_kind == "ehvi2d":
             ctx.ehvi2d(mu, var, pf_dev, r, s00, s01, mode=args.mode, out=acq)
+        elif acq_kind == "ehvi3d" and args.mode == "textbook":
+            ctx.ehvi_boxes(mu, var, coords, boxes, out=acq)
         elif acq_kind == "ehvi3d":
             ctx.ehvi3d_mc(mu, var, cache_dev, r, hv_pf, out=acq, raised=raised)
         else:
@@ -300,7 +305,9 @@ def main():
 
     if rank == 0:
         total = N * world_size * args.steps
-        label = {"ehvi2d": f"2-obj EHVI ({args.mode} mode)", "ehvi3d": "3-obj EHVI (reference Monte-Carlo form)",
+        ehvi3d_label = ("3-obj EHVI (reference Monte-Carlo form)" if args.mode == "reference"
+                        else "3-obj exact EHVI (box decomposition in LDS)")
+        label = {"ehvi2d": f"2-obj EHVI ({args.mode} mode)", "ehvi3d": ehvi3d_label,
                  "ei_tch": "ParEGO Tchebicheff EI (mono surrogate)"}[acq_kind]
         out = {
             "metric": METRIC if args.config == 3 else f"{label} candidate evals/sec (BASELINE config {args.config})",

@@ -46,6 +46,7 @@ enum {
 
 enum { OMB_KERNEL_MATERN52 = 0, OMB_KERNEL_RBF = 1 };
 enum { OMB_EHVI_REFERENCE = 0, OMB_EHVI_TEXTBOOK = 1, OMB_EHVI_SIGMA = 2 };
+enum { OMB_EI_PLAIN = 0, OMB_EI_PARETO = 1, OMB_EI_CONSTRAINED = 2 };
 
 /* Scalarisation ids (optimobo/scalarisations.py:37-397) and their params[] layout. */
 enum {
@@ -141,6 +142,16 @@ int omb_expdec(omb_ctx* ctx, int k, const double* mu_dev, const double* var_dev,
  * keep.py:118-137 with var_eps = 1e-6). */
 int omb_ei(omb_ctx* ctx, const double* mu_dev, const double* var_dev, int64_t N, double best,
            double var_eps, double* out_dev);
+/* EI and its products with further models, over k posterior rows (row o at mu_dev + o·ld):
+ *   OMB_EI_PLAIN       k = 1   EI(μ0, σ²0 + var_eps)                              (= omb_ei)
+ *   OMB_EI_PARETO      k = 2   μ1 · EI(μ0, σ²0 + var_eps), var_eps = 1e-6 in the reference:
+ *                              KEEP.pareto_expected_improvement (keep.py:118-151), row 1 = the
+ *                              Pareto-membership model
+ *   OMB_EI_CONSTRAINED k ≥ 2   EI(μ0, σ²0 + var_eps) · Π_{c=1}^{k-1} Φ(−μc / sqrt(σ²c + pof_eps)),
+ *                              var_eps = 0, pof_eps = 1e-5 in the reference:
+ *                              ParEGO_C2.consraint_ei (cparego.py:450-496), rows 1.. = constraints */
+int omb_ei_ext(omb_ctx* ctx, int kind, int k, const double* mu_dev, const double* var_dev, int64_t ld, int64_t N,
+               double best, double var_eps, double pof_eps, double* out_dev);
 
 /* Arg-max over vals_dev (N): lowest index among maxima, NaN and -inf never win
  * (replaces scipy differential_evolution(lambda x: -acq(x)), optimisers.py:87,118).
@@ -175,6 +186,8 @@ int omb_plan_expdec(omb_ctx* ctx, int k, const double* cache_host, int M, int sc
                     const double* weights_host, const double* ideal_host, const double* max_host, double agg_min);
 /* Expected improvement of objective 0 (k = 1): as omb_ei. */
 int omb_plan_ei(omb_ctx* ctx, double best, double var_eps);
+/* EI family over objectives 0..k-1: as omb_ei_ext. */
+int omb_plan_ei_ext(omb_ctx* ctx, int kind, int k, double best, double var_eps, double pof_eps);
 
 /* Scrambled Sobol' candidates generated on the device (replaces the host-side sampling that
  * feeds the maximiser; same sequence as scipy.stats.qmc.Sobol, which the reference uses for

@@ -16,6 +16,7 @@ ERROR_NAMES = {OMB_EINVAL: "OMB_EINVAL", OMB_EHIP: "OMB_EHIP", OMB_ENOMEM: "OMB_
                OMB_ESTATE: "OMB_ESTATE", OMB_EUNSUP: "OMB_EUNSUP"}
 KERNEL_MATERN52, KERNEL_RBF = 0, 1
 EHVI_REFERENCE, EHVI_TEXTBOOK, EHVI_SIGMA = 0, 1, 2
+EI_PLAIN, EI_PARETO, EI_CONSTRAINED = 0, 1, 2
 MAX_OBJ, MAX_DIM, MAX_TRAIN = 8, 32, 1024
 
 _p = ctypes.c_void_p
@@ -42,6 +43,7 @@ SIGNATURES = {
     "omb_hvpoi": (_i, [_p, _p, _p, _i64, _i64, _p, _i, _p]),
     "omb_expdec": (_i, [_p, _i, _p, _p, _i64, _i64, _p, _i, _i, _dp, _dp, _dp, _dp, _d, _p]),
     "omb_ei": (_i, [_p, _p, _p, _i64, _d, _d, _p]),
+    "omb_ei_ext": (_i, [_p, _i, _i, _p, _p, _i64, _i64, _d, _d, _d, _p]),
     "omb_argmax_dev": (_i, [_p, _p, _i64, _i64, _p]),
     "omb_argmax": (_i, [_p, _p, _i64, _i64, _dp, ctypes.POINTER(_i64)]),
     # fused chain (host pointers for plan geometry)
@@ -51,6 +53,7 @@ SIGNATURES = {
     "omb_plan_hvpoi": (_i, [_p, _p, _i]),
     "omb_plan_expdec": (_i, [_p, _i, _p, _i, _i, _dp, _dp, _dp, _dp, _d]),
     "omb_plan_ei": (_i, [_p, _d, _d]),
+    "omb_plan_ei_ext": (_i, [_p, _i, _i, _d, _d, _d]),
     "omb_set_sobol": (_i, [_p, _i, _i, _p, _p, _dp, _dp]),
     "omb_sobol": (_i, [_p, _i64, _i64, _p]),
     "omb_eval": (_i, [_p, _p, _i64, _p]),

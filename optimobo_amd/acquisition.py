@@ -93,6 +93,16 @@ class AcquisitionEngine:
         mu, var = self.posterior(Xc)
         return self.ctx.ei(mu[0], var[0], float(best), float(var_eps))
 
+    def pareto_ei(self, Xc, best, var_eps=1e-6):
+        """KEEP's μ_pareto · EI (keep.py:142-151); models = [scalarised, pareto membership]."""
+        mu, var = self.posterior(Xc)
+        return self.ctx.ei_ext("pareto", mu, var, float(best), float(var_eps))
+
+    def constrained_ei(self, Xc, best, var_eps=0.0, pof_eps=1e-5):
+        """ParEGO_C2's EI · Π PoF (cparego.py:486-496); models = [aggregate, constraint_1, ...]."""
+        mu, var = self.posterior(Xc)
+        return self.ctx.ei_ext("constrained", mu, var, float(best), float(var_eps), float(pof_eps))
+
     # ------------------------------------------------------------------ plans (fused chain)
     # One plan per BO iteration; each candidate batch is then a single omb_eval_argmax_sobol
     # (Sobol generation → posterior → acquisition → arg-max on the device).
@@ -119,6 +129,12 @@ class AcquisitionEngine:
 
     def plan_ei(self, best, var_eps=0.0):
         self.ctx.plan_ei(float(best), float(var_eps))
+
+    def plan_pareto_ei(self, best, var_eps=1e-6):
+        self.ctx.plan_ei_ext("pareto", 2, float(best), float(var_eps))
+
+    def plan_constrained_ei(self, best, var_eps=0.0, pof_eps=1e-5):
+        self.ctx.plan_ei_ext("constrained", self.n_obj, float(best), float(var_eps), float(pof_eps))
 
     # ------------------------------------------------------------------ maximiser
     def maximise(self, acq_fn, lower, upper, n_candidates=1 << 16, seed=0, refine_rounds=2, shrink=0.1):

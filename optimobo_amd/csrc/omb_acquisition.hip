@@ -410,19 +410,38 @@ hipError_t launch_expdec(hipStream_t stream, const ScalParams& sp, const double*
 // ------------------------------------------------------------------------------ EI
 // optimisers.py:325-344 / parego.py:126-145: σ = sqrt(σ² + eps); γ = (best − μ)/(σ + 1e-10);
 // EI = σ(γΦ(γ) + φ(γ)).
+// EI and its products with a second model (one thread per candidate).
+//   MODE 0  EI(μ0, σ²0 + var_eps)                           optimisers.py:325-344, parego.py:126-145
+//   MODE 1  μ1 · EI(μ0, σ²0 + var_eps)                      KEEP pareto_expected_improvement, keep.py:142-151
+//   MODE 2  EI(μ0, σ²0 + var_eps) · Π_{c=1}^{k-1} Φ(−μc / sqrt(σ²c + pof_eps))
+//                                                           ParEGO_C2.consraint_ei, cparego.py:471-496
+template <int MODE>
 __global__ __launch_bounds__(kAcqThreads) void ei_kernel(const double* __restrict__ mu, const double* __restrict__ var,
-                                                         int64_t N, double best, double var_eps,
-                                                         double* __restrict__ out) {
+                                                         int64_t ld, int64_t N, int k, double best, double var_eps,
+                                                         double pof_eps, double* __restrict__ out) {
   for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < N; c += (int64_t)gridDim.x * blockDim.x) {
     const double sigma = sqrt(var[c] + var_eps);
     const double gamma = (best - mu[c]) / (sigma + 1e-10);
-    out[c] = sigma * (gamma * ndtr(gamma) + npdf(gamma));
+    double v = sigma * (gamma * ndtr(gamma) + npdf(gamma));
+    if (MODE == 1) v = mu[ld + c] * v;
+    if (MODE == 2) {
+      double pof = 1.0;
+      for (int j = 1; j < k; ++j) pof *= ndtr((0.0 - mu[j * ld + c]) / sqrt(var[j * ld + c] + pof_eps));
+      v = v * pof;
+    }
+    out[c] = v;
   }
 }
 
-hipError_t launch_ei(hipStream_t stream, const double* mu, const double* var, int64_t N, double best,
-                     double var_eps, double* out) {
-  hipLaunchKernelGGL(ei_kernel, dim3(acq_grid(N)), dim3(kAcqThreads), 0, stream, mu, var, N, best, var_eps, out);
+hipError_t launch_ei(hipStream_t stream, int kind, int k, const double* mu, const double* var, int64_t ld, int64_t N,
+                     double best, double var_eps, double pof_eps, double* out) {
+  const dim3 grid(acq_grid(N)), block(kAcqThreads);
+  if (kind == OMB_EI_PARETO)
+    hipLaunchKernelGGL(ei_kernel<1>, grid, block, 0, stream, mu, var, ld, N, k, best, var_eps, pof_eps, out);
+  else if (kind == OMB_EI_CONSTRAINED)
+    hipLaunchKernelGGL(ei_kernel<2>, grid, block, 0, stream, mu, var, ld, N, k, best, var_eps, pof_eps, out);
+  else
+    hipLaunchKernelGGL(ei_kernel<0>, grid, block, 0, stream, mu, var, ld, N, k, best, var_eps, pof_eps, out);
   return hipGetLastError();
 }
 

@@ -30,7 +30,8 @@ struct Plan {
   int k = 0;                    // objectives the acquisition reads (posterior of 0..k-1)
   int P = 0, M = 0, C = 0, B = 0, mode = 0;
   double r[OMB_MAX_OBJ] = {};
-  double s00 = 0, s01 = 0, hv = 0, best = 0, var_eps = 0;
+  double s00 = 0, s01 = 0, hv = 0, best = 0, var_eps = 0, pof_eps = 0;
+  int ei_kind = OMB_EI_PLAIN;
   ScalParams sp{};
   const double* geo = nullptr;  // pf / cache / coords / cells on the device
   const uint16_t* boxes = nullptr;
@@ -150,6 +151,14 @@ int check_boxes(omb_ctx* ctx, int k, int C, int B) {
   if (C < 2 || (size_t)k * C * 9 > (size_t)kMaxLdsDoubles)
     return fail(ctx, OMB_EUNSUP, "grid size C=%d outside [2, %d] for k=%d", C, kMaxLdsDoubles / (9 * k), k);
   if (B < 1) return fail(ctx, OMB_EINVAL, "empty box list");
+  return OMB_OK;
+}
+
+int check_ei(omb_ctx* ctx, int kind, int k, double var_eps, double pof_eps) {
+  const bool ok = (kind == OMB_EI_PLAIN && k == 1) || (kind == OMB_EI_PARETO && k == 2) ||
+                  (kind == OMB_EI_CONSTRAINED && k >= 2 && k <= OMB_MAX_OBJ);
+  if (!ok) return fail(ctx, OMB_EINVAL, "EI kind %d does not take k=%d posterior rows", kind, k);
+  if (!(var_eps >= 0.0) || !(pof_eps >= 0.0)) return fail(ctx, OMB_EINVAL, "var_eps/pof_eps must be >= 0");
   return OMB_OK;
 }
 
@@ -315,7 +324,7 @@ int run_chain(omb_ctx* ctx, const double* Xc, bool sobol, int64_t start, int64_t
         e = launch_expdec(ctx->stream, pl.sp, mu, var, N, N, pl.geo, pl.M, vals);
         break;
       case PLAN_EI:
-        e = launch_ei(ctx->stream, mu, var, N, pl.best, pl.var_eps, vals);
+        e = launch_ei(ctx->stream, pl.ei_kind, k, mu, var, N, N, pl.best, pl.var_eps, pl.pof_eps, vals);
         break;
       default:
         return fail(ctx, OMB_ESTATE, "corrupt plan");
@@ -555,11 +564,17 @@ int omb_expdec(omb_ctx* ctx, int k, const double* mu_dev, const double* var_dev,
 
 int omb_ei(omb_ctx* ctx, const double* mu_dev, const double* var_dev, int64_t N, double best, double var_eps,
            double* out_dev) {
+  return omb_ei_ext(ctx, OMB_EI_PLAIN, 1, mu_dev, var_dev, N, N, best, var_eps, 0.0, out_dev);
+}
+
+int omb_ei_ext(omb_ctx* ctx, int kind, int k, const double* mu_dev, const double* var_dev, int64_t ld, int64_t N,
+               double best, double var_eps, double pof_eps, double* out_dev) {
   int rc = enter(ctx);
   if (rc) return rc;
-  if ((rc = check_moments(ctx, mu_dev, var_dev, N, N, 1, out_dev))) return rc;
+  if ((rc = check_ei(ctx, kind, k, var_eps, pof_eps))) return rc;
+  if ((rc = check_moments(ctx, mu_dev, var_dev, ld, N, k, out_dev))) return rc;
   if (N == 0) return OMB_OK;
-  hipError_t e = launch_ei(ctx->stream, mu_dev, var_dev, N, best, var_eps, out_dev);
+  hipError_t e = launch_ei(ctx->stream, kind, k, mu_dev, var_dev, ld, N, best, var_eps, pof_eps, out_dev);
   if (e != hipSuccess) return hip_fail(ctx, e, "ei");
   return OMB_OK;
 }
@@ -702,15 +717,21 @@ int omb_plan_expdec(omb_ctx* ctx, int k, const double* cache_host, int M, int sc
 }
 
 int omb_plan_ei(omb_ctx* ctx, double best, double var_eps) {
+  return omb_plan_ei_ext(ctx, OMB_EI_PLAIN, 1, best, var_eps, 0.0);
+}
+
+int omb_plan_ei_ext(omb_ctx* ctx, int kind, int k, double best, double var_eps, double pof_eps) {
   int rc = enter(ctx);
   if (rc) return rc;
   ctx->plan = Plan();
-  if (!(var_eps >= 0.0)) return fail(ctx, OMB_EINVAL, "var_eps=%g must be >= 0", var_eps);
+  if ((rc = check_ei(ctx, kind, k, var_eps, pof_eps))) return rc;
   Plan pl;
   pl.kind = PLAN_EI;
-  pl.k = 1;
+  pl.ei_kind = kind;
+  pl.k = k;
   pl.best = best;
   pl.var_eps = var_eps;
+  pl.pof_eps = pof_eps;
   ctx->plan = pl;
   return OMB_OK;
 }

@@ -75,8 +75,8 @@ struct ScalParams {
 hipError_t launch_expdec(hipStream_t stream, const ScalParams& sp, const double* mu, const double* var,
                          int64_t ld, int64_t N, const double* cache, int M, double* out);
 
-hipError_t launch_ei(hipStream_t stream, const double* mu, const double* var, int64_t N, double best,
-                     double var_eps, double* out);
+hipError_t launch_ei(hipStream_t stream, int kind, int k, const double* mu, const double* var, int64_t ld, int64_t N,
+                     double best, double var_eps, double pof_eps, double* out);
 
 // Two-pass deterministic arg-max; `partials` must hold kArgmaxMaxBlocks (val, idx) pairs.
 constexpr int kArgmaxMaxBlocks = 1024;

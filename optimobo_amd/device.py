@@ -176,6 +176,16 @@ class AcqContext:
         self._check(self.lib.omb_ei(self._h, _ptr(mu), _ptr(var), N, float(best), float(var_eps), _ptr(out)), "omb_ei")
         return out
 
+    def ei_ext(self, kind, mu, var, best, var_eps=0.0, pof_eps=0.0, out=None):
+        """EI family over rows 0..k-1 of (mu, var): kind "plain" | "pareto" (KEEP) | "constrained" (cParEGO)."""
+        k, N = mu.shape
+        kid = {"plain": _lib.EI_PLAIN, "pareto": _lib.EI_PARETO, "constrained": _lib.EI_CONSTRAINED}[kind]
+        out = out if out is not None else torch.empty(N, dtype=torch.float64, device=self.device)
+        self._stream()
+        self._check(self.lib.omb_ei_ext(self._h, kid, k, _ptr(mu), _ptr(var), mu.stride(0), N, float(best),
+                                        float(var_eps), float(pof_eps), _ptr(out)), "omb_ei_ext")
+        return out
+
     def argmax_dev(self, vals, offset=0, out=None):
         out = out if out is not None else torch.empty(2, dtype=torch.float64, device=self.device)
         self._stream()
@@ -220,6 +230,10 @@ class AcqContext:
 
     def plan_ei(self, best, var_eps=0.0):
         self._plan("omb_plan_ei", float(best), float(var_eps))
+
+    def plan_ei_ext(self, kind, k, best, var_eps=0.0, pof_eps=0.0):
+        kid = {"plain": _lib.EI_PLAIN, "pareto": _lib.EI_PARETO, "constrained": _lib.EI_CONSTRAINED}[kind]
+        self._plan("omb_plan_ei_ext", kid, int(k), float(best), float(var_eps), float(pof_eps))
 
     def set_sobol(self, d, lo, hi, seed=None, scramble=True, state=None):
         """Device Sobol' engine = scipy qmc.Sobol(d, scramble=scramble, seed=seed) over [lo, hi]."""

@@ -181,6 +181,31 @@ def ei(mu, var, best, var_eps=0.0):
     return sigma * (gamma * norm_cdf(gamma) + norm_pdf(gamma))
 
 
+def pareto_ei(mu, var, best, var_eps=1e-6):
+    """KEEP.pareto_expected_improvement (keep.py:142-151) with its EI (keep.py:118-137), batched.
+
+    mu, var: (2, N) — row 0 the scalarised model, row 1 the Pareto-membership model.
+    value = μ1 · EI(μ0, σ = sqrt(σ²0 + 1e-6)).
+    """
+    mu = np.asarray(mu, np.float64)
+    var = np.asarray(var, np.float64)
+    return mu[1] * ei(mu[0], var[0], best, var_eps)
+
+
+def constrained_ei(mu, var, best, var_eps=0.0, pof_eps=1e-5):
+    """ParEGO_C2.consraint_ei (cparego.py:486-496), batched.
+
+    mu, var: (1 + m, N) — row 0 the aggregate model (EI with σ = sqrt(σ²), cparego.py:450-469),
+    rows 1..m the constraint models; PoF_c = Φ((0 − μc) / sqrt(σ²c + 1e-5)) (cparego.py:471-484).
+    """
+    mu = np.asarray(mu, np.float64)
+    var = np.asarray(var, np.float64)
+    pof = np.ones(mu.shape[1])
+    for c in range(1, mu.shape[0]):
+        pof = pof * norm_cdf((0 - mu[c]) / np.sqrt(var[c] + pof_eps))
+    return ei(mu[0], var[0], best, var_eps) * pof
+
+
 def argmax(values, offset=0):
     """Arg-max with the build's rule: lowest index among maxima; NaN and −inf never win.
 
@@ -197,8 +222,8 @@ def argmax(values, offset=0):
 
 
 __all__ = ["norm_cdf", "norm_pdf", "psi_cal", "cache_stats", "change", "sample_cov2", "stripes_2d",
-           "ehvi2d_aux", "ehvi2d", "ehvi3d_reference", "hvpoi", "expected_decomposition", "ei",
-           "argmax", "scal_mod"]
+           "ehvi2d_aux", "ehvi2d", "ehvi3d_reference", "hvpoi", "expected_decomposition", "ei", "pareto_ei",
+           "constrained_ei", "argmax", "scal_mod"]
 
 
 def ehvi_exact_boxes(mu, var, lo, hi):

@@ -20,7 +20,7 @@ util_functions.py:410, emo.py:220); it is aliased to ``np.prod``.
 GP posterior fixtures come from scikit-learn's GaussianProcessRegressor (independent of
 both GPy and this build) with the reference's kernel (Matern-5/2 ARD, noise 0 + 1e-8).
 
-Usage:  python tests/golden/make_golden.py
+Usage:  python tests/golden/make_golden.py [ei_ext]
 """
 import os
 import sys
@@ -252,6 +252,29 @@ def make_ei(rng, opt_mod, parego_mod):
     np.savez_compressed(os.path.join(HERE, "ei.npz"), mu=mu, var=var, best=best, ei_mono=e_mono, ei_parego=e_par)
 
 
+def make_pei_cei(rng, keep_mod, cparego_mod):
+    """KEEP.pareto_expected_improvement and ParEGO_C2.consraint_ei on fixed posterior moments."""
+    keep = object.__new__(keep_mod.KEEP)
+    c2 = object.__new__(cparego_mod.ParEGO_C2)
+    N, m = 96, 3
+    mu = rng.uniform(-1, 1, (1 + m, N))
+    mu[1, :10] = rng.uniform(0, 1, 10)             # Pareto-membership predictions live in [0, 1]
+    var = 10 ** rng.uniform(-9, 0, (1 + m, N))
+    var[:, :3] = 0.0
+    best = -0.1
+    pei = np.empty(N)
+    cei = {c: np.empty(N) for c in (1, m)}
+    for i in range(N):
+        scalar = ConstModel(mu[0, i], var[0, i])
+        pei[i] = np.asarray(keep.pareto_expected_improvement(np.zeros(3), ConstModel(mu[1, i], var[1, i]), scalar,
+                                                             best)).reshape(-1)[0]
+        for c in cei:
+            cons = [ConstModel(mu[j, i], var[j, i]) for j in range(1, 1 + c)]
+            cei[c][i] = np.asarray(c2.consraint_ei(np.zeros(3), scalar, cons, best)).reshape(-1)[0]
+    np.savez_compressed(os.path.join(HERE, "ei_ext.npz"), mu=mu, var=var, best=best, pei=pei, cei1=cei[1],
+                        cei3=cei[m])
+
+
 def make_calc_pf(rng, uf):
     out = {}
     for t, (n, k) in enumerate([(1, 2), (40, 2), (60, 3)]):
@@ -271,14 +294,21 @@ def main():
     import optimobo.algorithms.optimisers as opt_mod
     import optimobo.algorithms.parego as parego_mod
 
+    import optimobo.algorithms.keep as keep_mod
+    import optimobo.algorithms.cparego as cparego_mod
+
+    only = set(sys.argv[1:])          # e.g. `make_golden.py ei_ext` regenerates one fixture
     rng = np.random.default_rng(20261015)
-    make_posterior(rng)
-    make_ehvi2d(rng, uf)
-    make_ehvi3d(rng, uf)
-    make_cells_hvpoi(rng, uf, emo_mod)
-    make_expdec(rng, uf, sc)
-    make_ei(rng, opt_mod, parego_mod)
-    make_calc_pf(rng, uf)
+    if not only:
+        make_posterior(rng)
+        make_ehvi2d(rng, uf)
+        make_ehvi3d(rng, uf)
+        make_cells_hvpoi(rng, uf, emo_mod)
+        make_expdec(rng, uf, sc)
+        make_ei(rng, opt_mod, parego_mod)
+        make_calc_pf(rng, uf)
+    if not only or "ei_ext" in only:
+        make_pei_cei(np.random.default_rng(20261016), keep_mod, cparego_mod)
     print("golden fixtures written to", HERE)
 
 

@@ -137,6 +137,12 @@ def _plans(ctx, Y):
                 lambda mu, var: oacq.expected_decomposition(mu, var, cache3, tch, w3, 0.4)))
     out.append(("ei", 1, lambda: ctx.plan_ei(0.3, 1e-6), lambda mu, var: ctx.ei(mu[0], var[0], 0.3, 1e-6),
                 lambda mu, var: oacq.ei(mu[0], var[0], 0.3, 1e-6)))
+    out.append(("pareto-ei", 2, lambda: ctx.plan_ei_ext("pareto", 2, 0.3, 1e-6),
+                lambda mu, var: ctx.ei_ext("pareto", mu, var, 0.3, 1e-6),
+                lambda mu, var: oacq.pareto_ei(mu, var, 0.3, 1e-6)))
+    out.append(("constrained-ei", 3, lambda: ctx.plan_ei_ext("constrained", 3, 0.3, 0.0, 1e-5),
+                lambda mu, var: ctx.ei_ext("constrained", mu, var, 0.3, 0.0, 1e-5),
+                lambda mu, var: oacq.constrained_ei(mu, var, 0.3, 0.0, 1e-5)))
     return out
 
 

@@ -200,6 +200,24 @@ def test_ei_vs_golden(ctx, golden_dir):
                                atol=1e-300)
 
 
+def test_ei_ext_vs_golden(ctx, golden_dir):
+    """KEEP Pareto-EI and cParEGO constrained EI against the reference's own functions."""
+    z = load(golden_dir, "ei_ext.npz")
+    mu, var, best = dev(z["mu"]), dev(z["var"]), float(z["best"])
+    out = ctx.ei_ext("pareto", mu[:2], var[:2], best, 1e-6).cpu().numpy()
+    np.testing.assert_allclose(out, z["pei"], rtol=1e-5, atol=1e-300)
+    out = ctx.ei_ext("constrained", mu[:2], var[:2], best, 0.0, 1e-5).cpu().numpy()
+    np.testing.assert_allclose(out, z["cei1"], rtol=1e-5, atol=1e-300)
+    out = ctx.ei_ext("constrained", mu, var, best, 0.0, 1e-5).cpu().numpy()
+    np.testing.assert_allclose(out, z["cei3"], rtol=1e-5, atol=1e-300)
+    np.testing.assert_array_equal(ctx.ei_ext("plain", mu[:1], var[:1], best, 1e-6).cpu().numpy(),
+                                  ctx.ei(mu[0], var[0], best, 1e-6).cpu().numpy())
+    from optimobo_amd import _lib
+    with pytest.raises(_lib.OMBError) as e:
+        ctx.ei_ext("pareto", mu[:3], var[:3], best)
+    assert e.value.code == _lib.OMB_EINVAL
+
+
 # ----------------------------------------------------------------------------- arg-max
 def test_argmax_rules(ctx):
     rng = np.random.default_rng(9)

@@ -141,3 +141,22 @@ def test_solve_mono_emo_parego():
                                                                         n_init_samples=8)
     for r in (r1, r2, r3):
         assert r.ysample.shape == (10, 2)
+
+
+def test_keep_solve_and_fitness(fitted):
+    from optimobo_amd.algorithms import KEEP
+    import optimobo_amd.scalarisations as sc
+    np.random.seed(3)
+    p = _myproblem()
+    keep = KEEP(p, [0, 0], [700, 12], n_candidates=2048, seed=6)
+    r = keep.solve(sc.Tchebicheff([0, 0], [700, 12]), budget=2, n_init_samples=8)
+    assert r.ysample.shape == (10, 2) and np.all(np.abs(r.Xsample) <= 2 + 1e-12)
+    # the fitness KEEP maximises, batched and single, against the oracle chain
+    X, Y, ls, models = fitted
+    Xc = np.random.default_rng(4).uniform(0, 1, (500, 4))
+    got = keep.pareto_expected_improvement(Xc, models[1], models[0], 0.3)
+    mo, vo = oracle_moments(X, Y, ls, Xc)
+    ref = oacq.pareto_ei(mo, vo, 0.3)
+    np.testing.assert_allclose(got, ref, rtol=1e-6, atol=1e-12)
+    one = keep.pareto_expected_improvement(Xc[7], models[1], models[0], 0.3)
+    assert one.shape == (1,) and one[0] == pytest.approx(ref[7], rel=1e-6, abs=1e-12)

@@ -119,6 +119,15 @@ def test_ei(golden_dir):
     np.testing.assert_allclose(acq.ei(z["mu"], z["var"], float(z["best"]), 1e-6), z["ei_parego"], rtol=1e-12, atol=1e-300)
 
 
+def test_pareto_and_constrained_ei(golden_dir):
+    """KEEP's Pareto EI (keep.py:142-151) and ParEGO_C2's constrained EI (cparego.py:486-496)."""
+    z = load(golden_dir, "ei_ext.npz")
+    mu, var, best = z["mu"], z["var"], float(z["best"])
+    np.testing.assert_allclose(acq.pareto_ei(mu[:2], var[:2], best), z["pei"], rtol=1e-12, atol=1e-300)
+    np.testing.assert_allclose(acq.constrained_ei(mu[:2], var[:2], best), z["cei1"], rtol=1e-12, atol=1e-300)
+    np.testing.assert_allclose(acq.constrained_ei(mu, var, best), z["cei3"], rtol=1e-12, atol=1e-300)
+
+
 def test_calc_pf(golden_dir):
     z = load(golden_dir, "calc_pf.npz")
     for t in range(3):

@@ -62,6 +62,9 @@ CONFIGS = {
     3: dict(problem="zdt1", n=512, d=6, log2=20, acq="ehvi2d"),
     4: dict(problem="dtlz2", n=256, d=6, log2=17, acq="ehvi3d"),
     5: dict(problem="zdt1", n=1024, d=30, log2=19, acq="ei_tch"),
+    # not a BASELINE config: TuRBO's Thompson-sampling step (turbo.py:75-153) — one trust region,
+    # n_cand = min(100·n_var, 5000) candidates, batch_size joint posterior draws, greedy arg-mins
+    6: dict(problem="zdt1", n=512, d=30, n_cand=3000, draws=64, acq="thompson"),
 }
 METRIC = "EHVI candidate evals/sec at n_train=512, 2-obj; 1/2/4/8-GPU scaling"
 
@@ -114,6 +117,115 @@ def cpu_baseline(X, Y, ls, variances, pf, r, cache, Xc, seconds):  # noqa: C901
                       f"reference-mode EHVI-2D + arg-max, {dt:.1f} s"}
 
 
+def thompson_flops(n, N, B):
+    """Algorithmic flops of one Thompson step: V = L⁻¹K* (triangular, n²N), Σ = K** − VᵀV (lower
+    triangle, nN(N+1)), Cholesky N³/3, draws L·z (triangular, B·N²); kernel evaluations not counted."""
+    return n * n * N + n * N * (N + 1) + N ** 3 / 3.0 + B * N * N
+
+
+def cpu_thompson(X, yagg, ls, var, Xc, B, seconds):
+    """The reference's own recipe on the host: GPy full-covariance predict (oracle restatement) +
+    numpy.random.multivariate_normal (SVD, as GPy's posterior_samples_f) + greedy arg-mins."""
+    from oracle import gp as ogp
+    from oracle import turbo as oturbo
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([p.get("num_threads", 1) for p in threadpool_info()] or [1])
+    except Exception:  # pragma: no cover
+        cores = os.cpu_count() or 1
+    g = ogp.ExactGP(X, yagg, ls, var)
+    steps = 0
+    t0 = time.perf_counter()
+    while True:
+        mu, cov = g.predict_full_cov(Xc)
+        y = np.random.default_rng(steps).multivariate_normal(mu, cov, B, method="svd")
+        oturbo.select(y.T[:, None, :])
+        steps += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": steps * len(Xc) / dt, "unit": "candidates/s", "cores": int(cores), "kind": "port",
+            "sample": f"{steps} Thompson step(s) of {len(Xc)} candidates x {B} draws (oracle full-cov posterior "
+                      f"+ numpy multivariate_normal (SVD) + greedy arg-min), {dt:.1f} s"}
+
+
+def run_thompson(args, cfg, world_size, rank, device, backend):
+    """TuRBO Thompson step per GPU: omb_posterior_samples + omb_thompson_select (synchronous)."""
+    import torch
+    import torch.distributed as dist
+    from optimobo_amd import scalarisations as sc
+    from optimobo_amd.device import AcqContext
+    from optimobo_amd.gp import GPState
+
+    n, d, N, B = cfg["n"], cfg["d"], cfg["n_cand"], cfg["draws"]
+    X, Y, ls, _ = setup_problem(n, d, problem=cfg["problem"])
+    tch = sc.Tchebicheff(Y.min(axis=0), Y.max(axis=0))
+    yagg = tch(Y, np.array([0.5, 0.5]))
+    var = float(np.var(yagg))
+    ctx = AcqContext(device.index)
+    ctx.set_gp_state(0, GPState(X, yagg, ls, var))
+    rng = np.random.default_rng(100 + rank)
+    # a trust region of side 0.2 around a training point (turbo.py:82-111), one per rank
+    centre = X[rank % n]
+    Xc_host = np.clip(centre + 0.2 * (rng.uniform(0, 1, (N, d)) - 0.5), 0, 1)
+    Xc = torch.as_tensor(Xc_host, device=device)
+    Z = torch.as_tensor(rng.standard_normal((B, N)), device=device)
+    Yd = torch.empty((B, N), dtype=torch.float64, device=device)
+    idx = torch.empty(B, dtype=torch.int64, device=device)
+    jit = [0.0]
+
+    def step():
+        _, jit[0] = ctx.posterior_samples(0, Xc, Z, out=Yd)
+        ctx.thompson_select(Yd, out=idx)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world_size > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world_size > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world_size > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    step_ms = elapsed / args.steps * 1e3
+    fl = thompson_flops(n, N, B)
+    cpu = None
+    if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
+        cpu = cpu_thompson(X, yagg, ls, var, Xc_host, B, args.cpu_seconds)
+    if rank == 0:
+        out = {
+            "metric": "TuRBO Thompson-sampling candidate evals/sec (joint posterior draws + greedy arg-min)",
+            "value": N * world_size * args.steps / elapsed,
+            "unit": "candidates/s", "n_gpus": world_size, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": step_ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f64", "data": "synthetic",
+            "config": {"workload": f"TuRBO Thompson step, ZDT1 Tchebicheff surrogate, n_train={n}, n_var={d}, "
+                                   f"n_cand={N} (min(100*n_var, 5000)), {B} joint draws, one trust region per GPU",
+                       "n_train": n, "n_var": d, "n_cand": N, "draws": B, "global_batch": N * world_size,
+                       "parallelism": f"dp{world_size}"},
+            "roofline": {"bound": "mfma", "achieved": fl / (step_ms * 1e-3) / 1e12, "peak": FP64_MFMA_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": fl / (step_ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS,
+                         "traffic": None,
+                         "kernel": "whole step (covariance GEMMs + blocked Cholesky + draws + select); "
+                                   "algorithmic flops per step = n^2 N + n N (N+1) + N^3/3 + B N^2",
+                         "ms_per_launch": step_ms},
+            "cpu_baseline": cpu, "jitter": jit[0],
+        }
+        print(json.dumps(out))
+    if world_size > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    ctx.close()
+
+
 def load_traffic(n, N):
     """HBM bytes per posterior launch from the committed rocprofv3 PMC summary, if present."""
     path = os.path.join(REPO, "profiles", "traffic.json")
@@ -157,6 +269,9 @@ def main():
         dist.init_process_group(backend=backend, init_method="env://")
     device = torch.device("cuda", gpu)
     local_rank = gpu
+
+    if cfg["acq"] == "thompson":
+        return run_thompson(args, cfg, world_size, rank, device, backend)
 
     from optimobo_amd import pareto
     from optimobo_amd import scalarisations as sc

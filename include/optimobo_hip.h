@@ -41,7 +41,8 @@ enum {
   OMB_EHIP = -2,     /* HIP runtime error */
   OMB_ENOMEM = -3,   /* device allocation failed */
   OMB_ESTATE = -4,   /* objective not set (omb_set_gp) */
-  OMB_EUNSUP = -5    /* size outside what the kernels support */
+  OMB_EUNSUP = -5,   /* size outside what the kernels support */
+  OMB_ENOTPD = -6    /* matrix not positive definite (Cholesky), even with the allowed jitter */
 };
 
 enum { OMB_KERNEL_MATERN52 = 0, OMB_KERNEL_RBF = 1 };
@@ -217,6 +218,34 @@ int omb_eval_argmax_sobol(omb_ctx* ctx, int64_t start, int64_t N, double* result
  * Changing the level discards unread records. */
 int omb_timing(omb_ctx* ctx, int enable);
 int omb_timing_read(omb_ctx* ctx, double* stage_ms /* [4] */, int64_t* chains);
+
+/* ---------------------------------------------------------------------------------------
+ * Thompson sampling — TuRBO's candidate scoring (turbo.py:75-117 create_candidates,
+ * turbo.py:142-153 / 365-383 candidate selection).  The reference draws `batch_size` joint
+ * samples with GPy's GP.posterior_samples(X_cand, size) (turbo.py:114): a full posterior
+ * covariance (PosteriorExact._raw_predict, full_cov=True) and numpy's multivariate_normal
+ * (SVD).  Here: Σ on FP64 MFMA, a blocked Cholesky of Σ + jitter·I, samples μ + L z.
+ * ------------------------------------------------------------------------------------- */
+/* μ (N) and the full symmetric posterior covariance cov_dev (N, N) of objective `obj` at Xc_dev
+ * (N, d):  Σ = K(X*, X*) − (L⁻¹K*)ᵀ(L⁻¹K*)  (GPy _raw_predict(full_cov=True) + σ_n² = 0).
+ * N ≤ 32768.  Asynchronous. */
+int omb_posterior_cov(omb_ctx* ctx, int obj, const double* Xc_dev, int64_t N, double* mu_dev, double* cov_dev);
+/* In-place lower Cholesky factor of A + jitter·I (A_dev (N, N) row-major with leading dimension
+ * lda; the lower triangle is read and overwritten, the upper triangle is left untouched —
+ * LAPACK dpotrf('L') on the row-major lower triangle).  Synchronises; *info = 0 on success,
+ * else the 1-based column of the first non-positive pivot (dpotrf's info). */
+int omb_cholesky(omb_ctx* ctx, double* A_dev, int64_t N, int64_t lda, double jitter, int* info);
+/* B joint posterior samples of objective `obj` at Xc_dev (N, d) (GPy posterior_samples_f):
+ *   Y_dev (B, N) row b = μ + L z_b,  L = chol(Σ + j I),  Zt_dev (B, N) standard normals z_b.
+ * Try t = 0 .. max_tries-1 uses j = jitter_rel · σ_f² · 10^t until the factorisation succeeds
+ * (OMB_ENOTPD otherwise); *jitter_used (may be NULL) receives the j used.  Synchronises. */
+int omb_posterior_samples(omb_ctx* ctx, int obj, const double* Xc_dev, int64_t N, const double* Zt_dev, int B,
+                          double jitter_rel, int max_tries, double* Y_dev, double* jitter_used);
+/* Greedy selection of TuRBO_1.select_candidates (turbo.py:142-153) / TuRBO_M._select_candidates
+ * (turbo.py:365-383): for b = 0 .. B-1, idx_dev[b] = np.argmin over row b of Y_dev (B, N)
+ * (first NaN, else the lowest index among minima), every earlier pick reading as +inf
+ * (the reference sets y_cand[pick, :] = inf).  N ≤ 2^18.  Y is not modified.  Asynchronous. */
+int omb_thompson_select(omb_ctx* ctx, const double* Y_dev, int B, int64_t N, int64_t* idx_dev);
 
 #ifdef __cplusplus
 }

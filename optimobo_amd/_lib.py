@@ -11,9 +11,9 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboptimobo_hip.so")
 
-OMB_OK, OMB_EINVAL, OMB_EHIP, OMB_ENOMEM, OMB_ESTATE, OMB_EUNSUP = 0, -1, -2, -3, -4, -5
+OMB_OK, OMB_EINVAL, OMB_EHIP, OMB_ENOMEM, OMB_ESTATE, OMB_EUNSUP, OMB_ENOTPD = 0, -1, -2, -3, -4, -5, -6
 ERROR_NAMES = {OMB_EINVAL: "OMB_EINVAL", OMB_EHIP: "OMB_EHIP", OMB_ENOMEM: "OMB_ENOMEM",
-               OMB_ESTATE: "OMB_ESTATE", OMB_EUNSUP: "OMB_EUNSUP"}
+               OMB_ESTATE: "OMB_ESTATE", OMB_EUNSUP: "OMB_EUNSUP", OMB_ENOTPD: "OMB_ENOTPD"}
 KERNEL_MATERN52, KERNEL_RBF = 0, 1
 EHVI_REFERENCE, EHVI_TEXTBOOK, EHVI_SIGMA = 0, 1, 2
 EI_PLAIN, EI_PARETO, EI_CONSTRAINED = 0, 1, 2
@@ -61,6 +61,11 @@ SIGNATURES = {
     "omb_eval_argmax_sobol": (_i, [_p, _i64, _i64, _p]),
     "omb_timing": (_i, [_p, _i]),
     "omb_timing_read": (_i, [_p, _dp, ctypes.POINTER(_i64)]),
+    # Thompson sampling (TuRBO)
+    "omb_posterior_cov": (_i, [_p, _i, _p, _i64, _p, _p]),
+    "omb_cholesky": (_i, [_p, _p, _i64, _i64, _d, ctypes.POINTER(_i)]),
+    "omb_posterior_samples": (_i, [_p, _i, _p, _i64, _p, _i, _d, _i, _p, _dp]),
+    "omb_thompson_select": (_i, [_p, _p, _i, _i64, _p]),
 }
 
 

@@ -17,8 +17,9 @@ struct ObjState {
   bool set = false;
   int n = 0, d = 0, DP = 0, R = 0, n_pad = 0, kind = 0;
   double variance = 0.0;
-  double* buf = nullptr;  // one allocation: Xs | xsq | alpha | ls | Lp
+  double* buf = nullptr;  // one allocation: Xs | xsq | alpha | ls | Lp | Ld
   size_t cap = 0;         // bytes
+  const double* Ld = nullptr;  // dense row-major L⁻¹ (n, n): the full-covariance path's GEMM operand
   GPDev dev{};
 };
 
@@ -60,6 +61,11 @@ struct omb_ctx {
   int timing = 0;
   std::vector<hipEvent_t> ev;
   size_t ev_used = 0;
+  // Thompson sampling: K* | V | μ | σ² | Σ workspace, and Cholesky info + step counters
+  void* tws = nullptr;
+  size_t tws_cap = 0;
+  void* ichol = nullptr;
+  size_t ichol_cap = 0;
 };
 
 namespace {
@@ -378,6 +384,8 @@ int omb_destroy(omb_ctx* ctx) {
   if (ctx->stage) (void)hipHostFree(ctx->stage);
   if (ctx->work) (void)hipFree(ctx->work);
   if (ctx->sob) (void)hipFree(ctx->sob);
+  if (ctx->tws) (void)hipFree(ctx->tws);
+  if (ctx->ichol) (void)hipFree(ctx->ichol);
   for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;
@@ -425,7 +433,7 @@ int omb_set_gp(omb_ctx* ctx, int obj, int kernel, int n, int d, const double* X_
   const int R = (n + 15) / 16;
   const int Q = (R + 3) / 4;
   const int n_pad = kChunkRows * Q;
-  const size_t doubles = (size_t)n_pad * DP + 2 * (size_t)n_pad + DP + (size_t)packed_L_size(R);
+  const size_t doubles = (size_t)n_pad * DP + 2 * (size_t)n_pad + DP + (size_t)packed_L_size(R) + (size_t)n * n;
   const size_t bytes = doubles * sizeof(double);
   if (bytes > s.cap) {
     if (s.buf) (void)hipFree(s.buf);
@@ -442,8 +450,11 @@ int omb_set_gp(omb_ctx* ctx, int obj, int kernel, int n, int d, const double* X_
   double* alpha_p = xsq + n_pad;
   double* ls_p = alpha_p + n_pad;
   double* Lp = ls_p + DP;
+  double* Ld = Lp + packed_L_size(R);
   hipError_t e = launch_pack_gp(ctx->stream, n, d, DP, X_dev, lengthscale_host, alpha_dev, Linv_dev, Xs, xsq,
                                 alpha_p, Lp, R, n_pad);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(Ld, Linv_dev, sizeof(double) * (size_t)n * n, hipMemcpyDeviceToDevice, ctx->stream);
   if (e != hipSuccess) {
     s.set = false;
     return hip_fail(ctx, e, "pack_gp");
@@ -456,6 +467,7 @@ int omb_set_gp(omb_ctx* ctx, int obj, int kernel, int n, int d, const double* X_
   s.n_pad = n_pad;
   s.kind = kernel;
   s.variance = variance;
+  s.Ld = Ld;
   s.dev = GPDev{Xs, xsq, alpha_p, Lp, ls_p, variance, n, R, kernel, 0};
   return OMB_OK;
 }
@@ -811,6 +823,138 @@ int omb_timing_read(omb_ctx* ctx, double* stage_ms, int64_t* chains) {
   }
   if (chains) *chains = (int64_t)n;
   ctx->ev_used = 0;
+  return OMB_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// Thompson sampling (TuRBO, turbo.py:75-153): full posterior covariance, Cholesky, joint
+// samples and the greedy per-sample arg-min (omb_linalg.hip).
+
+static int check_obj(omb_ctx* ctx, int obj) {
+  if (obj < 0 || obj >= OMB_MAX_OBJ || !ctx->obj[obj].set) return fail(ctx, OMB_ESTATE, "objective %d not set", obj);
+  return OMB_OK;
+}
+
+static int check_cov_n(omb_ctx* ctx, int64_t N) {
+  if (N < 0) return fail(ctx, OMB_EINVAL, "N=%lld < 0", (long long)N);
+  if (N > kMaxCovN) return fail(ctx, OMB_EUNSUP, "N=%lld candidates exceed the full-covariance limit %lld",
+                                (long long)N, (long long)kMaxCovN);
+  return OMB_OK;
+}
+
+// μ (N) and σ² (N) by the posterior kernel, K* (n, N) by the K block, V = L⁻¹K* (n, N) by GEMM.
+static hipError_t cov_prepare(omb_ctx* ctx, const ObjState& s, const double* Xc, int64_t N, double* Kst, double* V,
+                              double* mu, double* var) {
+  GPArgs args;
+  memset(&args, 0, sizeof(args));
+  args.gp[0] = s.dev;
+  args.d = s.d;
+  args.DP = s.DP;
+  hipError_t e = launch_posterior(ctx->stream, args, 1, s.R, Xc, N, mu, var);
+  if (e == hipSuccess) e = launch_kernel_block(ctx->stream, args, 0, Xc, N, Kst);
+  if (e == hipSuccess) e = launch_gemm_nn(ctx->stream, s.n, N, s.n, 1.0, s.Ld, s.n, Kst, N, 0.0, V, N);
+  return e;
+}
+
+// lower triangle of Σ = K(X*, X*) − VᵀV (GPy PosteriorExact._raw_predict, full_cov=True).
+static hipError_t cov_build(omb_ctx* ctx, const ObjState& s, const double* Xc, int64_t N, const double* V, double* S,
+                            int64_t lds) {
+  hipError_t e = launch_cand_cov(ctx->stream, s.dev, s.d, s.DP, Xc, N, S, lds);
+  if (e == hipSuccess) e = launch_gemm_tn_lower(ctx->stream, N, s.n, -1.0, V, N, 1.0, S, lds);
+  return e;
+}
+
+// In-place lower Cholesky of A + jitter·I; synchronises and returns LAPACK's info in *info.
+static int run_cholesky(omb_ctx* ctx, double* A, int64_t N, int64_t lda, double jitter, int* info) {
+  const size_t steps = (size_t)((N + 63) / 64);
+  int rc = grow_dev(ctx, &ctx->ichol, &ctx->ichol_cap, sizeof(int) * (steps + 1), "Cholesky counters");
+  if (rc) return rc;
+  int* dinfo = static_cast<int*>(ctx->ichol);
+  OMB_HIP(ctx, hipMemsetAsync(dinfo, 0, sizeof(int) * (steps + 1), ctx->stream));
+  OMB_HIP(ctx, launch_add_diag(ctx->stream, A, N, lda, jitter));
+  OMB_HIP(ctx, launch_cholesky(ctx->stream, A, N, lda, dinfo, dinfo + 1));
+  int h = 0;
+  OMB_HIP(ctx, hipMemcpyAsync(&h, dinfo, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  OMB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  *info = h;
+  return OMB_OK;
+}
+
+int omb_posterior_cov(omb_ctx* ctx, int obj, const double* Xc_dev, int64_t N, double* mu_dev, double* cov_dev) {
+  int rc = enter(ctx);
+  if (rc) return rc;
+  if ((rc = check_obj(ctx, obj)) || (rc = check_cov_n(ctx, N))) return rc;
+  if (N > 0 && (!Xc_dev || !mu_dev || !cov_dev)) return fail(ctx, OMB_EINVAL, "null device pointer");
+  if (N == 0) return OMB_OK;
+  const ObjState& s = ctx->obj[obj];
+  const size_t nN = (size_t)s.n * N;
+  if ((rc = grow_dev(ctx, &ctx->tws, &ctx->tws_cap, sizeof(double) * (2 * nN + N), "covariance workspace"))) return rc;
+  double* Kst = static_cast<double*>(ctx->tws);
+  double* V = Kst + nN;
+  double* var = V + nN;
+  hipError_t e = cov_prepare(ctx, s, Xc_dev, N, Kst, V, mu_dev, var);
+  if (e == hipSuccess) e = cov_build(ctx, s, Xc_dev, N, V, cov_dev, N);
+  if (e == hipSuccess) e = launch_mirror_lower(ctx->stream, cov_dev, N, N);
+  if (e != hipSuccess) return hip_fail(ctx, e, "posterior_cov");
+  return OMB_OK;
+}
+
+int omb_cholesky(omb_ctx* ctx, double* A_dev, int64_t N, int64_t lda, double jitter, int* info) {
+  int rc = enter(ctx);
+  if (rc) return rc;
+  if (!info || N < 0 || lda < N || (N > 0 && !A_dev)) return fail(ctx, OMB_EINVAL, "bad Cholesky arguments");
+  if (!(jitter >= 0.0)) return fail(ctx, OMB_EINVAL, "jitter=%g must be >= 0", jitter);
+  *info = 0;
+  if (N == 0) return OMB_OK;
+  return run_cholesky(ctx, A_dev, N, lda, jitter, info);
+}
+
+int omb_posterior_samples(omb_ctx* ctx, int obj, const double* Xc_dev, int64_t N, const double* Zt_dev, int B,
+                          double jitter_rel, int max_tries, double* Y_dev, double* jitter_used) {
+  int rc = enter(ctx);
+  if (rc) return rc;
+  if ((rc = check_obj(ctx, obj)) || (rc = check_cov_n(ctx, N))) return rc;
+  if (N < 1 || B < 1) return fail(ctx, OMB_EINVAL, "need N >= 1 candidates and B >= 1 samples (N=%lld, B=%d)",
+                                  (long long)N, B);
+  if (!Xc_dev || !Zt_dev || !Y_dev) return fail(ctx, OMB_EINVAL, "null device pointer");
+  if (!(jitter_rel >= 0.0) || max_tries < 1 || max_tries > 32)
+    return fail(ctx, OMB_EINVAL, "jitter_rel=%g must be >= 0 and max_tries=%d in [1, 32]", jitter_rel, max_tries);
+  const ObjState& s = ctx->obj[obj];
+  const size_t nN = (size_t)s.n * N;
+  const size_t doubles = 2 * nN + 2 * (size_t)N + (size_t)N * N;
+  if ((rc = grow_dev(ctx, &ctx->tws, &ctx->tws_cap, sizeof(double) * doubles, "sampling workspace"))) return rc;
+  double* Kst = static_cast<double*>(ctx->tws);
+  double* V = Kst + nN;
+  double* mu = V + nN;
+  double* var = mu + N;
+  double* S = var + N;
+  hipError_t e = cov_prepare(ctx, s, Xc_dev, N, Kst, V, mu, var);
+  if (e != hipSuccess) return hip_fail(ctx, e, "posterior_samples (posterior)");
+  double jit = jitter_rel * s.variance;
+  int info = -1, t = 0;
+  for (; t < max_tries; ++t, jit *= 10.0) {
+    if ((e = cov_build(ctx, s, Xc_dev, N, V, S, N)) != hipSuccess) return hip_fail(ctx, e, "posterior_samples (cov)");
+    if ((rc = run_cholesky(ctx, S, N, N, jit, &info))) return rc;
+    if (info == 0) break;
+  }
+  if (info != 0)
+    return fail(ctx, OMB_ENOTPD, "posterior covariance + %g I is not positive definite (column %d) after %d tries",
+                jit / 10.0, info, max_tries);
+  if ((e = launch_chol_samples(ctx->stream, S, N, N, mu, Zt_dev, B, Y_dev)) != hipSuccess)
+    return hip_fail(ctx, e, "posterior_samples (samples)");
+  if (jitter_used) *jitter_used = jit;
+  return OMB_OK;
+}
+
+int omb_thompson_select(omb_ctx* ctx, const double* Y_dev, int B, int64_t N, int64_t* idx_dev) {
+  int rc = enter(ctx);
+  if (rc) return rc;
+  if (B < 0 || N < 1) return fail(ctx, OMB_EINVAL, "need B >= 0 samples over N >= 1 candidates");
+  if (N > kSelectMaxN) return fail(ctx, OMB_EUNSUP, "N=%lld candidates exceed %lld", (long long)N,
+                                   (long long)kSelectMaxN);
+  if (B > 0 && (!Y_dev || !idx_dev)) return fail(ctx, OMB_EINVAL, "null device pointer");
+  hipError_t e = launch_select(ctx->stream, Y_dev, B, N, idx_dev);
+  if (e != hipSuccess) return hip_fail(ctx, e, "thompson_select");
   return OMB_OK;
 }
 

@@ -92,6 +92,28 @@ void sobol_pack_state(int d, int bits, const uint32_t* sv, const uint32_t* shift
 hipError_t launch_sobol(hipStream_t stream, const void* state_dev, int d, int bits, int64_t start, int64_t N,
                         double* X);
 
+// Dense fp64 linear algebra for Thompson sampling (omb_linalg.hip).  Row-major throughout.
+constexpr int64_t kSelectMaxN = 1 << 18;    // candidates per selection (LDS exclusion bitmap)
+constexpr int64_t kMaxCovN = 32768;         // candidates of one full posterior covariance
+// C (M, Nc) = β C + α A B, A (M, K), B (K, Nc).
+hipError_t launch_gemm_nn(hipStream_t s, int64_t M, int64_t Nc, int64_t K, double alpha, const double* A, int64_t lda,
+                          const double* B, int64_t ldb, double beta, double* C, int64_t ldc);
+// lower triangle of C (N, N) = β C + α AᵀA, A (K, N).
+hipError_t launch_gemm_tn_lower(hipStream_t s, int64_t N, int64_t K, double alpha, const double* A, int64_t lda,
+                                double beta, double* C, int64_t ldc);
+// lower triangle of K(X*, X*) of one GP's kernel (ℓ, σ_f² from g) at Xc (N, d).
+hipError_t launch_cand_cov(hipStream_t stream, const GPDev& g, int d, int DP, const double* Xc, int64_t N, double* S,
+                           int64_t lds);
+hipError_t launch_mirror_lower(hipStream_t stream, double* S, int64_t N, int64_t lds);
+hipError_t launch_add_diag(hipStream_t stream, double* S, int64_t N, int64_t lds, double v);
+// in-place lower Cholesky; info (device int, zeroed by the caller) = first bad column (1-based);
+// done_ctr: ⌈N/64⌉ device ints, zeroed by the caller.
+hipError_t launch_cholesky(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, int* done_ctr);
+// Y (B, N) = μ + Zt Lᵀ (L lower, N×N): row b of Y is the sample μ + L z_b.
+hipError_t launch_chol_samples(hipStream_t stream, const double* L, int64_t N, int64_t ldl, const double* mu,
+                               const double* Zt, int B, double* Y);
+hipError_t launch_select(hipStream_t stream, const double* Y, int B, int64_t N, int64_t* idx);
+
 // Packed-L^-1 size in doubles for R row tiles: Σ_{r<R} 4(r+1)·64 = 128·R·(R+1).
 inline int64_t packed_L_size(int R) { return 128ll * R * (R + 1); }
 

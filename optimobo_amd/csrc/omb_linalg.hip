@@ -1,0 +1,408 @@
+// Dense fp64 linear algebra on gfx950 for TuRBO's Thompson sampling.
+//
+// TuRBO draws `batch_size` joint samples of the GP at up to 5,000 trust-region candidates
+// (optimobo/algorithms/turbo.py:114, GPy GP.posterior_samples), i.e.
+//   PosteriorExact._raw_predict(full_cov=True):  μ = K*ᵀα,  Σ = K(X*, X*) − (L⁻¹K*)ᵀ(L⁻¹K*)
+//   numpy.random.multivariate_normal(μ, Σ, size)      (an O(N³) SVD on the host)
+// and then takes the arg-min of every sample, greedily excluding earlier picks
+// (TuRBO_1.select_candidates turbo.py:142-153, TuRBO_M._select_candidates turbo.py:365-383).
+//
+//   gemm_kernel        C = β·C + α·op(A)·op(B) (+ column bias) on v_mfma_f64_16x16x4f64: one 64×64 C
+//                      tile per 256-thread workgroup (4 waves × 32×32), k-slabs of 16 double-buffered
+//                      in LDS behind a register prefetch.  Variants: store the lower triangle only
+//                      (SYRK-shaped Σ update, Cholesky trailing update) and "op(B)(k, j) = 0 for k > j"
+//                      (a lower-triangular factor read transposed: the samples μ + L z).
+//   cand_cov_kernel    lower triangle of K(X*, X*) (GPy _unscaled_dist: diagonal forced to 0).
+//   chol_panel_kernel  one step of a blocked right-looking Cholesky: every workgroup factors the
+//                      64×64 diagonal block with its first wave (lane r keeps row r in registers,
+//                      pivots and multipliers broadcast by v_readlane), the last workgroup to finish
+//                      writes it back, and each thread solves one row of the panel below (the row in
+//                      64 registers, L_kk read from LDS as a broadcast).  The
+//                      trailing update A22 −= L21 L21ᵀ is the lower-triangle GEMM.
+//   select_kernel      the greedy per-sample arg-min (np.argmin order) with an LDS exclusion bitmap.
+// The factor is chol(Σ + jitter·I): numpy factors Σ by SVD instead; both draw from N(μ, Σ) up to
+// the jitter, which the caller bounds (omb_posterior_samples).
+#include "omb_internal.h"
+#include "omb_math.h"
+
+namespace omb {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+// ----------------------------------------------------------------------------- GEMM
+constexpr int kGT = 64;         // C tile edge
+constexpr int kGK = 16;         // k slab
+constexpr int kGP = kGT + 2;    // LDS row pitch in doubles (rows 528 B apart: conflict-free stores)
+
+template <bool TA, bool TB, bool BTRI, bool LOWER>
+__global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t Nc, int64_t K, double alpha,
+                                                   const double* __restrict__ A, int64_t lda,
+                                                   const double* __restrict__ B, int64_t ldb, double beta,
+                                                   double* __restrict__ C, int64_t ldc,
+                                                   const double* __restrict__ col_bias) {
+  const int64_t m0 = (int64_t)blockIdx.y * kGT, n0 = (int64_t)blockIdx.x * kGT;
+  if (LOWER && n0 > m0) return;   // tile strictly above the diagonal
+  __shared__ double As[2][kGK][kGP];   // As[k][m] = op(A)(m0 + m, k0 + k)
+  __shared__ double Bs[2][kGK][kGP];   // Bs[k][n] = op(B)(k0 + k, n0 + n)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  // with BTRI, slabs past the tile's last column are all zero in op(B)
+  const int64_t kend = BTRI ? (K < n0 + kGT ? K : n0 + kGT) : K;
+
+  // 1024 elements of each operand per slab, 4 per thread; consecutive threads walk the
+  // contiguous dimension of the stored matrix (coalesced), LDS stores land conflict-free.
+  double ra[4], rb[4];
+  auto fetch = [&](int64_t k0) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int idx = tid + 256 * e;
+      const int am = TA ? (idx & 63) : (idx >> 4), ak = TA ? (idx >> 6) : (idx & 15);
+      const int64_t gm = m0 + am, gka = k0 + ak;
+      ra[e] = (gm < M && gka < K) ? (TA ? A[gka * lda + gm] : A[gm * lda + gka]) : 0.0;
+      const int bn = TB ? (idx >> 4) : (idx & 63), bk = TB ? (idx & 15) : (idx >> 6);
+      const int64_t gn = n0 + bn, gkb = k0 + bk;
+      const bool ok = gn < Nc && gkb < K && !(BTRI && gkb > gn);
+      rb[e] = ok ? (TB ? B[gn * ldb + gkb] : B[gkb * ldb + gn]) : 0.0;
+    }
+  };
+  auto stash = [&](int buf) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int idx = tid + 256 * e;
+      As[buf][TA ? (idx >> 6) : (idx & 15)][TA ? (idx & 63) : (idx >> 4)] = ra[e];
+      Bs[buf][TB ? (idx & 15) : (idx >> 6)][TB ? (idx >> 4) : (idx & 63)] = rb[e];
+    }
+  };
+
+  d4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+
+  if (kend > 0) {
+    fetch(0);
+    stash(0);
+  }
+  __syncthreads();
+  int buf = 0;
+  for (int64_t k0 = 0; k0 < kend; k0 += kGK) {
+    const bool more = k0 + kGK < kend;
+    if (more) fetch(k0 + kGK);      // in flight while this slab multiplies
+#pragma unroll
+    for (int ks = 0; ks < kGK / 4; ++ks) {
+      const int kk = 4 * ks + (lane >> 4);
+      const double a0 = As[buf][kk][32 * wm + (lane & 15)];
+      const double a1 = As[buf][kk][32 * wm + 16 + (lane & 15)];
+      const double b0 = Bs[buf][kk][32 * wn + (lane & 15)];
+      const double b1 = Bs[buf][kk][32 * wn + 16 + (lane & 15)];
+      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    // the other buffer was last read in the previous slab, which every wave has finished
+    if (more) stash(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+
+  // C/D map of v_mfma_f64_16x16x4f64: col = lane & 15, row = (lane >> 4) + 4·i
+#pragma unroll
+  for (int rb2 = 0; rb2 < 2; ++rb2)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t row = m0 + 32 * wm + 16 * rb2 + (lane >> 4) + 4 * i;
+        const int64_t col = n0 + 32 * wn + 16 * cb + (lane & 15);
+        if (row < M && col < Nc && (!LOWER || col <= row)) {
+          double v = alpha * acc[rb2][cb][i];
+          if (beta != 0.0) v = fma(beta, C[row * ldc + col], v);
+          if (col_bias) v += col_bias[col];
+          C[row * ldc + col] = v;
+        }
+      }
+}
+
+template <bool TA, bool TB, bool BTRI, bool LOWER>
+static hipError_t gemm(hipStream_t stream, int64_t M, int64_t Nc, int64_t K, double alpha, const double* A,
+                       int64_t lda, const double* B, int64_t ldb, double beta, double* C, int64_t ldc,
+                       const double* col_bias) {
+  if (M <= 0 || Nc <= 0) return hipSuccess;
+  dim3 grid((unsigned)((Nc + kGT - 1) / kGT), (unsigned)((M + kGT - 1) / kGT));
+  hipLaunchKernelGGL((gemm_kernel<TA, TB, BTRI, LOWER>), grid, dim3(256), 0, stream, M, Nc, K, alpha, A, lda, B, ldb,
+                     beta, C, ldc, col_bias);
+  return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------- K(X*, X*)
+// GPy Stationary._unscaled_dist(X) on X/ℓ: r² = −2·(aᵢ·aⱼ) + (‖aᵢ‖² + ‖aⱼ‖²), diagonal forced
+// to 0, clipped at 0; then K_of_r.  Lower triangle only (j ≤ i), 16×16 tiles.
+template <int DP, int KIND>
+__global__ __launch_bounds__(256) void cand_cov_kernel(const double* __restrict__ Xc, int d, int64_t N,
+                                                       const double* __restrict__ ls, double variance,
+                                                       double* __restrict__ S, int64_t lds) {
+  if (blockIdx.x > blockIdx.y) return;
+  const int64_t i = (int64_t)blockIdx.y * 16 + (threadIdx.x >> 4);
+  const int64_t j = (int64_t)blockIdx.x * 16 + (threadIdx.x & 15);
+  if (i >= N || j > i) return;
+  double aa = 0.0, bb = 0.0, dot = 0.0;
+#pragma unroll
+  for (int k = 0; k < DP; ++k) {
+    if (k < d) {
+      const double a = Xc[i * d + k] / ls[k];
+      const double b = Xc[j * d + k] / ls[k];
+      aa += a * a;
+      bb += b * b;
+      dot = fma(a, b, dot);
+    }
+  }
+  const double r2 = (i == j) ? 0.0 : fma(-2.0, dot, aa + bb);
+  S[i * lds + j] = kernel_of_r2<KIND>(r2, variance);
+}
+
+__global__ __launch_bounds__(256) void mirror_lower_kernel(double* __restrict__ S, int64_t N, int64_t lds) {
+  // S[i][j] = S[j][i] for j > i, 32×32 tiles through LDS (both sides coalesced)
+  if (blockIdx.x < blockIdx.y) return;
+  __shared__ double t[32][33];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 × 8
+  const int64_t bi = (int64_t)blockIdx.y * 32, bj = (int64_t)blockIdx.x * 32;   // upper tile rows bi, cols bj
+  for (int r = ty; r < 32; r += 8) {
+    const int64_t src_row = bj + r, src_col = bi + tx;    // lower tile (rows bj.., cols bi..)
+    if (src_row < N && src_col < N) t[r][tx] = S[src_row * lds + src_col];
+  }
+  __syncthreads();
+  for (int r = ty; r < 32; r += 8) {
+    const int64_t row = bi + r, col = bj + tx;
+    if (row < N && col < N && col > row) S[row * lds + col] = t[tx][r];
+  }
+}
+
+__global__ void add_diag_kernel(double* __restrict__ S, int64_t N, int64_t lds, double v) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < N) S[i * lds + i] += v;
+}
+
+// ----------------------------------------------------------------------------- Cholesky
+constexpr int kNB = 64;
+
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(b & 0xffffffffll), l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __builtin_bit_cast(double, (long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// Step `step` (columns c0 = 64·step ..) of the lower Cholesky of the N×N matrix A (row-major,
+// lower triangle read and written, upper untouched).  info (1-based column of the first
+// non-positive pivot, LAPACK dpotrf convention) is set once and stops later steps.
+__global__ __launch_bounds__(256) void chol_panel_kernel(double* __restrict__ A, int64_t N, int64_t lda, int step,
+                                                         int* __restrict__ info, int* __restrict__ done_ctr) {
+  __shared__ double Ls[kNB][kNB + 1];
+  __shared__ double rinv[kNB];
+  if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+  const int64_t c0 = (int64_t)step * kNB;
+  const int nb = (int)((N - c0) < kNB ? (N - c0) : kNB);
+  const int tid = threadIdx.x;
+  if (tid < 64) {
+    // ---- factor the diagonal block with one wave: lane r keeps row r in 64 registers (identity
+    // rows pad a short block); column j's pivot and multipliers are broadcast with v_readlane.
+    const int r = tid;
+    double a[kNB];
+#pragma unroll
+    for (int c = 0; c < kNB; ++c) {
+      double v = (c == r) ? 1.0 : 0.0;
+      if (r < nb && c <= r) v = A[(c0 + r) * lda + c0 + c];
+      a[c] = v;
+    }
+    int bad = 0;
+    double my_inv = 1.0;
+#pragma unroll
+    for (int j = 0; j < kNB; ++j) {
+      double dj = readlane_f64(a[j], j);               // pivot (wave-uniform)
+      if (!(dj > 0.0)) {
+        if (bad == 0) bad = j + 1;
+        dj = 1.0;                                      // continue without NaNs; flagged
+      }
+      const double ljj = sqrt(dj);
+      const double inv = 1.0 / ljj;
+      if (r == j) my_inv = inv;
+      const double lrj = (r > j) ? a[j] * inv : (r == j ? ljj : 0.0);
+      a[j] = lrj;
+#pragma unroll
+      for (int k = j + 1; k < kNB; ++k) {
+        const double lkj = readlane_f64(lrj, k);
+        a[k] = (r >= k) ? fma(-lrj, lkj, a[k]) : a[k];
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < kNB; ++c) Ls[r][c] = a[c];
+    rinv[r] = my_inv;
+    // the last workgroup to finish factoring writes L_kk back: every other one has consumed its
+    // loads of A_kk by then (they fed the factorization before its counter increment)
+    int old = 0;
+    if (r == 0) old = atomicAdd(done_ctr + step, 1);
+    if (__builtin_amdgcn_readfirstlane(old) == (int)gridDim.x - 1) {
+      if (r < nb)
+        for (int c = 0; c <= r; ++c) A[(c0 + r) * lda + c0 + c] = Ls[r][c];
+      if (r == 0 && bad) atomicCAS(info, 0, (int)(c0 + bad));
+    }
+  }
+  __syncthreads();
+  // ---- panel: rows below the block solve x · L_kkᵀ = b (forward substitution)
+  const int64_t row = c0 + nb + (int64_t)blockIdx.x * blockDim.x + tid;
+  if (row >= N) return;
+  double* rp = A + row * lda + c0;
+  // rows below the block exist only while a full block remains (nb == 64): unconditional
+  // accesses keep x[] in registers (a per-column guard makes the compiler spill it)
+  double x[kNB];
+#pragma unroll
+  for (int c = 0; c < kNB; ++c) x[c] = rp[c];
+#pragma unroll
+  for (int j = 0; j < kNB; ++j) {
+    double s = x[j];
+#pragma unroll
+    for (int l = 0; l < j; ++l) s = fma(-x[l], Ls[j][l], s);
+    x[j] = s * rinv[j];
+  }
+#pragma unroll
+  for (int c = 0; c < kNB; ++c) rp[c] = x[c];
+}
+
+// ----------------------------------------------------------------------------- selection
+// np.argmin order: the first NaN wins, else the smallest value, lowest index among ties.
+__device__ __forceinline__ bool sel_better(double v, int64_t i, double bv, int64_t bi) {
+  if (i < 0) return false;
+  if (bi < 0) return true;
+  const bool vn = v != v, bn = bv != bv;
+  if (vn || bn) return vn && (!bn || i < bi);
+  return v < bv || (v == bv && i < bi);
+}
+
+__global__ __launch_bounds__(1024) void select_kernel(const double* __restrict__ Y, int B, int64_t N,
+                                                      int64_t* __restrict__ idx_out) {
+  __shared__ unsigned excl[kSelectMaxN / 32];
+  __shared__ double sv[16];
+  __shared__ int64_t si[16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  for (int64_t w = tid; w < (N + 31) / 32; w += blockDim.x) excl[w] = 0u;
+  __syncthreads();
+  for (int b = 0; b < B; ++b) {
+    const double* y = Y + (int64_t)b * N;
+    double bv = 0.0;
+    int64_t bi = -1;
+    for (int64_t i = tid; i < N; i += blockDim.x) {
+      // a picked candidate reads as +inf for every later sample (turbo.py:151, :381)
+      const double v = ((excl[i >> 5] >> (i & 31)) & 1u) ? __builtin_inf() : y[i];
+      if (sel_better(v, i, bv, bi)) {
+        bv = v;
+        bi = i;
+      }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const double ov = __shfl_down(bv, off);
+      const int64_t oi = (int64_t)__shfl_down((long long)bi, off);
+      if (sel_better(ov, oi, bv, bi)) {
+        bv = ov;
+        bi = oi;
+      }
+    }
+    if (lane == 0) {
+      sv[wave] = bv;
+      si[wave] = bi;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      for (int w = 1; w < nw; ++w)
+        if (sel_better(sv[w], si[w], bv, bi)) {
+          bv = sv[w];
+          bi = si[w];
+        }
+      idx_out[b] = bi;
+      if (bi >= 0) excl[bi >> 5] |= 1u << (bi & 31);
+    }
+    __syncthreads();
+  }
+}
+
+// ----------------------------------------------------------------------------- launchers
+hipError_t launch_gemm_nn(hipStream_t s, int64_t M, int64_t Nc, int64_t K, double alpha, const double* A, int64_t lda,
+                          const double* B, int64_t ldb, double beta, double* C, int64_t ldc) {
+  return gemm<false, false, false, false>(s, M, Nc, K, alpha, A, lda, B, ldb, beta, C, ldc, nullptr);
+}
+
+hipError_t launch_gemm_tn_lower(hipStream_t s, int64_t N, int64_t K, double alpha, const double* A, int64_t lda,
+                                double beta, double* C, int64_t ldc) {
+  return gemm<true, false, false, true>(s, N, N, K, alpha, A, lda, A, lda, beta, C, ldc, nullptr);
+}
+
+hipError_t launch_cand_cov(hipStream_t stream, const GPDev& g, int d, int DP, const double* Xc, int64_t N, double* S,
+                           int64_t lds) {
+  const unsigned nt = (unsigned)((N + 15) / 16);
+  dim3 grid(nt, nt);
+#define OMB_COV(DPV)                                                                                        \
+  case DPV:                                                                                                 \
+    if (g.kind == OMB_KERNEL_RBF)                                                                           \
+      hipLaunchKernelGGL((cand_cov_kernel<DPV, OMB_KERNEL_RBF>), grid, dim3(256), 0, stream, Xc, d, N, g.ls, \
+                         g.variance, S, lds);                                                               \
+    else                                                                                                    \
+      hipLaunchKernelGGL((cand_cov_kernel<DPV, OMB_KERNEL_MATERN52>), grid, dim3(256), 0, stream, Xc, d, N,  \
+                         g.ls, g.variance, S, lds);                                                         \
+    break;
+  switch (DP) {
+    OMB_COV(2) OMB_COV(4) OMB_COV(6) OMB_COV(8) OMB_COV(16) OMB_COV(32)
+    default: return hipErrorInvalidValue;
+  }
+#undef OMB_COV
+  return hipGetLastError();
+}
+
+hipError_t launch_mirror_lower(hipStream_t stream, double* S, int64_t N, int64_t lds) {
+  const unsigned nt = (unsigned)((N + 31) / 32);
+  hipLaunchKernelGGL(mirror_lower_kernel, dim3(nt, nt), dim3(256), 0, stream, S, N, lds);
+  return hipGetLastError();
+}
+
+hipError_t launch_add_diag(hipStream_t stream, double* S, int64_t N, int64_t lds, double v) {
+  if (v == 0.0 || N <= 0) return hipSuccess;
+  hipLaunchKernelGGL(add_diag_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, stream, S, N, lds, v);
+  return hipGetLastError();
+}
+
+hipError_t launch_cholesky(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, int* done_ctr) {
+  const int steps = (int)((N + kNB - 1) / kNB);
+  for (int k = 0; k < steps; ++k) {
+    const int64_t c0 = (int64_t)k * kNB;
+    const int64_t nb = (N - c0) < kNB ? (N - c0) : kNB;
+    const int64_t rest = N - c0 - nb;
+    const unsigned blocks = (unsigned)(rest > 0 ? (rest + 255) / 256 : 1);
+    hipLaunchKernelGGL(chol_panel_kernel, dim3(blocks), dim3(256), 0, stream, A, N, lda, k, info, done_ctr);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (rest > 0) {
+      // A22 −= L21 L21ᵀ (lower triangle): op(A) = L21, op(B) = L21ᵀ
+      double* L21 = A + (c0 + nb) * lda + c0;
+      e = gemm<false, true, false, true>(stream, rest, rest, nb, -1.0, L21, lda, L21, lda, 1.0,
+                                         A + (c0 + nb) * lda + c0 + nb, lda, nullptr);
+      if (e != hipSuccess) return e;
+    }
+  }
+  return hipSuccess;
+}
+
+hipError_t launch_chol_samples(hipStream_t stream, const double* L, int64_t N, int64_t ldl, const double* mu,
+                               const double* Zt, int B, double* Y) {
+  // Y (B, N) = Zt · Lᵀ + μ  with  op(B)(k, j) = L[j][k] for k ≤ j (the factor's upper part is ignored)
+  return gemm<false, true, true, false>(stream, B, N, N, 1.0, Zt, N, L, ldl, 0.0, Y, N, mu);
+}
+
+hipError_t launch_select(hipStream_t stream, const double* Y, int B, int64_t N, int64_t* idx) {
+  if (B <= 0) return hipSuccess;
+  hipLaunchKernelGGL(select_kernel, dim3(1), dim3(1024), 0, stream, Y, B, N, idx);
+  return hipGetLastError();
+}
+
+}  // namespace omb

@@ -274,6 +274,55 @@ class AcqContext:
         self._check(self.lib.omb_eval_argmax_sobol(self._h, int(start), int(N), _ptr(out)), "omb_eval_argmax_sobol")
         return out
 
+    # ------------------------------------------------------------------ Thompson sampling (TuRBO)
+    def posterior_cov(self, obj, Xc, out=None):
+        """μ (N,), Σ (N, N): GPy predict(Xc, full_cov=True) of objective ``obj`` (σ_n² = 0)."""
+        Xc = _dev_f64(Xc, self.device)
+        N = Xc.shape[0]
+        mu, cov = out if out is not None else (torch.empty(N, dtype=torch.float64, device=self.device),
+                                               torch.empty((N, N), dtype=torch.float64, device=self.device))
+        self._stream()
+        self._check(self.lib.omb_posterior_cov(self._h, int(obj), _ptr(Xc), N, _ptr(mu), _ptr(cov)),
+                    "omb_posterior_cov")
+        return mu, cov
+
+    def cholesky(self, A, jitter=0.0):
+        """In place: lower triangle of A (N, N) ← chol(A + jitter·I); returns LAPACK's info (0 = ok)."""
+        if A.dtype != torch.float64 or A.dim() != 2 or A.shape[0] != A.shape[1] or A.stride(1) != 1:
+            raise ValueError("cholesky: A must be a square fp64 device matrix with unit column stride")
+        info = ctypes.c_int()
+        self._stream()
+        self._check(self.lib.omb_cholesky(self._h, _ptr(A), A.shape[0], A.stride(0), float(jitter), ctypes.byref(info)),
+                    "omb_cholesky")
+        return info.value
+
+    def posterior_samples(self, obj, Xc, Zt, jitter_rel=1e-10, max_tries=8, out=None):
+        """Y (B, N): B joint posterior samples μ + chol(Σ + jI) z_b at Xc, z_b = row b of Zt (B, N).
+
+        Returns (Y, j) with j the absolute jitter that made Σ + jI factorisable."""
+        Xc = _dev_f64(Xc, self.device)
+        Zt = _dev_f64(Zt, self.device)
+        N = Xc.shape[0]
+        B = Zt.shape[0]
+        if Zt.dim() != 2 or Zt.shape[1] != N:
+            raise ValueError(f"Zt must be (B, {N}), got {tuple(Zt.shape)}")
+        Y = out if out is not None else torch.empty((B, N), dtype=torch.float64, device=self.device)
+        used = ctypes.c_double()
+        self._stream()
+        self._check(self.lib.omb_posterior_samples(self._h, int(obj), _ptr(Xc), N, _ptr(Zt), B, float(jitter_rel),
+                                                   int(max_tries), _ptr(Y), ctypes.byref(used)),
+                    "omb_posterior_samples")
+        return Y, used.value
+
+    def thompson_select(self, Y, out=None):
+        """TuRBO's greedy per-sample arg-min over Y (B, N) → indices (B,) int64 (device)."""
+        Y = _dev_f64(Y, self.device)
+        B, N = Y.shape
+        idx = out if out is not None else torch.empty(B, dtype=torch.int64, device=self.device)
+        self._stream()
+        self._check(self.lib.omb_thompson_select(self._h, _ptr(Y), B, N, _ptr(idx)), "omb_thompson_select")
+        return idx
+
     def timing(self, level=2):
         """0 off, 1 posterior only, 2 every stage of the fused chain (see omb_timing)."""
         self._stream()

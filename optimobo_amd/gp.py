@@ -154,7 +154,6 @@ class GPRegression:
         self.Gaussian_noise.variance.values[:] = noise_var
         self.likelihood = self.Gaussian_noise
         self._state = None
-        self._ctx = None
 
     # -- fitted state
     def state(self):
@@ -233,22 +232,49 @@ class GPRegression:
 
     # -- device prediction (hot path)
     def _context(self):
-        from .device import AcqContext
-        if self._ctx is None:
-            self._ctx = AcqContext(0)
-        return self._ctx
+        """The process-wide device context with this model's state in objective slot 0."""
+        from .acquisition import engine_for
+        return engine_for([self]).ctx
 
     def predict(self, Xnew, full_cov=False):
-        """μ (m,1), σ² (m,1) at Xnew on the GPU (GPy GPRegression.predict semantics)."""
-        if full_cov:
-            raise NotImplementedError("full_cov prediction is not on the acquisition hot path")
+        """μ (m,1), σ² (m,1) — or with full_cov the (m, m) covariance — at Xnew on the GPU
+        (GPy GPRegression.predict semantics: σ_n² is added to the variance / diagonal)."""
         import torch
         ctx = self._context()
-        ctx.set_gp_state(0, self.state())
         Xnew = np.atleast_2d(np.asarray(Xnew, np.float64))
-        mu, var = ctx.posterior(torch.as_tensor(Xnew, device=ctx.device), n_obj=1)
+        Xd = torch.as_tensor(Xnew, device=ctx.device)
         noise = float(self.Gaussian_noise.variance)
+        if full_cov:
+            mu, cov = ctx.posterior_cov(0, Xd)
+            cov = cov.cpu().numpy()
+            cov[np.diag_indices_from(cov)] += noise
+            return mu.cpu().numpy()[:, None], cov
+        mu, var = ctx.posterior(Xd, n_obj=1)
         return mu[0].cpu().numpy()[:, None], var[0].cpu().numpy()[:, None] + noise
+
+    def posterior_samples_device(self, Xnew, size=10, jitter_rel=1e-10):
+        """(size, m) device tensor of joint posterior draws at Xnew, and the jitter used.
+
+        GPy's posterior_samples_f (the call of turbo.py:114) draws with
+        ``numpy.random.multivariate_normal(μ, Σ, size)``; here Σ, its Cholesky factor and
+        μ + L z run on the GPU (omb_posterior_samples), z from numpy's global generator."""
+        import torch
+        ctx = self._context()
+        Xnew = np.atleast_2d(np.asarray(Xnew, np.float64))
+        Z = np.random.standard_normal((int(size), len(Xnew)))
+        return ctx.posterior_samples(0, torch.as_tensor(Xnew, device=ctx.device),
+                                     torch.as_tensor(Z, device=ctx.device), jitter_rel=jitter_rel)
+
+    def posterior_samples_f(self, X, size=10, **kw):
+        """GPy GP.posterior_samples_f: (m, 1, size) joint draws of the latent function."""
+        Y, _ = self.posterior_samples_device(X, size)
+        return Y.T.cpu().numpy()[:, None, :]
+
+    def posterior_samples(self, X, size=10, **kw):
+        """GPy GP.posterior_samples: latent draws through the Gaussian likelihood (σ_n² = 0 here)."""
+        f = self.posterior_samples_f(X, size)
+        noise = float(self.Gaussian_noise.variance)
+        return f + np.sqrt(noise) * np.random.standard_normal(f.shape) if noise > 0 else f
 
 
 class kern:  # noqa: N801  — GPy.kern namespace look-alike

@@ -104,6 +104,17 @@ class ExactGP:
         var = (self.variance - np.square(tmp).sum(0))[:, None] + self.noise
         return mu, var
 
+    def predict_full_cov(self, Xnew):
+        """μ (m,), Σ (m, m) as GPy PosteriorExact._raw_predict(full_cov=True): Kxx − tdot(tmp.T),
+        tmp = dtrtrs(L, Kx), plus σ_n² I (= 0) from GPRegression.predict (the call inside
+        GP.posterior_samples that TuRBO makes, optimobo/algorithms/turbo.py:114)."""
+        Xnew = np.atleast_2d(np.asarray(Xnew, dtype=np.float64))
+        Kx = KERNELS[self.kernel](self.X, Xnew, self.lengthscale, self.variance)
+        mu = (Kx.T @ self.alpha)[:, 0]
+        tmp = linalg.solve_triangular(self.L, Kx, lower=True)
+        Kxx = KERNELS[self.kernel](Xnew, None, self.lengthscale, self.variance)
+        return mu, Kxx - tmp.T @ tmp + self.noise * np.eye(len(Xnew))
+
 
 def sklearn_posterior(X, y, lengthscale, variance, Xnew):
     """Independent pin: scikit-learn GaussianProcessRegressor with the same kernel."""

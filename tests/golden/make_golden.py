@@ -20,7 +20,7 @@ util_functions.py:410, emo.py:220); it is aliased to ``np.prod``.
 GP posterior fixtures come from scikit-learn's GaussianProcessRegressor (independent of
 both GPy and this build) with the reference's kernel (Matern-5/2 ARD, noise 0 + 1e-8).
 
-Usage:  python tests/golden/make_golden.py [ei_ext]
+Usage:  python tests/golden/make_golden.py [ei_ext] [turbo]
 """
 import os
 import sys
@@ -275,6 +275,93 @@ def make_pei_cei(rng, keep_mod, cparego_mod):
                         cei3=cei[m])
 
 
+def make_turbo(rng, turbo_mod):
+    """TuRBO host logic from the reference's own methods (turbo.py): candidate generation
+    (create_candidates :75-117, np.random seeded; the GP is a duck that only supplies
+    lengthscales and zero samples), greedy selection (select_candidates :142-153,
+    _select_candidates :365-383) and the trust-region length rules (_adjust_length :127-140,
+    :347-363)."""
+    out = {}
+
+    class DuckGP:
+        def __init__(self, ls):
+            self.kern = types.SimpleNamespace(lengthscale=np.asarray(ls, np.float64))
+
+        def posterior_samples(self, X, size):
+            return np.zeros((len(X), 1, size))
+
+    for c, (d, length) in enumerate([(3, 0.4), (30, 0.8), (2, 1.6), (6, 0.05)]):
+        t1 = object.__new__(turbo_mod.TuRBO_1)
+        t1.n_vars, t1.n_cand, t1.batch_size = d, min(100 * d, 600), 4      # fixture-sized n_cand
+        Xs = rng.uniform(0, 1, (12, d))
+        ys = rng.standard_normal((12, 1))
+        ls = rng.uniform(0.1, 2.0, d)
+        np.random.seed(100 + c)
+        Xc, _ = t1.create_candidates(Xs, ys, DuckGP(ls), length)
+        out.update({f"cc{c}_Xs": Xs, f"cc{c}_ys": ys, f"cc{c}_ls": ls, f"cc{c}_length": np.float64(length),
+                    f"cc{c}_seed": np.int64(100 + c), f"cc{c}_Xc": Xc})
+
+    t1 = object.__new__(turbo_mod.TuRBO_1)
+    t1.n_vars = 3
+    for c, (N, B) in enumerate([(40, 5), (7, 9), (300, 32)]):
+        y = rng.standard_normal((N, 1, B))
+        y[3, 0, :] = y[5, 0, :]
+        if c == 0:
+            y[10, 0, 2] = np.nan
+        X = rng.uniform(0, 1, (N, 3))
+        t1.batch_size = B
+        out.update({f"s1_{c}_y": y, f"s1_{c}_X": X, f"s1_{c}_Xnext": t1.select_candidates(X, y.copy())})
+    tm = object.__new__(turbo_mod.TuRBO_M)
+    tm.n_vars = 2
+    for c, (T, N, B) in enumerate([(3, 50, 6), (2, 5, 10)]):
+        tm.n_trust_regions, tm.n_cand, tm.batch_size = T, N, B
+        y = rng.standard_normal((T, N, B))
+        y[1, 2] = y[0, 3]
+        X = rng.uniform(0, 1, (T, N, 2))
+        Xn, idx_next = tm._select_candidates(X, y.copy())
+        out.update({f"sm_{c}_y": y, f"sm_{c}_X": X, f"sm_{c}_Xnext": Xn, f"sm_{c}_idx": idx_next})
+
+    # trust-region length rules on a fixed sequence of batches
+    t1 = object.__new__(turbo_mod.TuRBO_1)
+    t1.batch_size, t1.n_vars = 4, 5
+    t1.failtol = np.ceil(np.max([4.0 / 4, 5 / 4]))
+    t1.succtol, t1.length_max, t1.length_init = 3, 1.6, 0.4
+    t1._restart()
+    t1._aggregated_samples = rng.uniform(0, 1, (6, 1))
+    init = t1._aggregated_samples.copy()
+    seq = [rng.uniform(-1.5, 1.5, 4) for _ in range(40)]
+    traj = []
+    for fx in seq:
+        t1._adjust_length(fx)
+        traj.append((t1.length, t1.succcount, t1.failcount))
+        t1._aggregated_samples = np.vstack((t1._aggregated_samples, fx.reshape(-1, 1)))
+    out.update({"al1_init": init, "al1_seq": np.asarray(seq), "al1_traj": np.asarray(traj)})
+
+    tm = object.__new__(turbo_mod.TuRBO_M)
+    tm.n_trust_regions, tm.batch_size, tm.n_vars = 3, 4, 5
+    tm.length_init, tm.length_max, tm.succtol, tm.failtol = 0.4, 1.6, 3, 5
+    tm._idx = np.zeros((0, 1), dtype=int)
+    tm.failcount = np.zeros(3, dtype=int)
+    tm.succcount = np.zeros(3, dtype=int)
+    tm.length = 0.4 * np.ones(3)
+    tm.ysample = rng.uniform(0, 1, (9, 2))
+    tm._idx = np.repeat(np.arange(3), 3).reshape(-1, 1)
+    ys0, idx0 = tm.ysample.copy(), tm._idx.copy()
+    seqm, trajm = [], []
+    for s_ in range(40):
+        i = int(rng.integers(0, 3))
+        fx = rng.uniform(-1, 1, int(rng.integers(1, 4)))
+        seqm.append((i, fx))
+        tm._adjust_length(fx, i)
+        trajm.append(np.concatenate([tm.length, tm.succcount, tm.failcount]))
+        tm.ysample = np.vstack((tm.ysample, np.column_stack([fx, fx])))
+        tm._idx = np.vstack((tm._idx, i * np.ones((len(fx), 1), dtype=int)))
+    out.update({"alm_ys0": ys0, "alm_idx0": idx0, "alm_regions": np.array([q[0] for q in seqm]),
+                "alm_lens": np.array([len(q[1]) for q in seqm]),
+                "alm_vals": np.concatenate([q[1] for q in seqm]), "alm_traj": np.asarray(trajm)})
+    np.savez_compressed(os.path.join(HERE, "turbo.npz"), **out)
+
+
 def make_calc_pf(rng, uf):
     out = {}
     for t, (n, k) in enumerate([(1, 2), (40, 2), (60, 3)]):
@@ -296,6 +383,7 @@ def main():
 
     import optimobo.algorithms.keep as keep_mod
     import optimobo.algorithms.cparego as cparego_mod
+    import optimobo.algorithms.turbo as turbo_mod
 
     only = set(sys.argv[1:])          # e.g. `make_golden.py ei_ext` regenerates one fixture
     rng = np.random.default_rng(20261015)
@@ -309,6 +397,8 @@ def main():
         make_calc_pf(rng, uf)
     if not only or "ei_ext" in only:
         make_pei_cei(np.random.default_rng(20261016), keep_mod, cparego_mod)
+    if not only or "turbo" in only:
+        make_turbo(np.random.default_rng(20261017), turbo_mod)
     print("golden fixtures written to", HERE)
 
 

@@ -1,0 +1,245 @@
+"""GPU: TuRBO's Thompson-sampling path through the C-ABI — full posterior covariance, blocked
+Cholesky, joint samples and the greedy per-sample arg-min — against the oracle.
+
+Tolerances (written per test): covariance 1e-6 relative with an absolute floor of 1e-9·σ_f²
+(the posterior-variance floor of test_gpu_parity); Cholesky factor 1e-10 relative on
+well-conditioned SPD matrices; samples 1e-6·σ_f on the same normals; selection bit-exact.
+"""
+import numpy as np
+import pytest
+from scipy import linalg
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from oracle import gp as ogp  # noqa: E402
+from oracle import turbo as oturbo  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from optimobo_amd.device import AcqContext
+    c = AcqContext(0)
+    yield c
+    c.close()
+
+
+def dev(x):
+    return torch.as_tensor(np.ascontiguousarray(x, dtype=np.float64), device="cuda:0")
+
+
+def fit(ctx, n, d, seed, kernel="matern52"):
+    from optimobo_amd.gp import GPState
+    rng = np.random.default_rng(seed)
+    X = rng.uniform(0, 1, (n, d))
+    y = np.sin(3 * X).sum(1) + X[:, 0] ** 2
+    ls = rng.uniform(0.3, 1.5, d)
+    var = float(np.var(y))
+    ctx.set_gp_state(0, GPState(X, y, ls, var, kernel=kernel))
+    return X, y, ls, var, ogp.ExactGP(X, y, ls, var, kernel=kernel)
+
+
+# ----------------------------------------------------------------------------- covariance
+@pytest.mark.parametrize("n,d,N,kernel", [(20, 2, 1, "matern52"), (20, 2, 77, "matern52"), (300, 6, 700, "matern52"),
+                                          (129, 30, 257, "matern52"), (64, 4, 130, "rbf")])
+def test_posterior_cov_vs_oracle(ctx, n, d, N, kernel):
+    X, y, ls, var, og = fit(ctx, n, d, seed=n + d, kernel=kernel)
+    rng = np.random.default_rng(N)
+    Xc = rng.uniform(-0.1, 1.1, (N, d))
+    Xc[: min(3, N)] = X[: min(3, N)]                 # training points: Σ rows ≈ 0
+    mu, cov = ctx.posterior_cov(0, dev(Xc))
+    mu, cov = mu.cpu().numpy(), cov.cpu().numpy()
+    mu_o, cov_o = og.predict_full_cov(Xc)
+    np.testing.assert_allclose(mu, mu_o, rtol=1e-6, atol=1e-7 * np.sqrt(var))
+    np.testing.assert_allclose(cov, cov_o, rtol=1e-6, atol=1e-9 * var)
+    assert np.array_equal(cov, cov.T)
+    # the diagonal is the posterior variance of the fused posterior kernel
+    m2, v2 = ctx.posterior(dev(Xc), n_obj=1)
+    np.testing.assert_allclose(np.diag(cov), v2[0].cpu().numpy(), rtol=1e-9, atol=1e-11 * var)
+    assert np.array_equal(mu, m2[0].cpu().numpy())
+
+
+# ----------------------------------------------------------------------------- Cholesky
+def spd(N, seed):
+    rng = np.random.default_rng(seed)
+    G = rng.standard_normal((N, N))
+    return G @ G.T / N + 0.5 * np.eye(N)
+
+
+@pytest.mark.parametrize("N", [1, 2, 63, 64, 65, 130, 333, 1000])
+def test_cholesky_vs_lapack(ctx, N):
+    A = spd(N, N)
+    wide = np.full((N, N + 5), 7.0)                  # lda > N: the extra columns are never touched
+    wide[:, :N] = np.triu(np.full((N, N), -3.0), 1) + np.tril(A)   # upper triangle holds junk
+    At = dev(wide)
+    info = ctx.cholesky(At[:, :N], jitter=0.25)
+    assert info == 0
+    got = At.cpu().numpy()
+    ref = np.linalg.cholesky(A + 0.25 * np.eye(N))
+    np.testing.assert_allclose(np.tril(got[:, :N]), ref, rtol=1e-10, atol=1e-12)
+    assert np.array_equal(np.triu(got[:, :N], 1), np.triu(wide[:, :N], 1))
+    assert np.array_equal(got[:, N:], wide[:, N:])
+
+
+@pytest.mark.parametrize("bad", [0, 70, 199])
+def test_cholesky_info_matches_dpotrf(ctx, bad):
+    N = 200
+    A = spd(N, 5)
+    A[bad, bad] = -1.0
+    _, info_ref = linalg.lapack.dpotrf(A, lower=1)
+    info = ctx.cholesky(dev(A))
+    assert info == info_ref == bad + 1
+
+
+# ----------------------------------------------------------------------------- samples
+def test_posterior_samples_vs_oracle(ctx):
+    X, y, ls, var, og = fit(ctx, 40, 3, seed=11)
+    rng = np.random.default_rng(12)
+    Xc = rng.uniform(0, 1, (500, 3))
+    Z = rng.standard_normal((16, 500))
+    Y, jit = ctx.posterior_samples(0, dev(Xc), dev(Z), jitter_rel=1e-6)
+    assert jit >= 1e-6 * var
+    mu_o, cov_o = og.predict_full_cov(Xc)
+    Yo = oturbo.chol_samples(mu_o, cov_o, Z, jit)
+    np.testing.assert_allclose(Y.cpu().numpy(), Yo, rtol=0, atol=1e-6 * np.sqrt(var))
+
+
+def test_posterior_samples_moments(ctx):
+    """Size-independent property: the draws have mean μ and covariance Σ (+ jitter)."""
+    X, y, ls, var, og = fit(ctx, 30, 2, seed=21)
+    rng = np.random.default_rng(22)
+    Xc = rng.uniform(0, 1, (24, 2))
+    B = 20000
+    Z = rng.standard_normal((B, 24))
+    Y, jit = ctx.posterior_samples(0, dev(Xc), dev(Z))
+    Y = Y.cpu().numpy()
+    mu_o, cov_o = og.predict_full_cov(Xc)
+    sd = np.sqrt(np.maximum(np.diag(cov_o), 0)) + 1e-12
+    assert np.all(np.abs(Y.mean(0) - mu_o) <= 5 * sd / np.sqrt(B) + 1e-9)
+    np.testing.assert_allclose(np.cov(Y.T), cov_o + jit * np.eye(24), atol=0.05 * var)
+
+
+def test_posterior_samples_default_jitter_large_batch(ctx):
+    """TuRBO's largest candidate set (5,000) in a small trust region: Σ is numerically singular."""
+    X, y, ls, var, og = fit(ctx, 256, 6, seed=31)
+    rng = np.random.default_rng(32)
+    Xc = 0.45 + 0.1 * rng.uniform(0, 1, (5000, 6))
+    Z = rng.standard_normal((8, 5000))
+    Y, jit = ctx.posterior_samples(0, dev(Xc), dev(Z))
+    Y = Y.cpu().numpy()
+    assert np.all(np.isfinite(Y)) and jit <= 1e-2 * var
+    mu, v = og.predict(Xc)
+    # a draw stays within a few posterior standard deviations of the mean
+    dev_sd = np.abs(Y - mu[:, 0]) / np.sqrt(np.maximum(v[:, 0], 0) + jit)
+    assert np.mean(dev_sd < 6) > 0.999
+
+
+# ----------------------------------------------------------------------------- selection
+def check_select(ctx, y_cand):
+    B = y_cand.shape[-1]
+    Y = np.ascontiguousarray(np.moveaxis(y_cand, -1, 0).reshape(B, -1))
+    got = ctx.thompson_select(dev(Y)).cpu().numpy()
+    np.testing.assert_array_equal(got, oturbo.select(y_cand))
+
+
+def test_select_turbo1_shapes(ctx):
+    rng = np.random.default_rng(41)
+    for N, B in [(1, 1), (40, 5), (7, 9), (600, 64), (5000, 100), (65537, 3)]:
+        y = rng.standard_normal((N, 1, B))
+        if N > 10:
+            y[3, 0, :] = y[5, 0, :]                  # ties: lowest index wins
+            y[8, 0, 1] = np.nan                      # np.argmin: the first NaN wins
+            y[9, 0, 0] = np.inf
+        check_select(ctx, y)
+
+
+def test_select_turbo_m_shapes(ctx):
+    rng = np.random.default_rng(42)
+    for T, N, B in [(3, 50, 6), (2, 5, 10), (5, 3000, 32)]:
+        y = rng.standard_normal((T, N, B))
+        y[1, 2] = y[0, 3]                            # a tie across trust regions
+        check_select(ctx, y)
+
+
+def test_select_all_equal_and_exhausted(ctx):
+    check_select(ctx, np.zeros((4, 1, 9)))           # more samples than candidates: picks repeat index 0
+    check_select(ctx, np.full((6, 1, 3), np.inf))
+
+
+def test_thompson_errors(ctx):
+    from optimobo_amd import _lib
+    fit(ctx, 20, 2, seed=1)
+    with pytest.raises(_lib.OMBError) as e:
+        ctx.thompson_select(torch.zeros((2, 0), dtype=torch.float64, device="cuda:0"))
+    assert e.value.code == _lib.OMB_EINVAL
+    with pytest.raises(_lib.OMBError) as e:
+        ctx.posterior_cov(5, dev(np.zeros((3, 2))))
+    assert e.value.code == _lib.OMB_ESTATE
+    with pytest.raises(_lib.OMBError) as e:
+        ctx.posterior_samples(0, dev(np.zeros((40000, 2))), torch.zeros((1, 40000), dtype=torch.float64,
+                                                                          device="cuda:0"))
+    assert e.value.code == _lib.OMB_EUNSUP
+
+
+# ----------------------------------------------------------------------------- drop-in surface
+def _zdt(n_var):
+    from optimobo_amd.problem import ElementwiseProblem
+
+    class ZDT1(ElementwiseProblem):          # optimobo/problem.py:924-936
+        def __init__(self):
+            super().__init__(n_var=n_var, n_obj=2, xl=np.zeros(n_var), xu=np.ones(n_var))
+
+        def _evaluate(self, x, out, *args, **kwargs):
+            f1 = x[0]
+            g = 1 + 9.0 / (n_var - 1) * np.sum(x[1:])
+            out["F"] = [f1, g * (1 - np.sqrt(f1 / g))]
+    return ZDT1()
+
+
+def test_gp_full_cov_and_posterior_samples_shapes():
+    from optimobo_amd.gp import GPRegression, Matern52
+    rng = np.random.default_rng(51)
+    X = rng.uniform(0, 1, (25, 3))
+    y = np.sin(5 * X).sum(1, keepdims=True)
+    m = GPRegression(X, y, Matern52(3, variance=float(np.var(y)), lengthscale=[0.5, 0.8, 1.0], ARD=True))
+    m.Gaussian_noise.variance.fix(0)
+    Xc = rng.uniform(0, 1, (60, 3))
+    mu, cov = m.predict(Xc, full_cov=True)
+    mu_o, cov_o = ogp.ExactGP(X, y, [0.5, 0.8, 1.0], float(np.var(y))).predict_full_cov(Xc)
+    assert mu.shape == (60, 1) and cov.shape == (60, 60)
+    np.testing.assert_allclose(cov, cov_o, rtol=1e-6, atol=1e-9 * float(np.var(y)))
+    np.random.seed(0)
+    s = m.posterior_samples(Xc, size=7)
+    assert s.shape == (60, 1, 7) and np.all(np.isfinite(s))
+
+
+def test_select_candidates_host_values_match_reference_rule():
+    from optimobo_amd.algorithms.turbo import TuRBO_1, TuRBO_M
+    rng = np.random.default_rng(52)
+    t = object.__new__(TuRBO_1)
+    t.batch_size, t.device = 6, None
+    X = rng.uniform(0, 1, (40, 3))
+    y = rng.standard_normal((40, 1, 6))
+    np.testing.assert_array_equal(t.select_candidates(X, y), X[oturbo.select(y)])
+    m = object.__new__(TuRBO_M)
+    m.n_trust_regions, m.n_cand, m.batch_size, m.device = 3, 40, 6, None
+    Xm = rng.uniform(0, 1, (3, 40, 3))
+    ym = rng.standard_normal((3, 40, 6))
+    Xn, idx = m._select_candidates(Xm, ym)
+    flat = oturbo.select(ym)
+    i, j = np.unravel_index(flat, (3, 40))
+    np.testing.assert_array_equal(Xn, Xm[i, j])
+    np.testing.assert_array_equal(idx[:, 0], i)
+
+
+def test_turbo1_and_turbo_m_solve():
+    from optimobo_amd.algorithms import TuRBO_1, TuRBO_M
+    import optimobo_amd.scalarisations as sc
+    np.random.seed(5)
+    p = _zdt(4)
+    r1 = TuRBO_1(p, batch_size=4, ideal_point=[0, 0], max_point=[1, 10]).solve(
+        sc.Tchebicheff([0, 0], [1, 10]), budget=16, n_init_samples=6)
+    assert r1.ysample.shape[0] >= 16 and np.all((r1.Xsample >= 0) & (r1.Xsample <= 1))
+    rm = TuRBO_M(p, [0, 0], [1, 10], batch_size=4, n_trust_regions=2).solve(
+        sc.Tchebicheff([0, 0], [1, 10]), budget=20, n_init_samples=5)
+    assert rm.ysample.shape[0] >= 20 and rm.ysample.shape[1] == 2

@@ -229,3 +229,53 @@ def test_gp_fit_gradient_and_improvement():
     before = m.log_likelihood()
     m.optimize(max_f_eval=200)
     assert m.log_likelihood() >= before
+
+
+# ----------------------------------------------------------------------------- TuRBO host logic
+def test_turbo_candidate_points_golden(golden_dir):
+    """TuRBO_1 candidate generation (turbo.py:79-111) bit-exact against the reference run with
+    the same numpy seed (tests/golden/turbo.npz)."""
+    from optimobo_amd.algorithms.turbo import TuRBO_1
+    z = np.load(os.path.join(golden_dir, "turbo.npz"))
+
+    class Duck:
+        def __init__(self, ls):
+            self.kern = type("K", (), {"lengthscale": ls})()
+
+    for c in range(4):
+        Xs = z[f"cc{c}_Xs"]
+        t = object.__new__(TuRBO_1)
+        t.n_vars = Xs.shape[1]
+        t.n_cand = z[f"cc{c}_Xc"].shape[0]
+        np.random.seed(int(z[f"cc{c}_seed"]))
+        Xc = t._candidate_points(Xs, z[f"cc{c}_ys"], Duck(z[f"cc{c}_ls"]), float(z[f"cc{c}_length"]))
+        np.testing.assert_array_equal(Xc, z[f"cc{c}_Xc"])
+
+
+def test_turbo_adjust_length_golden(golden_dir):
+    """Trust-region length rules of TuRBO_1 (turbo.py:127-140) and TuRBO_M (:347-363)."""
+    from optimobo_amd.algorithms.turbo import TuRBO_1, TuRBO_M
+    z = np.load(os.path.join(golden_dir, "turbo.npz"))
+    t = object.__new__(TuRBO_1)
+    t.batch_size, t.n_vars = 4, 5
+    t.failtol = np.ceil(np.max([4.0 / 4, 5 / 4]))
+    t.succtol, t.length_max, t.length_init = 3, 1.6, 0.4
+    t._restart()
+    t._aggregated_samples = z["al1_init"].copy()
+    for fx, want in zip(z["al1_seq"], z["al1_traj"]):
+        t._adjust_length(fx)
+        assert (t.length, t.succcount, t.failcount) == tuple(want)
+        t._aggregated_samples = np.vstack((t._aggregated_samples, fx.reshape(-1, 1)))
+    m = object.__new__(TuRBO_M)
+    m.n_trust_regions, m.batch_size, m.n_vars = 3, 4, 5
+    m.length_init, m.length_max, m.succtol, m.failtol = 0.4, 1.6, 3, 5
+    m._restart()
+    m.ysample, m._idx = z["alm_ys0"].copy(), z["alm_idx0"].copy()
+    off = 0
+    for i, L, want in zip(z["alm_regions"], z["alm_lens"], z["alm_traj"]):
+        fx = z["alm_vals"][off:off + L]
+        off += L
+        m._adjust_length(fx, int(i))
+        np.testing.assert_array_equal(np.concatenate([m.length, m.succcount, m.failcount]), want)
+        m.ysample = np.vstack((m.ysample, np.column_stack([fx, fx])))
+        m._idx = np.vstack((m._idx, int(i) * np.ones((L, 1), dtype=int)))

@@ -179,3 +179,39 @@ def test_exact_ehvi3d_matches_monte_carlo():
     y = rng.standard_normal((40000, 3)) * sd + mu[:, 0]
     hvi = np.prod(np.clip(hi[None] - np.maximum(y[:, None, :], lo[None]), 0, None), axis=2).sum(1)
     assert abs(ex - hvi.mean()) < 4 * hvi.std() / np.sqrt(len(hvi))
+
+
+# ----------------------------------------------------------------------------- TuRBO selection
+def test_turbo_select_vs_reference_golden(golden_dir):
+    """oracle.turbo.select against TuRBO_1.select_candidates / TuRBO_M._select_candidates run
+    on the reference itself (turbo.py:142-153, 365-383)."""
+    from oracle import turbo as oturbo
+    z = np.load(os.path.join(golden_dir, "turbo.npz"))
+    for c in range(3):
+        idx = oturbo.select(z[f"s1_{c}_y"])
+        np.testing.assert_array_equal(z[f"s1_{c}_X"][idx], z[f"s1_{c}_Xnext"])
+    for c in range(2):
+        y = z[f"sm_{c}_y"]
+        idx = oturbo.select(y)
+        i, j = np.unravel_index(idx, y.shape[:2])
+        np.testing.assert_array_equal(z[f"sm_{c}_X"][i, j], z[f"sm_{c}_Xnext"])
+        np.testing.assert_array_equal(i, z[f"sm_{c}_idx"][:, 0])
+
+
+def test_full_cov_vs_sklearn():
+    """oracle.gp.ExactGP.predict_full_cov (GPy _raw_predict full_cov) against scikit-learn's
+    GaussianProcessRegressor.predict(return_cov=True) with the same kernel (independent pin)."""
+    from sklearn.gaussian_process import GaussianProcessRegressor
+    from sklearn.gaussian_process.kernels import ConstantKernel, Matern
+    rng = np.random.default_rng(7)
+    X = rng.uniform(0, 1, (60, 3))
+    y = np.sin(4 * X).sum(1)
+    ls = np.array([0.3, 0.7, 1.2])
+    var = float(np.var(y))
+    Xc = rng.uniform(0, 1, (90, 3))
+    mu, cov = ogp.ExactGP(X, y, ls, var).predict_full_cov(Xc)
+    kern = ConstantKernel(var, "fixed") * Matern(length_scale=ls, length_scale_bounds="fixed", nu=2.5)
+    gpr = GaussianProcessRegressor(kernel=kern, alpha=1e-8, optimizer=None).fit(X, y)
+    mu_s, cov_s = gpr.predict(Xc, return_cov=True)
+    np.testing.assert_allclose(mu, mu_s, rtol=1e-6, atol=1e-8)
+    np.testing.assert_allclose(cov, cov_s, rtol=1e-6, atol=1e-9 * var)

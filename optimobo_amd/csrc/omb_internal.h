@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "../../include/optimobo_hip.h"
+#include "omb_math.h"
 
 namespace omb {
 
@@ -32,6 +33,7 @@ struct GPArgs {
   GPDev gp[OMB_MAX_OBJ];
   int d;    // true n_var (≤ DP)
   int DP;   // padded dim used by the packed Xs
+  ExpCoef ec;      // exp_nonpos coefficients as kernel arguments (set by launch_posterior)
 };
 
 // ---------------------------------------------------------------------------------------

@@ -90,7 +90,7 @@ hipError_t launch_pack_gp(hipStream_t stream, int n, int d, int DP, const double
 // tools/ablate/ablate_kblock measured 3.47 → 4.20 TB/s for 64-row plain → 256-row nt.
 template <int DP, int KIND>
 __global__ __launch_bounds__(256) void kernel_block_kernel(GPDev g, int d, const double* __restrict__ Xc,
-                                                           int64_t N, double* __restrict__ K) {
+                                                           int64_t N, double* __restrict__ K, ExpCoef ec) {
   constexpr int kRows = kKBlockRows;
   const int64_t c = 2 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
   if (c >= N) return;
@@ -115,8 +115,8 @@ __global__ __launch_bounds__(256) void kernel_block_kernel(GPDev g, int d, const
       dot1 = fma(xr[j], b1[j], dot1);
     }
     const double xk = g.xsq[k];
-    double v0 = kernel_of_r2<KIND>(fma(-2.0, dot0, xk + s0), g.variance);
-    double v1 = kernel_of_r2<KIND>(fma(-2.0, dot1, xk + s1), g.variance);
+    double v0, v1;
+    kernel_of_r2_k_x2<KIND>(fma(-2.0, dot0, xk + s0), fma(-2.0, dot1, xk + s1), g.variance, ec, v0, v1);
     double* dst = K + (int64_t)k * N + c;
     if (two && ((N & 1) == 0)) {
       __builtin_nontemporal_store(d2{v0, v1}, reinterpret_cast<d2*>(dst));
@@ -132,7 +132,9 @@ __global__ __launch_bounds__(256) void kernel_block_kernel(GPDev g, int d, const
 // transform by the raw dot product, bit 2 skips the MFMA phase, bit 4 feeds a constant A
 // operand instead of loading L⁻¹, bit 8 drops the per-chunk barrier (barrier mode only), bit 16
 // uses libm exp/sqrt, bit 32 selects the 2-buffer / block-barrier pipeline instead of the
-// counter-synchronised 3-buffer ring (tools/ablate: 12.03 → 11.23 ms at n = 512, N = 2^20).
+// counter-synchronised 3-buffer ring (tools/ablate: 12.03 → 11.23 ms at n = 512, N = 2^20); bit 128
+// gives waves 4-7 static priority 1, bit 256 drops the σ_f² multiply, bit 512 starts the distance
+// chain at ‖x‖² + ‖x*‖² with −2x* pre-scaled (one fma fewer per element).
 // NW = waves per workgroup (8 or 16): waves w, w+4, w+8, w+12 share a SIMD.
 template <int RT, int CT, int DP, int KIND, int NW = 8, int ABL = 0>
 __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args, const double* __restrict__ Xc,
@@ -186,6 +188,14 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
     }
   }
   const int gen_ct = cg >> 4, gen_cc = cg & 15;
+  if constexpr ((ABL & 128) != 0) {
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+  }
+  double bm2[(ABL & 512) && !kCandLds ? DP : 1];
+  if constexpr ((ABL & 512) && !kCandLds) {
+#pragma unroll
+    for (int j = 0; j < DP; ++j) bm2[j] = -2.0 * b[j];
+  }
 
   // ---- row-tile slots of this wave (SIMD balanced, see header): SIMD group s = wave & 3 owns
   // tile 4q + ((s + q) & 3) of every quad q; the G waves of the group take quads in snake order
@@ -211,23 +221,67 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
     for (int ct = 0; ct < CT; ++ct) acc[j][ct] = d4{0.0, 0.0, 0.0, 0.0};
   double mu_part = 0.0;
 
+  // one K* element: Matern (or RBF) of training row k and this thread's candidate
+  auto element = [&](int k) -> double {
+    const double* xr = g.Xs + (int64_t)k * DP;
+    if constexpr ((ABL & 512) && !kCandLds) {
+      double r2 = g.xsq[k] + csq;
+#pragma unroll
+      for (int j = 0; j < DP; ++j) r2 = fma(xr[j], bm2[j], r2);
+      return (ABL & 16) ? kernel_of_r2<KIND, false>(r2, (ABL & 256) ? 1.0 : g.variance)
+                        : kernel_of_r2_k<KIND>(r2, (ABL & 256) ? 1.0 : g.variance, args.ec);
+    } else {
+      double dot = 0.0;
+#pragma unroll
+      for (int j = 0; j < DP; ++j) dot = fma(xr[j], kCandLds ? cand[j * BN + cg] : b[j], dot);
+      if constexpr (ABL & 1) return dot;
+      return (ABL & 16) ? kernel_of_r2<KIND, false>(fma(-2.0, dot, g.xsq[k] + csq), (ABL & 256) ? 1.0 : g.variance)
+                        : kernel_of_r2_k<KIND>(fma(-2.0, dot, g.xsq[k] + csq), (ABL & 256) ? 1.0 : g.variance,
+                                               args.ec);
+    }
+  };
+  // row of the chunk this lane generates in pass i; with BN = 64 a wave covers exactly one row, so
+  // the row is wave-uniform and Xs / xsq / α come through scalar loads
+  auto chunk_row = [&](int i) { return (BN == 64) ? wave + NW * i : (tid + NT * i) / BN; };
+  static_assert(EPT % 2 == 0, "generation runs two rows per step");
+  // the lockstep pair needs ~20 more VGPRs: variants already near the register limit keep one row per step
+  constexpr bool kPairs = !kCandLds && !(ABL & (1 | 16 | 512));
   auto generate = [&](int kc, double* buf) {
+    if (kPairs && (kc + 1) * kChunkRows <= g.n) {
+      // whole chunk inside the training set: no per-row guard, and two independent rows per step
+      // so the scheduler interleaves their ~50-deep fp64 dependency chains (one chain alone leaves
+      // the VALU waiting on its own results about half the time)
+#pragma unroll
+      for (int i = 0; i < EPT; i += 2) {
+        const int kl0 = chunk_row(i), kl1 = chunk_row(i + 1);
+        const int k0 = kc * kChunkRows + kl0, k1 = kc * kChunkRows + kl1;
+        double v0, v1;
+        {
+          const double* x0 = g.Xs + (int64_t)k0 * DP;
+          const double* x1 = g.Xs + (int64_t)k1 * DP;
+          double d0 = 0.0, d1 = 0.0;
+#pragma unroll
+          for (int j = 0; j < DP; ++j) {
+            d0 = fma(x0[j], b[j], d0);
+            d1 = fma(x1[j], b[j], d1);
+          }
+          kernel_of_r2_k_x2<KIND>(fma(-2.0, d0, g.xsq[k0] + csq), fma(-2.0, d1, g.xsq[k1] + csq),
+                                  (ABL & 256) ? 1.0 : g.variance, args.ec, v0, v1);
+        }
+        mu_part = fma(g.alpha[k0], v0, mu_part);
+        mu_part = fma(g.alpha[k1], v1, mu_part);
+        buf[((kl0 >> 2) * CT + gen_ct) * 64 + (kl0 & 3) * 16 + gen_cc] = v0;
+        buf[((kl1 >> 2) * CT + gen_ct) * 64 + (kl1 & 3) * 16 + gen_cc] = v1;
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < EPT; ++i) {
-      // row of the chunk this lane generates; with BN = 64 a wave covers exactly one row, so the
-      // row is wave-uniform and Xs / xsq / α come through scalar loads
-      const int kl = (BN == 64) ? wave + NW * i : (tid + NT * i) / BN;
+      const int kl = chunk_row(i);
       const int k = kc * kChunkRows + kl;
       double val = 0.0;
       if (k < g.n) {
-        const double* xr = g.Xs + (int64_t)k * DP;
-        double dot = 0.0;
-#pragma unroll
-        for (int j = 0; j < DP; ++j) dot = fma(xr[j], kCandLds ? cand[j * BN + cg] : b[j], dot);
-        if constexpr (ABL & 1)
-          val = dot;
-        else
-          val = kernel_of_r2<KIND, !(ABL & 16)>(fma(-2.0, dot, g.xsq[k] + csq), g.variance);
+        val = element(k);
         mu_part = fma(g.alpha[k], val, mu_part);
       }
       buf[((kl >> 2) * CT + gen_ct) * 64 + (kl & 3) * 16 + gen_cc] = val;
@@ -427,7 +481,8 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior2p_kernel(GPArgs arg
       if constexpr (ABL & 1)
         val = dot;
       else
-        val = kernel_of_r2<KIND, !(ABL & 16)>(fma(-2.0, dot, g.xsq[k] + csq), g.variance);
+        val = (ABL & 16) ? kernel_of_r2<KIND, false>(fma(-2.0, dot, g.xsq[k] + csq), g.variance)
+                         : kernel_of_r2_k<KIND>(fma(-2.0, dot, g.xsq[k] + csq), g.variance, args.ec);
       mu_part = fma(g.alpha[k], val, mu_part);
     }
     if (k < n_pad) kbuf[((k >> 2) * CT + gen_ct) * 64 + (k & 3) * 16 + gen_cc] = val;
@@ -541,8 +596,10 @@ static hipError_t launch_posterior_kind(hipStream_t stream, const GPArgs& args, 
   }
 }
 
-hipError_t launch_posterior(hipStream_t stream, const GPArgs& args, int n_obj, int max_R, const double* Xc,
+hipError_t launch_posterior(hipStream_t stream, const GPArgs& args_in, int n_obj, int max_R, const double* Xc,
                             int64_t N, double* mu, double* var) {
+  GPArgs args = args_in;
+  args.ec = exp_coef();
   if (args.gp[0].kind == OMB_KERNEL_RBF) return launch_posterior_kind<OMB_KERNEL_RBF>(stream, args, n_obj, max_R, Xc, N, mu, var);
   return launch_posterior_kind<OMB_KERNEL_MATERN52>(stream, args, n_obj, max_R, Xc, N, mu, var);
 }
@@ -554,7 +611,7 @@ static hipError_t launch_kblock_kind(hipStream_t stream, const GPArgs& args, int
   dim3 grid((unsigned)((N + 511) / 512), (unsigned)((g.n + kKBlockRows - 1) / kKBlockRows));
   switch (args.DP) {
 #define OMB_KB(DPV) \
-  case DPV: hipLaunchKernelGGL((kernel_block_kernel<DPV, KIND>), grid, dim3(256), 0, stream, g, args.d, Xc, N, K); break;
+  case DPV: hipLaunchKernelGGL((kernel_block_kernel<DPV, KIND>), grid, dim3(256), 0, stream, g, args.d, Xc, N, K, exp_coef()); break;
     OMB_KB(2) OMB_KB(4) OMB_KB(6) OMB_KB(8) OMB_KB(16) OMB_KB(32)
 #undef OMB_KB
     default: return hipErrorInvalidValue;

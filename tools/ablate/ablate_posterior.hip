@@ -74,6 +74,7 @@ int main(int argc, char** argv) {
   for (int o = 0; o < 2; ++o) b.a.gp[o] = GPDev{Xs, xsq, al, Lp, ls, 1.0, n, R, 0, 0};
   b.a.d = d;
   b.a.DP = DP;
+  b.a.ec = exp_coef();
   b.Xc = Xc;
   b.N = N;
   b.mu = mu;
@@ -87,6 +88,11 @@ int main(int argc, char** argv) {
       {"no Matern (1)", run<4, 4, 8, 1>},
       {"no MFMA (2)", run<4, 4, 8, 2>},
       {"16 waves ring", run<2, 4, 16, 0>},
+      {"setprio waves 4-7 (128)", run<4, 4, 8, 128>},
+      {"no sigma_f^2 mul (256)", run<4, 4, 8, 256>},
+      {"fused r2 chain (512)", run<4, 4, 8, 512>},
+      {"256+512", run<4, 4, 8, 768>},
+      {"128+256+512", run<4, 4, 8, 896>},
   };
   const int NV = sizeof(vs) / sizeof(vs[0]);
   std::vector<float> t(NV, 0.f);

@@ -15,13 +15,15 @@
 //   cand_cov_kernel    lower triangle of K(X*, X*) (GPy _unscaled_dist: diagonal forced to 0).
 //   chol_panel_kernel  one step of a blocked right-looking Cholesky: every workgroup factors the
 //                      64×64 diagonal block with its first wave (lane r keeps row r in registers,
-//                      pivots and multipliers broadcast by v_readlane), the last workgroup to finish
+//                      pivots by v_readlane, multipliers by LDS broadcast), the last workgroup to finish
 //                      writes it back, and each thread solves one row of the panel below (the row in
 //                      64 registers, L_kk read from LDS as a broadcast).  The
 //                      trailing update A22 −= L21 L21ᵀ is the lower-triangle GEMM.
 //   select_kernel      the greedy per-sample arg-min (np.argmin order) with an LDS exclusion bitmap.
 // The factor is chol(Σ + jitter·I): numpy factors Σ by SVD instead; both draw from N(μ, Σ) up to
 // the jitter, which the caller bounds (omb_posterior_samples).
+#include <type_traits>
+
 #include "omb_internal.h"
 #include "omb_math.h"
 
@@ -195,20 +197,49 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
   return __builtin_bit_cast(double, (long long)(((unsigned long long)hi << 32) | lo));
 }
 
+// v[k] += s·w[k] for k = j+1 .. 63, w a same-address (broadcast) LDS row: the loads go out 16
+// values (8 ds_read_b128) at a time ahead of their fmas, so the LDS latency is paid once per 16
+// columns instead of once per load (j is a compile-time constant in the unrolled callers).
+template <int J>
+__device__ __forceinline__ void axpy_tail(double (&v)[kNB], double s, const double* w) {
+#pragma unroll
+  for (int kb = (J + 1) / 16 * 16; kb < kNB; kb += 16) {
+    double2 wv[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) wv[q] = reinterpret_cast<const double2*>(w + kb)[q];
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      if (kb + q > J) v[kb + q] = fma(s, (q & 1) ? wv[q >> 1].y : wv[q >> 1].x, v[kb + q]);
+  }
+}
+
+// Compile-time loop: f(std::integral_constant<int, I>) for I = B .. E-1.
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
 // Step `step` (columns c0 = 64·step ..) of the lower Cholesky of the N×N matrix A (row-major,
 // lower triangle read and written, upper untouched).  info (1-based column of the first
 // non-positive pivot, LAPACK dpotrf convention) is set once and stops later steps.
+// ABL (tools/ablate only; the library uses 0): bit 1 skips the diagonal factorisation (identity
+// factor), bit 2 skips the panel solve.
+template <int ABL = 0>
 __global__ __launch_bounds__(256) void chol_panel_kernel(double* __restrict__ A, int64_t N, int64_t lda, int step,
                                                          int* __restrict__ info, int* __restrict__ done_ctr) {
-  __shared__ double Ls[kNB][kNB + 1];
+  __shared__ __attribute__((aligned(16))) double LsT[kNB][kNB + 2];   // LsT[c][r] = L_kk[r][c]
   __shared__ double rinv[kNB];
+  __shared__ __attribute__((aligned(16))) double col[kNB];
   if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
   const int64_t c0 = (int64_t)step * kNB;
   const int nb = (int)((N - c0) < kNB ? (N - c0) : kNB);
   const int tid = threadIdx.x;
   if (tid < 64) {
     // ---- factor the diagonal block with one wave: lane r keeps row r in 64 registers (identity
-    // rows pad a short block); column j's pivot and multipliers are broadcast with v_readlane.
+    // rows pad a short block); column j's pivot comes by v_readlane, its multipliers through LDS.
     const int r = tid;
     double a[kNB];
 #pragma unroll
@@ -219,26 +250,32 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(double* __restrict__ A,
     }
     int bad = 0;
     double my_inv = 1.0;
-#pragma unroll
-    for (int j = 0; j < kNB; ++j) {
+    static_for<0, ((ABL & 1) ? 0 : kNB)>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
       double dj = readlane_f64(a[j], j);               // pivot (wave-uniform)
       if (!(dj > 0.0)) {
         if (bad == 0) bad = j + 1;
         dj = 1.0;                                      // continue without NaNs; flagged
       }
-      const double ljj = sqrt(dj);
-      const double inv = 1.0 / ljj;
+      // the column step's serial chain: sqrt_nonneg and a Newton-refined v_rcp_f64 instead of the
+      // IEEE sqrt and divide sequences (≤ 1 ulp apart; both enter every later column)
+      const double ljj = sqrt_nonneg(dj);
+      const double r0 = __builtin_amdgcn_rcp(ljj);
+      const double r1 = fma(r0, fma(-ljj, r0, 1.0), r0);
+      const double inv = fma(r1, fma(-ljj, r1, 1.0), r1);
       if (r == j) my_inv = inv;
       const double lrj = (r > j) ? a[j] * inv : (r == j ? ljj : 0.0);
       a[j] = lrj;
+      // column j to every lane through LDS (one store, then same-address broadcast reads; the
+      // wave's LDS accesses complete in order).  The update runs on every row unmasked: entries
+      // above the diagonal (k > r) collect junk that nothing reads.
+      col[r] = lrj;
+      __builtin_amdgcn_wave_barrier();
+      axpy_tail<j>(a, -lrj, col);
+      __builtin_amdgcn_wave_barrier();
+    });
 #pragma unroll
-      for (int k = j + 1; k < kNB; ++k) {
-        const double lkj = readlane_f64(lrj, k);
-        a[k] = (r >= k) ? fma(-lrj, lkj, a[k]) : a[k];
-      }
-    }
-#pragma unroll
-    for (int c = 0; c < kNB; ++c) Ls[r][c] = a[c];
+    for (int c = 0; c < kNB; ++c) LsT[c][r] = a[c];
     rinv[r] = my_inv;
     // the last workgroup to finish factoring writes L_kk back: every other one has consumed its
     // loads of A_kk by then (they fed the factorization before its counter increment)
@@ -246,27 +283,28 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(double* __restrict__ A,
     if (r == 0) old = atomicAdd(done_ctr + step, 1);
     if (__builtin_amdgcn_readfirstlane(old) == (int)gridDim.x - 1) {
       if (r < nb)
-        for (int c = 0; c <= r; ++c) A[(c0 + r) * lda + c0 + c] = Ls[r][c];
+        for (int c = 0; c <= r; ++c) A[(c0 + r) * lda + c0 + c] = LsT[c][r];
       if (r == 0 && bad) atomicCAS(info, 0, (int)(c0 + bad));
     }
   }
   __syncthreads();
   // ---- panel: rows below the block solve x · L_kkᵀ = b (forward substitution)
   const int64_t row = c0 + nb + (int64_t)blockIdx.x * blockDim.x + tid;
-  if (row >= N) return;
+  if ((ABL & 2) || row >= N) return;
   double* rp = A + row * lda + c0;
   // rows below the block exist only while a full block remains (nb == 64): unconditional
   // accesses keep x[] in registers (a per-column guard makes the compiler spill it)
   double x[kNB];
 #pragma unroll
   for (int c = 0; c < kNB; ++c) x[c] = rp[c];
-#pragma unroll
-  for (int j = 0; j < kNB; ++j) {
-    double s = x[j];
-#pragma unroll
-    for (int l = 0; l < j; ++l) s = fma(-x[l], Ls[j][l], s);
-    x[j] = s * rinv[j];
-  }
+  // column-oriented (right-looking) substitution: after x_j is final, every later x_k is updated
+  // independently — 63 independent fmas per step instead of one 2016-long dependent chain
+  static_for<0, kNB>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    const double xj = x[j] * rinv[j];
+    x[j] = xj;
+    axpy_tail<j>(x, -xj, LsT[j]);
+  });
 #pragma unroll
   for (int c = 0; c < kNB; ++c) rp[c] = x[c];
 }
@@ -379,7 +417,7 @@ hipError_t launch_cholesky(hipStream_t stream, double* A, int64_t N, int64_t lda
     const int64_t nb = (N - c0) < kNB ? (N - c0) : kNB;
     const int64_t rest = N - c0 - nb;
     const unsigned blocks = (unsigned)(rest > 0 ? (rest + 255) / 256 : 1);
-    hipLaunchKernelGGL(chol_panel_kernel, dim3(blocks), dim3(256), 0, stream, A, N, lda, k, info, done_ctr);
+    hipLaunchKernelGGL(chol_panel_kernel<0>, dim3(blocks), dim3(256), 0, stream, A, N, lda, k, info, done_ctr);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (rest > 0) {

@@ -164,7 +164,7 @@ def run_solve(args, cfg, world_size, rank):
             "config": {"workload": "README MyProblem (2-var, 2-obj), Tchebicheff expected decomposition, budget "
                                    f"{budget}, n_init 20, sample_exponent 3, {opt.n_candidates} device candidates "
                                    f"x {opt.refine_rounds + 1} rounds per iteration", "parallelism": "dp1"},
-            "split_s": {"gp_fit_host": split["fit"], "device_maximiser": split["maximise"],
+            "split_s": {"gp_fit": split["fit"], "device_maximiser": split["maximise"],
                         "other": el - split["fit"] - split["maximise"]},
             "final_hv": float(res.hypervolume_convergence[-1]), "n_evaluations": int(len(res.ysample)),
             "roofline": None, "cpu_baseline": None,

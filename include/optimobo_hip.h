@@ -247,6 +247,23 @@ int omb_posterior_samples(omb_ctx* ctx, int obj, const double* Xc_dev, int64_t N
  * (the reference sets y_cand[pick, :] = inf).  N ≤ 2^18.  Y is not modified.  Asynchronous. */
 int omb_thompson_select(omb_ctx* ctx, const double* Y_dev, int B, int64_t N, int64_t* idx_dev);
 
+/* ---------------------------------------------------------------------------------------
+ * GP fit on the device — GPy GPRegression(X, y, Matern52(d, ARD=True)) with the noise variance
+ * fixed (optimisers.py:223-231 and every other driver's fit): exact inference with GPy's jitchol
+ * (Ky = K + (σ_n² + 1e-8) I; on failure + mean(diag Ky)·1e-6·10^t, t < 5), the log marginal
+ * likelihood and its gradient for the hyperparameter search.  X_dev (n, d), y_dev (n) device.
+ * ------------------------------------------------------------------------------------- */
+/* *lml = log p(y | X, θ) = −½ yᵀα − Σ log L_ii − ½ n log 2π;  grad_host (d + 1) = ∂ lml / ∂(log σ_f²,
+ * log ℓ_1 .. log ℓ_d);  *jitter_used (may be NULL) = jitchol's extra jitter.  n ≤ 16384.
+ * Synchronises.  OMB_ENOTPD when even the jittered matrix is not positive definite. */
+int omb_gp_lml_grad(omb_ctx* ctx, int kernel, int n, int d, const double* X_dev, const double* y_dev,
+                    const double* lengthscale_host, double variance, double noise, double* lml, double* grad_host,
+                    double* jitter_used);
+/* Fit the exact-inference state of objective `obj` on the device (Cholesky, L⁻¹, α) and install
+ * it as omb_set_gp would — the device replacement for the host O(n³) factorisation. */
+int omb_gp_fit_state(omb_ctx* ctx, int obj, int kernel, int n, int d, const double* X_dev, const double* y_dev,
+                     const double* lengthscale_host, double variance, double noise, double* jitter_used);
+
 #ifdef __cplusplus
 }
 #endif

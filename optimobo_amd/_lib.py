@@ -66,6 +66,9 @@ SIGNATURES = {
     "omb_cholesky": (_i, [_p, _p, _i64, _i64, _d, ctypes.POINTER(_i)]),
     "omb_posterior_samples": (_i, [_p, _i, _p, _i64, _p, _i, _d, _i, _p, _dp]),
     "omb_thompson_select": (_i, [_p, _p, _i, _i64, _p]),
+    # GP fit on the device
+    "omb_gp_lml_grad": (_i, [_p, _i, _i, _i, _p, _p, _dp, _d, _d, _dp, _dp, _dp]),
+    "omb_gp_fit_state": (_i, [_p, _i, _i, _i, _i, _p, _p, _dp, _d, _d, _dp]),
 }
 
 

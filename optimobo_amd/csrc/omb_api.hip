@@ -66,6 +66,9 @@ struct omb_ctx {
   size_t tws_cap = 0;
   void* ichol = nullptr;
   size_t ichol_cap = 0;
+  // GP fit: Ky | L⁻¹ | Ky⁻¹ | scratch workspace
+  void* fws = nullptr;
+  size_t fws_cap = 0;
 };
 
 namespace {
@@ -386,6 +389,7 @@ int omb_destroy(omb_ctx* ctx) {
   if (ctx->sob) (void)hipFree(ctx->sob);
   if (ctx->tws) (void)hipFree(ctx->tws);
   if (ctx->ichol) (void)hipFree(ctx->ichol);
+  if (ctx->fws) (void)hipFree(ctx->fws);
   for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;
@@ -956,6 +960,120 @@ int omb_thompson_select(omb_ctx* ctx, const double* Y_dev, int B, int64_t N, int
   hipError_t e = launch_select(ctx->stream, Y_dev, B, N, idx_dev);
   if (e != hipSuccess) return hip_fail(ctx, e, "thompson_select");
   return OMB_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// GP fit on the device: GPy ExactGaussianInference + jitchol, log marginal
+// likelihood and its gradient for the L-BFGS hyperparameter search (optimisers.py:226-231).
+
+struct GPFactor {
+  double* Ky;      // (n, n): Ky, then its Cholesky factor (lower)
+  double* Linv;    // (n, n): L⁻¹ (upper triangle zero)
+  double* Kinv;    // (n, n): Ky⁻¹ (lower triangle)
+  double* T;       // (64, n) scratch of the triangular inverse
+  double* alpha;   // (n)
+  double* v;       // (n)
+  double* ls;      // (DP)
+  double* part;    // gp_grad_blocks(n)·(DP+1)
+  double* out;     // DP + 3
+  double jitter;   // jitter added by jitchol (0 when the first factorisation succeeded)
+};
+
+// Ky = K + (noise + 1e-8) I, L = jitchol(Ky) (GPy.util.linalg.jitchol: on failure add
+// mean(diag)·1e-6·10^t, t = 0..4), L⁻¹, α = Ky⁻¹ y.  Synchronises (the factorisation status).
+static int gp_factor(omb_ctx* ctx, int kernel, int n, int d, const double* X, const double* y, const double* ls_host,
+                     double variance, double noise, GPFactor* f) {
+  const int DP = pad_dim(d);
+  const size_t nn = (size_t)n * n;
+  const size_t doubles = 3 * nn + 64 * (size_t)n + 2 * (size_t)n + DP +
+                         (size_t)gp_grad_blocks(n) * (DP + 1) + DP + 3;
+  int rc = grow_dev(ctx, &ctx->fws, &ctx->fws_cap, sizeof(double) * doubles, "GP fit workspace");
+  if (rc) return rc;
+  double* p = static_cast<double*>(ctx->fws);
+  f->Ky = p; p += nn;
+  f->Linv = p; p += nn;
+  f->Kinv = p; p += nn;
+  f->T = p; p += 64 * (size_t)n;
+  f->alpha = p; p += n;
+  f->v = p; p += n;
+  f->ls = p; p += DP;
+  f->part = p; p += (size_t)gp_grad_blocks(n) * (DP + 1);
+  f->out = p;
+  void* h = nullptr;
+  if ((rc = stage_begin(ctx, sizeof(double) * DP, &h))) return rc;
+  for (int j = 0; j < DP; ++j) static_cast<double*>(h)[j] = (j < d) ? ls_host[j] : 1.0;
+  OMB_HIP(ctx, hipMemcpyAsync(f->ls, h, sizeof(double) * DP, hipMemcpyHostToDevice, ctx->stream));
+  GPDev g{};
+  g.ls = f->ls;
+  g.variance = variance;
+  g.kind = kernel;
+  const double base = noise + 1e-8;
+  const double mean_diag = variance + base;
+  int info = -1;
+  f->jitter = 0.0;
+  for (int t = -1; t < 5; ++t) {
+    const double jit = (t < 0) ? 0.0 : mean_diag * 1e-6 * pow(10.0, (double)t);
+    OMB_HIP(ctx, launch_cand_cov(ctx->stream, g, d, DP, X, n, f->Ky, n));
+    if ((rc = run_cholesky(ctx, f->Ky, n, n, base + jit, &info))) return rc;
+    if (info == 0) {
+      f->jitter = jit;
+      break;
+    }
+  }
+  if (info != 0) return fail(ctx, OMB_ENOTPD, "K + jitter is not positive definite, even with jitter (column %d)", info);
+  OMB_HIP(ctx, hipMemsetAsync(f->Linv, 0, sizeof(double) * nn, ctx->stream));
+  OMB_HIP(ctx, launch_trinv(ctx->stream, f->Ky, n, n, f->Linv, n, f->T));
+  // α = L⁻ᵀ (L⁻¹ y)
+  OMB_HIP(ctx, launch_gemm_nn(ctx->stream, n, 1, n, 1.0, f->Linv, n, y, 1, 0.0, f->v, 1));
+  OMB_HIP(ctx, launch_gemm_tn(ctx->stream, n, 1, n, 1.0, f->Linv, n, f->v, 1, 0.0, f->alpha, 1));
+  return OMB_OK;
+}
+
+int omb_gp_lml_grad(omb_ctx* ctx, int kernel, int n, int d, const double* X_dev, const double* y_dev,
+                    const double* lengthscale_host, double variance, double noise, double* lml, double* grad,
+                    double* jitter_used) {
+  int rc = enter(ctx);
+  if (rc) return rc;
+  if (kernel != OMB_KERNEL_MATERN52 && kernel != OMB_KERNEL_RBF) return fail(ctx, OMB_EINVAL, "unknown kernel %d", kernel);
+  if (n < 1 || n > 16384) return fail(ctx, OMB_EUNSUP, "n_train=%d outside [1, 16384]", n);
+  if (d < 1 || d > OMB_MAX_DIM) return fail(ctx, OMB_EUNSUP, "n_var=%d outside [1, %d]", d, OMB_MAX_DIM);
+  if (!X_dev || !y_dev || !lengthscale_host || !lml || !grad) return fail(ctx, OMB_EINVAL, "null pointer");
+  for (int j = 0; j < d; ++j)
+    if (!(lengthscale_host[j] > 0.0)) return fail(ctx, OMB_EINVAL, "lengthscale[%d]=%g must be > 0", j, lengthscale_host[j]);
+  if (!(variance > 0.0) || !(noise >= 0.0)) return fail(ctx, OMB_EINVAL, "variance must be > 0 and noise >= 0");
+  GPFactor f;
+  if ((rc = gp_factor(ctx, kernel, n, d, X_dev, y_dev, lengthscale_host, variance, noise, &f))) return rc;
+  const int DP = pad_dim(d);
+  // Ky⁻¹ = L⁻ᵀ L⁻¹ (lower triangle), then the gradient sums, log det and yᵀα
+  OMB_HIP(ctx, launch_gemm_tn_lower(ctx->stream, n, n, 1.0, f.Linv, n, 0.0, f.Kinv, n));
+  OMB_HIP(ctx, launch_gp_grad(ctx->stream, kernel, DP, X_dev, d, n, f.ls, variance, f.alpha, f.Kinv, n, f.part,
+                              f.Ky, n, y_dev, f.out));
+  double h[OMB_MAX_DIM + 3];
+  OMB_HIP(ctx, hipMemcpyAsync(h, f.out, sizeof(double) * (DP + 3), hipMemcpyDeviceToHost, ctx->stream));
+  OMB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  // GPy: log p(y) = −½ yᵀα − Σ log L_ii − ½ n log 2π
+  *lml = -0.5 * h[DP + 2] - h[DP + 1] - 0.5 * n * log(2.0 * M_PI);
+  for (int q = 0; q <= d; ++q) grad[q] = h[q];
+  if (jitter_used) *jitter_used = f.jitter;
+  return OMB_OK;
+}
+
+int omb_gp_fit_state(omb_ctx* ctx, int obj, int kernel, int n, int d, const double* X_dev, const double* y_dev,
+                     const double* lengthscale_host, double variance, double noise, double* jitter_used) {
+  int rc = enter(ctx);
+  if (rc) return rc;
+  if (obj < 0 || obj >= OMB_MAX_OBJ) return fail(ctx, OMB_EINVAL, "obj=%d outside [0, %d)", obj, OMB_MAX_OBJ);
+  if (kernel != OMB_KERNEL_MATERN52 && kernel != OMB_KERNEL_RBF) return fail(ctx, OMB_EINVAL, "unknown kernel %d", kernel);
+  if (n < 1 || n > OMB_MAX_TRAIN) return fail(ctx, OMB_EUNSUP, "n_train=%d outside [1, %d]", n, OMB_MAX_TRAIN);
+  if (d < 1 || d > OMB_MAX_DIM) return fail(ctx, OMB_EUNSUP, "n_var=%d outside [1, %d]", d, OMB_MAX_DIM);
+  if (!X_dev || !y_dev || !lengthscale_host) return fail(ctx, OMB_EINVAL, "null pointer");
+  for (int j = 0; j < d; ++j)
+    if (!(lengthscale_host[j] > 0.0)) return fail(ctx, OMB_EINVAL, "lengthscale[%d]=%g must be > 0", j, lengthscale_host[j]);
+  if (!(variance > 0.0) || !(noise >= 0.0)) return fail(ctx, OMB_EINVAL, "variance must be > 0 and noise >= 0");
+  GPFactor f;
+  if ((rc = gp_factor(ctx, kernel, n, d, X_dev, y_dev, lengthscale_host, variance, noise, &f))) return rc;
+  if (jitter_used) *jitter_used = f.jitter;
+  return omb_set_gp(ctx, obj, kernel, n, d, X_dev, lengthscale_host, variance, f.alpha, f.Linv);
 }
 
 }  // extern "C"

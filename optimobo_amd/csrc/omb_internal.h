@@ -115,6 +115,18 @@ hipError_t launch_cholesky(hipStream_t stream, double* A, int64_t N, int64_t lda
 hipError_t launch_chol_samples(hipStream_t stream, const double* L, int64_t N, int64_t ldl, const double* mu,
                                const double* Zt, int B, double* Y);
 hipError_t launch_select(hipStream_t stream, const double* Y, int B, int64_t N, int64_t* idx);
+// C (M, Nc) = β C + α AᵀB, A (K, M), B (K, Nc).
+hipError_t launch_gemm_tn(hipStream_t s, int64_t M, int64_t Nc, int64_t K, double alpha, const double* A, int64_t lda,
+                          const double* B, int64_t ldb, double beta, double* C, int64_t ldc);
+// X (n, n) = L⁻¹ for lower-triangular L; X zeroed by the caller; T: workspace of 64·n doubles.
+hipError_t launch_trinv(hipStream_t stream, const double* L, int64_t n, int64_t lda, double* X, int64_t ldx,
+                        double* T);
+// GP log-marginal-likelihood pieces: out[0..DP] = ½ Σ W ∂K/∂θ (θ = log σ_f², log ℓ_j; entries past
+// d are 0), out[DP+1] = Σ log L_ii, out[DP+2] = yᵀα.  partials: gp_grad_blocks(n)·(DP+1) doubles.
+int64_t gp_grad_blocks(int64_t n);
+hipError_t launch_gp_grad(hipStream_t stream, int kind, int DP, const double* X, int d, int64_t n, const double* ls,
+                          double variance, const double* alpha, const double* Kinv, int64_t ldk, double* partials,
+                          const double* L, int64_t lda, const double* y, double* out);
 
 // Packed-L^-1 size in doubles for R row tiles: Σ_{r<R} 4(r+1)·64 = 128·R·(R+1).
 inline int64_t packed_L_size(int R) { return 128ll * R * (R + 1); }

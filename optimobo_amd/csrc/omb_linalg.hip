@@ -309,6 +309,140 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(double* __restrict__ A,
   for (int c = 0; c < kNB; ++c) rp[c] = x[c];
 }
 
+// ----------------------------------------------------------------------------- triangular inverse
+// X = L⁻¹ for a lower-triangular L (n×n).  The 64×64 diagonal blocks are inverted in parallel (one
+// wave per block; lane c solves L_ii x = e_c by column-oriented substitution, the column of L_ii
+// read as an LDS broadcast), then block row i of X is −X_ii·(L[i, :i]·X[:i, :i]), two GEMMs per
+// block row (trinv_rows).  The caller zeroes X first (its upper triangle stays zero).
+__global__ __launch_bounds__(64) void trinv_diag_kernel(const double* __restrict__ L, int64_t n, int64_t lda,
+                                                        double* __restrict__ X, int64_t ldx) {
+  __shared__ __attribute__((aligned(16))) double LsT[kNB][kNB + 2];   // LsT[c][r] = L_ii[r][c]
+  __shared__ double rinv[kNB];
+  const int64_t c0 = (int64_t)blockIdx.x * kNB;
+  const int nb = (int)((n - c0) < kNB ? (n - c0) : kNB);
+  const int lane = threadIdx.x;
+  for (int c = 0; c < kNB; ++c) {
+    double v = (c == lane) ? 1.0 : 0.0;
+    if (lane < nb && c <= lane) v = L[(c0 + lane) * lda + c0 + c];
+    LsT[c][lane] = v;
+  }
+  __builtin_amdgcn_wave_barrier();
+  rinv[lane] = 1.0 / LsT[lane][lane];
+  __builtin_amdgcn_wave_barrier();
+  double x[kNB];
+#pragma unroll
+  for (int r = 0; r < kNB; ++r) x[r] = (r == lane) ? 1.0 : 0.0;
+  static_for<0, kNB>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    const double xj = x[j] * rinv[j];
+    x[j] = xj;
+    axpy_tail<j>(x, -xj, LsT[j]);
+  });
+  if (lane >= nb) return;
+  double* dst = X + c0 * ldx + c0 + lane;   // column `lane` of the block
+  if (nb == kNB) {
+#pragma unroll
+    for (int r = 0; r < kNB; ++r) dst[r * ldx] = x[r];
+  } else {
+    for (int r = 0; r < nb; ++r) {
+      double v = 0.0;
+#pragma unroll
+      for (int q = 0; q < kNB; ++q) v = (q == r) ? x[q] : v;
+      dst[r * ldx] = v;
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------- GP marginal likelihood
+// Gradient of GPy's log marginal likelihood for exact inference with a stationary ARD kernel,
+//   dL/dθ = ½ Σ_ik W_ik ∂K_ik/∂θ,  W = ααᵀ − Ky⁻¹   (ExactGaussianInference: dL_dK = ½(ααᵀ − Wi)),
+// θ = (log σ_f², log ℓ_1..d):  ∂K/∂log σ_f² = K (no noise),  ∂K/∂log ℓ_j = −(dK/dr / r)·(Δ_j/ℓ_j)².
+// One 16×16 tile per workgroup over the lower triangle (off-diagonal pairs count twice); each
+// workgroup writes its d+1 partial sums; gp_reduce_kernel adds them in a fixed order.
+template <int DP, int KIND>
+__global__ __launch_bounds__(256) void gp_grad_kernel(const double* __restrict__ X, int d, int64_t n,
+                                                      const double* __restrict__ ls, double variance,
+                                                      const double* __restrict__ alpha,
+                                                      const double* __restrict__ Kinv, int64_t ldk,
+                                                      double* __restrict__ partials) {
+  __shared__ double red[4][DP + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t i = (int64_t)blockIdx.y * 16 + (tid >> 4);
+  const int64_t k = (int64_t)blockIdx.x * 16 + (tid & 15);
+  double acc[DP + 1];
+#pragma unroll
+  for (int q = 0; q <= DP; ++q) acc[q] = 0.0;
+  if (blockIdx.x <= blockIdx.y && i < n && k <= i) {
+    double a[DP], b[DP], aa = 0.0, bb = 0.0, dot = 0.0;
+#pragma unroll
+    for (int j = 0; j < DP; ++j) {
+      a[j] = (j < d) ? X[i * d + j] / ls[j] : 0.0;
+      b[j] = (j < d) ? X[k * d + j] / ls[j] : 0.0;
+      aa += a[j] * a[j];
+      bb += b[j] * b[j];
+      dot = fma(a[j], b[j], dot);
+    }
+    double r2 = (i == k) ? 0.0 : fma(-2.0, dot, aa + bb);
+    r2 = r2 > 0.0 ? r2 : 0.0;
+    const double r = sqrt_nonneg(r2);
+    double Kik, dkr;   // K and (dK/dr)/r
+    if constexpr (KIND == OMB_KERNEL_MATERN52) {
+      const double e = exp_nonpos(-(kSqrt5 * r));
+      Kik = (variance * ((1.0 + kSqrt5 * r) + kFiveThirds * (r * r))) * e;
+      dkr = -kFiveThirds * variance * (1.0 + kSqrt5 * r) * e;
+    } else {
+      const double e = exp_nonpos(-0.5 * (r * r));
+      Kik = variance * e;
+      dkr = -variance * e;
+    }
+    const double f = (i == k) ? 0.5 : 1.0;
+    const double W = f * (alpha[i] * alpha[k] - Kinv[i * ldk + k]);
+    acc[0] = W * Kik;
+#pragma unroll
+    for (int j = 0; j < DP; ++j) {
+      const double dj = a[j] - b[j];
+      acc[1 + j] = W * (-dkr) * (dj * dj);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q <= DP; ++q) {
+    double v = acc[q];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off);
+    if (lane == 0) red[wave][q] = v;
+  }
+  __syncthreads();
+  const int64_t blk = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+  if (tid <= DP) partials[blk * (DP + 1) + tid] = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
+}
+
+// out[q] = Σ_blocks partials (q ≤ DP, fixed order); out[DP+1] = Σ log L_ii; out[DP+2] = yᵀα.
+__global__ __launch_bounds__(256) void gp_reduce_kernel(const double* __restrict__ partials, int64_t nblk, int P,
+                                                        const double* __restrict__ L, int64_t n, int64_t lda,
+                                                        const double* __restrict__ y,
+                                                        const double* __restrict__ alpha, double* __restrict__ out) {
+  __shared__ double red[256];
+  const int tid = threadIdx.x;
+  for (int q = 0; q < P + 2; ++q) {
+    double v = 0.0;
+    if (q < P) {
+      for (int64_t b = tid; b < nblk; b += 256) v += partials[b * P + q];
+    } else if (q == P) {
+      for (int64_t t = tid; t < n; t += 256) v += log(L[t * lda + t]);
+    } else {
+      for (int64_t t = tid; t < n; t += 256) v = fma(y[t], alpha[t], v);
+    }
+    red[tid] = v;
+    __syncthreads();
+    for (int s2 = 128; s2 > 0; s2 >>= 1) {
+      if (tid < s2) red[tid] += red[tid + s2];
+      __syncthreads();
+    }
+    if (tid == 0) out[q] = red[0];
+    __syncthreads();
+  }
+}
+
 // ----------------------------------------------------------------------------- selection
 // np.argmin order: the first NaN wins, else the smallest value, lowest index among ties.
 __device__ __forceinline__ bool sel_better(double v, int64_t i, double bv, int64_t bi) {
@@ -435,6 +569,58 @@ hipError_t launch_chol_samples(hipStream_t stream, const double* L, int64_t N, i
                                const double* Zt, int B, double* Y) {
   // Y (B, N) = Zt · Lᵀ + μ  with  op(B)(k, j) = L[j][k] for k ≤ j (the factor's upper part is ignored)
   return gemm<false, true, true, false>(stream, B, N, N, 1.0, Zt, N, L, ldl, 0.0, Y, N, mu);
+}
+
+hipError_t launch_gemm_tn(hipStream_t s, int64_t M, int64_t Nc, int64_t K, double alpha, const double* A, int64_t lda,
+                          const double* B, int64_t ldb, double beta, double* C, int64_t ldc) {
+  return gemm<true, false, false, false>(s, M, Nc, K, alpha, A, lda, B, ldb, beta, C, ldc, nullptr);
+}
+
+hipError_t launch_trinv(hipStream_t stream, const double* L, int64_t n, int64_t lda, double* X, int64_t ldx,
+                        double* T) {
+  const int64_t nbk = (n + kNB - 1) / kNB;
+  hipLaunchKernelGGL(trinv_diag_kernel, dim3((unsigned)nbk), dim3(64), 0, stream, L, n, lda, X, ldx);
+  hipError_t e = hipGetLastError();
+  for (int64_t i = 1; i < nbk && e == hipSuccess; ++i) {
+    const int64_t r0 = i * kNB, rows = (n - r0) < kNB ? (n - r0) : kNB;
+    // T (rows, r0) = L[r0:, :r0] · X[:r0, :r0];  X[r0:, :r0] = −X_ii · T
+    e = gemm<false, false, false, false>(stream, rows, r0, r0, 1.0, L + r0 * lda, lda, X, ldx, 0.0, T, r0, nullptr);
+    if (e == hipSuccess)
+      e = gemm<false, false, false, false>(stream, rows, r0, rows, -1.0, X + r0 * ldx + r0, ldx, T, r0, 0.0,
+                                           X + r0 * ldx, ldx, nullptr);
+  }
+  return e;
+}
+
+int64_t gp_grad_blocks(int64_t n) {
+  const int64_t t = (n + 15) / 16;
+  return t * t;
+}
+
+hipError_t launch_gp_grad(hipStream_t stream, int kind, int DP, const double* X, int d, int64_t n, const double* ls,
+                          double variance, const double* alpha, const double* Kinv, int64_t ldk, double* partials,
+                          const double* L, int64_t lda, const double* y, double* out) {
+  const unsigned t = (unsigned)((n + 15) / 16);
+  dim3 grid(t, t);
+#define OMB_GG(DPV)                                                                                              \
+  case DPV:                                                                                                      \
+    if (kind == OMB_KERNEL_RBF)                                                                                  \
+      hipLaunchKernelGGL((gp_grad_kernel<DPV, OMB_KERNEL_RBF>), grid, dim3(256), 0, stream, X, d, n, ls, variance, \
+                         alpha, Kinv, ldk, partials);                                                            \
+    else                                                                                                         \
+      hipLaunchKernelGGL((gp_grad_kernel<DPV, OMB_KERNEL_MATERN52>), grid, dim3(256), 0, stream, X, d, n, ls,      \
+                         variance, alpha, Kinv, ldk, partials);                                                  \
+    break;
+  switch (DP) {
+    OMB_GG(2) OMB_GG(4) OMB_GG(6) OMB_GG(8) OMB_GG(16) OMB_GG(32)
+    default: return hipErrorInvalidValue;
+  }
+#undef OMB_GG
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(gp_reduce_kernel, dim3(1), dim3(256), 0, stream, partials, (int64_t)t * t, DP + 1, L, n, lda, y,
+                     alpha, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_select(hipStream_t stream, const double* Y, int B, int64_t N, int64_t* idx) {

@@ -84,6 +84,9 @@ class AcqContext:
         self.gp_info[obj] = dict(n=n, d=d, variance=float(variance), kernel=kernel)
 
     def set_gp_state(self, obj, state):
+        if hasattr(state, "upload"):          # DeviceGPState: factorised on the device
+            state.upload(self, obj)
+            return
         self.set_gp(obj, state.X, state.lengthscale, state.variance, state.alpha, state.Linv, state.kernel)
 
     # ------------------------------------------------------------------ posterior
@@ -273,6 +276,40 @@ class AcqContext:
         self._stream()
         self._check(self.lib.omb_eval_argmax_sobol(self._h, int(start), int(N), _ptr(out)), "omb_eval_argmax_sobol")
         return out
+
+    # ------------------------------------------------------------------ GP fit on the device
+    def gp_lml_grad(self, X, y, lengthscale, variance, noise=0.0, kernel="matern52"):
+        """GPy's exact-inference log marginal likelihood at (σ_f², ℓ) with the noise fixed, its gradient
+        w.r.t. (log σ_f², log ℓ_1..d) and jitchol's extra jitter: (lml, grad (d+1,), jitter)."""
+        X = _dev_f64(X, self.device)
+        y = _dev_f64(y, self.device).reshape(-1)
+        n, d = X.shape
+        if y.shape[0] != n:
+            raise ValueError(f"gp_lml_grad: y has {y.shape[0]} values for {n} inputs")
+        ls = np.broadcast_to(np.asarray(lengthscale, np.float64), (d,))
+        kid = {"matern52": _lib.KERNEL_MATERN52, "rbf": _lib.KERNEL_RBF}[kernel]
+        lml, jit = ctypes.c_double(), ctypes.c_double()
+        grad = (ctypes.c_double * (d + 1))()
+        self._stream()
+        self._check(self.lib.omb_gp_lml_grad(self._h, kid, n, d, _ptr(X), _ptr(y), _lib.darr(ls), float(variance),
+                                             float(noise), ctypes.byref(lml), grad, ctypes.byref(jit)),
+                    "omb_gp_lml_grad")
+        return lml.value, np.array(grad[:]), jit.value
+
+    def gp_fit_state(self, obj, X, y, lengthscale, variance, noise=0.0, kernel="matern52"):
+        """Factorise on the device and install objective ``obj`` (omb_gp_fit_state); returns the jitter."""
+        X = _dev_f64(X, self.device)
+        y = _dev_f64(y, self.device).reshape(-1)
+        n, d = X.shape
+        ls = np.broadcast_to(np.asarray(lengthscale, np.float64), (d,))
+        kid = {"matern52": _lib.KERNEL_MATERN52, "rbf": _lib.KERNEL_RBF}[kernel]
+        jit = ctypes.c_double()
+        self._stream()
+        self._check(self.lib.omb_gp_fit_state(self._h, int(obj), kid, n, d, _ptr(X), _ptr(y), _lib.darr(ls),
+                                              float(variance), float(noise), ctypes.byref(jit)), "omb_gp_fit_state")
+        self._gp_keep[obj] = (X, y)
+        self.gp_info[obj] = dict(n=n, d=d, variance=float(variance), kernel=kernel)
+        return jit.value
 
     # ------------------------------------------------------------------ Thompson sampling (TuRBO)
     def posterior_cov(self, obj, Xc, out=None):

@@ -8,9 +8,12 @@ Mirrors the part of GPy the reference uses (optimobo/algorithms/optimisers.py:22
     mu, var = model.predict(x[None, :])          # (1,1), (1,1)
 
 The fit (kernel matrix, jittered Cholesky, α, L⁻¹, and the L-BFGS hyperparameter search) is
-O(n³) once per BO iteration and runs on the host.  ``predict`` — the
-hot path — runs on the GPU through the HIP posterior kernel (optimobo_amd.device); there is
-no CPU prediction path.
+O(n³) per likelihood evaluation.  With a GPU it runs on the device: each
+L-BFGS-B evaluation is one omb_gp_lml_grad call (K, Cholesky, L⁻¹, Ky⁻¹ and the gradient sums in
+HIP; scipy's L-BFGS-B drives it on the host) and the final state is factorised in place by
+omb_gp_fit_state.  Without a GPU (the CPU test suite) the same arithmetic runs in numpy.
+``predict`` — the hot path — runs on the GPU through the HIP posterior kernel
+(optimobo_amd.device); there is no CPU prediction path.
 """
 import numpy as np
 from scipy import linalg, optimize
@@ -137,6 +140,34 @@ class GPState:
         return self.X.shape[0]
 
 
+class DeviceGPState:
+    """Fitted state factorised on the device (omb_gp_fit_state): holds only X, y and θ on the host."""
+
+    def __init__(self, X, y, lengthscale, variance, kernel="matern52", noise=0.0):
+        self.X = np.ascontiguousarray(X, dtype=np.float64)
+        self.y = np.asarray(y, np.float64).reshape(-1, 1)
+        self.lengthscale = np.broadcast_to(np.asarray(lengthscale, np.float64), (self.X.shape[1],)).copy()
+        self.variance = float(variance)
+        self.kernel = kernel
+        self.noise = float(noise)
+        self.jitter = None
+
+    @property
+    def n(self):
+        return self.X.shape[0]
+
+    def upload(self, ctx, obj):
+        self.jitter = ctx.gp_fit_state(obj, self.X, self.y, self.lengthscale, self.variance, self.noise, self.kernel)
+
+
+def _device_available():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:  # pragma: no cover
+        return False
+
+
 # ----------------------------------------------------------------------------- GPRegression
 class _Noise:
     def __init__(self):
@@ -146,9 +177,12 @@ class _Noise:
 class GPRegression:
     """GPy.models.GPRegression subset: exact inference, fixed or fitted noise, device predict."""
 
-    def __init__(self, X, Y, kernel=None, noise_var=1.0):
+    def __init__(self, X, Y, kernel=None, noise_var=1.0, device_fit=None):
         self.X = np.ascontiguousarray(X, dtype=np.float64)
         self.Y = np.asarray(Y, np.float64).reshape(-1, 1)
+        # device_fit None: on the GPU when one is present (the CPU suite exercises the numpy path)
+        self.device_fit = _device_available() if device_fit is None else bool(device_fit)
+        self._dev_xy = None
         self.kern = kernel if kernel is not None else Matern52(self.X.shape[1], ARD=True)
         self.Gaussian_noise = _Noise()
         self.Gaussian_noise.variance.values[:] = noise_var
@@ -158,8 +192,9 @@ class GPRegression:
     # -- fitted state
     def state(self):
         if self._state is None:
-            self._state = GPState(self.X, self.Y, self.kern.ls_vector(), float(self.kern.variance), self.kern.kind,
-                                  noise=float(self.Gaussian_noise.variance))
+            cls = DeviceGPState if self.device_fit else GPState
+            self._state = cls(self.X, self.Y, self.kern.ls_vector(), float(self.kern.variance), self.kern.kind,
+                              noise=float(self.Gaussian_noise.variance))
         return self._state
 
     def log_likelihood(self):
@@ -179,6 +214,27 @@ class GPRegression:
         if not self.Gaussian_noise.variance.fixed:
             self.Gaussian_noise.variance.values[:] = np.exp(theta[1 + nl])
         self._state = None
+
+    def _neg_lml_and_grad_device(self, theta):
+        """−log p(y) and its gradient from omb_gp_lml_grad (noise fixed, as every driver fits it)."""
+        import torch
+        from . import _lib
+        self._set_free(theta)
+        from .acquisition import engine_for
+        ctx = engine_for([]).ctx          # the shared context, without installing this model
+        if self._dev_xy is None:
+            self._dev_xy = (torch.as_tensor(self.X, device=ctx.device), torch.as_tensor(self.Y[:, 0], device=ctx.device))
+        Xd, yd = self._dev_xy
+        try:
+            lml, g, _ = ctx.gp_lml_grad(Xd, yd, self.kern.ls_vector(), float(self.kern.variance),
+                                        float(self.Gaussian_noise.variance), self.kern.kind)
+        except _lib.OMBError as e:
+            if e.code != _lib.OMB_ENOTPD:
+                raise
+            return 1e25, np.zeros_like(theta)
+        nl = self.kern.lengthscale.values.size
+        grad = [g[0]] + ([float(np.sum(g[1:]))] if nl == 1 else list(g[1:1 + nl]))
+        return -lml, -np.asarray(grad)
 
     def _neg_lml_and_grad(self, theta):
         self._set_free(theta)
@@ -214,7 +270,9 @@ class GPRegression:
     def optimize(self, messages=False, max_f_eval=1000, max_iters=None):
         theta0 = self._get_free()
         bounds = [(np.log(1e-10), np.log(1e10))] * len(theta0)
-        res = optimize.minimize(self._neg_lml_and_grad, theta0, jac=True, method="L-BFGS-B", bounds=bounds,
+        on_device = self.device_fit and self.Gaussian_noise.variance.fixed
+        fun = self._neg_lml_and_grad_device if on_device else self._neg_lml_and_grad
+        res = optimize.minimize(fun, theta0, jac=True, method="L-BFGS-B", bounds=bounds,
                                 options={"maxfun": int(max_f_eval), "maxiter": int(max_iters or max_f_eval)})
         self._set_free(res.x)
         return res

@@ -1,0 +1,109 @@
+"""GPU: the GP fit on the device (omb_gp_lml_grad, omb_gp_fit_state) — GPy's exact-inference log
+marginal likelihood and its gradient against scikit-learn (an independent implementation,
+pinned in tests/test_oracle.py) and against the host numpy fit; the device-factorised state
+against the oracle posterior.
+
+Tolerances: log marginal likelihood 1e-7 relative (+1e-6 absolute); gradient 1e-5 relative to
+its largest entry; posterior as tests/test_gpu_parity.py (1e-6 relative, floors 1e-7·σ_f on μ
+and 1e-9·σ_f² on σ²).
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from oracle import gp as ogp  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from optimobo_amd.device import AcqContext
+    c = AcqContext(0)
+    yield c
+    c.close()
+
+
+def data(n, d, seed):
+    rng = np.random.default_rng(seed)
+    X = rng.uniform(0, 1, (n, d))
+    y = np.sin(3 * X).sum(1) + 0.3 * X[:, 0] ** 2
+    ls = rng.uniform(0.3, 2.0, d)
+    return X, y, ls, max(float(np.var(y)), 0.5)
+
+
+def sklearn_lml_grad(X, y, ls, var, nu=2.5):
+    from sklearn.gaussian_process import GaussianProcessRegressor
+    from sklearn.gaussian_process.kernels import RBF, ConstantKernel, Matern
+    base = Matern(length_scale=ls, nu=nu) if nu else RBF(length_scale=ls)
+    gpr = GaussianProcessRegressor(kernel=ConstantKernel(var) * base, alpha=1e-8, optimizer=None).fit(X, y)
+    lml, g = gpr.log_marginal_likelihood(gpr.kernel_.theta, eval_gradient=True)
+    return lml, g
+
+
+@pytest.mark.parametrize("n,d", [(1, 1), (20, 2), (100, 6), (300, 6), (257, 30), (700, 4)])
+def test_lml_grad_vs_sklearn(ctx, n, d):
+    X, y, ls, var = data(n, d, n + d)
+    lml, g, jit = ctx.gp_lml_grad(X, y, ls, var)
+    lml_s, g_s = sklearn_lml_grad(X, y, ls, var)
+    assert jit == 0.0
+    assert lml == pytest.approx(lml_s, rel=1e-7, abs=1e-6)
+    np.testing.assert_allclose(g, g_s, rtol=1e-5, atol=1e-5 * np.max(np.abs(g_s)))
+
+
+def test_rbf_lml_grad_vs_sklearn(ctx):
+    X, y, ls, var = data(80, 3, 5)
+    lml, g, _ = ctx.gp_lml_grad(X, y, ls, var, kernel="rbf")
+    lml_s, g_s = sklearn_lml_grad(X, y, ls, var, nu=None)
+    assert lml == pytest.approx(lml_s, rel=1e-7, abs=1e-6)
+    np.testing.assert_allclose(g, g_s, rtol=1e-5, atol=1e-5 * np.max(np.abs(g_s)))
+
+
+def test_lml_grad_matches_host_fit(ctx):
+    """The device evaluation is the host numpy one (optimobo_amd.gp, log parametrisation)."""
+    from optimobo_amd.gp import GPRegression, Matern52
+    X, y, ls, var = data(150, 5, 9)
+    m = GPRegression(X, y[:, None], Matern52(5, variance=var, lengthscale=ls, ARD=True), device_fit=False)
+    m.Gaussian_noise.variance.fix(0)
+    theta = m._get_free()
+    f_h, g_h = m._neg_lml_and_grad(theta)
+    md = GPRegression(X, y[:, None], Matern52(5, variance=var, lengthscale=ls, ARD=True), device_fit=True)
+    md.Gaussian_noise.variance.fix(0)
+    f_d, g_d = md._neg_lml_and_grad_device(theta)
+    assert f_d == pytest.approx(f_h, rel=1e-7, abs=1e-6)
+    np.testing.assert_allclose(g_d, g_h, rtol=1e-5, atol=1e-5 * np.max(np.abs(g_h)))
+
+
+def test_fit_state_posterior_matches_oracle(ctx):
+    X, y, ls, var = data(400, 6, 13)
+    jit = ctx.gp_fit_state(0, X, y, ls, var)
+    assert jit == 0.0
+    Xc = np.random.default_rng(14).uniform(0, 1, (3000, 6))
+    Xc[:5] = X[:5]
+    mu, v = ctx.posterior(torch.as_tensor(Xc, device="cuda:0"), n_obj=1)
+    mo, vo = ogp.ExactGP(X, y, ls, var).predict(Xc)
+    np.testing.assert_allclose(mu[0].cpu().numpy(), mo[:, 0], rtol=1e-6, atol=1e-7 * np.sqrt(var))
+    np.testing.assert_allclose(v[0].cpu().numpy(), vo[:, 0], rtol=1e-6, atol=1e-9 * var)
+
+
+def test_device_optimize_reaches_host_optimum():
+    from optimobo_amd.gp import GPRegression, Matern52
+    X, y, ls, var = data(60, 3, 17)
+    out = []
+    for dev_fit in (False, True):
+        m = GPRegression(X, y[:, None], Matern52(3, ARD=True), device_fit=dev_fit)
+        m.Gaussian_noise.variance.fix(0)
+        m.optimize(max_f_eval=300)
+        out.append(m._neg_lml_and_grad(m._get_free())[0])
+    assert out[1] <= out[0] + 1e-4 * abs(out[0])
+
+
+def test_gp_fit_errors(ctx):
+    from optimobo_amd import _lib
+    X, y, ls, var = data(10, 2, 1)
+    with pytest.raises(_lib.OMBError) as e:
+        ctx.gp_lml_grad(X, y, [0.5, -1.0], var)
+    assert e.value.code == _lib.OMB_EINVAL
+    with pytest.raises(_lib.OMBError) as e:
+        ctx.gp_fit_state(0, np.zeros((2000, 2)), np.zeros(2000), [1, 1], 1.0)
+    assert e.value.code == _lib.OMB_EUNSUP

@@ -807,6 +807,12 @@ int omb_timing(omb_ctx* ctx, int enable) {
   if (enable < 0 || enable > 2) return fail(ctx, OMB_EINVAL, "timing level %d outside [0, 2]", enable);
   ctx->timing = enable;
   ctx->ev_used = 0;
+  // create the events of the first 256 chains now, not inside the timed chains
+  while (enable && ctx->ev.size() < 5 * 256) {
+    hipEvent_t e;
+    OMB_HIP(ctx, hipEventCreate(&e));
+    ctx->ev.push_back(e);
+  }
   return OMB_OK;
 }
 

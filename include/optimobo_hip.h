@@ -34,6 +34,7 @@ extern "C" {
 #define OMB_MAX_OBJ 8      /* objectives held by one context */
 #define OMB_MAX_DIM 32     /* n_var */
 #define OMB_MAX_TRAIN 1024 /* n_train handled by the fused posterior kernel */
+#define OMB_MAX_TRAIN_DENSE 16384 /* n_train of the GEMM-based posterior path used above OMB_MAX_TRAIN */
 
 enum {
   OMB_OK = 0,
@@ -96,7 +97,9 @@ int omb_kernel_block(omb_ctx* ctx, int obj, const double* Xc_dev, int64_t N, dou
 
 /* Posterior μ, σ² of objectives 0..n_obj-1 at N candidates Xc_dev (N, d)
  * (GPy PosteriorExact._raw_predict via model.predict, util_functions.py:155-158):
- * mu_dev/var_dev (n_obj, N).  Fused K-block generation + FP64-MFMA L^-1 K* + reductions. */
+ * mu_dev/var_dev (n_obj, N).  Fused K-block generation + FP64-MFMA L^-1 K* + reductions for
+ * n_train ≤ OMB_MAX_TRAIN; above it (≤ OMB_MAX_TRAIN_DENSE) candidate chunks go through the K block,
+ * an FP64-MFMA GEMM V = L^-1 K* and a column reduction. */
 int omb_posterior(omb_ctx* ctx, int n_obj, const double* Xc_dev, int64_t N, double* mu_dev,
                   double* var_dev);
 

@@ -69,6 +69,9 @@ struct omb_ctx {
   // GP fit: Ky | L⁻¹ | Ky⁻¹ | scratch workspace
   void* fws = nullptr;
   size_t fws_cap = 0;
+  // dense posterior path (n_train > OMB_MAX_TRAIN): K* | V chunk workspace
+  void* dws = nullptr;
+  size_t dws_cap = 0;
 };
 
 namespace {
@@ -256,6 +259,38 @@ int plan_begin(omb_ctx* ctx, size_t bytes, void** host) {
   return bytes ? stage_begin(ctx, bytes, host) : OMB_OK;
 }
 
+// Posterior of objectives 0..n_obj-1 (their state in args.gp, dense L⁻¹ in Ld[o]): the fused kernel
+// when every n_train fits it, else per objective and candidate chunk K block → V = L⁻¹K* (GEMM) →
+// column reduction.
+hipError_t posterior_any(omb_ctx* ctx, const GPArgs& args, const double* const* Ld, int n_obj, int max_R,
+                         const double* Xc, int64_t N, double* mu, double* var) {
+  if (16 * max_R <= OMB_MAX_TRAIN) return launch_posterior(ctx->stream, args, n_obj, max_R, Xc, N, mu, var);
+  for (int o = 0; o < n_obj; ++o) {
+    const int64_t n = args.gp[o].n;
+    int64_t Nc = (int64_t)(((size_t)256 << 20) / (16 * (size_t)n));   // K* and V chunks of 128 MiB each
+    Nc = Nc < 256 ? 256 : (Nc / 256) * 256;
+    if (Nc > N) Nc = N;
+    if (grow_dev(ctx, &ctx->dws, &ctx->dws_cap, sizeof(double) * 2 * (size_t)n * Nc, "dense posterior workspace"))
+      return hipErrorOutOfMemory;
+    double* Kst = static_cast<double*>(ctx->dws);
+    double* V = Kst + (size_t)n * Nc;
+    for (int64_t c0 = 0; c0 < N; c0 += Nc) {
+      const int64_t nc = (N - c0) < Nc ? (N - c0) : Nc;
+      hipError_t e = launch_kernel_block(ctx->stream, args, o, Xc + c0 * args.d, nc, Kst);
+      if (e == hipSuccess) e = launch_gemm_nn(ctx->stream, n, nc, n, 1.0, Ld[o], n, Kst, nc, 0.0, V, nc);
+      if (e == hipSuccess)
+        e = launch_post_colreduce(ctx->stream, Kst, V, n, nc, args.gp[o].alpha, args.gp[o].variance,
+                                  mu + (int64_t)o * N + c0, var + (int64_t)o * N + c0);
+      if (e != hipSuccess) return e;
+    }
+  }
+  return hipSuccess;
+}
+
+void gather_Ld(omb_ctx* ctx, int n_obj, const double** Ld) {
+  for (int o = 0; o < n_obj; ++o) Ld[o] = ctx->obj[o].Ld;
+}
+
 // The fused chain: [Sobol →] posterior(0..k-1) → planned acquisition → [arg-max].
 int run_chain(omb_ctx* ctx, const double* Xc, bool sobol, int64_t start, int64_t N, int64_t offset, double* vals_out,
               double* result_dev) {
@@ -313,7 +348,9 @@ int run_chain(omb_ctx* ctx, const double* Xc, bool sobol, int64_t start, int64_t
   if (e == hipSuccess && sobol && N > 0) e = launch_sobol(ctx->stream, ctx->sob, ctx->sob_d, ctx->sob_bits, start, N, Xs);
   if (sobol) Xc = Xs;
   if (e == hipSuccess) e = mark(1);
-  if (e == hipSuccess && N > 0) e = launch_posterior(ctx->stream, args, k, max_R, Xc, N, mu, var);
+  const double* Ld[OMB_MAX_OBJ];
+  gather_Ld(ctx, k, Ld);
+  if (e == hipSuccess && N > 0) e = posterior_any(ctx, args, Ld, k, max_R, Xc, N, mu, var);
   if (e == hipSuccess) e = mark(2);
   if (e == hipSuccess && N > 0) {
     switch (pl.kind) {
@@ -390,6 +427,7 @@ int omb_destroy(omb_ctx* ctx) {
   if (ctx->tws) (void)hipFree(ctx->tws);
   if (ctx->ichol) (void)hipFree(ctx->ichol);
   if (ctx->fws) (void)hipFree(ctx->fws);
+  if (ctx->dws) (void)hipFree(ctx->dws);
   for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;
@@ -423,7 +461,8 @@ int omb_set_gp(omb_ctx* ctx, int obj, int kernel, int n, int d, const double* X_
   if (rc) return rc;
   if (obj < 0 || obj >= OMB_MAX_OBJ) return fail(ctx, OMB_EINVAL, "obj=%d outside [0, %d)", obj, OMB_MAX_OBJ);
   if (kernel != OMB_KERNEL_MATERN52 && kernel != OMB_KERNEL_RBF) return fail(ctx, OMB_EINVAL, "unknown kernel %d", kernel);
-  if (n < 1 || n > OMB_MAX_TRAIN) return fail(ctx, OMB_EUNSUP, "n_train=%d outside [1, %d]", n, OMB_MAX_TRAIN);
+  if (n < 1 || n > OMB_MAX_TRAIN_DENSE)
+    return fail(ctx, OMB_EUNSUP, "n_train=%d outside [1, %d]", n, OMB_MAX_TRAIN_DENSE);
   if (d < 1 || d > OMB_MAX_DIM) return fail(ctx, OMB_EUNSUP, "n_var=%d outside [1, %d]", d, OMB_MAX_DIM);
   if (!X_dev || !lengthscale_host || !alpha_dev || !Linv_dev) return fail(ctx, OMB_EINVAL, "null pointer");
   for (int j = 0; j < d; ++j)
@@ -437,7 +476,8 @@ int omb_set_gp(omb_ctx* ctx, int obj, int kernel, int n, int d, const double* X_
   const int R = (n + 15) / 16;
   const int Q = (R + 3) / 4;
   const int n_pad = kChunkRows * Q;
-  const size_t doubles = (size_t)n_pad * DP + 2 * (size_t)n_pad + DP + (size_t)packed_L_size(R) + (size_t)n * n;
+  const int R_pack = (n <= OMB_MAX_TRAIN) ? R : 0;   // the packed L⁻¹ feeds only the fused kernel
+  const size_t doubles = (size_t)n_pad * DP + 2 * (size_t)n_pad + DP + (size_t)packed_L_size(R_pack) + (size_t)n * n;
   const size_t bytes = doubles * sizeof(double);
   if (bytes > s.cap) {
     if (s.buf) (void)hipFree(s.buf);
@@ -454,9 +494,9 @@ int omb_set_gp(omb_ctx* ctx, int obj, int kernel, int n, int d, const double* X_
   double* alpha_p = xsq + n_pad;
   double* ls_p = alpha_p + n_pad;
   double* Lp = ls_p + DP;
-  double* Ld = Lp + packed_L_size(R);
+  double* Ld = Lp + packed_L_size(R_pack);
   hipError_t e = launch_pack_gp(ctx->stream, n, d, DP, X_dev, lengthscale_host, alpha_dev, Linv_dev, Xs, xsq,
-                                alpha_p, Lp, R, n_pad);
+                                alpha_p, Lp, R_pack, n_pad);
   if (e == hipSuccess)
     e = hipMemcpyAsync(Ld, Linv_dev, sizeof(double) * (size_t)n * n, hipMemcpyDeviceToDevice, ctx->stream);
   if (e != hipSuccess) {
@@ -503,7 +543,9 @@ int omb_posterior(omb_ctx* ctx, int n_obj, const double* Xc_dev, int64_t N, doub
   if (rc) return rc;
   if (N == 0) return OMB_OK;
   if ((N + 31) / 32 > 0x7fffffffLL) return fail(ctx, OMB_EUNSUP, "N=%lld too large", (long long)N);
-  hipError_t e = launch_posterior(ctx->stream, args, n_obj, max_R, Xc_dev, N, mu_dev, var_dev);
+  const double* Ld[OMB_MAX_OBJ];
+  gather_Ld(ctx, n_obj, Ld);
+  hipError_t e = posterior_any(ctx, args, Ld, n_obj, max_R, Xc_dev, N, mu_dev, var_dev);
   if (e != hipSuccess) return hip_fail(ctx, e, "posterior");
   return OMB_OK;
 }
@@ -860,7 +902,8 @@ static hipError_t cov_prepare(omb_ctx* ctx, const ObjState& s, const double* Xc,
   args.gp[0] = s.dev;
   args.d = s.d;
   args.DP = s.DP;
-  hipError_t e = launch_posterior(ctx->stream, args, 1, s.R, Xc, N, mu, var);
+  const double* Ld[1] = {s.Ld};
+  hipError_t e = posterior_any(ctx, args, Ld, 1, s.R, Xc, N, mu, var);
   if (e == hipSuccess) e = launch_kernel_block(ctx->stream, args, 0, Xc, N, Kst);
   if (e == hipSuccess) e = launch_gemm_nn(ctx->stream, s.n, N, s.n, 1.0, s.Ld, s.n, Kst, N, 0.0, V, N);
   return e;
@@ -1070,7 +1113,8 @@ int omb_gp_fit_state(omb_ctx* ctx, int obj, int kernel, int n, int d, const doub
   if (rc) return rc;
   if (obj < 0 || obj >= OMB_MAX_OBJ) return fail(ctx, OMB_EINVAL, "obj=%d outside [0, %d)", obj, OMB_MAX_OBJ);
   if (kernel != OMB_KERNEL_MATERN52 && kernel != OMB_KERNEL_RBF) return fail(ctx, OMB_EINVAL, "unknown kernel %d", kernel);
-  if (n < 1 || n > OMB_MAX_TRAIN) return fail(ctx, OMB_EUNSUP, "n_train=%d outside [1, %d]", n, OMB_MAX_TRAIN);
+  if (n < 1 || n > OMB_MAX_TRAIN_DENSE)
+    return fail(ctx, OMB_EUNSUP, "n_train=%d outside [1, %d]", n, OMB_MAX_TRAIN_DENSE);
   if (d < 1 || d > OMB_MAX_DIM) return fail(ctx, OMB_EUNSUP, "n_var=%d outside [1, %d]", d, OMB_MAX_DIM);
   if (!X_dev || !y_dev || !lengthscale_host) return fail(ctx, OMB_EINVAL, "null pointer");
   for (int j = 0; j < d; ++j)

@@ -124,6 +124,9 @@ hipError_t launch_trinv(hipStream_t stream, const double* L, int64_t n, int64_t 
 // GP log-marginal-likelihood pieces: out[0..DP] = ½ Σ W ∂K/∂θ (θ = log σ_f², log ℓ_j; entries past
 // d are 0), out[DP+1] = Σ log L_ii, out[DP+2] = yᵀα.  partials: gp_grad_blocks(n)·(DP+1) doubles.
 int64_t gp_grad_blocks(int64_t n);
+// dense posterior path: μ, σ² of a candidate chunk from K* (n, Nc) and V = L⁻¹K* (n, Nc).
+hipError_t launch_post_colreduce(hipStream_t stream, const double* Kst, const double* V, int64_t n, int64_t Nc,
+                                 const double* alpha, double variance, double* mu, double* var);
 hipError_t launch_gp_grad(hipStream_t stream, int kind, int DP, const double* X, int d, int64_t n, const double* ls,
                           double variance, const double* alpha, const double* Kinv, int64_t ldk, double* partials,
                           const double* L, int64_t lda, const double* y, double* out);

@@ -623,6 +623,32 @@ hipError_t launch_gp_grad(hipStream_t stream, int kind, int DP, const double* X,
   return hipGetLastError();
 }
 
+// Dense posterior path (n_train > OMB_MAX_TRAIN): μ_c = Σ_k α_k K*_kc, σ²_c = σ_f² − Σ_k V_kc² for the
+// columns of one candidate chunk; one thread per candidate, rows walked in order (coalesced).
+__global__ __launch_bounds__(256) void post_colreduce_kernel(const double* __restrict__ Kst,
+                                                             const double* __restrict__ V, int64_t n, int64_t Nc,
+                                                             const double* __restrict__ alpha, double variance,
+                                                             double* __restrict__ mu, double* __restrict__ var) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= Nc) return;
+  double m = 0.0, s = 0.0;
+  for (int64_t k = 0; k < n; ++k) {
+    m = fma(alpha[k], Kst[k * Nc + c], m);
+    const double v = V[k * Nc + c];
+    s = fma(v, v, s);
+  }
+  mu[c] = m;
+  var[c] = variance - s;
+}
+
+hipError_t launch_post_colreduce(hipStream_t stream, const double* Kst, const double* V, int64_t n, int64_t Nc,
+                                 const double* alpha, double variance, double* mu, double* var) {
+  if (Nc <= 0) return hipSuccess;
+  hipLaunchKernelGGL(post_colreduce_kernel, dim3((unsigned)((Nc + 255) / 256)), dim3(256), 0, stream, Kst, V, n, Nc,
+                     alpha, variance, mu, var);
+  return hipGetLastError();
+}
+
 hipError_t launch_select(hipStream_t stream, const double* Y, int B, int64_t N, int64_t* idx) {
   if (B <= 0) return hipSuccess;
   hipLaunchKernelGGL(select_kernel, dim3(1), dim3(1024), 0, stream, Y, B, N, idx);

@@ -79,6 +79,7 @@ hipError_t launch_pack_gp(hipStream_t stream, int n, int d, int DP, const double
                      alpha, Xs, xsq, alpha_p, ls_p);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  if (R == 0) return hipSuccess;   // n_train above OMB_MAX_TRAIN: the dense path reads L^-1 unpacked
   hipLaunchKernelGGL(pack_L_kernel, dim3(4, R), dim3(256), 0, stream, n, Linv, Lp);
   return hipGetLastError();
 }

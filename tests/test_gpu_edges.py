@@ -38,9 +38,10 @@ def test_error_codes(ctx):
     with pytest.raises(_lib.OMBError) as e:
         ctx.posterior(dev(np.zeros((4, 2))), n_obj=2)
     assert e.value.code == _lib.OMB_EINVAL
-    with pytest.raises(_lib.OMBError) as e:
-        ctx.set_gp(2, np.zeros((1025, 2)), [1, 1], 1.0, np.zeros(1025), np.eye(1025))
-    assert e.value.code == _lib.OMB_EUNSUP
+    import ctypes
+    rc = ctx.lib.omb_set_gp(ctx._h, 2, 0, _lib.MAX_TRAIN_DENSE + 1, 2, ctypes.c_void_p(8), _lib.darr([1, 1]), 1.0,
+                            ctypes.c_void_p(8), ctypes.c_void_p(8))      # rejected before any access
+    assert rc == _lib.OMB_EUNSUP
     with pytest.raises(_lib.OMBError) as e:
         ctx.set_gp(2, np.zeros((4, 33)), np.ones(33), 1.0, np.zeros(4), np.eye(4))
     assert e.value.code == _lib.OMB_EUNSUP
@@ -108,3 +109,44 @@ def test_duplicate_training_points(ctx):
     m, v = ogp.ExactGP(X, y, [0.3, 0.3], 1.0).predict(Xc)
     np.testing.assert_allclose(mu[0].cpu().numpy(), m[:, 0], rtol=1e-6, atol=1e-7)
     np.testing.assert_allclose(var[0].cpu().numpy(), v[:, 0], rtol=1e-6, atol=1e-9)
+
+
+# ----------------------------------------------------------------------------- n_train > 1024
+@pytest.mark.parametrize("n,d,N", [(1025, 2, 700), (1500, 6, 3000), (2600, 30, 513)])
+def test_dense_posterior_path_vs_oracle(ctx, n, d, N):
+    """n_train above the fused kernel's 1024: K block → GEMM V = L⁻¹K* → column reduction."""
+    from oracle import gp as ogp
+    from optimobo_amd.gp import GPState
+    rng = np.random.default_rng(n)
+    X = rng.uniform(0, 1, (n, d))
+    y = np.sin(3 * X).sum(1)
+    ls = rng.uniform(0.5, 2.0, d)
+    var = float(np.var(y))
+    ctx.set_gp_state(0, GPState(X, y, ls, var))
+    Xc = rng.uniform(0, 1, (N, d))
+    Xc[:3] = X[:3]
+    mu, v = ctx.posterior(dev(Xc), n_obj=1)
+    mo, vo = ogp.ExactGP(X, y, ls, var).predict(Xc)
+    np.testing.assert_allclose(mu[0].cpu().numpy(), mo[:, 0], rtol=1e-6, atol=1e-7 * np.sqrt(var))
+    np.testing.assert_allclose(v[0].cpu().numpy(), vo[:, 0], rtol=1e-6, atol=1e-9 * var)
+
+
+def test_dense_path_in_fused_chain(ctx):
+    """The fused chain (plan → eval_argmax) runs the dense path too; same values as per-kernel calls."""
+    from optimobo_amd import pareto
+    from optimobo_amd.gp import GPState
+    rng = np.random.default_rng(77)
+    n, d, N = 1100, 4, 5000
+    X = rng.uniform(0, 1, (n, d))
+    Y = np.column_stack([X[:, 0], 1 - np.sqrt(X[:, 0]) + X[:, 1:].sum(1)])
+    ls = np.full(d, 0.8)
+    for o in range(2):
+        ctx.set_gp_state(o, GPState(X, Y[:, o], ls, float(np.var(Y[:, o]))))
+    pf = pareto.stripes_2d(pareto.calc_pf(Y))
+    r = Y.max(0) + 0.1
+    ctx.plan_ehvi2d(pf, r, 1.0, 0.0, mode="textbook")
+    Xc = dev(rng.uniform(0, 1, (N, d)))
+    fused = ctx.eval(Xc).cpu().numpy()
+    mu, var = ctx.posterior(Xc, n_obj=2)
+    sep = ctx.ehvi2d(mu, var, dev(pf), r, 1.0, 0.0, mode="textbook").cpu().numpy()
+    assert np.array_equal(fused, sep)

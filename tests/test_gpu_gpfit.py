@@ -104,6 +104,7 @@ def test_gp_fit_errors(ctx):
     with pytest.raises(_lib.OMBError) as e:
         ctx.gp_lml_grad(X, y, [0.5, -1.0], var)
     assert e.value.code == _lib.OMB_EINVAL
-    with pytest.raises(_lib.OMBError) as e:
-        ctx.gp_fit_state(0, np.zeros((2000, 2)), np.zeros(2000), [1, 1], 1.0)
-    assert e.value.code == _lib.OMB_EUNSUP
+    import ctypes
+    rc = ctx.lib.omb_gp_fit_state(ctx._h, 0, 0, _lib.MAX_TRAIN_DENSE + 1, 2, ctypes.c_void_p(8), ctypes.c_void_p(8),
+                                  _lib.darr([1, 1]), 1.0, 0.0, None)      # rejected before any access
+    assert rc == _lib.OMB_EUNSUP

@@ -227,7 +227,8 @@ __device__ __forceinline__ void static_for(F&& f) {
 // non-positive pivot, LAPACK dpotrf convention) is set once and stops later steps.
 // ABL (tools/ablate only; the library uses 0): bit 1 skips the diagonal factorisation (identity
 // factor), bit 2 skips the panel solve.
-template <int ABL = 0>
+// VEC: every panel row starts 16-byte aligned (even lda, aligned A): 16-byte row loads and stores.
+template <int ABL = 0, bool VEC = false>
 __global__ __launch_bounds__(256) void chol_panel_kernel(double* __restrict__ A, int64_t N, int64_t lda, int step,
                                                          int* __restrict__ info, int* __restrict__ done_ctr) {
   __shared__ __attribute__((aligned(16))) double LsT[kNB][kNB + 2];   // LsT[c][r] = L_kk[r][c]
@@ -295,8 +296,17 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(double* __restrict__ A,
   // rows below the block exist only while a full block remains (nb == 64): unconditional
   // accesses keep x[] in registers (a per-column guard makes the compiler spill it)
   double x[kNB];
+  if constexpr (VEC) {
 #pragma unroll
-  for (int c = 0; c < kNB; ++c) x[c] = rp[c];
+    for (int c = 0; c < kNB; c += 2) {
+      const double2 v = reinterpret_cast<const double2*>(rp)[c >> 1];
+      x[c] = v.x;
+      x[c + 1] = v.y;
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < kNB; ++c) x[c] = rp[c];
+  }
   // column-oriented (right-looking) substitution: after x_j is final, every later x_k is updated
   // independently — 63 independent fmas per step instead of one 2016-long dependent chain
   static_for<0, kNB>([&](auto jc) {
@@ -305,8 +315,13 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(double* __restrict__ A,
     x[j] = xj;
     axpy_tail<j>(x, -xj, LsT[j]);
   });
+  if constexpr (VEC) {
 #pragma unroll
-  for (int c = 0; c < kNB; ++c) rp[c] = x[c];
+    for (int c = 0; c < kNB; c += 2) reinterpret_cast<double2*>(rp)[c >> 1] = double2{x[c], x[c + 1]};
+  } else {
+#pragma unroll
+    for (int c = 0; c < kNB; ++c) rp[c] = x[c];
+  }
 }
 
 // ----------------------------------------------------------------------------- triangular inverse
@@ -546,12 +561,16 @@ hipError_t launch_add_diag(hipStream_t stream, double* S, int64_t N, int64_t lds
 
 hipError_t launch_cholesky(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, int* done_ctr) {
   const int steps = (int)((N + kNB - 1) / kNB);
+  const bool vec = (lda % 2 == 0) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
   for (int k = 0; k < steps; ++k) {
     const int64_t c0 = (int64_t)k * kNB;
     const int64_t nb = (N - c0) < kNB ? (N - c0) : kNB;
     const int64_t rest = N - c0 - nb;
     const unsigned blocks = (unsigned)(rest > 0 ? (rest + 255) / 256 : 1);
-    hipLaunchKernelGGL(chol_panel_kernel<0>, dim3(blocks), dim3(256), 0, stream, A, N, lda, k, info, done_ctr);
+    if (vec)
+      hipLaunchKernelGGL((chol_panel_kernel<0, true>), dim3(blocks), dim3(256), 0, stream, A, N, lda, k, info, done_ctr);
+    else
+      hipLaunchKernelGGL((chol_panel_kernel<0, false>), dim3(blocks), dim3(256), 0, stream, A, N, lda, k, info, done_ctr);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (rest > 0) {

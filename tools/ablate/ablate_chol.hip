@@ -11,17 +11,17 @@ using namespace omb;
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); exit(1);} } while (0)
 
-template <int ABL>
+template <int ABL, bool VEC = false>
 float step_ms(double* A, int64_t N, int* ctr, int reps) {
   const unsigned blocks = (unsigned)((N - 64 + 255) / 256);
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   CK(hipMemset(ctr, 0, 8 * 1024));
-  hipLaunchKernelGGL(chol_panel_kernel<ABL>, dim3(blocks), dim3(256), 0, 0, A, N, N, 0, ctr, ctr + 1);
+  hipLaunchKernelGGL((chol_panel_kernel<ABL, VEC>), dim3(blocks), dim3(256), 0, 0, A, N, N, 0, ctr, ctr + 1);
   CK(hipEventRecord(e0));
   for (int i = 0; i < reps; ++i)
-    hipLaunchKernelGGL(chol_panel_kernel<ABL>, dim3(blocks), dim3(256), 0, 0, A, N, N, 1 + i, ctr, ctr + 1);
+    hipLaunchKernelGGL((chol_panel_kernel<ABL, VEC>), dim3(blocks), dim3(256), 0, 0, A, N, N, 1 + i, ctr, ctr + 1);
   CK(hipEventRecord(e1));
   CK(hipEventSynchronize(e1));
   float ms;
@@ -40,14 +40,15 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&ctr, 8 * 1024));
   CK(hipMemcpy(A, h.data(), N * N * 8, hipMemcpyHostToDevice));
   // steps 1.. (the matrix stays positive definite: diagonally dominant); timed over 20 steps each
-  float full = 0, nodiag = 0, nopanel = 0, none = 0;
+  float full = 0, nodiag = 0, nopanel = 0, none = 0, vec = 0;
   for (int r = 0; r < 3; ++r) {
     full += step_ms<0>(A, N, ctr, 20);
+    vec += step_ms<0, true>(A, N, ctr, 20);
     nodiag += step_ms<1>(A, N, ctr, 20);
     nopanel += step_ms<2>(A, N, ctr, 20);
     none += step_ms<3>(A, N, ctr, 20);
   }
-  printf("N=%lld  full %.1f us  no-diag %.1f us  no-panel %.1f us  neither %.1f us\n", (long long)N,
-         full / 3 * 1e3, nodiag / 3 * 1e3, nopanel / 3 * 1e3, none / 3 * 1e3);
+  printf("N=%lld  full %.1f us  16B rows %.1f us  no-diag %.1f us  no-panel %.1f us  neither %.1f us\n",
+         (long long)N, full / 3 * 1e3, vec / 3 * 1e3, nodiag / 3 * 1e3, nopanel / 3 * 1e3, none / 3 * 1e3);
   return 0;
 }

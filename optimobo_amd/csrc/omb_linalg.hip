@@ -258,12 +258,13 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(double* __restrict__ A,
         if (bad == 0) bad = j + 1;
         dj = 1.0;                                      // continue without NaNs; flagged
       }
-      // the column step's serial chain: sqrt_nonneg and a Newton-refined v_rcp_f64 instead of the
-      // IEEE sqrt and divide sequences (≤ 1 ulp apart; both enter every later column)
-      const double ljj = sqrt_nonneg(dj);
-      const double r0 = __builtin_amdgcn_rcp(ljj);
-      const double r1 = fma(r0, fma(-ljj, r0, 1.0), r0);
-      const double inv = fma(r1, fma(-ljj, r1, 1.0), r1);
+      // 1/sqrt(d) by v_rsq_f64 and two Newton steps (y ← y + y·(½ − ½ d y²)), then sqrt(d) = d·y:
+      // the shortest dependent chain for both (the column step is latency-bound)
+      const double y0 = __builtin_amdgcn_rsq(dj);
+      const double hd = 0.5 * dj;
+      const double y1 = fma(y0, fma(-hd * y0, y0, 0.5), y0);
+      const double inv = fma(y1, fma(-hd * y1, y1, 0.5), y1);
+      const double ljj = dj * inv;
       if (r == j) my_inv = inv;
       const double lrj = (r > j) ? a[j] * inv : (r == j ? ljj : 0.0);
       a[j] = lrj;

@@ -20,7 +20,7 @@ util_functions.py:410, emo.py:220); it is aliased to ``np.prod``.
 GP posterior fixtures come from scikit-learn's GaussianProcessRegressor (independent of
 both GPy and this build) with the reference's kernel (Matern-5/2 ARD, noise 0 + 1e-8).
 
-Usage:  python tests/golden/make_golden.py [ei_ext] [turbo]
+Usage:  python tests/golden/make_golden.py [ei_ext] [turbo] [cparego]
 """
 import os
 import sys
@@ -362,6 +362,113 @@ def make_turbo(rng, turbo_mod):
     np.savez_compressed(os.path.join(HERE, "turbo.npz"), **out)
 
 
+def _das_dennis(n_dim, p):
+    """pymoo get_reference_directions("das-dennis", n_dim, n_partitions=p), restated (recursion order)."""
+    out = []
+
+    def rec(ref, beta, depth):
+        if depth == n_dim - 1:
+            ref[depth] = beta / (1.0 * p)
+            out.append(ref[None, :])
+        else:
+            for i in range(beta + 1):
+                ref[depth] = 1.0 * i / (1.0 * p)
+                rec(np.copy(ref), beta - i, depth + 1)
+    rec(np.full(n_dim, np.nan), p, 0)
+    return np.concatenate(out, axis=0)
+
+
+class _BNHTight:
+    """BNH-like constrained problem with a tighter first constraint (feasible and infeasible points)."""
+    n_var, n_obj, n_ieq_constr, n_eq_constr = 2, 2, 2, 0
+    xl = np.array([0.0, 0.0])
+    xu = np.array([5.0, 3.0])
+
+    def evaluate(self, x):
+        x = np.asarray(x, np.float64)
+        return np.array([4 * x[0] ** 2 + 4 * x[1] ** 2, (x[0] - 5) ** 2 + (x[1] - 5) ** 2])
+
+    def evaluate_constraints(self, x):
+        x = np.asarray(x, np.float64)
+        return np.array([(x[0] - 5) ** 2 + x[1] ** 2 - 9.0, 7.7 - (x[0] - 8) ** 2 - (x[1] + 3) ** 2])
+
+
+def make_cparego(rng, cparego_mod, sc):
+    """ParEGO_C1/C2 host logic from the reference (cparego.py): select_subset in each of its branches,
+    select_current_best, and the first weight step of solve() — penalisation, subset and the GP
+    training targets — captured by a recording GPy.models.GPRegression double."""
+    out = {}
+    prob = _BNHTight()
+    for cls_name, with_g in (("ParEGO_C1", False), ("ParEGO_C2", True)):
+        obj = object.__new__(getattr(cparego_mod, cls_name))
+        obj.test_problem, obj.n_vars, obj.n_obj = prob, 2, 2
+        obj.n_ieq_constr, obj.n_eq_constr = 2, 0
+
+        def rows(m):
+            X = np.column_stack([rng.uniform(0, 5, m), rng.uniform(0, 3, m)])
+            Y = np.array([prob.evaluate(x) for x in X]).reshape(m, 2)
+            G = np.array([prob.evaluate_constraints(x) for x in X]).reshape(m, 2)
+            S = rng.uniform(0, 1, (m, 1))
+            return np.hstack([X, Y, G, S] if with_g else [X, Y, S])
+        for c, (nf, ni, nmax) in enumerate([(3, 2, 10), (12, 0, 10), (0, 12, 10), (8, 7, 10), (8, 3, 10),
+                                            (3, 8, 10)]):
+            fp, ip = rows(nf), rows(ni)
+            ref_dir = np.array([0.3, 0.7])
+            out[f"{cls_name}_ss{c}_fp"], out[f"{cls_name}_ss{c}_ip"] = fp, ip
+            out[f"{cls_name}_ss{c}_nmax"] = np.int64(nmax)
+            out[f"{cls_name}_ss{c}_out"] = obj.select_subset(fp, ip, ref_dir, nmax)
+            if with_g:
+                out[f"{cls_name}_ss{c}_best"] = np.float64(obj.select_current_best(fp, ip) if nf + ni else np.nan)
+
+    # first weight step of solve()
+    captured = []
+
+    class Stop(Exception):
+        pass
+
+    class RecGP:
+        def __init__(self, X, Y, kern=None):
+            captured.append((np.array(X), np.array(Y)))
+            self.Gaussian_noise = types.SimpleNamespace(variance=types.SimpleNamespace(fix=lambda *a: None))
+
+        def optimize(self, **kw):
+            pass
+
+    sys.modules["GPy"].models.GPRegression = RecGP
+    sys.modules["GPy"].kern.Matern52 = lambda *a, **k: None
+    cparego_mod.get_reference_directions = lambda name, n_dim, n_partitions=None: _das_dennis(n_dim, n_partitions)
+
+    class HV:
+        def __init__(self, ref_point):
+            self.r = np.asarray(ref_point, np.float64)
+
+        def __call__(self, Y):
+            return opareto.hypervolume(Y, self.r)
+    cparego_mod.HV = HV
+    for cls_name in ("ParEGO_C1", "ParEGO_C2"):
+        for t, (seed, n_init, nmax) in enumerate([(3, 12, 8), (4, 30, 10), (5, 6, 100)]):
+            captured.clear()
+            inst = getattr(cparego_mod, cls_name)(prob)
+            best = []
+
+            def stop(*a):
+                best.append(a[-1])
+                raise Stop()
+            inst._get_proposed = stop
+            np.random.seed(seed)
+            try:
+                inst.solve(sc.Tchebicheff(), budget=11, n_init_samples=n_init, N_max=nmax)
+            except Stop:
+                pass
+            key = f"{cls_name}_step{t}"
+            out[f"{key}_seed"], out[f"{key}_ninit"], out[f"{key}_nmax"] = np.int64(seed), np.int64(n_init), np.int64(nmax)
+            out[f"{key}_best"] = np.float64(best[0])
+            out[f"{key}_nmodels"] = np.int64(len(captured))
+            for m, (X, Y) in enumerate(captured):
+                out[f"{key}_X{m}"], out[f"{key}_Y{m}"] = X, Y
+    np.savez_compressed(os.path.join(HERE, "cparego.npz"), **out)
+
+
 def make_calc_pf(rng, uf):
     out = {}
     for t, (n, k) in enumerate([(1, 2), (40, 2), (60, 3)]):
@@ -399,6 +506,8 @@ def main():
         make_pei_cei(np.random.default_rng(20261016), keep_mod, cparego_mod)
     if not only or "turbo" in only:
         make_turbo(np.random.default_rng(20261017), turbo_mod)
+    if not only or "cparego" in only:
+        make_cparego(np.random.default_rng(20261018), cparego_mod, sc)
     print("golden fixtures written to", HERE)
 
 

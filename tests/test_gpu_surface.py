@@ -160,3 +160,41 @@ def test_keep_solve_and_fitness(fitted):
     np.testing.assert_allclose(got, ref, rtol=1e-6, atol=1e-12)
     one = keep.pareto_expected_improvement(Xc[7], models[1], models[0], 0.3)
     assert one.shape == (1,) and one[0] == pytest.approx(ref[7], rel=1e-6, abs=1e-12)
+
+
+def test_cparego_c1_c2_solve():
+    """Constrained ParEGO end to end: device fit, device EI / EI·PoF plans, Constrained_Res."""
+    from optimobo_amd.algorithms import ParEGO_C1, ParEGO_C2
+    from optimobo_amd.problem import ElementwiseProblem
+    import optimobo_amd.scalarisations as sc
+
+    class BNH(ElementwiseProblem):          # optimobo/problem.py BNH demo, 2 inequality constraints
+        def __init__(self):
+            super().__init__(n_var=2, n_obj=2, n_ieq_constr=2, xl=np.array([0.0, 0.0]), xu=np.array([5.0, 3.0]))
+
+        def _evaluate(self, x, out, *args, **kwargs):
+            out["F"] = [4 * x[0] ** 2 + 4 * x[1] ** 2, (x[0] - 5) ** 2 + (x[1] - 5) ** 2]
+
+        def _evaluate_constraints(self, x, out, *args, **kwargs):
+            out["G"] = [(x[0] - 5) ** 2 + x[1] ** 2 - 9.0, 7.7 - (x[0] - 8) ** 2 - (x[1] + 3) ** 2]
+
+    for cls in (ParEGO_C1, ParEGO_C2):
+        np.random.seed(4)
+        r = cls(BNH(), n_candidates=2048, seed=9).solve(sc.Tchebicheff(), budget=11, n_init_samples=8, N_max=10)
+        assert r.ysample.shape == (19, 2) and r.Xsample.shape == (19, 2)
+        assert np.all((r.Xsample >= 0) & (r.Xsample <= np.array([5.0, 3.0]) + 1e-12))
+        assert len(r.X_feasible) + len(r.X_infeasible) == 18    # the last weight step's split
+        assert len(r.hypervolume_convergence) == 1
+
+
+def test_cparego_constraint_ei_matches_oracle(fitted):
+    """ParEGO_C2.consraint_ei (cparego.py:486-496) on the device against the oracle chain."""
+    from optimobo_amd.algorithms import ParEGO_C2
+    X, Y, ls, models = fitted
+    Xc = np.random.default_rng(11).uniform(0, 1, (400, 4))
+    c2 = object.__new__(ParEGO_C2)
+    c2.device = None
+    got = c2.consraint_ei(Xc, models[0], [models[1]], 0.2)
+    mo, vo = oracle_moments(X, Y, ls, Xc)
+    ref = oacq.constrained_ei(mo, vo, 0.2)
+    np.testing.assert_allclose(got, ref, rtol=1e-6, atol=1e-12)

@@ -279,3 +279,63 @@ def test_turbo_adjust_length_golden(golden_dir):
         np.testing.assert_array_equal(np.concatenate([m.length, m.succcount, m.failcount]), want)
         m.ysample = np.vstack((m.ysample, np.column_stack([fx, fx])))
         m._idx = np.vstack((m._idx, int(i) * np.ones((L, 1), dtype=int)))
+
+
+# ----------------------------------------------------------------------------- constrained ParEGO host logic
+class _BNHTight:
+    n_var, n_obj, n_ieq_constr, n_eq_constr = 2, 2, 2, 0
+    xl = np.array([0.0, 0.0])
+    xu = np.array([5.0, 3.0])
+
+    def evaluate(self, x):
+        x = np.asarray(x, np.float64)
+        return np.array([4 * x[0] ** 2 + 4 * x[1] ** 2, (x[0] - 5) ** 2 + (x[1] - 5) ** 2])
+
+    def evaluate_constraints(self, x):
+        x = np.asarray(x, np.float64)
+        return np.array([(x[0] - 5) ** 2 + x[1] ** 2 - 9.0, 7.7 - (x[0] - 8) ** 2 - (x[1] + 3) ** 2])
+
+
+@pytest.mark.parametrize("cls_name", ["ParEGO_C1", "ParEGO_C2"])
+def test_cparego_select_subset_golden(golden_dir, cls_name):
+    """select_subset in each of its six branches (cparego.py:98-189 / 548-644) and C2's
+    select_current_best (:498-512) against the reference (tests/golden/cparego.npz)."""
+    from optimobo_amd.algorithms import cparego
+    z = np.load(os.path.join(golden_dir, "cparego.npz"))
+    obj = getattr(cparego, cls_name)(_BNHTight())
+    for c in range(6):
+        fp, ip = z[f"{cls_name}_ss{c}_fp"], z[f"{cls_name}_ss{c}_ip"]
+        got = obj.select_subset(fp, ip, np.array([0.3, 0.7]), int(z[f"{cls_name}_ss{c}_nmax"]))
+        np.testing.assert_array_equal(got, z[f"{cls_name}_ss{c}_out"])
+        if cls_name == "ParEGO_C2":
+            assert obj.select_current_best(fp, ip) == z[f"{cls_name}_ss{c}_best"]
+
+
+@pytest.mark.parametrize("cls_name", ["ParEGO_C1", "ParEGO_C2"])
+def test_cparego_first_weight_step_golden(golden_dir, cls_name):
+    """solve()'s first weight step — LHS init, shuffled weights, penalised scalarisation, subset,
+    GP training targets and the incumbent — against the reference under the same numpy seed."""
+    import optimobo_amd.scalarisations as sc
+    from optimobo_amd.algorithms import cparego
+    z = np.load(os.path.join(golden_dir, "cparego.npz"))
+
+    class Stop(Exception):
+        pass
+    for t in range(3):
+        key = f"{cls_name}_step{t}"
+        inst = getattr(cparego, cls_name)(_BNHTight())
+        fits, best = [], []
+        inst._fit = lambda X, y: fits.append((np.array(X), np.reshape(y, (-1, 1)))) or object()
+
+        def stop(*a):
+            best.append(a[-1])
+            raise Stop()
+        inst._get_proposed = stop
+        np.random.seed(int(z[f"{key}_seed"]))
+        with pytest.raises(Stop):
+            inst.solve(sc.Tchebicheff(), budget=11, n_init_samples=int(z[f"{key}_ninit"]), N_max=int(z[f"{key}_nmax"]))
+        assert len(fits) == int(z[f"{key}_nmodels"])
+        for m, (X, y) in enumerate(fits):
+            np.testing.assert_array_equal(X, z[f"{key}_X{m}"])
+            np.testing.assert_allclose(y, z[f"{key}_Y{m}"], rtol=1e-12, atol=0)
+        assert best[0] == pytest.approx(float(z[f"{key}_best"]), rel=1e-12)

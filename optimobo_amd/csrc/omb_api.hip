@@ -477,7 +477,8 @@ int omb_set_gp(omb_ctx* ctx, int obj, int kernel, int n, int d, const double* X_
   const int Q = (R + 3) / 4;
   const int n_pad = kChunkRows * Q;
   const int R_pack = (n <= OMB_MAX_TRAIN) ? R : 0;   // the packed L⁻¹ feeds only the fused kernel
-  const size_t doubles = (size_t)n_pad * DP + 2 * (size_t)n_pad + DP + (size_t)packed_L_size(R_pack) + (size_t)n * n;
+  const size_t doubles = (size_t)n_pad * DP + 2 * (size_t)n_pad + DP + (size_t)packed_L_size(R_pack) + (size_t)n * n +
+                         (size_t)packed_X_size(n_pad, DP);
   const size_t bytes = doubles * sizeof(double);
   if (bytes > s.cap) {
     if (s.buf) (void)hipFree(s.buf);
@@ -495,8 +496,10 @@ int omb_set_gp(omb_ctx* ctx, int obj, int kernel, int n, int d, const double* X_
   double* ls_p = alpha_p + n_pad;
   double* Lp = ls_p + DP;
   double* Ld = Lp + packed_L_size(R_pack);
+  double* Xf = Ld + (size_t)n * n;
   hipError_t e = launch_pack_gp(ctx->stream, n, d, DP, X_dev, lengthscale_host, alpha_dev, Linv_dev, Xs, xsq,
                                 alpha_p, Lp, R_pack, n_pad);
+  if (e == hipSuccess) e = launch_pack_x(ctx->stream, DP, n_pad, Xs, Xf);
   if (e == hipSuccess)
     e = hipMemcpyAsync(Ld, Linv_dev, sizeof(double) * (size_t)n * n, hipMemcpyDeviceToDevice, ctx->stream);
   if (e != hipSuccess) {
@@ -512,7 +515,7 @@ int omb_set_gp(omb_ctx* ctx, int obj, int kernel, int n, int d, const double* X_
   s.kind = kernel;
   s.variance = variance;
   s.Ld = Ld;
-  s.dev = GPDev{Xs, xsq, alpha_p, Lp, ls_p, variance, n, R, kernel, 0};
+  s.dev = GPDev{Xs, xsq, alpha_p, Lp, ls_p, variance, n, R, kernel, 0, Xf};
   return OMB_OK;
 }
 

@@ -19,6 +19,8 @@
 //     of quad q, quads split between the two waves of a pair in Gray-code order.
 //   * μ accumulates in VALU during generation; σ² is a wave reduction of the squared MFMA
 //     accumulators followed by a fixed-order cross-wave LDS reduction (deterministic).
+#include <algorithm>
+
 #include "omb_internal.h"
 #include "omb_math.h"
 
@@ -81,6 +83,28 @@ hipError_t launch_pack_gp(hipStream_t stream, int n, int d, int DP, const double
   if (e != hipSuccess) return e;
   if (R == 0) return hipSuccess;   // n_train above OMB_MAX_TRAIN: the dense path reads L^-1 unpacked
   hipLaunchKernelGGL(pack_L_kernel, dim3(4, R), dim3(256), 0, stream, n, Linv, Lp);
+  return hipGetLastError();
+}
+// Xf: the training rows as the A operand of the cross-term MFMA (posterior_kernel, kMfmaGen):
+// row tile T (rows 16T..16T+15), k-step s = 2P + h (dims 4s..4s+3), pairs P < packed_X_pairs(DP):
+//     Xf[(T·pairs + P)·128 + 2·lane + h] = Xs[16T + (lane&15)][4s + (lane>>4)]   (0 past DP)
+// so a lane loads the A values of two k-steps with one 16-byte load, a wave 1 KiB contiguous.
+__global__ void pack_X_kernel(int DP, int pairs, int64_t total, const double* __restrict__ Xs,
+                              double* __restrict__ Xf) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t T = t / (128 * pairs);
+    const int rem = (int)(t % (128 * pairs));
+    const int P = rem >> 7, lane = (rem & 127) >> 1, h = rem & 1;
+    const int j = 4 * (2 * P + h) + (lane >> 4);
+    const int64_t row = 16 * T + (lane & 15);
+    Xf[t] = (j < DP) ? Xs[row * DP + j] : 0.0;
+  }
+}
+
+hipError_t launch_pack_x(hipStream_t stream, int DP, int n_pad, const double* Xs, double* Xf) {
+  const int64_t total = packed_X_size(n_pad, DP);
+  const unsigned blocks = (unsigned)std::min<int64_t>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(pack_X_kernel, dim3(blocks), dim3(256), 0, stream, DP, packed_X_pairs(DP), total, Xs, Xf);
   return hipGetLastError();
 }
 
@@ -189,6 +213,44 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
     }
   }
   const int gen_ct = cg >> 4, gen_cc = cg & 15;
+  // ---- MFMA generation: the cross term (x/ℓ)·(x*/ℓ) of a 16×16 K* tile is
+  // KSD MFMA k-steps, A = training rows (lane l: row l&15, dim l>>4), B = this wave's 16
+  // candidates (kept in registers for the whole kernel).  The accumulator's register e holds rows
+  // 4e + (l>>4) of the tile — exactly the B fragment of k-step 4t+e of the chunk — so each lane
+  // applies the Matern transform to its 4 values and stores them to the ring as they are.
+  constexpr bool kMfmaGen = !(ABL & 2048);   // ABL 2048: VALU dot products (ablation)
+  constexpr int KSD = (DP + 3) / 4;
+  constexpr int KSDP = (KSD + 1) / 2;                          // = packed_X_pairs(DP)
+  constexpr int TPC = 4 * CT;                                  // K* tiles per chunk
+  constexpr int TPW = TPC >= NW ? TPC / NW : 1;                 // tiles per generating wave
+  static_assert(!kMfmaGen || (NW % CT == 0 && (TPC % NW == 0 || NW % TPC == 0)), "tile deal");
+  const int mg_ct = wave % CT;
+  double bfr[kMfmaGen ? KSD : 1];
+  double csq_m = 0.0;
+  if constexpr (kMfmaGen && kCandLds) {
+#pragma unroll
+    for (int s = 0; s < KSD; ++s) {
+      const int j = 4 * s + (lane >> 4);
+      bfr[s] = (j < DP) ? cand[j * BN + 16 * mg_ct + (lane & 15)] : 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < DP; ++j) {
+      const double c = cand[j * BN + 16 * mg_ct + (lane & 15)];
+      csq_m = fma(c, c, csq_m);
+    }
+  } else if constexpr (kMfmaGen) {
+    const int64_t ci = min(c0 + 16 * mg_ct + (lane & 15), N - 1);
+#pragma unroll
+    for (int s = 0; s < KSD; ++s) {
+      const int j = 4 * s + (lane >> 4);
+      bfr[s] = (j < d) ? Xc[ci * d + j] / g.ls[j] : 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < DP; ++j) {
+      const double c = (j < d) ? Xc[ci * d + j] / g.ls[j] : 0.0;
+      csq_m = fma(c, c, csq_m);
+    }
+  }
   if constexpr ((ABL & 128) != 0) {
     if (wave >= 4) __builtin_amdgcn_s_setprio(1);
   }
@@ -247,7 +309,43 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
   static_assert(EPT % 2 == 0, "generation runs two rows per step");
   // the lockstep pair needs ~20 more VGPRs: variants already near the register limit keep one row per step
   constexpr bool kPairs = !kCandLds && !(ABL & (1 | 16 | 512));
+  auto generate_mfma = [&](int kc, double* buf) {
+    if constexpr (kMfmaGen) {
+      if (NW > TPC && (wave / TPC) != kc % (NW / TPC)) return;   // other waves take this chunk
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) {
+        const int u = (NW > TPC) ? wave % TPC : wave + NW * i;
+        const int t = u / CT;                                    // row tile of the chunk (0..3)
+        const int rowbase = kc * kChunkRows + 16 * t;
+        const d2* xa = reinterpret_cast<const d2*>(g.Xf + (int64_t)(4 * kc + t) * (KSDP * 128) + 2 * lane);
+        d2 a[KSDP];
+#pragma unroll
+        for (int p = 0; p < KSDP; ++p) a[p] = xa[64 * p];
+        d4 cr = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s = 0; s < KSD; ++s)
+          cr = __builtin_amdgcn_mfma_f64_16x16x4f64((s & 1) ? a[s >> 1].y : a[s >> 1].x, bfr[s], cr, 0, 0, 0);
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {
+          const int k0 = rowbase + 4 * e + (lane >> 4), k1 = k0 + 4;
+          double v0, v1;
+          kernel_of_r2_k_x2<KIND>(fma(-2.0, cr[e], g.xsq[k0] + csq_m), fma(-2.0, cr[e + 1], g.xsq[k1] + csq_m),
+                                  (ABL & 256) ? 1.0 : g.variance, args.ec, v0, v1);
+          v0 = (k0 < g.n) ? v0 : 0.0;
+          v1 = (k1 < g.n) ? v1 : 0.0;
+          mu_part = fma(g.alpha[k0], v0, mu_part);
+          mu_part = fma(g.alpha[k1], v1, mu_part);
+          buf[((4 * t + e) * CT + mg_ct) * 64 + lane] = v0;
+          buf[((4 * t + e + 1) * CT + mg_ct) * 64 + lane] = v1;
+        }
+      }
+    }
+  };
   auto generate = [&](int kc, double* buf) {
+    if constexpr (kMfmaGen) {
+      generate_mfma(kc, buf);
+      return;
+    }
     if (kPairs && (kc + 1) * kChunkRows <= g.n) {
       // whole chunk inside the training set: no per-row guard, and two independent rows per step
       // so the scheduler interleaves their ~50-deep fp64 dependency chains (one chain alone leaves
@@ -412,14 +510,26 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) red[wave * BN + ct * 16 + lane] = part[ct];
   }
-  redmu[tid] = mu_part;
+  if constexpr (kMfmaGen) {
+    // lanes l, l^16, l^32, l^48 hold the same candidate 16·(wave mod CT) + (l&15)
+    double s = mu_part;
+    s += __shfl_xor(s, 16);
+    s += __shfl_xor(s, 32);
+    if (lane < 16) redmu[wave * 16 + lane] = s;
+  } else {
+    redmu[tid] = mu_part;
+  }
   __syncthreads();
   if (tid < BN) {
     double s = 0.0;
 #pragma unroll
     for (int w = 0; w < NW; ++w) s += red[w * BN + tid];
     double m = 0.0;
-    for (int t = tid; t < NT; t += BN) m += redmu[t];
+    if constexpr (kMfmaGen) {
+      for (int w = tid >> 4; w < NW; w += CT) m += redmu[w * 16 + (tid & 15)];
+    } else {
+      for (int t = tid; t < NT; t += BN) m += redmu[t];
+    }
     const int64_t c = c0 + tid;
     if (c < N) {
       mu_out[(int64_t)obj * N + c] = m;

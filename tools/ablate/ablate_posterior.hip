@@ -1,6 +1,7 @@
 // Ablation timing of posterior_kernel variants (tools only; not part of the library).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/ablate/ablate_posterior tools/ablate/ablate_posterior.hip
-// Run on the GPU box: ./tools/ablate/ablate_posterior [n] [N]
+// Run on the GPU box: ./tools/ablate/ablate_posterior [n] [N] [d] [n_obj]
+//   d = 6: config 3 variants (RT 4, CT 4); d = 30: config 5 variants (RT 8, CT 2, candidates in LDS)
 // Variants are timed interleaved in one process (cdna_hip_programming.md §5.4 rule 24).
 #include <cstdio>
 #include <cstdlib>
@@ -16,19 +17,20 @@ struct Bench {
   GPArgs a;
   const double* Xc;
   int64_t N;
+  int n_obj;
   double *mu, *var;
 };
 
-template <int RT, int CT, int NW, int ABL>
+template <int RT, int CT, int NW, int ABL, int DP = 6>
 float run(const Bench& b, int reps) {
-  dim3 grid((unsigned)((b.N + 16 * CT - 1) / (16 * CT)), 2);
+  dim3 grid((unsigned)((b.N + 16 * CT - 1) / (16 * CT)), b.n_obj);
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  hipLaunchKernelGGL((posterior_kernel<RT, CT, 6, 0, NW, ABL>), grid, dim3(64 * NW), 0, 0, b.a, b.Xc, b.N, b.mu, b.var);
+  hipLaunchKernelGGL((posterior_kernel<RT, CT, DP, 0, NW, ABL>), grid, dim3(64 * NW), 0, 0, b.a, b.Xc, b.N, b.mu, b.var);
   CK(hipEventRecord(e0));
   for (int i = 0; i < reps; ++i)
-    hipLaunchKernelGGL((posterior_kernel<RT, CT, 6, 0, NW, ABL>), grid, dim3(64 * NW), 0, 0, b.a, b.Xc, b.N, b.mu,
+    hipLaunchKernelGGL((posterior_kernel<RT, CT, DP, 0, NW, ABL>), grid, dim3(64 * NW), 0, 0, b.a, b.Xc, b.N, b.mu,
                        b.var);
   CK(hipEventRecord(e1));
   CK(hipEventSynchronize(e1));
@@ -47,7 +49,10 @@ struct Variant {
 int main(int argc, char** argv) {
   int n = argc > 1 ? atoi(argv[1]) : 512;
   int64_t N = argc > 2 ? atoll(argv[2]) : (1 << 20);
-  const int d = 6, DP = 6;
+  const int d = argc > 3 ? atoi(argv[3]) : 6;
+  const int n_obj = argc > 4 ? atoi(argv[4]) : 2;
+  if (d != 6 && d != 30) { printf("d must be 6 or 30\n"); return 1; }
+  const int DP = d == 6 ? 6 : 32;
   int R = (n + 15) / 16, Q = (R + 3) / 4, n_pad = 64 * Q;
   std::vector<double> hXs(n_pad * DP), hxsq(n_pad), ha(n_pad), hL(packed_L_size(R)), hls(DP, 1.0), hXc(N * d);
   srand(1);
@@ -71,34 +76,49 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(ls, hls.data(), DP * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(Xc, hXc.data(), hXc.size() * 8, hipMemcpyHostToDevice));
   Bench b{};
-  for (int o = 0; o < 2; ++o) b.a.gp[o] = GPDev{Xs, xsq, al, Lp, ls, 1.0, n, R, 0, 0};
+  double* Xf;
+  CK(hipMalloc(&Xf, packed_X_size(n_pad, DP) * 8));
+  CK(launch_pack_x(0, DP, n_pad, Xs, Xf));
+  for (int o = 0; o < 2; ++o) b.a.gp[o] = GPDev{Xs, xsq, al, Lp, ls, 1.0, n, R, 0, 0, Xf};
   b.a.d = d;
   b.a.DP = DP;
   b.a.ec = exp_coef();
   b.Xc = Xc;
   b.N = N;
+  b.n_obj = n_obj;
   b.mu = mu;
   b.var = var;
-  const Variant vs[] = {
-      {"default (ring, A PD=2)", run<4, 4, 8, 0>},
-      {"A PD=1 (64)", run<4, 4, 8, 64>},
+  const Variant wide[] = {
+      {"default RT8 CT2 (MFMA gen)", run<8, 2, 8, 0, 32>},
+      {"VALU gen (2048)", run<8, 2, 8, 2048, 32>},
+      {"const A (4)", run<8, 2, 8, 4, 32>},
+      {"generation only (2)", run<8, 2, 8, 2, 32>},
+      {"VALU generation only (2050)", run<8, 2, 8, 2050, 32>},
+      {"no Matern (1)", run<8, 2, 8, 1, 32>},
+      {"16 waves RT4 CT2 MFMA gen", run<4, 2, 16, 0, 32>},
+      {"16 waves RT4 CT2 VALU gen", run<4, 2, 16, 2048, 32>},
+      {"16 waves generation only", run<4, 2, 16, 2, 32>},
+  };
+  const Variant narrow[] = {
+      {"default (ring, MFMA gen)", run<4, 4, 8, 0>},
+      {"generation only (2)", run<4, 4, 8, 2>},
+      {"VALU gen (2048)", run<4, 4, 8, 2048>},
+      {"A PD=2 (64)", run<4, 4, 8, 64>},
       {"const A (4)", run<4, 4, 8, 4>},
       {"barrier pipeline (32)", run<4, 4, 8, 32>},
-      {"libm exp/sqrt (16)", run<4, 4, 8, 16>},
-      {"no Matern (1)", run<4, 4, 8, 1>},
-      {"no MFMA (2)", run<4, 4, 8, 2>},
+      {"VALU gen, libm exp/sqrt", run<4, 4, 8, 2048 + 16>},
+      {"VALU gen, no Matern", run<4, 4, 8, 2048 + 1>},
+      {"VALU gen, no MFMA", run<4, 4, 8, 2048 + 2>},
       {"16 waves ring", run<2, 4, 16, 0>},
       {"setprio waves 4-7 (128)", run<4, 4, 8, 128>},
       {"no sigma_f^2 mul (256)", run<4, 4, 8, 256>},
-      {"fused r2 chain (512)", run<4, 4, 8, 512>},
-      {"256+512", run<4, 4, 8, 768>},
-      {"128+256+512", run<4, 4, 8, 896>},
   };
-  const int NV = sizeof(vs) / sizeof(vs[0]);
+  const Variant* vs = d == 6 ? narrow : wide;
+  const int NV = d == 6 ? (int)(sizeof(narrow) / sizeof(narrow[0])) : (int)(sizeof(wide) / sizeof(wide[0]));
   std::vector<float> t(NV, 0.f);
   for (int round = 0; round < 3; ++round)
     for (int i = 0; i < NV; ++i) t[i] += vs[i].fn(b, 5);
-  double flops = 2.0 * N * ((double)n * (n + 1) + 2 * n + 2 * n + n * (2 * d + 2) + 10 * n);
+  double flops = (double)n_obj * N * ((double)n * (n + 1) + 2 * n + 2 * n + n * (2 * d + 2) + 10 * n);
   for (int i = 0; i < NV; ++i)
     printf("%-26s %8.3f ms  %6.1f TFLOP/s-equiv\n", vs[i].name, t[i] / 3, flops / (t[i] / 3 * 1e-3) / 1e12);
   return 0;

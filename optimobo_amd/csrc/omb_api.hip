@@ -499,7 +499,7 @@ int omb_set_gp(omb_ctx* ctx, int obj, int kernel, int n, int d, const double* X_
   double* Xf = Ld + (size_t)n * n;
   hipError_t e = launch_pack_gp(ctx->stream, n, d, DP, X_dev, lengthscale_host, alpha_dev, Linv_dev, Xs, xsq,
                                 alpha_p, Lp, R_pack, n_pad);
-  if (e == hipSuccess) e = launch_pack_x(ctx->stream, DP, n_pad, Xs, Xf);
+  if (e == hipSuccess) e = launch_pack_x(ctx->stream, d, DP, n_pad, Xs, xsq, Xf);
   if (e == hipSuccess)
     e = hipMemcpyAsync(Ld, Linv_dev, sizeof(double) * (size_t)n * n, hipMemcpyDeviceToDevice, ctx->stream);
   if (e != hipSuccess) {

@@ -43,7 +43,8 @@ hipError_t launch_pack_gp(hipStream_t stream, int n, int d, int DP, const double
                           const double* alpha, const double* Linv, double* Xs, double* xsq, double* alpha_p,
                           double* Lp, int R, int n_pad);
 // Xf = Xs in the A-fragment order of the posterior kernel's MFMA cross term (after launch_pack_gp)
-hipError_t launch_pack_x(hipStream_t stream, int DP, int n_pad, const double* Xs, double* Xf);
+hipError_t launch_pack_x(hipStream_t stream, int d, int DP, int n_pad, const double* Xs, const double* xsq,
+                         double* Xf);
 
 hipError_t launch_kernel_block(hipStream_t stream, const GPArgs& args, int obj, const double* Xc, int64_t N,
                                double* K);
@@ -136,8 +137,8 @@ hipError_t launch_gp_grad(hipStream_t stream, int kind, int DP, const double* X,
 
 // Packed-L^-1 size in doubles for R row tiles: Σ_{r<R} 4(r+1)·64 = 128·R·(R+1).
 inline int64_t packed_L_size(int R) { return 128ll * R * (R + 1); }
-// k-step pairs of the training-row A fragments: ⌈⌈DP/4⌉/2⌉
-inline int packed_X_pairs(int DP) { return ((DP + 3) / 4 + 1) / 2; }
+// k-step pairs of the training-row A fragments [x/ℓ, ‖x/ℓ‖², 1]: ⌈⌈(DP+2)/4⌉/2⌉
+inline int packed_X_pairs(int DP) { return ((DP + 5) / 4 + 1) / 2; }
 inline int64_t packed_X_size(int n_pad, int DP) { return (int64_t)(n_pad / 16) * packed_X_pairs(DP) * 128; }
 
 }  // namespace omb

@@ -85,26 +85,30 @@ hipError_t launch_pack_gp(hipStream_t stream, int n, int d, int DP, const double
   hipLaunchKernelGGL(pack_L_kernel, dim3(4, R), dim3(256), 0, stream, n, Linv, Lp);
   return hipGetLastError();
 }
-// Xf: the training rows as the A operand of the cross-term MFMA (posterior_kernel, kMfmaGen):
-// row tile T (rows 16T..16T+15), k-step s = 2P + h (dims 4s..4s+3), pairs P < packed_X_pairs(DP):
-//     Xf[(T·pairs + P)·128 + 2·lane + h] = Xs[16T + (lane&15)][4s + (lane>>4)]   (0 past DP)
+// Xf: the training rows as the A operand of the r²-MFMA (posterior_kernel, kMfmaGen), augmented
+// with two columns so that one dot product gives r² (the B side holds [−2·x*/ℓ, 1, ‖x*/ℓ‖²]):
+//     A[k][j] = Xs[k][j] (j < d),  ‖Xs[k]‖² (j = d),  1 (j = d+1),  0 beyond.
+// Row tile T (rows 16T..16T+15), k-step s = 2P + h (dims 4s..4s+3), pairs P < packed_X_pairs(DP):
+//     Xf[(T·pairs + P)·128 + 2·lane + h] = A[16T + (lane&15)][4s + (lane>>4)]
 // so a lane loads the A values of two k-steps with one 16-byte load, a wave 1 KiB contiguous.
-__global__ void pack_X_kernel(int DP, int pairs, int64_t total, const double* __restrict__ Xs,
-                              double* __restrict__ Xf) {
+__global__ void pack_X_kernel(int d, int DP, int pairs, int64_t total, const double* __restrict__ Xs,
+                              const double* __restrict__ xsq, double* __restrict__ Xf) {
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t T = t / (128 * pairs);
     const int rem = (int)(t % (128 * pairs));
     const int P = rem >> 7, lane = (rem & 127) >> 1, h = rem & 1;
     const int j = 4 * (2 * P + h) + (lane >> 4);
     const int64_t row = 16 * T + (lane & 15);
-    Xf[t] = (j < DP) ? Xs[row * DP + j] : 0.0;
+    Xf[t] = (j < d) ? Xs[row * DP + j] : (j == d ? xsq[row] : (j == d + 1 ? 1.0 : 0.0));
   }
 }
 
-hipError_t launch_pack_x(hipStream_t stream, int DP, int n_pad, const double* Xs, double* Xf) {
+hipError_t launch_pack_x(hipStream_t stream, int d, int DP, int n_pad, const double* Xs, const double* xsq,
+                         double* Xf) {
   const int64_t total = packed_X_size(n_pad, DP);
   const unsigned blocks = (unsigned)std::min<int64_t>((total + 255) / 256, 4096);
-  hipLaunchKernelGGL(pack_X_kernel, dim3(blocks), dim3(256), 0, stream, DP, packed_X_pairs(DP), total, Xs, Xf);
+  hipLaunchKernelGGL(pack_X_kernel, dim3(blocks), dim3(256), 0, stream, d, DP, packed_X_pairs(DP), total, Xs, xsq,
+                     Xf);
   return hipGetLastError();
 }
 
@@ -213,42 +217,42 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
     }
   }
   const int gen_ct = cg >> 4, gen_cc = cg & 15;
-  // ---- MFMA generation: the cross term (x/ℓ)·(x*/ℓ) of a 16×16 K* tile is
-  // KSD MFMA k-steps, A = training rows (lane l: row l&15, dim l>>4), B = this wave's 16
-  // candidates (kept in registers for the whole kernel).  The accumulator's register e holds rows
-  // 4e + (l>>4) of the tile — exactly the B fragment of k-step 4t+e of the chunk — so each lane
-  // applies the Matern transform to its 4 values and stores them to the ring as they are.
+  // ---- MFMA generation: r² of a 16×16 K* tile is ⌈(d+2)/4⌉ MFMA k-steps,
+  // A = training rows [x/ℓ, ‖x/ℓ‖², 1] (lane l: row l&15, dim l>>4; pre-packed Xf), B = this wave's
+  // 16 candidates [−2·x*/ℓ, 1, ‖x*/ℓ‖²] (registers, loaded once).  The accumulator's register e
+  // holds rows 4e + (l>>4) of the tile — exactly the B fragment of k-step 4t+e of the chunk — so
+  // each lane applies the Matern transform to its 4 values and stores them to the ring as they are.
+  // Rows past n need no guard: α and the L⁻¹ columns there are zero, and r² stays finite.
   constexpr bool kMfmaGen = !(ABL & 2048);   // ABL 2048: VALU dot products (ablation)
-  constexpr int KSD = (DP + 3) / 4;
-  constexpr int KSDP = (KSD + 1) / 2;                          // = packed_X_pairs(DP)
+  // d ≤ 8: r² straight from the MFMA (−1% time at config 3).  Wider inputs keep the cross-term form:
+  // the extra k-step bought nothing at d = 30 and its registers make the CT = 4 variants spill.
+  constexpr bool kAug = DP <= 8 && !(ABL & 4096);   // ABL 4096: cross term only (ablation)
+  constexpr int KSD = kAug ? (DP + 5) / 4 : (DP + 3) / 4;
+  constexpr int KSDP = ((DP + 5) / 4 + 1) / 2;                 // = packed_X_pairs(DP)
   constexpr int TPC = 4 * CT;                                  // K* tiles per chunk
   constexpr int TPW = TPC >= NW ? TPC / NW : 1;                 // tiles per generating wave
   static_assert(!kMfmaGen || (NW % CT == 0 && (TPC % NW == 0 || NW % TPC == 0)), "tile deal");
   const int mg_ct = wave % CT;
   double bfr[kMfmaGen ? KSD : 1];
   double csq_m = 0.0;
-  if constexpr (kMfmaGen && kCandLds) {
-#pragma unroll
-    for (int s = 0; s < KSD; ++s) {
-      const int j = 4 * s + (lane >> 4);
-      bfr[s] = (j < DP) ? cand[j * BN + 16 * mg_ct + (lane & 15)] : 0.0;
-    }
-#pragma unroll
-    for (int j = 0; j < DP; ++j) {
-      const double c = cand[j * BN + 16 * mg_ct + (lane & 15)];
-      csq_m = fma(c, c, csq_m);
-    }
-  } else if constexpr (kMfmaGen) {
+  if constexpr (kMfmaGen) {
     const int64_t ci = min(c0 + 16 * mg_ct + (lane & 15), N - 1);
+    auto coord = [&](int j) -> double {
+      if constexpr (kCandLds) return cand[j * BN + 16 * mg_ct + (lane & 15)];
+      return (j < d) ? Xc[ci * d + j] / g.ls[j] : 0.0;
+    };
+#pragma unroll
+    for (int j = 0; j < DP; ++j) {
+      const double c = coord(j);
+      csq_m = fma(c, c, csq_m);
+    }
 #pragma unroll
     for (int s = 0; s < KSD; ++s) {
       const int j = 4 * s + (lane >> 4);
-      bfr[s] = (j < d) ? Xc[ci * d + j] / g.ls[j] : 0.0;
-    }
-#pragma unroll
-    for (int j = 0; j < DP; ++j) {
-      const double c = (j < d) ? Xc[ci * d + j] / g.ls[j] : 0.0;
-      csq_m = fma(c, c, csq_m);
+      if constexpr (kAug)
+        bfr[s] = (j < d) ? -2.0 * coord(j) : (j == d ? 1.0 : (j == d + 1 ? csq_m : 0.0));
+      else
+        bfr[s] = (j < d) ? coord(j) : 0.0;
     }
   }
   if constexpr ((ABL & 128) != 0) {
@@ -318,9 +322,9 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
         const int t = u / CT;                                    // row tile of the chunk (0..3)
         const int rowbase = kc * kChunkRows + 16 * t;
         const d2* xa = reinterpret_cast<const d2*>(g.Xf + (int64_t)(4 * kc + t) * (KSDP * 128) + 2 * lane);
-        d2 a[KSDP];
+        d2 a[(KSD + 1) / 2];
 #pragma unroll
-        for (int p = 0; p < KSDP; ++p) a[p] = xa[64 * p];
+        for (int p = 0; p < (KSD + 1) / 2; ++p) a[p] = xa[64 * p];
         d4 cr = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int s = 0; s < KSD; ++s)
@@ -329,10 +333,14 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
         for (int e = 0; e < 4; e += 2) {
           const int k0 = rowbase + 4 * e + (lane >> 4), k1 = k0 + 4;
           double v0, v1;
-          kernel_of_r2_k_x2<KIND>(fma(-2.0, cr[e], g.xsq[k0] + csq_m), fma(-2.0, cr[e + 1], g.xsq[k1] + csq_m),
-                                  (ABL & 256) ? 1.0 : g.variance, args.ec, v0, v1);
-          v0 = (k0 < g.n) ? v0 : 0.0;
-          v1 = (k1 < g.n) ? v1 : 0.0;
+          if constexpr (kAug) {
+            kernel_of_r2_k_x2<KIND>(cr[e], cr[e + 1], (ABL & 256) ? 1.0 : g.variance, args.ec, v0, v1);
+          } else {
+            kernel_of_r2_k_x2<KIND>(fma(-2.0, cr[e], g.xsq[k0] + csq_m), fma(-2.0, cr[e + 1], g.xsq[k1] + csq_m),
+                                    (ABL & 256) ? 1.0 : g.variance, args.ec, v0, v1);
+            v0 = (k0 < g.n) ? v0 : 0.0;
+            v1 = (k1 < g.n) ? v1 : 0.0;
+          }
           mu_part = fma(g.alpha[k0], v0, mu_part);
           mu_part = fma(g.alpha[k1], v1, mu_part);
           buf[((4 * t + e) * CT + mg_ct) * 64 + lane] = v0;

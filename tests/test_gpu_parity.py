@@ -81,7 +81,8 @@ def test_posterior_vs_golden(ctx, golden_dir, name):
 @pytest.mark.parametrize("n,d,N", [(1, 1, 5), (16, 2, 64), (17, 3, 65), (64, 6, 1000), (100, 4, 257),
                                    (256, 6, 333), (300, 9, 129), (512, 6, 2048), (700, 2, 100),
                                    (1024, 6, 300), (128, 30, 200), (64, 32, 64),
-                                   (1024, 30, 300), (600, 17, 100), (513, 16, 77), (777, 5, 129)])
+                                   (1024, 30, 300), (600, 17, 100), (513, 16, 77), (777, 5, 129),
+                                   (200, 8, 100), (150, 7, 99), (90, 5, 33), (1000, 8, 65)])
 def test_posterior_sizes(ctx, n, d, N):
     rng = np.random.default_rng(n * 1000 + d)
     X = rng.uniform(0, 1, (n, d))

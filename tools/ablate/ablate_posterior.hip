@@ -78,7 +78,7 @@ int main(int argc, char** argv) {
   Bench b{};
   double* Xf;
   CK(hipMalloc(&Xf, packed_X_size(n_pad, DP) * 8));
-  CK(launch_pack_x(0, DP, n_pad, Xs, Xf));
+  CK(launch_pack_x(0, d, DP, n_pad, Xs, xsq, Xf));
   for (int o = 0; o < 2; ++o) b.a.gp[o] = GPDev{Xs, xsq, al, Lp, ls, 1.0, n, R, 0, 0, Xf};
   b.a.d = d;
   b.a.DP = DP;
@@ -91,6 +91,7 @@ int main(int argc, char** argv) {
   const Variant wide[] = {
       {"default RT8 CT2 (MFMA gen)", run<8, 2, 8, 0, 32>},
       {"VALU gen (2048)", run<8, 2, 8, 2048, 32>},
+      {"cross term only (4096)", run<8, 2, 8, 4096, 32>},
       {"const A (4)", run<8, 2, 8, 4, 32>},
       {"generation only (2)", run<8, 2, 8, 2, 32>},
       {"VALU generation only (2050)", run<8, 2, 8, 2050, 32>},
@@ -102,6 +103,7 @@ int main(int argc, char** argv) {
   const Variant narrow[] = {
       {"default (ring, MFMA gen)", run<4, 4, 8, 0>},
       {"generation only (2)", run<4, 4, 8, 2>},
+      {"cross term only (4096)", run<4, 4, 8, 4096>},
       {"VALU gen (2048)", run<4, 4, 8, 2048>},
       {"A PD=2 (64)", run<4, 4, 8, 64>},
       {"const A (4)", run<4, 4, 8, 4>},

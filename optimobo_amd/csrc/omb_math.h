@@ -72,14 +72,37 @@ __device__ __forceinline__ double sqrt_nonneg(double a) {
 // operand, whereas a literal coefficient makes the compiler emit the v_fmac form with the addend
 // materialised by two v_mov_b32 per Horner step (20 extra VALU issues per element in the posterior
 // and K-block generation loops).
+// The same struct carries the constants of the table-driven exp (exp_tab below) in t[].
 struct ExpCoef {
   double c[10];
+  double t[8];   // −√5·64/ln2, ln2_hi/64, ln2_lo/64, 1/120, 1/24, 1/6, 1/2, r²_min
 };
 __host__ __device__ constexpr ExpCoef exp_coef() {
   return ExpCoef{{2.5110037605963777e-08, 2.763263963904103e-07, 2.755724091857897e-06, 2.4801485482328494e-05,
                   0.00019841269890047113, 0.0013888888952314775, 0.008333333333319601, 0.0416666666664881,
-                  0.1666666666666668, 0.5000000000000019}};
+                  0.1666666666666668, 0.5000000000000019},
+                 {-2.23606797749979 * 92.33248261689366, 6.93147180369123816490e-01 / 64, 1.90821492927058770002e-10 / 64, 1.0 / 120,
+                  1.0 / 24, 1.0 / 6, 0.5, 1e-300}};
 }
+
+// 2^(j/64), j = 0..63, correctly rounded (computed with 50-digit decimal arithmetic).
+__device__ constexpr double kExp2Tab64[64] = {
+    0x1.0000000000000p+0, 0x1.02c9a3e778061p+0, 0x1.059b0d3158574p+0, 0x1.0874518759bc8p+0,
+    0x1.0b5586cf9890fp+0, 0x1.0e3ec32d3d1a2p+0, 0x1.11301d0125b51p+0, 0x1.1429aaea92de0p+0,
+    0x1.172b83c7d517bp+0, 0x1.1a35beb6fcb75p+0, 0x1.1d4873168b9aap+0, 0x1.2063b88628cd6p+0,
+    0x1.2387a6e756238p+0, 0x1.26b4565e27cddp+0, 0x1.29e9df51fdee1p+0, 0x1.2d285a6e4030bp+0,
+    0x1.306fe0a31b715p+0, 0x1.33c08b26416ffp+0, 0x1.371a7373aa9cbp+0, 0x1.3a7db34e59ff7p+0,
+    0x1.3dea64c123422p+0, 0x1.4160a21f72e2ap+0, 0x1.44e086061892dp+0, 0x1.486a2b5c13cd0p+0,
+    0x1.4bfdad5362a27p+0, 0x1.4f9b2769d2ca7p+0, 0x1.5342b569d4f82p+0, 0x1.56f4736b527dap+0,
+    0x1.5ab07dd485429p+0, 0x1.5e76f15ad2148p+0, 0x1.6247eb03a5585p+0, 0x1.6623882552225p+0,
+    0x1.6a09e667f3bcdp+0, 0x1.6dfb23c651a2fp+0, 0x1.71f75e8ec5f74p+0, 0x1.75feb564267c9p+0,
+    0x1.7a11473eb0187p+0, 0x1.7e2f336cf4e62p+0, 0x1.82589994cce13p+0, 0x1.868d99b4492edp+0,
+    0x1.8ace5422aa0dbp+0, 0x1.8f1ae99157736p+0, 0x1.93737b0cdc5e5p+0, 0x1.97d829fde4e50p+0,
+    0x1.9c49182a3f090p+0, 0x1.a0c667b5de565p+0, 0x1.a5503b23e255dp+0, 0x1.a9e6b5579fdbfp+0,
+    0x1.ae89f995ad3adp+0, 0x1.b33a2b84f15fbp+0, 0x1.b7f76f2fb5e47p+0, 0x1.bcc1e904bc1d2p+0,
+    0x1.c199bdd85529cp+0, 0x1.c67f12e57d14bp+0, 0x1.cb720dcef9069p+0, 0x1.d072d4a07897cp+0,
+    0x1.d5818dcfba487p+0, 0x1.da9e603db3285p+0, 0x1.dfc97337b9b5fp+0, 0x1.e502ee78b3ff6p+0,
+    0x1.ea4afa2a490dap+0, 0x1.efa1bee615a27p+0, 0x1.f50765b6e4540p+0, 0x1.fa7c1819e90d8p+0};
 
 // a·b + c with c a wave-uniform value: the VOP3 v_fma_f64 takes c straight from an SGPR pair (the
 // compiler otherwise picks the two-address v_fmac and first copies c into VGPRs, 2 v_mov_b32 each).
@@ -174,6 +197,83 @@ __device__ __forceinline__ void kernel_of_r2_k_x2(double r2a, double r2b, double
     outa = variance * ea;
     outb = variance * eb;
   }
+}
+
+// Two kernel values from r² (lockstep pair), with the table-driven exp and a one-correction sqrt —
+// the posterior kernel's generation step, where every fp64 VALU instruction is taken from the
+// MFMA's time (FP64 VALU and MFMA share the pipe):
+//   * exp(x), x ≤ 0: x = (64m + j)·ln2/64 + f with |f| ≤ ln2/128 (Cody–Waite, fdlibm's ln2 split);
+//     exp(x) = 2^m · T[j] · (1 + p(f)), p the degree-5 Taylor polynomial (remainder < 3.5e-17).
+//     ≤ 1 ulp against np.exp over [−740, 0]; 12 instead of 17 fp64 instructions.  `tab` = the
+//     64-entry kExp2Tab64 staged in LDS.
+//   * sqrt: v_rsq_f64 seed, one Goldschmidt step, one residual correction (≤ 1 ulp; the second
+//     correction of sqrt_nonneg only settles round-to-nearest ties).  r² is clamped to ≥ 1e-300 in
+//     place of the zero test: r = 1e-150 gives exactly σ_f², as r = 0 does.
+//   * Matern polynomial from r² itself: 1 + √5 r + 5/3 r² (GPy squares r; ≤ 1 ulp apart).
+// v_max_f64 without the canonicalising v_max x,x that fmax() adds for IEEE maxNum semantics (the
+// inputs here are never signalling NaNs).
+__device__ __forceinline__ double vmax_vs(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "s"(b));
+  return r;
+}
+
+// Round-to-nearest-even of y with |y| < 2^51, as a double and as an int, from one add: the
+// 1.5·2^52 shift leaves the integer in the low word (replaces v_rndne + v_cvt_i32).
+struct RoundedK {
+  double k;
+  int ki;
+};
+__device__ __forceinline__ RoundedK round_shift(double y_plus_shift) {
+  return RoundedK{y_plus_shift - 6755399441055744.0, __double2loint(y_plus_shift)};
+}
+
+// pm = (σ_f², √5·σ_f², 5/3·σ_f²): the Matern polynomial with the variance folded in.
+template <int KIND>
+__device__ __forceinline__ void kernel_of_r2_tab_x2(double r2a, double r2b, const double (&pm)[3], const ExpCoef& ec,
+                                                    const double* tab, double& outa, double& outb) {
+  double xa, xb, ka_, kb_, pa_ = pm[0], pb_ = pm[0];
+  if constexpr (KIND == OMB_KERNEL_MATERN52) {
+    r2a = vmax_vs(r2a, ec.t[7]);
+    r2b = vmax_vs(r2b, ec.t[7]);
+    const double ya = __builtin_amdgcn_rsq(r2a), yb = __builtin_amdgcn_rsq(r2b);
+    double ga = r2a * ya, gb = r2b * yb, ha = 0.5 * ya, hb = 0.5 * yb;
+    const double qa = fma(-ga, ha, 0.5), qb = fma(-gb, hb, 0.5);
+    ga = fma(ga, qa, ga);
+    gb = fma(gb, qb, gb);
+    ha = fma(ha, qa, ha);
+    hb = fma(hb, qb, hb);
+    ga = fma(fma(-ga, ga, r2a), ha, ga);
+    gb = fma(fma(-gb, gb, r2b), hb, gb);
+    pa_ = fma(pm[2], r2a, fma(pm[1], ga, pm[0]));
+    pb_ = fma(pm[2], r2b, fma(pm[1], gb, pm[0]));
+    xa = -(kSqrt5 * ga);
+    xb = -(kSqrt5 * gb);
+    ka_ = fma(ga, ec.t[0], 6755399441055744.0);     // −√5·r·64/ln2 + 1.5·2^52
+    kb_ = fma(gb, ec.t[0], 6755399441055744.0);
+  } else {
+    xa = -0.5 * vmax_vs(r2a, 0.0);
+    xb = -0.5 * vmax_vs(r2b, 0.0);
+    ka_ = fma(xa, -ec.t[0] / kSqrt5, 6755399441055744.0);
+    kb_ = fma(xb, -ec.t[0] / kSqrt5, 6755399441055744.0);
+  }
+  const RoundedK rka = round_shift(ka_), rkb = round_shift(kb_);
+  const double ka = rka.k, kb = rkb.k;
+  double fa = fma(-ka, ec.t[1], xa), fb = fma(-kb, ec.t[1], xb);
+  fa = fma(-ka, ec.t[2], fa);
+  fb = fma(-kb, ec.t[2], fb);
+  double qa = fma(fa, ec.t[3], ec.t[4]), qb = fma(fb, ec.t[3], ec.t[4]);
+  qa = fma_vvs(qa, fa, ec.t[5]);
+  qb = fma_vvs(qb, fb, ec.t[5]);
+  qa = fma_vvs(qa, fa, ec.t[6]);
+  qb = fma_vvs(qb, fb, ec.t[6]);
+  qa = fma(qa, fa, 1.0);
+  qb = fma(qb, fb, 1.0);
+  const int ia = rka.ki, ib = rkb.ki;
+  const double Ta = tab[ia & 63], Tb = tab[ib & 63];
+  const double ea = ldexp(fma(Ta, qa * fa, Ta), ia >> 6), eb = ldexp(fma(Tb, qb * fb, Tb), ib >> 6);
+  outa = pa_ * ea;
+  outb = pb_ * eb;
 }
 
 // GPy Matern52.K_of_r: variance*(1+sqrt(5)*r+5/3*r**2)*exp(-sqrt(5)*r)  (r ≥ 0)

@@ -185,7 +185,7 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
   // as [j][c] (lanes read consecutive doubles) so the 256-VGPR budget stays with the MFMA tiles.
   constexpr bool kCandLds = DP > 8 || RT >= 8;
   constexpr int kCtrDoubles = kCounters ? kMaxChunks : 0;
-  __shared__ double kbuf[NBUF * CHUNK + kCtrDoubles + (kCandLds ? DP * BN : 0)];
+  __shared__ double kbuf[NBUF * CHUNK + kCtrDoubles + (kCandLds ? DP * BN : 0) + 64];
 
   const int obj = blockIdx.y;
   const GPDev g = args.gp[obj];
@@ -198,6 +198,9 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
   const int cg = tid % BN;
   double b[kCandLds ? 1 : DP];
   double* cand = kbuf + NBUF * CHUNK + kCtrDoubles;
+  double* etab = cand + (kCandLds ? DP * BN : 0);   // 2^(j/64) for kernel_of_r2_tab_x2
+  if (tid < 64) etab[tid] = kExp2Tab64[tid];
+  __syncthreads();
   double csq = 0.0;
   if constexpr (kCandLds) {
     for (int e = tid; e < DP * BN; e += NT) {
@@ -313,6 +316,8 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
   static_assert(EPT % 2 == 0, "generation runs two rows per step");
   // the lockstep pair needs ~20 more VGPRs: variants already near the register limit keep one row per step
   constexpr bool kPairs = !kCandLds && !(ABL & (1 | 16 | 512));
+  const double pm_s = (ABL & 256) ? 1.0 : g.variance;
+  const double pm[3] = {pm_s, kSqrt5 * pm_s, kFiveThirds * pm_s};
   auto generate_mfma = [&](int kc, double* buf) {
     if constexpr (kMfmaGen) {
       if (NW > TPC && (wave / TPC) != kc % (NW / TPC)) return;   // other waves take this chunk
@@ -333,11 +338,14 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
         for (int e = 0; e < 4; e += 2) {
           const int k0 = rowbase + 4 * e + (lane >> 4), k1 = k0 + 4;
           double v0, v1;
-          if constexpr (kAug) {
-            kernel_of_r2_k_x2<KIND>(cr[e], cr[e + 1], (ABL & 256) ? 1.0 : g.variance, args.ec, v0, v1);
-          } else {
-            kernel_of_r2_k_x2<KIND>(fma(-2.0, cr[e], g.xsq[k0] + csq_m), fma(-2.0, cr[e + 1], g.xsq[k1] + csq_m),
-                                    (ABL & 256) ? 1.0 : g.variance, args.ec, v0, v1);
+          const double sf2 = (ABL & 256) ? 1.0 : g.variance;
+          const double r2a = kAug ? cr[e] : fma(-2.0, cr[e], g.xsq[k0] + csq_m);
+          const double r2b = kAug ? cr[e + 1] : fma(-2.0, cr[e + 1], g.xsq[k1] + csq_m);
+          if constexpr (ABL & 8192)   // ablation: the 17-instruction polynomial exp, two sqrt corrections
+            kernel_of_r2_k_x2<KIND>(r2a, r2b, sf2, args.ec, v0, v1);
+          else
+            kernel_of_r2_tab_x2<KIND>(r2a, r2b, pm, args.ec, etab, v0, v1);
+          if constexpr (!kAug) {
             v0 = (k0 < g.n) ? v0 : 0.0;
             v1 = (k1 < g.n) ? v1 : 0.0;
           }

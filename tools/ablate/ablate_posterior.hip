@@ -91,7 +91,7 @@ int main(int argc, char** argv) {
   const Variant wide[] = {
       {"default RT8 CT2 (MFMA gen)", run<8, 2, 8, 0, 32>},
       {"VALU gen (2048)", run<8, 2, 8, 2048, 32>},
-      {"cross term only (4096)", run<8, 2, 8, 4096, 32>},
+      {"polynomial exp (8192)", run<8, 2, 8, 8192, 32>},
       {"const A (4)", run<8, 2, 8, 4, 32>},
       {"generation only (2)", run<8, 2, 8, 2, 32>},
       {"VALU generation only (2050)", run<8, 2, 8, 2050, 32>},
@@ -104,6 +104,8 @@ int main(int argc, char** argv) {
       {"default (ring, MFMA gen)", run<4, 4, 8, 0>},
       {"generation only (2)", run<4, 4, 8, 2>},
       {"cross term only (4096)", run<4, 4, 8, 4096>},
+      {"polynomial exp (8192)", run<4, 4, 8, 8192>},
+      {"polynomial exp, gen only", run<4, 4, 8, 8194>},
       {"VALU gen (2048)", run<4, 4, 8, 2048>},
       {"A PD=2 (64)", run<4, 4, 8, 64>},
       {"const A (4)", run<4, 4, 8, 4>},

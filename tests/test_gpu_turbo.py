@@ -66,7 +66,7 @@ def spd(N, seed):
     return G @ G.T / N + 0.5 * np.eye(N)
 
 
-@pytest.mark.parametrize("N", [1, 2, 63, 64, 65, 130, 333, 1000])
+@pytest.mark.parametrize("N", [1, 2, 63, 64, 65, 130, 192, 193, 333, 1000, 3000])
 def test_cholesky_vs_lapack(ctx, N):
     A = spd(N, N)
     wide = np.full((N, N + 5), 7.0)                  # lda > N: the extra columns are never touched
@@ -81,9 +81,8 @@ def test_cholesky_vs_lapack(ctx, N):
     assert np.array_equal(got[:, N:], wide[:, N:])
 
 
-@pytest.mark.parametrize("bad", [0, 70, 199])
-def test_cholesky_info_matches_dpotrf(ctx, bad):
-    N = 200
+@pytest.mark.parametrize("N,bad", [(200, 0), (200, 70), (200, 199), (700, 300), (700, 650), (700, 699)])
+def test_cholesky_info_matches_dpotrf(ctx, N, bad):
     A = spd(N, 5)
     A[bad, bad] = -1.0
     _, info_ref = linalg.lapack.dpotrf(A, lower=1)

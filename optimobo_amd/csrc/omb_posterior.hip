@@ -8,9 +8,11 @@
 // All arithmetic is fp64 (fp32 fails parity by orders of magnitude).
 //
 // Fused posterior kernel (one workgroup = 512 threads = 8 waves, BN candidates):
-//   * K* is generated 64 training rows at a time ("chunk") by all 8 waves (VALU fp64) into a
-//     double-buffered LDS tile stored directly in the B-operand fragment order of
-//     v_mfma_f64_16x16x4_f64, so each wave reads a fragment as 64 consecutive doubles.
+//   * K* is generated 64 training rows at a time ("chunk") as 16×16 tiles: r² (or, for d > 8, the
+//     cross term) of a tile is a few FP64 MFMA k-steps against fragment-packed training rows,
+//     then the Matern transform runs in VALU (table-driven exp).  The values land in a 3-buffer
+//     LDS ring in the B-operand fragment order of v_mfma_f64_16x16x4_f64, so each wave reads a
+//     fragment as 64 consecutive doubles; waves synchronise per chunk through LDS counters.
 //   * The triangular product V = L⁻¹ K* runs on FP64 MFMA: the A operand (L⁻¹) is read from a
 //     packed, fragment-ordered copy (zero blocks above the diagonal are never stored or read);
 //     it is L2-resident (1.06 MiB per objective at n = 512) and shared by every workgroup.
@@ -546,136 +548,6 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
     } else {
       for (int t = tid; t < NT; t += BN) m += redmu[t];
     }
-    const int64_t c = c0 + tid;
-    if (c < N) {
-      mu_out[(int64_t)obj * N + c] = m;
-      var_out[(int64_t)obj * N + c] = g.variance - s;
-    }
-  }
-}
-
-// ----------------------------------------------------------------------------- two-phase posterior
-// For n_pad·BN ≤ 16384 (n ≤ 512 at BN = 32, n ≤ 256 at BN = 64): phase 1 generates K* for ALL
-// training rows of the block's candidates into one 128 KiB LDS tile (fragment order, as above);
-// after a single barrier, phase 2 runs every wave's whole triangular row-tile work with no
-// further synchronisation.  FP64 VALU (generation) and FP64 MFMA share one pipe on gfx950
-// (tools/microbench), so overlapping the two phases buys nothing — removing the per-chunk
-// barriers does.  Same SIMD-balanced row-tile assignment as posterior_kernel.
-constexpr int kTwoPhaseLds = 16384;   // doubles (128 KiB)
-
-template <int RT, int CT, int DP, int KIND, int NW = 16, int ABL = 0>
-__global__ __launch_bounds__(64 * NW, NW / 4) void posterior2p_kernel(GPArgs args, const double* __restrict__ Xc,
-                                                                       int64_t N, double* __restrict__ mu_out,
-                                                                       double* __restrict__ var_out) {
-  constexpr int NT = 64 * NW;
-  constexpr int G = NW / 4;
-  constexpr int BN = 16 * CT;
-  constexpr int RPI = NT / BN;                // K* rows generated per pass of the block
-  static_assert(NT % BN == 0, "BN must divide the block");
-  static_assert(kTwoPhaseLds >= NW * BN + NT, "epilogue scratch must fit");
-  __shared__ double kbuf[kTwoPhaseLds];
-
-  const int obj = blockIdx.y;
-  const GPDev g = args.gp[obj];
-  const int d = args.d;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t c0 = (int64_t)blockIdx.x * BN;
-  const int Q = (g.R + 3) >> 2;
-  const int n_pad = kChunkRows * Q;
-
-  // ---- phase 1: K* (n_pad × BN) into LDS, μ partials in registers
-  const int cg = tid % BN;
-  const int64_t ci = min(c0 + cg, N - 1);
-  double b[DP];
-  double csq = 0.0;
-#pragma unroll
-  for (int j = 0; j < DP; ++j) {
-    b[j] = (j < d) ? Xc[ci * d + j] / g.ls[j] : 0.0;
-    csq += b[j] * b[j];
-  }
-  const int gen_ct = cg >> 4, gen_cc = cg & 15;
-  const int row_in_pass = (BN == 64) ? wave : tid / BN;
-  double mu_part = 0.0;
-  for (int k0 = 0; k0 < n_pad; k0 += RPI) {
-    const int k = k0 + row_in_pass;
-    double val = 0.0;
-    if (k < g.n) {
-      const double* xr = g.Xs + (int64_t)k * DP;
-      double dot = 0.0;
-#pragma unroll
-      for (int j = 0; j < DP; ++j) dot = fma(xr[j], b[j], dot);
-      if constexpr (ABL & 1)
-        val = dot;
-      else
-        val = (ABL & 16) ? kernel_of_r2<KIND, false>(fma(-2.0, dot, g.xsq[k] + csq), g.variance)
-                         : kernel_of_r2_k<KIND>(fma(-2.0, dot, g.xsq[k] + csq), g.variance, args.ec);
-      mu_part = fma(g.alpha[k], val, mu_part);
-    }
-    if (k < n_pad) kbuf[((k >> 2) * CT + gen_ct) * 64 + (k & 3) * 16 + gen_cc] = val;
-  }
-  __syncthreads();
-
-  // ---- phase 2: V = L⁻¹ K* on FP64 MFMA, one slot (16-row tile) after the other
-  const int simd = wave & 3, h = wave >> 2;
-  d4 acc[RT][CT];
-#pragma unroll
-  for (int j = 0; j < RT; ++j) {
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct) acc[j][ct] = d4{0.0, 0.0, 0.0, 0.0};
-    if constexpr (ABL & 2) continue;
-    const int q = 2 * G * (j >> 1) + ((j & 1) ? (2 * G - 1 - h) : h);
-    const int r = 4 * q + ((simd + q) & 3);
-    if (r >= g.R) continue;
-    const double* A = g.Lp + 128ll * r * (r + 1) + 2 * lane;
-    const int npairs = 2 * (r + 1);
-    d2 a_cur = (ABL & 4) ? d2{1e-3 * lane, 2e-3} : *reinterpret_cast<const d2*>(A);
-    for (int P = 0; P < npairs; ++P) {
-      d2 a_nxt = a_cur;
-      if (P + 1 < npairs) {
-        if constexpr (ABL & 4)
-          a_nxt = d2{a_cur.y, a_cur.x};
-        else
-          a_nxt = *reinterpret_cast<const d2*>(A + 128 * (P + 1));
-      }
-      const double* bp = kbuf + (2 * P) * CT * 64 + lane;
-#pragma unroll
-      for (int ct = 0; ct < CT; ++ct) {
-        acc[j][ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(a_cur.x, bp[ct * 64], acc[j][ct], 0, 0, 0);
-        acc[j][ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(a_cur.y, bp[(CT + ct) * 64], acc[j][ct], 0, 0, 0);
-      }
-      a_cur = a_nxt;
-    }
-  }
-  __syncthreads();   // every wave is done reading K* before the epilogue reuses the LDS
-
-  // ---- epilogue (as posterior_kernel)
-  double part[CT];
-#pragma unroll
-  for (int ct = 0; ct < CT; ++ct) {
-    double s = 0.0;
-#pragma unroll
-    for (int j = 0; j < RT; ++j)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) s = fma(acc[j][ct][i], acc[j][ct][i], s);
-    s += __shfl_xor(s, 16);
-    s += __shfl_xor(s, 32);
-    part[ct] = s;
-  }
-  double* red = kbuf;
-  double* redmu = kbuf + NW * BN;
-  if (lane < 16) {
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct) red[wave * BN + ct * 16 + lane] = part[ct];
-  }
-  redmu[tid] = mu_part;
-  __syncthreads();
-  if (tid < BN) {
-    double s = 0.0;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) s += red[w * BN + tid];
-    double m = 0.0;
-    for (int t = tid; t < NT; t += BN) m += redmu[t];
     const int64_t c = c0 + tid;
     if (c < N) {
       mu_out[(int64_t)obj * N + c] = m;

@@ -116,44 +116,66 @@ hipError_t launch_pack_x(hipStream_t stream, int d, int DP, int n_pad, const dou
 
 // ----------------------------------------------------------------------------- K block
 // Standalone K(X_train, X*) (n, N) row-major — the HBM-bound kernel of the north star.
-// Each thread owns two adjacent candidates (16-byte stores), each block 256 training rows;
-// K is written with non-temporal stores (written once, never re-read by this kernel):
-// tools/ablate/ablate_kblock measured 3.47 → 4.20 TB/s for 64-row plain → 256-row nt.
+// K block with r² on MFMA (the posterior kernel's generation step, stored instead of multiplied):
+// a workgroup covers 64 candidates × kKBlockRows training rows, wave w the candidates' 16-wide
+// tile w.  Per 16-row tile: ⌈(d+2)/4⌉ MFMA k-steps against the fragment-packed rows (Xf) give r²
+// (d ≤ 8; for d > 8 the cross term, r² then one fma), the Matern transform runs on the lane's 4
+// values (kernel_of_r2_tab_x2), and each store instruction writes 4 rows × 16 consecutive
+// candidates (128-byte segments), non-temporal (written once, never re-read here).  Against the
+// previous VALU dot products (d FMAs plus d loads per element; tools/ablate/ablate_kblock2):
+// 1.18 → 1.03 ms at n = 512, d = 6, N = 2^20 and 2.43 → 1.66 ms at n = 1024, d = 30, N = 2^19.
 template <int DP, int KIND>
-__global__ __launch_bounds__(256) void kernel_block_kernel(GPDev g, int d, const double* __restrict__ Xc,
-                                                           int64_t N, double* __restrict__ K, ExpCoef ec) {
-  constexpr int kRows = kKBlockRows;
-  const int64_t c = 2 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
-  if (c >= N) return;
-  const bool two = (c + 1) < N;
-  double b0[DP], b1[DP];
-  double s0 = 0.0, s1 = 0.0;
+__global__ __launch_bounds__(256) void kernel_block_mfma_kernel(GPDev g, int d, const double* __restrict__ Xc,
+                                                                int64_t N, double* __restrict__ K, ExpCoef ec) {
+  constexpr bool kAug = DP <= 8;
+  constexpr int KSD = kAug ? (DP + 5) / 4 : (DP + 3) / 4;
+  constexpr int KSDP = ((DP + 5) / 4 + 1) / 2;   // = packed_X_pairs(DP)
+  __shared__ double etab[64];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (tid < 64) etab[tid] = kExp2Tab64[tid];
+  const int64_t col = (int64_t)blockIdx.x * 64 + 16 * wave + (lane & 15);
+  const int64_t ci = col < N ? col : N - 1;
+  double csq = 0.0;
 #pragma unroll
   for (int j = 0; j < DP; ++j) {
-    b0[j] = (j < d) ? Xc[c * d + j] / g.ls[j] : 0.0;
-    b1[j] = (j < d && two) ? Xc[(c + 1) * d + j] / g.ls[j] : 0.0;
-    s0 += b0[j] * b0[j];
-    s1 += b1[j] * b1[j];
+    const double c = (j < d) ? Xc[ci * d + j] / g.ls[j] : 0.0;
+    csq = fma(c, c, csq);
   }
-  const int k0 = blockIdx.y * kRows;
-  const int k1 = min(g.n, k0 + kRows);
-  for (int k = k0; k < k1; ++k) {
-    const double* xr = g.Xs + (int64_t)k * DP;
-    double dot0 = 0.0, dot1 = 0.0;
+  double bfr[KSD];
 #pragma unroll
-    for (int j = 0; j < DP; ++j) {
-      dot0 = fma(xr[j], b0[j], dot0);
-      dot1 = fma(xr[j], b1[j], dot1);
-    }
-    const double xk = g.xsq[k];
-    double v0, v1;
-    kernel_of_r2_k_x2<KIND>(fma(-2.0, dot0, xk + s0), fma(-2.0, dot1, xk + s1), g.variance, ec, v0, v1);
-    double* dst = K + (int64_t)k * N + c;
-    if (two && ((N & 1) == 0)) {
-      __builtin_nontemporal_store(d2{v0, v1}, reinterpret_cast<d2*>(dst));
-    } else {
-      __builtin_nontemporal_store(v0, dst);
-      if (two) __builtin_nontemporal_store(v1, dst + 1);
+  for (int s = 0; s < KSD; ++s) {
+    const int j = 4 * s + (lane >> 4);
+    const double c = (j < d) ? Xc[ci * d + j] / g.ls[j] : 0.0;
+    if constexpr (kAug)
+      bfr[s] = (j < d) ? -2.0 * c : (j == d ? 1.0 : (j == d + 1 ? csq : 0.0));
+    else
+      bfr[s] = c;
+  }
+  const double pm[3] = {g.variance, kSqrt5 * g.variance, kFiveThirds * g.variance};
+  __syncthreads();
+  const int T0 = blockIdx.y * (kKBlockRows / 16);
+  const int T1 = min((g.n + 15) / 16, T0 + kKBlockRows / 16);
+  for (int T = T0; T < T1; ++T) {
+    const d2* xa = reinterpret_cast<const d2*>(g.Xf + (int64_t)T * (KSDP * 128) + 2 * lane);
+    d2 a[(KSD + 1) / 2];
+#pragma unroll
+    for (int p = 0; p < (KSD + 1) / 2; ++p) a[p] = xa[64 * p];
+    d4 cr = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < KSD; ++s)
+      cr = __builtin_amdgcn_mfma_f64_16x16x4f64((s & 1) ? a[s >> 1].y : a[s >> 1].x, bfr[s], cr, 0, 0, 0);
+#pragma unroll
+    for (int e = 0; e < 4; e += 2) {
+      const int k0 = 16 * T + 4 * e + (lane >> 4), k1 = k0 + 4;
+      const double r2a = kAug ? cr[e] : fma(-2.0, cr[e], g.xsq[k0] + csq);
+      const double r2b = kAug ? cr[e + 1] : fma(-2.0, cr[e + 1], g.xsq[k1] + csq);
+      double v0, v1;
+      kernel_of_r2_tab_x2<KIND>(r2a, r2b, pm, ec, etab, v0, v1);
+      if (col < N) {
+        if (k0 < g.n) __builtin_nontemporal_store(v0, K + (int64_t)k0 * N + col);
+        if (k1 < g.n) __builtin_nontemporal_store(v1, K + (int64_t)k1 * N + col);
+      }
     }
   }
 }
@@ -607,10 +629,10 @@ template <int KIND>
 static hipError_t launch_kblock_kind(hipStream_t stream, const GPArgs& args, int obj, const double* Xc, int64_t N,
                                      double* K) {
   const GPDev& g = args.gp[obj];
-  dim3 grid((unsigned)((N + 511) / 512), (unsigned)((g.n + kKBlockRows - 1) / kKBlockRows));
+  dim3 grid((unsigned)((N + 63) / 64), (unsigned)((g.n + kKBlockRows - 1) / kKBlockRows));
   switch (args.DP) {
 #define OMB_KB(DPV) \
-  case DPV: hipLaunchKernelGGL((kernel_block_kernel<DPV, KIND>), grid, dim3(256), 0, stream, g, args.d, Xc, N, K, exp_coef()); break;
+  case DPV: hipLaunchKernelGGL((kernel_block_mfma_kernel<DPV, KIND>), grid, dim3(256), 0, stream, g, args.d, Xc, N, K, exp_coef()); break;
     OMB_KB(2) OMB_KB(4) OMB_KB(6) OMB_KB(8) OMB_KB(16) OMB_KB(32)
 #undef OMB_KB
     default: return hipErrorInvalidValue;

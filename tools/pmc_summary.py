@@ -31,7 +31,7 @@ def main():
     kernels = sorted({k for k, _ in m})
     res = {}
     for kern in kernels:
-        if ("posterior_kernel" not in kern) and ("kernel_block_kernel" not in kern):
+        if ("posterior_kernel" not in kern) and ("kernel_block" not in kern):
             continue
         f = m.get((kern, "FETCH_SIZE"), 0.0) * 1024
         w = m.get((kern, "WRITE_SIZE"), 0.0) * 1024

@@ -130,10 +130,14 @@ __global__ __launch_bounds__(256) void kernel_block_mfma_kernel(GPDev g, int d, 
   constexpr bool kAug = DP <= 8;
   constexpr int KSD = kAug ? (DP + 5) / 4 : (DP + 3) / 4;
   constexpr int KSDP = ((DP + 5) / 4 + 1) / 2;   // = packed_X_pairs(DP)
-  __shared__ double etab[64];
+  constexpr bool kTab256 = KIND == OMB_KERNEL_MATERN52;
+  __shared__ double etab[kTab256 ? 256 : 64];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  if (tid < 64) etab[tid] = kExp2Tab64[tid];
+  if constexpr (kTab256)
+    etab[tid] = kExp2Tab256[tid];   // 256 threads
+  else if (tid < 64)
+    etab[tid] = kExp2Tab64[tid];
   const int64_t col = (int64_t)blockIdx.x * 64 + 16 * wave + (lane & 15);
   const int64_t ci = col < N ? col : N - 1;
   double csq = 0.0;
@@ -171,7 +175,10 @@ __global__ __launch_bounds__(256) void kernel_block_mfma_kernel(GPDev g, int d, 
       const double r2a = kAug ? cr[e] : fma(-2.0, cr[e], g.xsq[k0] + csq);
       const double r2b = kAug ? cr[e + 1] : fma(-2.0, cr[e + 1], g.xsq[k1] + csq);
       double v0, v1;
-      kernel_of_r2_tab_x2<KIND>(r2a, r2b, pm, ec, etab, v0, v1);
+      if constexpr (kTab256)
+        matern_r2_tab256_x2(r2a, r2b, pm, ec, etab, v0, v1);
+      else
+        kernel_of_r2_tab_x2<KIND>(r2a, r2b, pm, ec, etab, v0, v1);
       if (col < N) {
         if (k0 < g.n) __builtin_nontemporal_store(v0, K + (int64_t)k0 * N + col);
         if (k1 < g.n) __builtin_nontemporal_store(v1, K + (int64_t)k1 * N + col);
@@ -209,7 +216,12 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
   // as [j][c] (lanes read consecutive doubles) so the 256-VGPR budget stays with the MFMA tiles.
   constexpr bool kCandLds = DP > 8 || RT >= 8;
   constexpr int kCtrDoubles = kCounters ? kMaxChunks : 0;
-  __shared__ double kbuf[NBUF * CHUNK + kCtrDoubles + (kCandLds ? DP * BN : 0) + 64];
+  // Matern: 256-entry exp table (matern_r2_tab256_x2).  ABL 16384 keeps the 64-entry table of the
+  // RBF path (ablation: 10.21 → 10.12 ms at config 3, max rel. error 3.9e-14 → 1.6e-14), ABL 32768
+  // drops the sqrt correction (a further −1.2%, but 5e-13 max rel. error: not used).
+  constexpr bool kTab256 = !(ABL & 16384) && KIND == OMB_KERNEL_MATERN52;
+  constexpr int kTabN = kTab256 ? 256 : 64;
+  __shared__ double kbuf[NBUF * CHUNK + kCtrDoubles + (kCandLds ? DP * BN : 0) + kTabN];
 
   const int obj = blockIdx.y;
   const GPDev g = args.gp[obj];
@@ -222,8 +234,8 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
   const int cg = tid % BN;
   double b[kCandLds ? 1 : DP];
   double* cand = kbuf + NBUF * CHUNK + kCtrDoubles;
-  double* etab = cand + (kCandLds ? DP * BN : 0);   // 2^(j/64) for kernel_of_r2_tab_x2
-  if (tid < 64) etab[tid] = kExp2Tab64[tid];
+  double* etab = cand + (kCandLds ? DP * BN : 0);   // 2^(j/kTabN) for the table-driven exp
+  for (int i = tid; i < kTabN; i += NT) etab[i] = kTab256 ? kExp2Tab256[i] : kExp2Tab64[i];
   __syncthreads();
   double csq = 0.0;
   if constexpr (kCandLds) {
@@ -367,6 +379,8 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
           const double r2b = kAug ? cr[e + 1] : fma(-2.0, cr[e + 1], g.xsq[k1] + csq_m);
           if constexpr (ABL & 8192)   // ablation: the 17-instruction polynomial exp, two sqrt corrections
             kernel_of_r2_k_x2<KIND>(r2a, r2b, sf2, args.ec, v0, v1);
+          else if constexpr (kTab256)
+            matern_r2_tab256_x2<(ABL & 32768) != 0>(r2a, r2b, pm, args.ec, etab, v0, v1);
           else
             kernel_of_r2_tab_x2<KIND>(r2a, r2b, pm, args.ec, etab, v0, v1);
           if constexpr (!kAug) {

@@ -4,7 +4,9 @@
 //   d = 6: config 3 variants (RT 4, CT 4); d = 30: config 5 variants (RT 8, CT 2, candidates in LDS)
 // Variants are timed interleaved in one process (cdna_hip_programming.md §5.4 rule 24).
 #include <cstdio>
+#include <cmath>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "../../optimobo_amd/csrc/omb_posterior.hip"
@@ -39,6 +41,57 @@ float run(const Bench& b, int reps) {
   CK(hipEventDestroy(e0));
   CK(hipEventDestroy(e1));
   return ms / reps;
+}
+
+// Accuracy of the table-driven Matern transforms against a long-double host reference.
+__global__ void matern_acc_kernel(const double* r2, int M, ExpCoef ec, double* out) {
+  __shared__ double t64[64], t256[256];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+    t256[i] = kExp2Tab256[i];
+    if (i < 64) t64[i] = kExp2Tab64[i];
+  }
+  __syncthreads();
+  const double pm[3] = {1.0, kSqrt5, kFiveThirds};
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; 2 * i + 1 < M; i += gridDim.x * blockDim.x) {
+    double a, b;
+    kernel_of_r2_tab_x2<0>(r2[2 * i], r2[2 * i + 1], pm, ec, t64, a, b);
+    out[2 * i] = a; out[2 * i + 1] = b;
+    matern_r2_tab256_x2<false>(r2[2 * i], r2[2 * i + 1], pm, ec, t256, a, b);
+    out[M + 2 * i] = a; out[M + 2 * i + 1] = b;
+    matern_r2_tab256_x2<true>(r2[2 * i], r2[2 * i + 1], pm, ec, t256, a, b);
+    out[2 * M + 2 * i] = a; out[2 * M + 2 * i + 1] = b;
+  }
+}
+
+void matern_accuracy() {
+  const int M = 1 << 20;
+  std::vector<double> r2(M), out(3 * M);
+  for (int i = 0; i < M; ++i) {
+    // half log-uniform over [1e-20, 1e4], half uniform over [0, 40]
+    r2[i] = (i & 1) ? 40.0 * (i >> 1) / (M / 2) : pow(10.0, -20.0 + 24.0 * (i >> 1) / (M / 2));
+  }
+  r2[0] = 0.0;
+  double *dr2, *dout;
+  CK(hipMalloc(&dr2, M * 8)); CK(hipMalloc(&dout, 3 * M * 8));
+  CK(hipMemcpy(dr2, r2.data(), M * 8, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(matern_acc_kernel, dim3(1024), dim3(256), 0, 0, dr2, M, exp_coef(), dout);
+  CK(hipDeviceSynchronize());
+  CK(hipMemcpy(out.data(), dout, 3 * M * 8, hipMemcpyDeviceToHost));
+  const char* names[3] = {"tab64 (library default)", "tab256", "tab256 short sqrt"};
+  for (int v = 0; v < 3; ++v) {
+    double worst = 0, worst_r2 = 0, sum = 0;
+    for (int i = 0; i < M; ++i) {
+      long double r = sqrtl((long double)r2[i]);
+      long double ref = (1.0L + sqrtl(5.0L) * r + 5.0L / 3.0L * r * r) * expl(-sqrtl(5.0L) * r);
+      if (ref < 1e-300L) continue;
+      double e = (double)fabsl(((long double)out[v * M + i] - ref) / ref);
+      sum += e;
+      if (e > worst) { worst = e; worst_r2 = r2[i]; }
+    }
+    printf("accuracy %-24s max rel err %.3e (%.2f ulp) at r2 = %.3e, mean %.3e\n", names[v], worst,
+           worst / 1.1102230246251565e-16, worst_r2, sum / M);
+  }
+  CK(hipFree(dr2)); CK(hipFree(dout));
 }
 
 struct Variant {
@@ -90,6 +143,8 @@ int main(int argc, char** argv) {
   b.var = var;
   const Variant wide[] = {
       {"default RT8 CT2 (MFMA gen)", run<8, 2, 8, 0, 32>},
+      {"tab64 exp (16384)", run<8, 2, 8, 16384, 32>},
+      {"tab256 + short sqrt (32768)", run<8, 2, 8, 32768, 32>},
       {"VALU gen (2048)", run<8, 2, 8, 2048, 32>},
       {"polynomial exp (8192)", run<8, 2, 8, 8192, 32>},
       {"const A (4)", run<8, 2, 8, 4, 32>},
@@ -102,7 +157,11 @@ int main(int argc, char** argv) {
   };
   const Variant narrow[] = {
       {"default (ring, MFMA gen)", run<4, 4, 8, 0>},
+      {"tab64 exp (16384)", run<4, 4, 8, 16384>},
+      {"tab256 + short sqrt (32768)", run<4, 4, 8, 32768>},
       {"generation only (2)", run<4, 4, 8, 2>},
+      {"tab64 gen only", run<4, 4, 8, 16384 + 2>},
+      {"short sqrt gen only", run<4, 4, 8, 32768 + 2>},
       {"cross term only (4096)", run<4, 4, 8, 4096>},
       {"polynomial exp (8192)", run<4, 4, 8, 8192>},
       {"polynomial exp, gen only", run<4, 4, 8, 8194>},
@@ -117,11 +176,33 @@ int main(int argc, char** argv) {
       {"setprio waves 4-7 (128)", run<4, 4, 8, 128>},
       {"no sigma_f^2 mul (256)", run<4, 4, 8, 256>},
   };
+  matern_accuracy();
   const Variant* vs = d == 6 ? narrow : wide;
   const int NV = d == 6 ? (int)(sizeof(narrow) / sizeof(narrow[0])) : (int)(sizeof(wide) / sizeof(wide[0]));
   std::vector<float> t(NV, 0.f);
   for (int round = 0; round < 3; ++round)
     for (int i = 0; i < NV; ++i) t[i] += vs[i].fn(b, 5);
+  // outputs of every full variant against the default variant (max relative difference, μ and σ²)
+  {
+    std::vector<double> m0(n_obj * N), v0(n_obj * N), m1(n_obj * N), v1(n_obj * N);
+    vs[0].fn(b, 1);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(m0.data(), mu, n_obj * N * 8, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(v0.data(), var, n_obj * N * 8, hipMemcpyDeviceToHost));
+    for (int i = 1; i < NV; ++i) {
+      if (strstr(vs[i].name, "only") || strstr(vs[i].name, "const") || strstr(vs[i].name, "no ")) continue;
+      vs[i].fn(b, 1);
+      CK(hipDeviceSynchronize());
+      CK(hipMemcpy(m1.data(), mu, n_obj * N * 8, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(v1.data(), var, n_obj * N * 8, hipMemcpyDeviceToHost));
+      double em = 0, ev = 0;
+      for (int64_t j = 0; j < n_obj * N; ++j) {
+        em = fmax(em, fabs(m1[j] - m0[j]) / fmax(fabs(m0[j]), 1e-300));
+        ev = fmax(ev, fabs(v1[j] - v0[j]) / fmax(fabs(v0[j]), 1e-300));
+      }
+      printf("vs default: %-26s mu max rel %.2e  var max rel %.2e\n", vs[i].name, em, ev);
+    }
+  }
   double flops = (double)n_obj * N * ((double)n * (n + 1) + 2 * n + 2 * n + n * (2 * d + 2) + 10 * n);
   for (int i = 0; i < NV; ++i)
     printf("%-26s %8.3f ms  %6.1f TFLOP/s-equiv\n", vs[i].name, t[i] / 3, flops / (t[i] / 3 * 1e-3) / 1e12);

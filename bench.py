@@ -281,13 +281,14 @@ def run_thompson(args, cfg, world_size, rank, device, backend):
     ctx.close()
 
 
-def load_traffic(n, N):
-    """HBM bytes per posterior launch from the committed rocprofv3 PMC summary, if present."""
+def load_traffic(n, N, kernel="posterior"):
+    """HBM bytes per launch of the posterior ("posterior") or K-block ("kblock") kernel from the
+    committed rocprofv3 PMC summary (profiles/traffic.json, tools/pmc_summary.py), if present."""
     path = os.path.join(REPO, "profiles", "traffic.json")
     try:
         with open(path) as f:
             t = json.load(f)
-        key = f"posterior_n{n}_N{N}"
+        key = f"{kernel}_n{n}_N{N}"
         return t.get(key, {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None
@@ -460,7 +461,8 @@ def main():
         kb_ms = e0.elapsed_time(e1) / reps
         kb_bytes = 8.0 * (n + d) * N + 8.0 * n * (d + 1)      # 8(n+d) per candidate + model state
         kblock = {"bound": "hbm", "achieved": kb_bytes / (kb_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                  "frac": kb_bytes / (kb_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "ms": kb_ms,
+                  "frac": kb_bytes / (kb_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": load_traffic(n, N, "kblock"),
+                  "ms": kb_ms,
                   "note": f"omb_kernel_block writes K ({n}, {N}) fp64 to HBM"}
         del K
 

@@ -124,7 +124,7 @@ hipError_t launch_pack_x(hipStream_t stream, int d, int DP, int n_pad, const dou
 // candidates (128-byte segments), non-temporal (written once, never re-read here).  Against the
 // previous VALU dot products (d FMAs plus d loads per element; tools/ablate/ablate_kblock2):
 // 1.18 → 1.03 ms at n = 512, d = 6, N = 2^20 and 2.43 → 1.66 ms at n = 1024, d = 30, N = 2^19.
-template <int DP, int KIND>
+template <int DP, int KIND, bool kNT = true>   // kNT = false: plain stores (tools/ablate/ablate_kblock2.hip)
 __global__ __launch_bounds__(256) void kernel_block_mfma_kernel(GPDev g, int d, const double* __restrict__ Xc,
                                                                 int64_t N, double* __restrict__ K, ExpCoef ec) {
   constexpr bool kAug = DP <= 8;
@@ -180,8 +180,13 @@ __global__ __launch_bounds__(256) void kernel_block_mfma_kernel(GPDev g, int d, 
       else
         kernel_of_r2_tab_x2<KIND>(r2a, r2b, pm, ec, etab, v0, v1);
       if (col < N) {
-        if (k0 < g.n) __builtin_nontemporal_store(v0, K + (int64_t)k0 * N + col);
-        if (k1 < g.n) __builtin_nontemporal_store(v1, K + (int64_t)k1 * N + col);
+        if constexpr (kNT) {
+          if (k0 < g.n) __builtin_nontemporal_store(v0, K + (int64_t)k0 * N + col);
+          if (k1 < g.n) __builtin_nontemporal_store(v1, K + (int64_t)k1 * N + col);
+        } else {
+          if (k0 < g.n) K[(int64_t)k0 * N + col] = v0;
+          if (k1 < g.n) K[(int64_t)k1 * N + col] = v1;
+        }
       }
     }
   }

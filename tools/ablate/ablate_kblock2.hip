@@ -93,11 +93,16 @@ void bench(int n, int64_t N, int d) {
   dim3 g2((unsigned)((N + 63) / 64), (unsigned)((n + kKBlockRows - 1) / kKBlockRows));
   auto old_k = [&] { hipLaunchKernelGGL((kernel_block_kernel<DP, 0>), g1, dim3(256), 0, 0, g, d, Xc, N, K1, ec); };
   auto new_k = [&] { hipLaunchKernelGGL((kernel_block_mfma_kernel<DP, 0>), g2, dim3(256), 0, 0, g, d, Xc, N, K2, ec); };
-  float t1 = 0, t2 = 0;
+  auto plain_k = [&] {
+    hipLaunchKernelGGL((kernel_block_mfma_kernel<DP, 0, false>), g2, dim3(256), 0, 0, g, d, Xc, N, K2, ec);
+  };
+  float t1 = 0, t2 = 0, t3 = 0;
   for (int r = 0; r < 3; ++r) {
     t1 += time_ms(old_k, 5);
     t2 += time_ms(new_k, 5);
+    t3 += time_ms(plain_k, 5);
   }
+  printf("MFMA r2 with plain stores %.3f ms (%.0f GB/s)\n", t3 / 3, 8.0 * (n + d) * N / (t3 / 3 * 1e6));
   std::vector<double> h1((size_t)n * N), h2((size_t)n * N);
   CK(hipMemcpy(h1.data(), K1, h1.size() * 8, hipMemcpyDeviceToHost));
   CK(hipMemcpy(h2.data(), K2, h2.size() * 8, hipMemcpyDeviceToHost));

@@ -82,7 +82,8 @@ def test_posterior_vs_golden(ctx, golden_dir, name):
                                    (256, 6, 333), (300, 9, 129), (512, 6, 2048), (700, 2, 100),
                                    (1024, 6, 300), (128, 30, 200), (64, 32, 64),
                                    (1024, 30, 300), (600, 17, 100), (513, 16, 77), (777, 5, 129),
-                                   (200, 8, 100), (150, 7, 99), (90, 5, 33), (1000, 8, 65)])
+                                   (200, 8, 100), (150, 7, 99), (90, 5, 33), (1000, 8, 65),
+                                   (200, 30, 97), (256, 17, 65), (129, 3, 31)])
 def test_posterior_sizes(ctx, n, d, N):
     rng = np.random.default_rng(n * 1000 + d)
     X = rng.uniform(0, 1, (n, d))

@@ -121,7 +121,8 @@ int main(int argc, char** argv) {
   double *Xs, *xsq, *al, *Lp, *ls, *Xc, *mu, *var;
   CK(hipMalloc(&Xs, hXs.size() * 8)); CK(hipMalloc(&xsq, n_pad * 8)); CK(hipMalloc(&al, n_pad * 8));
   CK(hipMalloc(&Lp, hL.size() * 8)); CK(hipMalloc(&ls, DP * 8)); CK(hipMalloc(&Xc, hXc.size() * 8));
-  CK(hipMalloc(&mu, 2 * N * 8)); CK(hipMalloc(&var, 2 * N * 8));
+  CK(hipMalloc(&mu, 3 * N * 8)); CK(hipMalloc(&var, 3 * N * 8));
+  if (n_obj < 1 || n_obj > 3) { printf("n_obj must be 1..3\n"); return 1; }
   CK(hipMemcpy(Xs, hXs.data(), hXs.size() * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(xsq, hxsq.data(), n_pad * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(al, ha.data(), n_pad * 8, hipMemcpyHostToDevice));
@@ -132,7 +133,7 @@ int main(int argc, char** argv) {
   double* Xf;
   CK(hipMalloc(&Xf, packed_X_size(n_pad, DP) * 8));
   CK(launch_pack_x(0, d, DP, n_pad, Xs, xsq, Xf));
-  for (int o = 0; o < 2; ++o) b.a.gp[o] = GPDev{Xs, xsq, al, Lp, ls, 1.0, n, R, 0, 0, Xf};
+  for (int o = 0; o < 3; ++o) b.a.gp[o] = GPDev{Xs, xsq, al, Lp, ls, 1.0, n, R, 0, 0, Xf};
   b.a.d = d;
   b.a.DP = DP;
   b.a.ec = exp_coef();
@@ -157,6 +158,7 @@ int main(int argc, char** argv) {
   };
   const Variant narrow[] = {
       {"default (ring, MFMA gen)", run<4, 4, 8, 0>},
+      {"RT4 CT2 counter ring", run<4, 2, 8, 0>},
       {"tab64 exp (16384)", run<4, 4, 8, 16384>},
       {"tab256 + short sqrt (32768)", run<4, 4, 8, 32768>},
       {"generation only (2)", run<4, 4, 8, 2>},
@@ -176,9 +178,24 @@ int main(int argc, char** argv) {
       {"setprio waves 4-7 (128)", run<4, 4, 8, 128>},
       {"no sigma_f^2 mul (256)", run<4, 4, 8, 256>},
   };
+  // n ≤ 256 (configs 2 and 4): the library launches RT = 2 (n ≤ 256) or 1 (n ≤ 128), CT = 4, barrier pipeline
+  const Variant small[] = {
+      {"RT2 CT4 barrier (library n<=256)", run<2, 4, 8, 32>},
+      {"RT2 CT4 counter ring", run<2, 4, 8, 0>},
+      {"RT2 CT2 barrier", run<2, 2, 8, 32>},
+      {"RT2 CT2 counter ring", run<2, 2, 8, 0>},
+      {"RT1 CT4 16 waves barrier", run<1, 4, 16, 32>},
+      {"RT1 CT2 16 waves ring", run<1, 2, 16, 0>},
+      {"RT4 CT4 counter ring", run<4, 4, 8, 0>},
+      {"RT1 CT4 barrier (library n<=128)", run<1, 4, 8, 32>},
+      {"RT1 CT2 counter ring", run<1, 2, 8, 0>},
+      {"RT1 CT2 barrier", run<1, 2, 8, 32>},
+  };
   matern_accuracy();
-  const Variant* vs = d == 6 ? narrow : wide;
-  const int NV = d == 6 ? (int)(sizeof(narrow) / sizeof(narrow[0])) : (int)(sizeof(wide) / sizeof(wide[0]));
+  const bool is_small = d == 6 && n <= 256;
+  const Variant* vs = is_small ? small : (d == 6 ? narrow : wide);
+  const int NV = is_small ? (int)(sizeof(small) / sizeof(small[0]))
+                          : (d == 6 ? (int)(sizeof(narrow) / sizeof(narrow[0])) : (int)(sizeof(wide) / sizeof(wide[0])));
   std::vector<float> t(NV, 0.f);
   for (int round = 0; round < 3; ++round)
     for (int i = 0; i < NV; ++i) t[i] += vs[i].fn(b, 5);

@@ -1093,9 +1093,25 @@ int omb_gp_lml_grad(omb_ctx* ctx, int kernel, int n, int d, const double* X_dev,
   for (int j = 0; j < d; ++j)
     if (!(lengthscale_host[j] > 0.0)) return fail(ctx, OMB_EINVAL, "lengthscale[%d]=%g must be > 0", j, lengthscale_host[j]);
   if (!(variance > 0.0) || !(noise >= 0.0)) return fail(ctx, OMB_EINVAL, "variance must be > 0 and noise >= 0");
+  const int DP = pad_dim(d);
+  if (gp_lml_small_fits(n, DP)) {
+    // one workgroup, one launch, one synchronisation (launch_gp_lml_small)
+    if ((rc = grow_dev(ctx, &ctx->fws, &ctx->fws_cap, sizeof(double) * (DP + 5), "GP fit workspace"))) return rc;
+    double* dout = static_cast<double*>(ctx->fws);
+    OMB_HIP(ctx, launch_gp_lml_small(ctx->stream, kernel, DP, X_dev, d, n, lengthscale_host, variance, noise + 1e-8,
+                                     y_dev, dout));
+    double h[OMB_MAX_DIM + 5];
+    OMB_HIP(ctx, hipMemcpyAsync(h, dout, sizeof(double) * (DP + 5), hipMemcpyDeviceToHost, ctx->stream));
+    OMB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (h[DP + 4] != 0.0)
+      return fail(ctx, OMB_ENOTPD, "K + jitter is not positive definite, even with jitter (column %d)", (int)h[DP + 4]);
+    *lml = -0.5 * h[DP + 2] - h[DP + 1] - 0.5 * n * log(2.0 * M_PI);
+    for (int q = 0; q <= d; ++q) grad[q] = h[q];
+    if (jitter_used) *jitter_used = h[DP + 3];
+    return OMB_OK;
+  }
   GPFactor f;
   if ((rc = gp_factor(ctx, kernel, n, d, X_dev, y_dev, lengthscale_host, variance, noise, &f))) return rc;
-  const int DP = pad_dim(d);
   // Ky⁻¹ = L⁻ᵀ L⁻¹ (lower triangle), then the gradient sums, log det and yᵀα
   OMB_HIP(ctx, launch_gemm_tn_lower(ctx->stream, n, n, 1.0, f.Linv, n, 0.0, f.Kinv, n));
   OMB_HIP(ctx, launch_gp_grad(ctx->stream, kernel, DP, X_dev, d, n, f.ls, variance, f.alpha, f.Kinv, n, f.part,

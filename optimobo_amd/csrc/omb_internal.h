@@ -128,6 +128,12 @@ hipError_t launch_trinv(hipStream_t stream, const double* L, int64_t n, int64_t 
 // GP log-marginal-likelihood pieces: out[0..DP] = ½ Σ W ∂K/∂θ (θ = log σ_f², log ℓ_j; entries past
 // d are 0), out[DP+1] = Σ log L_ii, out[DP+2] = yᵀα.  partials: gp_grad_blocks(n)·(DP+1) doubles.
 int64_t gp_grad_blocks(int64_t n);
+// n ≤ 128 and n_var ≤ 8 (gp_lml_small_fits): the whole evaluation in one workgroup (sweep-operator
+// inverse in LDS, jitter retries in-kernel); out (DP+5 doubles): the launch_gp_grad layout +
+// out[DP+3] = jitter, out[DP+4] = info.
+bool gp_lml_small_fits(int n, int DP);
+hipError_t launch_gp_lml_small(hipStream_t stream, int kind, int DP, const double* X, int d, int n,
+                               const double* ls_host, double variance, double base, const double* y, double* out);
 // dense posterior path: μ, σ² of a candidate chunk from K* (n, Nc) and V = L⁻¹K* (n, Nc).
 hipError_t launch_post_colreduce(hipStream_t stream, const double* Kst, const double* V, int64_t n, int64_t Nc,
                                  const double* alpha, double variance, double* mu, double* var);

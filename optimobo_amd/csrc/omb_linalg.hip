@@ -459,6 +459,249 @@ __global__ __launch_bounds__(256) void gp_reduce_kernel(const double* __restrict
   }
 }
 
+// ----------------------------------------------------------------------------- GP fit, n ≤ 128: one workgroup
+// The whole log-marginal-likelihood + gradient evaluation in one launch for the training-set sizes
+// of a BO loop (n_init .. budget, the README run has n ≤ 120), where the blocked path above is ~15
+// dependent launches and two host synchronisations.  Ky (n×n, full, row pitch n+1) lives in LDS:
+//   * Ky⁻¹ by the sweep operator (Goodnight) on the lower triangle (each thread owns fixed packed
+//     entries): sweeping pivot k applies the Schur-complement update
+//     A_ij −= A_ik A_kj / d (i, j ≠ k), scales row and column k by 1/d and sets A_kk = −1/d; after all
+//     n pivots A = −Ky⁻¹.  The unswept block evolves exactly as right-looking LDLᵀ, so the pivots d_k
+//     are the Cholesky pivots L_kk² (log|Ky| = Σ log d_k, positive-definiteness test !(d_k > 0) as in
+//     chol_panel_kernel, GPy jitchol's jitter retries in-kernel).  One barrier per pivot: the column
+//     of pivot k+1 is double-buffered in LDS by the threads that update it during sweep k.
+//   * α = Ky⁻¹y, then ½ Σ_ik W_ik ∂K_ik/∂θ with W = ααᵀ − Ky⁻¹ over the full matrix (the same sums as
+//     gp_grad_kernel), all reductions in a fixed order (deterministic).
+// out[0..DP] gradient, out[DP+1] = Σ log L_ii, out[DP+2] = yᵀα, out[DP+3] = jitter, out[DP+4] = info
+// (0, or the 1-based column of the failed pivot after the last retry).
+constexpr int kSmallFitN = 128;
+constexpr int kSmallFitLD = kSmallFitN + 1;
+constexpr int kSmallFitThreads = 1024;
+constexpr int kSmallFitXs = 1024;   // LDS doubles for X/ℓ: n·DP ≤ 1024 (d ≤ 8 at n = 128)
+
+struct FitLs {
+  double v[OMB_MAX_DIM];
+};
+
+// K and (dK/dr)/r of scaled rows a (LDS, wave-uniform row) and b (registers): gp_grad_kernel's arithmetic
+template <int DP, int KIND>
+__device__ __forceinline__ void fit_pair(const double* __restrict__ a, const double (&b)[DP], bool diag,
+                                         double variance, double& K, double& dkr) {
+  double aa = 0.0, bb = 0.0, dot = 0.0;
+#pragma unroll
+  for (int j = 0; j < DP; ++j) {
+    aa += a[j] * a[j];
+    bb += b[j] * b[j];
+    dot = fma(a[j], b[j], dot);
+  }
+  double r2 = diag ? 0.0 : fma(-2.0, dot, aa + bb);
+  r2 = r2 > 0.0 ? r2 : 0.0;
+  const double r = sqrt_nonneg(r2);
+  if constexpr (KIND == OMB_KERNEL_MATERN52) {
+    const double e = exp_nonpos(-(kSqrt5 * r));
+    K = (variance * ((1.0 + kSqrt5 * r) + kFiveThirds * (r * r))) * e;
+    dkr = -kFiveThirds * variance * (1.0 + kSqrt5 * r) * e;
+  } else {
+    const double e = exp_nonpos(-0.5 * (r * r));
+    K = variance * e;
+    dkr = -variance * e;
+  }
+}
+
+// Thread map: wave w owns rows i ≡ w (mod 16), lane l owns columns l and l + 64.
+template <int DP, int KIND>
+__global__ __launch_bounds__(kSmallFitThreads) void gp_lml_small_kernel(const double* __restrict__ X, int d, int n,
+                                                                        FitLs ls, double variance, double base,
+                                                                        const double* __restrict__ y,
+                                                                        double* __restrict__ out) {
+  constexpr int NW = kSmallFitThreads / 64, LD = kSmallFitLD, RPW = kSmallFitN / NW;
+  __shared__ double A[kSmallFitN * LD];
+  __shared__ double xs[kSmallFitXs];
+  __shared__ double col[2][kSmallFitN];
+  __shared__ double piv[kSmallFitN], alpha[kSmallFitN];
+  __shared__ double red[NW][DP + 3];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  for (int e = tid; e < n * DP; e += kSmallFitThreads) {
+    const int i = e / DP, j = e - i * DP;
+    xs[e] = (j < d) ? X[i * d + j] / ls.v[j] : 0.0;
+  }
+  __syncthreads();
+  const int j0 = lane, j1 = lane + 64;
+  const bool h0 = j0 < n, h1 = j1 < n;
+  // this lane's two columns' scaled coordinates (LDS; loaded where used so they are not live across the sweep)
+  auto load_cols = [&](double (&b0)[DP], double (&b1)[DP]) {
+#pragma unroll
+    for (int q = 0; q < DP; ++q) {
+      b0[q] = h0 ? xs[j0 * DP + q] : 0.0;
+      b1[q] = h1 ? xs[j1 * DP + q] : 0.0;
+    }
+  };
+  // the sweep updates the lower triangle only: thread t owns packed entries e = t + 1024·q
+  constexpr int kPairs = (kSmallFitN * (kSmallFitN + 1) / 2 + kSmallFitThreads - 1) / kSmallFitThreads;
+  int pij[kPairs];   // i << 8 | j, or −1
+#pragma unroll
+  for (int q = 0; q < kPairs; ++q) {
+    const int e = tid + kSmallFitThreads * q;
+    int i = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+    while (i * (i + 1) / 2 > e) --i;
+    while ((i + 1) * (i + 2) / 2 <= e) ++i;
+    pij[q] = (i < n) ? (i << 8 | (e - i * (i + 1) / 2)) : -1;
+  }
+  const double mean_diag = variance + base;
+  int bad = 0;
+  double jit = 0.0;
+  for (int t = -1; t < 5; ++t) {
+    jit = (t < 0) ? 0.0 : mean_diag * 1e-6 * pow(10.0, (double)t);
+    double b0[DP], b1[DP];
+    load_cols(b0, b1);
+#pragma unroll 2
+    for (int m = 0; m < RPW; ++m) {
+      const int i = wave + NW * m;
+      if (i >= n) break;
+      double K, dkr;
+      if (h0) {
+        fit_pair<DP, KIND>(xs + i * DP, b0, i == j0, variance, K, dkr);
+        A[i * LD + j0] = (i == j0) ? K + (base + jit) : K;
+      }
+      if (h1) {
+        fit_pair<DP, KIND>(xs + i * DP, b1, i == j1, variance, K, dkr);
+        A[i * LD + j1] = (i == j1) ? K + (base + jit) : K;
+      }
+    }
+    __syncthreads();
+    if (tid < n) col[0][tid] = A[tid * LD];
+    __syncthreads();
+    bad = 0;
+    for (int k = 0; k < n; ++k) {
+      const double* c = col[k & 1];
+      double* cn = col[(k + 1) & 1];
+      const double dk = c[k];
+      if (!(dk > 0.0)) {   // uniform: every thread read the same pivot
+        bad = k + 1;
+        break;
+      }
+      // 1/d by v_rcp_f64 and two Newton steps (the per-pivot dependent chain is the critical path)
+      double ip = __builtin_amdgcn_rcp(dk);
+      ip = fma(ip, fma(-dk, ip, 1.0), ip);
+      ip = fma(ip, fma(-dk, ip, 1.0), ip);
+      if (tid == 0) piv[k] = dk;
+#pragma unroll
+      for (int q = 0; q < kPairs; ++q) {
+        if (pij[q] < 0) continue;
+        const int i = pij[q] >> 8, j = pij[q] & 255;
+        const double ci = c[i] * ip, cj = c[j];
+        double v = fma(-ci, cj, A[i * LD + j]);
+        if (j == k) v = ci;
+        if (i == k) v = (j == k) ? -ip : cj * ip;
+        A[i * LD + j] = v;
+        if (j == k + 1) cn[i] = v;
+        if (i == k + 1) cn[j] = v;
+      }
+      __syncthreads();
+    }
+    if (!bad) break;
+    __syncthreads();
+  }
+  if (bad) {
+    if (tid == 0) {
+      for (int q = 0; q < DP + 3; ++q) out[q] = 0.0;
+      out[DP + 3] = jit;
+      out[DP + 4] = (double)bad;
+    }
+    return;
+  }
+  // α = Ky⁻¹ y = −A y: one wave per row, lanes over columns, fixed-order wave reduction
+  const double y0 = h0 ? y[j0] : 0.0, y1 = h1 ? y[j1] : 0.0;
+  for (int m = 0; m < RPW; ++m) {
+    const int i = wave + NW * m;
+    if (i >= n) break;
+    double s = h0 ? A[max(i, j0) * LD + min(i, j0)] * y0 : 0.0;
+    if (h1) s = fma(A[max(i, j1) * LD + min(i, j1)], y1, s);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    if (lane == 0) alpha[i] = -s;
+  }
+  __syncthreads();
+  double acc[DP + 3];
+#pragma unroll
+  for (int q = 0; q < DP + 3; ++q) acc[q] = 0.0;
+  const double al0 = h0 ? alpha[j0] : 0.0, al1 = h1 ? alpha[j1] : 0.0;
+  double b0[DP], b1[DP];
+  load_cols(b0, b1);
+  for (int m = 0; m < RPW; ++m) {
+    const int i = wave + NW * m;
+    if (i >= n) break;
+    const double* a = xs + i * DP;
+    const double ai = alpha[i];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h == 0 ? !h0 : !h1) continue;
+      const int k = h == 0 ? j0 : j1;
+      double K, dkr;
+      fit_pair<DP, KIND>(a, h == 0 ? b0 : b1, i == k, variance, K, dkr);
+      const double W = 0.5 * (ai * (h == 0 ? al0 : al1) + A[max(i, k) * LD + min(i, k)]);   // ½ (ααᵀ − Ky⁻¹)
+      acc[0] = fma(W, K, acc[0]);
+      const double wd = W * (-dkr);
+#pragma unroll
+      for (int q = 0; q < DP; ++q) {
+        const double dq = a[q] - (h == 0 ? b0[q] : b1[q]);
+        acc[1 + q] = fma(wd, dq * dq, acc[1 + q]);
+      }
+    }
+  }
+  if (tid < n) {
+    acc[DP + 1] = 0.5 * log(piv[tid]);
+    acc[DP + 2] = y[tid] * alpha[tid];
+  }
+#pragma unroll
+  for (int q = 0; q < DP + 3; ++q) {
+    double v = acc[q];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if (lane == 0) red[wave][q] = v;
+  }
+  __syncthreads();
+  if (tid < DP + 3) {
+    double v = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v += red[w][tid];
+    out[tid] = v;
+  }
+  if (tid == 0) {
+    out[DP + 3] = jit;
+    out[DP + 4] = 0.0;
+  }
+}
+
+// DP ≤ 8: the two candidate columns' scaled coordinates stay in registers (DP = 16 spills at 1024 threads).
+// n ≤ 96: the sweep is one CU's work, n steps of n²/2 entries with a barrier each; measured per evaluation
+// (tools/bench_gpfit.py, profiles/r01_v19_gpfit.jsonl) 0.08 / 0.11 / 0.19 / 0.33 ms at n = 32 / 64 / 96 / 128
+// against 0.24 ms for the blocked multi-launch path at n = 128.
+bool gp_lml_small_fits(int n, int DP) { return n >= 1 && n <= 96 && DP <= 8 && n * DP <= kSmallFitXs; }
+
+hipError_t launch_gp_lml_small(hipStream_t stream, int kind, int DP, const double* X, int d, int n,
+                               const double* ls_host, double variance, double base, const double* y, double* out) {
+  if (!gp_lml_small_fits(n, DP) || d < 1 || d > DP || DP > OMB_MAX_DIM) return hipErrorInvalidValue;
+  FitLs ls{};
+  for (int j = 0; j < OMB_MAX_DIM; ++j) ls.v[j] = (j < d) ? ls_host[j] : 1.0;
+#define OMB_GS(DPV)                                                                                              \
+  case DPV:                                                                                                      \
+    if (kind == OMB_KERNEL_RBF)                                                                                  \
+      hipLaunchKernelGGL((gp_lml_small_kernel<DPV, OMB_KERNEL_RBF>), dim3(1), dim3(kSmallFitThreads), 0, stream, \
+                         X, d, n, ls, variance, base, y, out);                                                   \
+    else                                                                                                         \
+      hipLaunchKernelGGL((gp_lml_small_kernel<DPV, OMB_KERNEL_MATERN52>), dim3(1), dim3(kSmallFitThreads), 0,    \
+                         stream, X, d, n, ls, variance, base, y, out);                                           \
+    break;
+  switch (DP) {
+    OMB_GS(2) OMB_GS(4) OMB_GS(6) OMB_GS(8)
+    default: return hipErrorInvalidValue;
+  }
+#undef OMB_GS
+  return hipGetLastError();
+}
+
 // ----------------------------------------------------------------------------- selection
 // np.argmin order: the first NaN wins, else the smallest value, lowest index among ties.
 __device__ __forceinline__ bool sel_better(double v, int64_t i, double bv, int64_t bi) {

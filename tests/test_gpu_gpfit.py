@@ -41,7 +41,8 @@ def sklearn_lml_grad(X, y, ls, var, nu=2.5):
     return lml, g
 
 
-@pytest.mark.parametrize("n,d", [(1, 1), (20, 2), (100, 6), (300, 6), (257, 30), (700, 4)])
+@pytest.mark.parametrize("n,d", [(1, 1), (20, 2), (96, 8), (97, 2), (100, 6), (64, 9), (129, 3), (300, 6),
+                                 (257, 30), (700, 4)])
 def test_lml_grad_vs_sklearn(ctx, n, d):
     X, y, ls, var = data(n, d, n + d)
     lml, g, jit = ctx.gp_lml_grad(X, y, ls, var)
@@ -108,3 +109,31 @@ def test_gp_fit_errors(ctx):
     rc = ctx.lib.omb_gp_fit_state(ctx._h, 0, 0, _lib.MAX_TRAIN_DENSE + 1, 2, ctypes.c_void_p(8), ctypes.c_void_p(8),
                                   _lib.darr([1, 1]), 1.0, 0.0, None)      # rejected before any access
     assert rc == _lib.OMB_EUNSUP
+
+
+@pytest.mark.parametrize("n", [40, 96, 97])
+def test_lml_grad_small_and_blocked_paths_agree_with_jitter(ctx, n):
+    """Exact duplicate inputs with σ_f² = 1e10 (the 1e-8 jitter is below half an ulp of the diagonal)
+    make K + 1e-8·I singular in fp64: both the one-workgroup path (n ≤ 128) and the blocked path must
+    take GPy jitchol's jitter retries, and match the host evaluation at the jitter they report."""
+    rng = np.random.default_rng(n)
+    base = rng.uniform(0, 1, (6, 2))
+    X = base[np.arange(n) % 6]
+    y = np.sin(3 * X).sum(1)
+    ls, var = np.array([0.5, 0.8]), 1e10
+    lml, g, jit = ctx.gp_lml_grad(X, y, ls, var)
+    assert jit > 0.0
+    # host numpy at the same diagonal shift
+    K = ogp.matern52_K(X, X, ls, var) + (1e-8 + jit) * np.eye(n)
+    L = np.linalg.cholesky(K)
+    a = np.linalg.solve(K, y)
+    lml_h = -0.5 * y @ a - np.log(np.diag(L)).sum() - 0.5 * n * np.log(2 * np.pi)
+    assert lml == pytest.approx(lml_h, rel=1e-6, abs=1e-4)
+    assert np.all(np.isfinite(g))
+
+
+def test_lml_grad_small_path_deterministic(ctx):
+    X, y, ls, var = data(100, 4, 3)
+    r1 = ctx.gp_lml_grad(X, y, ls, var)
+    r2 = ctx.gp_lml_grad(X, y, ls, var)
+    assert r1[0] == r2[0] and np.array_equal(r1[1], r2[1])

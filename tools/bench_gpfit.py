@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     import torch
     from optimobo_amd.gp import GPRegression, Matern52
-    for n in (128, 512, 1024):
+    for n in (32, 64, 96, 128, 512, 1024):
         rng = np.random.default_rng(n)
         X = rng.uniform(0, 1, (n, 6))
         y = (np.sin(3 * X).sum(1) + 0.3 * X[:, 0] ** 2)[:, None]

@@ -507,6 +507,10 @@ def main():
             "stage_ms": stage_ms,
             "best": {"value": float(best[0]), "index": int(best[1])},
         }
+        if acq_kind == "ehvi2d" and args.mode == "reference" and s01 < 0:
+            out["best"]["note"] = ("reference-mode EHVI passes sigma_B = var_0*s01 (util_functions.py:163-167); this "
+                                   f"cache has s01 = {s01:.4g} < 0, so the acquisition is <= 0 everywhere and the "
+                                   "arg-max is the lowest index among its maxima (DESIGN.md section 2, quirk 2)")
         print(json.dumps(out))
     if world_size > 1:
         dist.barrier()

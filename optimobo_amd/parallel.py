@@ -26,17 +26,20 @@ def shard_range(n_total, world_size, rank):
 
 
 def reduce_pairs(pairs):
-    """pairs (W, 2) float64 {value, index}: best value, lowest index; invalid index < 0."""
+    """pairs (W, 2) float64 {value, index}: best value, lowest index; invalid index < 0.
+
+    Pure device arithmetic (no host synchronisation), so a multi-rank step loop never waits on the host.
+    """
     vals = pairs[:, 0]
     idx = pairs[:, 1]
     valid = idx >= 0
-    if not bool(valid.any()):
-        return pairs.new_tensor([float("-inf"), -1.0])
     v = torch.where(valid, vals, torch.full_like(vals, float("-inf")))
     best = v.max()
     cand = valid & (v == best)
-    big = torch.full_like(idx, float("inf"))
-    i = torch.where(cand, idx, big).min()
+    i = torch.where(cand, idx, torch.full_like(idx, float("inf"))).min()
+    none = ~valid.any()
+    best = torch.where(none, torch.full_like(best, float("-inf")), best)
+    i = torch.where(none, torch.full_like(i, -1.0), i)
     return torch.stack([best, i])
 
 

@@ -468,8 +468,8 @@ __global__ __launch_bounds__(256) void gp_reduce_kernel(const double* __restrict
 //     A_ij −= A_ik A_kj / d (i, j ≠ k), scales row and column k by 1/d and sets A_kk = −1/d; after all
 //     n pivots A = −Ky⁻¹.  The unswept block evolves exactly as right-looking LDLᵀ, so the pivots d_k
 //     are the Cholesky pivots L_kk² (log|Ky| = Σ log d_k, positive-definiteness test !(d_k > 0) as in
-//     chol_panel_kernel, GPy jitchol's jitter retries in-kernel).  One barrier per pivot: the column
-//     of pivot k+1 is double-buffered in LDS by the threads that update it during sweep k.
+//     chol_panel_kernel, GPy jitchol's jitter retries in-kernel).  Pivots go two per barrier; the
+//     columns of the next pair are double-buffered in LDS by the threads that update them.
 //   * α = Ky⁻¹y, then ½ Σ_ik W_ik ∂K_ik/∂θ with W = ααᵀ − Ky⁻¹ over the full matrix (the same sums as
 //     gp_grad_kernel), all reductions in a fixed order (deterministic).
 // out[0..DP] gradient, out[DP+1] = Σ log L_ii, out[DP+2] = yᵀα, out[DP+3] = jitter, out[DP+4] = info
@@ -477,6 +477,7 @@ __global__ __launch_bounds__(256) void gp_reduce_kernel(const double* __restrict
 constexpr int kSmallFitN = 128;
 constexpr int kSmallFitLD = kSmallFitN + 1;
 constexpr int kSmallFitThreads = 1024;
+constexpr int kSmallFitMax = 96;    // above this the blocked multi-launch path is faster (see gp_lml_small_fits)
 constexpr int kSmallFitXs = 1024;   // LDS doubles for X/ℓ: n·DP ≤ 1024 (d ≤ 8 at n = 128)
 
 struct FitLs {
@@ -517,7 +518,7 @@ __global__ __launch_bounds__(kSmallFitThreads) void gp_lml_small_kernel(const do
   constexpr int NW = kSmallFitThreads / 64, LD = kSmallFitLD, RPW = kSmallFitN / NW;
   __shared__ double A[kSmallFitN * LD];
   __shared__ double xs[kSmallFitXs];
-  __shared__ double col[2][kSmallFitN];
+  __shared__ double col[2][2][kSmallFitN];   // [buffer][pivot column k, k+1][row]
   __shared__ double piv[kSmallFitN], alpha[kSmallFitN];
   __shared__ double red[NW][DP + 3];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -570,33 +571,86 @@ __global__ __launch_bounds__(kSmallFitThreads) void gp_lml_small_kernel(const do
       }
     }
     __syncthreads();
-    if (tid < n) col[0][tid] = A[tid * LD];
+    if (tid < n) {
+      col[0][0][tid] = A[tid * LD];                                    // column 0
+      if (n > 1) col[0][1][tid] = A[max(tid, 1) * LD + min(tid, 1)];   // column 1
+    }
     __syncthreads();
     bad = 0;
-    for (int k = 0; k < n; ++k) {
-      const double* c = col[k & 1];
-      double* cn = col[(k + 1) & 1];
-      const double dk = c[k];
-      if (!(dk > 0.0)) {   // uniform: every thread read the same pivot
+    // two pivots per barrier: sweeping k then k+1, written as the two sequential sweeps' arithmetic
+    // (t = c1/a, u = c2 − b·t = column k+1 after sweep k, d2 = c − b²/a) for their stability
+    int k = 0;
+    for (; k + 1 < n; k += 2) {
+      const double* C1 = col[(k >> 1) & 1][0];
+      const double* C2 = col[(k >> 1) & 1][1];
+      double* N1 = col[((k >> 1) + 1) & 1][0];
+      double* N2 = col[((k >> 1) + 1) & 1][1];
+      const double a = C1[k], b = C1[k + 1], c = C2[k + 1];
+      if (!(a > 0.0)) {   // uniform: every thread read the same pivots
         bad = k + 1;
         break;
       }
-      // 1/d by v_rcp_f64 and two Newton steps (the per-pivot dependent chain is the critical path)
-      double ip = __builtin_amdgcn_rcp(dk);
-      ip = fma(ip, fma(-dk, ip, 1.0), ip);
-      ip = fma(ip, fma(-dk, ip, 1.0), ip);
-      if (tid == 0) piv[k] = dk;
+      double ia = __builtin_amdgcn_rcp(a);
+      ia = fma(ia, fma(-a, ia, 1.0), ia);
+      ia = fma(ia, fma(-a, ia, 1.0), ia);
+      const double ba = b * ia;
+      const double d2 = fma(-b, ba, c);
+      if (!(d2 > 0.0)) {
+        bad = k + 2;
+        break;
+      }
+      double id2 = __builtin_amdgcn_rcp(d2);
+      id2 = fma(id2, fma(-d2, id2, 1.0), id2);
+      id2 = fma(id2, fma(-d2, id2, 1.0), id2);
+      const double gk = ba * id2;
+      if (tid == 0) {
+        piv[k] = a;
+        piv[k + 1] = d2;
+      }
 #pragma unroll
       for (int q = 0; q < kPairs; ++q) {
         if (pij[q] < 0) continue;
         const int i = pij[q] >> 8, j = pij[q] & 255;
-        const double ci = c[i] * ip, cj = c[j];
-        double v = fma(-ci, cj, A[i * LD + j]);
-        if (j == k) v = ci;
-        if (i == k) v = (j == k) ? -ip : cj * ip;
+        const double ti = C1[i] * ia, tj = C1[j] * ia;
+        const double ui = fma(-b, ti, C2[i]), uj = fma(-b, tj, C2[j]);
+        const double vi = ui * id2;
+        const bool iK = (i == k) || (i == k + 1), jK = (j == k) || (j == k + 1);
+        double v = fma(-vi, uj, fma(-ti, C1[j], A[i * LD + j]));
+        if (!iK && j == k) v = fma(-ui, gk, ti);
+        if (!iK && j == k + 1) v = vi;
+        if (i == k && !jK) v = fma(-uj, gk, tj);
+        if (i == k + 1 && !jK) v = uj * id2;
+        if (i == k && j == k) v = fma(-ba, gk, -ia);
+        if (i == k + 1 && j == k) v = gk;
+        if (i == k + 1 && j == k + 1) v = -id2;
         A[i * LD + j] = v;
-        if (j == k + 1) cn[i] = v;
-        if (i == k + 1) cn[j] = v;
+        if (j == k + 2) N1[i] = v;
+        if (i == k + 2) N1[j] = v;
+        if (j == k + 3) N2[i] = v;
+        if (i == k + 3) N2[j] = v;
+      }
+      __syncthreads();
+    }
+    if (!bad && k < n) {   // odd n: the last pivot alone (its column is in buffer slot 0)
+      const double* C = col[(k >> 1) & 1][0];
+      const double dk = C[k];
+      if (!(dk > 0.0)) {
+        bad = k + 1;
+      } else {
+        double ip = __builtin_amdgcn_rcp(dk);
+        ip = fma(ip, fma(-dk, ip, 1.0), ip);
+        ip = fma(ip, fma(-dk, ip, 1.0), ip);
+        if (tid == 0) piv[k] = dk;
+#pragma unroll
+        for (int q = 0; q < kPairs; ++q) {
+          if (pij[q] < 0) continue;
+          const int i = pij[q] >> 8, j = pij[q] & 255;
+          const double ci = C[i] * ip, cj = C[j];
+          double v = fma(-ci, cj, A[i * LD + j]);
+          if (j == k) v = ci;
+          if (i == k) v = (j == k) ? -ip : cj * ip;
+          A[i * LD + j] = v;
+        }
       }
       __syncthreads();
     }
@@ -675,10 +729,11 @@ __global__ __launch_bounds__(kSmallFitThreads) void gp_lml_small_kernel(const do
 }
 
 // DP ≤ 8: the two candidate columns' scaled coordinates stay in registers (DP = 16 spills at 1024 threads).
-// n ≤ 96: the sweep is one CU's work, n steps of n²/2 entries with a barrier each; measured per evaluation
-// (tools/bench_gpfit.py, profiles/r01_v19_gpfit.jsonl) 0.08 / 0.11 / 0.19 / 0.33 ms at n = 32 / 64 / 96 / 128
-// against 0.24 ms for the blocked multi-launch path at n = 128.
-bool gp_lml_small_fits(int n, int DP) { return n >= 1 && n <= 96 && DP <= 8 && n * DP <= kSmallFitXs; }
+// n ≤ 96: the sweep is one CU's work, n/2 steps of n²/2 entries with a barrier each; measured per evaluation
+// (tools/bench_gpfit.py, profiles/r01_v20_gpfit.jsonl) 0.076 / 0.10 / 0.18 / 0.32 ms at n = 32 / 64 / 96 / 128
+// against 0.25 ms for the blocked multi-launch path at n = 128 (one pivot per barrier: 0.33 ms at n = 128,
+// so the barriers are not what limits it: the sweep touches every entry at every step, n³/2 updates).
+bool gp_lml_small_fits(int n, int DP) { return n >= 1 && n <= kSmallFitMax && DP <= 8 && n * DP <= kSmallFitXs; }
 
 hipError_t launch_gp_lml_small(hipStream_t stream, int kind, int DP, const double* X, int d, int n,
                                const double* ls_host, double variance, double base, const double* y, double* out) {

@@ -98,9 +98,10 @@ def test_posterior_sizes(ctx, n, d, N):
     assert_posterior(mu.cpu().numpy(), var.cpu().numpy(), mu_o, var_o, variances)
 
 
-def test_posterior_rbf_kernel(ctx):
+@pytest.mark.parametrize("n", [96, 200, 400, 900])   # every posterior dispatch shape (RT 1/2/4/8)
+def test_posterior_rbf_kernel(ctx, n):
     rng = np.random.default_rng(5)
-    X = rng.uniform(0, 1, (96, 5))
+    X = rng.uniform(0, 1, (n, 5))
     Y = np.column_stack([X.sum(1), (X ** 2).sum(1)])
     ls = np.full(5, 0.8)
     variances = [1.3, 0.7]

@@ -32,7 +32,7 @@ extern "C" {
 
 #define OMB_ABI_VERSION 1
 #define OMB_MAX_OBJ 8      /* objectives held by one context */
-#define OMB_MAX_DIM 32     /* n_var */
+#define OMB_MAX_DIM 64     /* n_var */
 #define OMB_MAX_TRAIN 1024 /* n_train handled by the fused posterior kernel */
 #define OMB_MAX_TRAIN_DENSE 16384 /* n_train of the GEMM-based posterior path used above OMB_MAX_TRAIN */
 

@@ -17,7 +17,7 @@ ERROR_NAMES = {OMB_EINVAL: "OMB_EINVAL", OMB_EHIP: "OMB_EHIP", OMB_ENOMEM: "OMB_
 KERNEL_MATERN52, KERNEL_RBF = 0, 1
 EHVI_REFERENCE, EHVI_TEXTBOOK, EHVI_SIGMA = 0, 1, 2
 EI_PLAIN, EI_PARETO, EI_CONSTRAINED = 0, 1, 2
-MAX_OBJ, MAX_DIM, MAX_TRAIN, MAX_TRAIN_DENSE = 8, 32, 1024, 16384
+MAX_OBJ, MAX_DIM, MAX_TRAIN, MAX_TRAIN_DENSE = 8, 64, 1024, 16384
 
 _p = ctypes.c_void_p
 _d = ctypes.c_double

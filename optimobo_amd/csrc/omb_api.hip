@@ -103,7 +103,7 @@ constexpr int kMaxLdsDoubles = 8192;
 constexpr int kMaxStripes = (kMaxLdsDoubles - 1) / 2;
 
 int pad_dim(int d) {
-  const int opts[] = {2, 4, 6, 8, 16, 32};
+  const int opts[] = {2, 4, 6, 8, 16, 32, 64};
   for (int o : opts)
     if (d <= o) return o;
   return -1;

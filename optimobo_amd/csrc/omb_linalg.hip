@@ -839,7 +839,7 @@ hipError_t launch_cand_cov(hipStream_t stream, const GPDev& g, int d, int DP, co
                          g.ls, g.variance, S, lds);                                                         \
     break;
   switch (DP) {
-    OMB_COV(2) OMB_COV(4) OMB_COV(6) OMB_COV(8) OMB_COV(16) OMB_COV(32)
+    OMB_COV(2) OMB_COV(4) OMB_COV(6) OMB_COV(8) OMB_COV(16) OMB_COV(32) OMB_COV(64)
     default: return hipErrorInvalidValue;
   }
 #undef OMB_COV
@@ -930,7 +930,7 @@ hipError_t launch_gp_grad(hipStream_t stream, int kind, int DP, const double* X,
                          variance, alpha, Kinv, ldk, partials);                                                  \
     break;
   switch (DP) {
-    OMB_GG(2) OMB_GG(4) OMB_GG(6) OMB_GG(8) OMB_GG(16) OMB_GG(32)
+    OMB_GG(2) OMB_GG(4) OMB_GG(6) OMB_GG(8) OMB_GG(16) OMB_GG(32) OMB_GG(64)
     default: return hipErrorInvalidValue;
   }
 #undef OMB_GG

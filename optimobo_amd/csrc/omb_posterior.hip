@@ -634,6 +634,7 @@ static hipError_t launch_posterior_kind(hipStream_t stream, const GPArgs& args, 
     case 8: return launch_posterior_dp<8, KIND>(stream, args, n_obj, max_R, Xc, N, mu, var);
     case 16: return launch_posterior_dp<16, KIND>(stream, args, n_obj, max_R, Xc, N, mu, var);
     case 32: return launch_posterior_dp<32, KIND>(stream, args, n_obj, max_R, Xc, N, mu, var);
+    case 64: return launch_posterior_dp<64, KIND>(stream, args, n_obj, max_R, Xc, N, mu, var);
     default: return hipErrorInvalidValue;
   }
 }
@@ -654,7 +655,7 @@ static hipError_t launch_kblock_kind(hipStream_t stream, const GPArgs& args, int
   switch (args.DP) {
 #define OMB_KB(DPV) \
   case DPV: hipLaunchKernelGGL((kernel_block_mfma_kernel<DPV, KIND>), grid, dim3(256), 0, stream, g, args.d, Xc, N, K, exp_coef()); break;
-    OMB_KB(2) OMB_KB(4) OMB_KB(6) OMB_KB(8) OMB_KB(16) OMB_KB(32)
+    OMB_KB(2) OMB_KB(4) OMB_KB(6) OMB_KB(8) OMB_KB(16) OMB_KB(32) OMB_KB(64)
 #undef OMB_KB
     default: return hipErrorInvalidValue;
   }

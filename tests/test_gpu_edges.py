@@ -43,7 +43,7 @@ def test_error_codes(ctx):
                             ctypes.c_void_p(8), ctypes.c_void_p(8))      # rejected before any access
     assert rc == _lib.OMB_EUNSUP
     with pytest.raises(_lib.OMBError) as e:
-        ctx.set_gp(2, np.zeros((4, 33)), np.ones(33), 1.0, np.zeros(4), np.eye(4))
+        ctx.set_gp(2, np.zeros((4, _lib.MAX_DIM + 1)), np.ones(_lib.MAX_DIM + 1), 1.0, np.zeros(4), np.eye(4))
     assert e.value.code == _lib.OMB_EUNSUP
     with pytest.raises(_lib.OMBError):
         ctx.set_gp(2, np.zeros((4, 2)), [1.0, -1.0], 1.0, np.zeros(4), np.eye(4))   # ℓ ≤ 0

@@ -42,7 +42,7 @@ def sklearn_lml_grad(X, y, ls, var, nu=2.5):
 
 
 @pytest.mark.parametrize("n,d", [(1, 1), (20, 2), (96, 8), (97, 2), (100, 6), (64, 9), (129, 3), (300, 6),
-                                 (257, 30), (700, 4)])
+                                 (257, 30), (700, 4), (150, 50)])
 def test_lml_grad_vs_sklearn(ctx, n, d):
     X, y, ls, var = data(n, d, n + d)
     lml, g, jit = ctx.gp_lml_grad(X, y, ls, var)

@@ -83,7 +83,8 @@ def test_posterior_vs_golden(ctx, golden_dir, name):
                                    (1024, 6, 300), (128, 30, 200), (64, 32, 64),
                                    (1024, 30, 300), (600, 17, 100), (513, 16, 77), (777, 5, 129),
                                    (200, 8, 100), (150, 7, 99), (90, 5, 33), (1000, 8, 65),
-                                   (200, 30, 97), (256, 17, 65), (129, 3, 31)])
+                                   (200, 30, 97), (256, 17, 65), (129, 3, 31),
+                                   (100, 40, 70), (300, 50, 100), (500, 64, 65), (700, 50, 65)])
 def test_posterior_sizes(ctx, n, d, N):
     rng = np.random.default_rng(n * 1000 + d)
     X = rng.uniform(0, 1, (n, d))
@@ -112,7 +113,7 @@ def test_posterior_rbf_kernel(ctx, n):
     assert_posterior(mu.cpu().numpy(), var.cpu().numpy(), mu_o, var_o, variances)
 
 
-@pytest.mark.parametrize("n,d,N", [(20, 2, 100), (512, 6, 4099), (100, 30, 77)])
+@pytest.mark.parametrize("n,d,N", [(20, 2, 100), (512, 6, 4099), (100, 30, 77), (300, 64, 129)])
 def test_kernel_block(ctx, n, d, N):
     rng = np.random.default_rng(n + d)
     X = rng.uniform(0, 1, (n, d))

@@ -41,7 +41,7 @@ def fit(ctx, n, d, seed, kernel="matern52"):
 
 # ----------------------------------------------------------------------------- covariance
 @pytest.mark.parametrize("n,d,N,kernel", [(20, 2, 1, "matern52"), (20, 2, 77, "matern52"), (300, 6, 700, "matern52"),
-                                          (129, 30, 257, "matern52"), (64, 4, 130, "rbf")])
+                                          (129, 30, 257, "matern52"), (64, 4, 130, "rbf"), (150, 60, 200, "matern52")])
 def test_posterior_cov_vs_oracle(ctx, n, d, N, kernel):
     X, y, ls, var, og = fit(ctx, n, d, seed=n + d, kernel=kernel)
     rng = np.random.default_rng(N)

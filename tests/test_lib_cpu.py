@@ -50,3 +50,16 @@ def test_device_context_refuses_without_gpu():
     from optimobo_amd.device import AcqContext
     with pytest.raises(RuntimeError):
         AcqContext(0)
+
+
+def test_host_limits_match_header():
+    """The ctypes layer's limits are the header's (#define OMB_MAX_*)."""
+    import re
+
+    from optimobo_amd import _lib
+    src = open(os.path.join(REPO, "include", "optimobo_hip.h")).read()
+    val = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define OMB_(MAX_\w+)\s+(\d+)", src)}
+    assert val["MAX_OBJ"] == _lib.MAX_OBJ
+    assert val["MAX_DIM"] == _lib.MAX_DIM
+    assert val["MAX_TRAIN"] == _lib.MAX_TRAIN
+    assert val["MAX_TRAIN_DENSE"] == _lib.MAX_TRAIN_DENSE

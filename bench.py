@@ -89,16 +89,24 @@ def candidates(d, start, count):
     return s.random(count)
 
 
-def cpu_baseline(X, Y, ls, variances, pf, r, cache, Xc, seconds):  # noqa: C901
-    """The oracle (numpy fp64, batched, BLAS-threaded) on a bounded sample of the same workload."""
-    from oracle import acquisition as oacq
-    from oracle import gp as ogp
+def blas_threads():
+    """Threads the numpy BLAS actually runs with (threadpoolctl), and the host's logical CPU count."""
     try:
         from threadpoolctl import threadpool_info
-        cores = max([p.get("num_threads", 1) for p in threadpool_info()] or [1])
+        threads = max([p.get("num_threads", 1) for p in threadpool_info()] or [1])
     except Exception:  # pragma: no cover
-        cores = os.cpu_count() or 1
-    gps = [ogp.ExactGP(X, Y[:, o], ls, variances[o]) for o in range(2)]
+        threads = 1
+    return int(threads), int(os.cpu_count() or 1)
+
+
+def cpu_baseline(X, targets, ls, variances, Xc, acq_fn, label, seconds):
+    """The oracle (numpy fp64, batched, BLAS-threaded) on a bounded sample of the same workload:
+    oracle posterior (GPy restatement, dtrtrs) for every surrogate → ``acq_fn(mu, var)`` → arg-max,
+    in chunks of 4096 candidates for about ``seconds`` seconds."""
+    from oracle import acquisition as oacq
+    from oracle import gp as ogp
+    threads, ncpu = blas_threads()
+    gps = [ogp.ExactGP(X, targets[:, o], ls, variances[o]) for o in range(targets.shape[1])]
     chunk = 4096
     done = 0
     t0 = time.perf_counter()
@@ -109,15 +117,14 @@ def cpu_baseline(X, Y, ls, variances, pf, r, cache, Xc, seconds):  # noqa: C901
             m, v = g.predict(xc)
             mus.append(m[:, 0])
             vs.append(v[:, 0])
-        acq = oacq.ehvi2d(np.array(mus), np.array(vs), pf, r, cache, mode="reference")
-        oacq.argmax(acq)
+        oacq.argmax(acq_fn(np.array(mus), np.array(vs)))
         done += len(xc)
         if time.perf_counter() - t0 >= seconds:
             break
     dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "candidates/s", "cores": int(cores), "kind": "port",
+    return {"value": done / dt, "unit": "candidates/s", "cores": threads, "host_cpu_count": ncpu, "kind": "port",
             "sample": f"{done} of the {len(Xc)} candidates (chunks of {chunk}), oracle posterior (dtrtrs) + "
-                      f"reference-mode EHVI-2D + arg-max, {dt:.1f} s"}
+                      f"{label} + arg-max, {dt:.1f} s; cores = numpy BLAS threads used (threadpoolctl)"}
 
 
 def run_solve(args, cfg, world_size, rank):
@@ -183,11 +190,7 @@ def cpu_thompson(X, yagg, ls, var, Xc, B, seconds):
     numpy.random.multivariate_normal (SVD, as GPy's posterior_samples_f) + greedy arg-mins."""
     from oracle import gp as ogp
     from oracle import turbo as oturbo
-    try:
-        from threadpoolctl import threadpool_info
-        cores = max([p.get("num_threads", 1) for p in threadpool_info()] or [1])
-    except Exception:  # pragma: no cover
-        cores = os.cpu_count() or 1
+    cores, ncpu = blas_threads()
     g = ogp.ExactGP(X, yagg, ls, var)
     steps = 0
     t0 = time.perf_counter()
@@ -199,7 +202,8 @@ def cpu_thompson(X, yagg, ls, var, Xc, B, seconds):
         if time.perf_counter() - t0 >= seconds:
             break
     dt = time.perf_counter() - t0
-    return {"value": steps * len(Xc) / dt, "unit": "candidates/s", "cores": int(cores), "kind": "port",
+    return {"value": steps * len(Xc) / dt, "unit": "candidates/s", "cores": int(cores), "host_cpu_count": ncpu,
+            "kind": "port",
             "sample": f"{steps} Thompson step(s) of {len(Xc)} candidates x {B} draws (oracle full-cov posterior "
                       f"+ numpy multivariate_normal (SVD) + greedy arg-min), {dt:.1f} s"}
 
@@ -307,6 +311,10 @@ def main():
     ap.add_argument("--no-kblock", action="store_true")
     ap.add_argument("--chain", default="fused", choices=["fused", "separate", "sobol"])
     ap.add_argument("--stage-timing", action="store_true", help="events around every stage (adds ~5 us/stage)")
+    ap.add_argument("--cache-seed", type=int, default=1,
+                    help="Sobol seed of the MC sample cache (optimisers.py:121-141, unseeded in the reference). "
+                         "1: s01 = +0.070, reference-mode EHVI positive where it improves (default); "
+                         "0: s01 = -0.028, reference-mode EHVI <= 0 everywhere (degenerate arg-max)")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
 
@@ -316,13 +324,23 @@ def main():
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus > 1 and world_size != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world_size}: launch one rank per GPU with "
+                         "python -m torch.distributed.run --nproc-per-node N bench.py --gpus N")
     # OMB_DIST_BACKEND=gloo rehearses the multi-rank path on a box with fewer GPUs than ranks
     # (ranks then share GPUs round-robin); the driver's multi-GPU runs use nccl (= RCCL).
     backend = os.environ.get("OMB_DIST_BACKEND", "nccl")
     gpu = local_rank % max(1, torch.cuda.device_count()) if backend == "gloo" else local_rank
+    dist_info = {"backend": None, "world_size": 1}
     if world_size > 1:
         torch.cuda.set_device(gpu)
         dist.init_process_group(backend=backend, init_method="env://")
+        dist_info = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                     "rccl_version": ".".join(map(str, torch.cuda.nccl.version())) if dist.get_backend() == "nccl"
+                     else None}
+        if "OMB_DIST_BACKEND" not in os.environ:
+            assert dist_info["backend"] == "nccl", f"multi-GPU bench must run over RCCL, got {dist_info['backend']}"
+        assert dist_info["world_size"] == world_size
     device = torch.device("cuda", gpu)
     local_rank = gpu
 
@@ -343,7 +361,7 @@ def main():
     k_obj = Y.shape[1]
     pf = pareto.calc_pf(Y)
     r = Y.max(axis=0) + 0.1 * (Y.max(axis=0) - Y.min(axis=0))
-    cache = pareto.cached_samples(k_obj, 5, seed=0)
+    cache = pareto.cached_samples(k_obj, 5, seed=args.cache_seed)
 
     ctx = AcqContext(local_rank)
     if acq_kind == "ei_tch":
@@ -489,8 +507,26 @@ def main():
                 "ms_per_launch": post_ms}
 
     cpu = None
-    if rank == 0 and world_size == 1 and not args.no_cpu_baseline and acq_kind == "ehvi2d":
-        cpu = cpu_baseline(X, Y, ls, variances, pf, r, cache, Xc_host, args.cpu_seconds)
+    if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
+        from oracle import acquisition as oacq
+        if acq_kind == "ehvi2d":
+            cpu = cpu_baseline(X, Y, ls, variances, Xc_host,
+                               lambda m, v: oacq.ehvi2d(m, v, pf, r, cache, mode=args.mode),
+                               f"{args.mode}-mode EHVI-2D", args.cpu_seconds)
+        elif acq_kind == "ehvi3d" and args.mode == "reference":
+            def mc3(m, v):
+                val, raised = oacq.ehvi3d_reference(m, v, hv_pf, r, cache)
+                return np.where(raised, np.nan, val)
+            cpu = cpu_baseline(X, Y, ls, variances, Xc_host, mc3, "reference Monte-Carlo EHVI-3D", args.cpu_seconds)
+        elif acq_kind == "ehvi3d":
+            from oracle import pareto as opar
+            lo_b, hi_b = opar.nondominated_boxes(pf, r)
+            cpu = cpu_baseline(X, Y, ls, variances, Xc_host, lambda m, v: oacq.ehvi_exact_boxes(m, v, lo_b, hi_b),
+                               "exact EHVI-3D over the box decomposition", args.cpu_seconds)
+        else:
+            cpu = cpu_baseline(X, yagg[:, None], ls, [states[0].variance], Xc_host,
+                               lambda m, v: oacq.ei(m[0], v[0], best_y, 1e-6), "ParEGO EI (var + 1e-6)",
+                               args.cpu_seconds)
 
     if rank == 0:
         total = N * world_size * args.steps
@@ -521,8 +557,14 @@ def main():
             "chain": args.chain,
             "stage_ms": stage_ms,
             "state_install_ms": state_ms,
-            "best": {"value": float(best[0]), "index": int(best[1])},
+            "best": {"value": float(best[0]), "index": int(best[1]),
+                     "x": candidates(d, int(best[1]), 1)[0].tolist() if best[1] >= 0 else None},
+            "distributed": dict(dist_info, candidates_per_rank=N, rank_shard=f"Sobol indices [r*{N}, (r+1)*{N})",
+                                collective="all_gather of one 16-B {value, index} pair per step"),
+            "cache": {"seed": args.cache_seed, "samples": int(cache.shape[0])},
         }
+        if acq_kind == "ehvi2d":
+            out["cache"].update(s00=s00, s01=s01)
         if acq_kind == "ehvi2d" and args.mode == "reference" and s01 < 0:
             out["best"]["note"] = ("reference-mode EHVI passes sigma_B = var_0*s01 (util_functions.py:163-167); this "
                                    f"cache has s01 = {s01:.4g} < 0, so the acquisition is <= 0 everywhere and the "

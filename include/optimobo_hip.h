@@ -80,6 +80,16 @@ int omb_use_own_stream(omb_ctx* ctx);
 int omb_synchronize(omb_ctx* ctx);
 const char* omb_last_error(const omb_ctx* ctx);
 
+/* Device fault word.  The fused posterior kernel's waves hand K* chunks to each other through
+ * LDS counters; every wait is bounded (by default 2^22 polls).  A wait that runs out — which
+ * only a broken invariant can cause — marks the context's fault word (pinned host memory) and
+ * lets the kernel finish.  The next call on the context that enters the library (and
+ * omb_synchronize after its sync) then returns OMB_EHIP once, describing the fault: the moments
+ * and acquisition values computed since the previous report are invalid.
+ * omb_debug_set(ctx, OMB_DEBUG_SPIN_LIMIT, polls) changes the bound (tests force the path with 0). */
+enum { OMB_DEBUG_SPIN_LIMIT = 1 };
+int omb_debug_set(omb_ctx* ctx, int what, int64_t value);
+
 /* Fitted-GP state of objective `obj` — replaces the fitted GPy model
  * (GPRegression + Matern52(ARD) with noise fixed to 0, optimisers.py:223-231).
  *   X_dev     (n, d)  training inputs, unscaled

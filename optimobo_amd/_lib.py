@@ -17,6 +17,7 @@ ERROR_NAMES = {OMB_EINVAL: "OMB_EINVAL", OMB_EHIP: "OMB_EHIP", OMB_ENOMEM: "OMB_
 KERNEL_MATERN52, KERNEL_RBF = 0, 1
 EHVI_REFERENCE, EHVI_TEXTBOOK, EHVI_SIGMA = 0, 1, 2
 EI_PLAIN, EI_PARETO, EI_CONSTRAINED = 0, 1, 2
+DEBUG_SPIN_LIMIT = 1
 MAX_OBJ, MAX_DIM, MAX_TRAIN, MAX_TRAIN_DENSE = 8, 64, 1024, 16384
 
 _p = ctypes.c_void_p
@@ -34,6 +35,7 @@ SIGNATURES = {
     "omb_use_own_stream": (_i, [_p]),
     "omb_synchronize": (_i, [_p]),
     "omb_last_error": (ctypes.c_char_p, [_p]),
+    "omb_debug_set": (_i, [_p, _i, _i64]),
     "omb_set_gp": (_i, [_p, _i, _i, _i, _i, _p, _dp, _d, _p, _p]),
     "omb_kernel_block": (_i, [_p, _i, _p, _i64, _p]),
     "omb_posterior": (_i, [_p, _i, _p, _i64, _p, _p]),

@@ -12,6 +12,7 @@ from .. import pareto
 from .. import util_functions
 from ..acquisition import engine_for
 from ..gp import GPRegression, Matern52
+from ..parallel import agree_host_rng
 from ..result import Res
 
 
@@ -33,7 +34,8 @@ class BODriver:
         self.mode = mode
         self.n_candidates = int(n_candidates)
         self.refine_rounds = int(refine_rounds)
-        self.seed = seed
+        # several ranks (torch.distributed initialised): one seed and one numpy state for all of them
+        self.seed = agree_host_rng(seed)
         self.device = device
         self._iteration = 0
 

@@ -72,6 +72,10 @@ struct omb_ctx {
   // dense posterior path (n_train > OMB_MAX_TRAIN): K* | V chunk workspace
   void* dws = nullptr;
   size_t dws_cap = 0;
+  // device fault word (pinned, mapped host memory): kernels mark it, enter() reports it
+  int* fault_host = nullptr;
+  int* fault_dev = nullptr;
+  int spin_limit = kDefaultSpinLimit;
 };
 
 namespace {
@@ -109,17 +113,33 @@ int pad_dim(int d) {
   return -1;
 }
 
+// Reports (once) a fault a kernel marked since the last report.
+int check_fault(omb_ctx* ctx) {
+  const int f = __atomic_exchange_n(ctx->fault_host, 0, __ATOMIC_ACQ_REL);
+  if (f & kFaultSpin)
+    return fail(ctx, OMB_EHIP, "posterior kernel: an LDS counter-ring wait exceeded %d polls; the posterior "
+                "moments (and acquisition values) computed since the previous call are invalid", ctx->spin_limit);
+  return OMB_OK;
+}
+
 int enter(omb_ctx* ctx) {
   if (!ctx) return OMB_EINVAL;
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
-  return OMB_OK;
+  return check_fault(ctx);
+}
+
+// GPArgs of the posterior launches: zeroed, with the context's fault word and spin bound.
+void init_args(omb_ctx* ctx, GPArgs* args) {
+  memset(args, 0, sizeof(*args));
+  args->fault = ctx->fault_dev;
+  args->spin_limit = ctx->spin_limit;
 }
 
 // GP state of objectives 0..n_obj-1, all set, sharing d.
 int gather_gp(omb_ctx* ctx, int n_obj, GPArgs* args, int* max_R) {
   if (n_obj < 1 || n_obj > OMB_MAX_OBJ) return fail(ctx, OMB_EINVAL, "n_obj=%d outside [1, %d]", n_obj, OMB_MAX_OBJ);
-  memset(args, 0, sizeof(*args));
+  init_args(ctx, args);
   *max_R = 0;
   for (int o = 0; o < n_obj; ++o) {
     const ObjState& s = ctx->obj[o];
@@ -402,10 +422,13 @@ int omb_create(int device, omb_ctx** out) {
       hipMalloc(&ctx->partials, sizeof(double) * 2 * kArgmaxMaxBlocks) != hipSuccess ||
       hipMalloc(&ctx->result_dev, sizeof(double) * 2) != hipSuccess ||
       hipHostMalloc(&ctx->result_host, sizeof(double) * 2, hipHostMallocDefault) != hipSuccess ||
-      hipMalloc(&ctx->sob, sobol_state_bytes(OMB_MAX_DIM, 32)) != hipSuccess) {
+      hipMalloc(&ctx->sob, sobol_state_bytes(OMB_MAX_DIM, 32)) != hipSuccess ||
+      hipHostMalloc(&ctx->fault_host, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->fault_dev), ctx->fault_host, 0) != hipSuccess) {
     omb_destroy(ctx);
     return OMB_ENOMEM;
   }
+  *ctx->fault_host = 0;
   ctx->stream = ctx->own_stream;
   *out = ctx;
   return OMB_OK;
@@ -428,6 +451,7 @@ int omb_destroy(omb_ctx* ctx) {
   if (ctx->ichol) (void)hipFree(ctx->ichol);
   if (ctx->fws) (void)hipFree(ctx->fws);
   if (ctx->dws) (void)hipFree(ctx->dws);
+  if (ctx->fault_host) (void)hipHostFree(ctx->fault_host);
   for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;
@@ -450,7 +474,17 @@ int omb_synchronize(omb_ctx* ctx) {
   int rc = enter(ctx);
   if (rc) return rc;
   OMB_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  return OMB_OK;
+  return check_fault(ctx);
+}
+
+int omb_debug_set(omb_ctx* ctx, int what, int64_t value) {
+  if (!ctx) return OMB_EINVAL;
+  if (what == OMB_DEBUG_SPIN_LIMIT) {
+    if (value < 0 || value > 0x7fffffff) return fail(ctx, OMB_EINVAL, "spin limit %lld outside [0, 2^31)", (long long)value);
+    ctx->spin_limit = (int)value;
+    return OMB_OK;
+  }
+  return fail(ctx, OMB_EINVAL, "unknown debug setting %d", what);
 }
 
 const char* omb_last_error(const omb_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
@@ -526,7 +560,7 @@ int omb_kernel_block(omb_ctx* ctx, int obj, const double* Xc_dev, int64_t N, dou
   if (N < 0 || (N > 0 && (!Xc_dev || !K_dev))) return fail(ctx, OMB_EINVAL, "bad candidate/output arguments");
   if (N == 0) return OMB_OK;
   GPArgs args;
-  memset(&args, 0, sizeof(args));
+  init_args(ctx, &args);
   args.gp[obj] = ctx->obj[obj].dev;
   args.d = ctx->obj[obj].d;
   args.DP = ctx->obj[obj].DP;
@@ -901,7 +935,7 @@ static int check_cov_n(omb_ctx* ctx, int64_t N) {
 static hipError_t cov_prepare(omb_ctx* ctx, const ObjState& s, const double* Xc, int64_t N, double* Kst, double* V,
                               double* mu, double* var) {
   GPArgs args;
-  memset(&args, 0, sizeof(args));
+  init_args(ctx, &args);
   args.gp[0] = s.dev;
   args.d = s.d;
   args.DP = s.DP;

@@ -35,7 +35,12 @@ struct GPArgs {
   int d;    // true n_var (≤ DP)
   int DP;   // padded dim used by the packed Xs
   ExpCoef ec;      // exp_nonpos coefficients as kernel arguments (set by launch_posterior)
+  int* fault;      // context fault word (pinned host memory): bit 0 = an LDS-counter wait ran out
+  int spin_limit;  // polls per LDS-counter wait before the fault word is marked
 };
+
+constexpr int kFaultSpin = 1;          // fault word bit: posterior counter-ring wait exhausted
+constexpr int kDefaultSpinLimit = 1 << 22;
 
 // ---------------------------------------------------------------------------------------
 // Launchers (host functions; each launches on `stream` and returns hipGetLastError()).

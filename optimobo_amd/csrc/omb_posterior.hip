@@ -199,7 +199,8 @@ __global__ __launch_bounds__(256) void kernel_block_mfma_kernel(GPDev g, int d, 
 // uses libm exp/sqrt, bit 32 selects the 2-buffer / block-barrier pipeline instead of the
 // counter-synchronised 3-buffer ring (tools/ablate: 12.03 → 11.23 ms at n = 512, N = 2^20); bit 128
 // gives waves 4-7 static priority 1, bit 256 drops the σ_f² multiply, bit 512 starts the distance
-// chain at ‖x‖² + ‖x*‖² with −2x* pre-scaled (one fma fewer per element).
+// chain at ‖x‖² + ‖x*‖² with −2x* pre-scaled (one fma fewer per element), bit 65536 forces a spin
+// bound of 0 on the counter-ring waits (the fault-word path).
 // NW = waves per workgroup (8 or 16): waves w, w+4, w+8, w+12 share a SIMD.
 template <int RT, int CT, int DP, int KIND, int NW = 8, int ABL = 0>
 __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args, const double* __restrict__ Xc,
@@ -214,7 +215,6 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
   constexpr bool kCounters = (ABL & 32) == 0;   // counter-synchronised 3-buffer ring (default)
   constexpr int NBUF = kCounters ? 3 : 2;
   constexpr int kMaxChunks = OMB_MAX_TRAIN / kChunkRows;
-  constexpr int kSpinLimit = 1 << 22;
   static_assert(NT % BN == 0 && CHUNK % NT == 0, "BN must divide the block");
   static_assert(2 * CHUNK >= NW * BN + NT, "epilogue scratch must fit in the K* buffers");
   // Candidate coordinates (x*/ℓ) live in registers for n_var ≤ 8; wider ones are staged in LDS
@@ -500,7 +500,7 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
     // finished multiplying chunk c.  A wave multiplies chunk c once ready[c] == NW and refills
     // ring slot (c+2)%3 once done[c-1] == NW, so fast waves run up to a chunk ahead of slow
     // ones.  Every wait refers to an earlier stage of every other wave (no cycle); the spins are
-    // bounded anyway (kSpinLimit) so a broken invariant cannot hang the GPU.
+    // bounded anyway (args.spin_limit) so a broken invariant cannot hang the GPU, and reported.
     int* ready = reinterpret_cast<int*>(kbuf + NBUF * CHUNK);
     int* done = ready + kMaxChunks;
     if (tid < 2 * kMaxChunks) ready[tid] = 0;
@@ -509,10 +509,17 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
+    // a wait that exhausts its bound marks the context's fault word (a system-scope vector store to
+    // pinned host memory) so the next library call reports OMB_EHIP instead of returning bad moments
+    const int spin_limit = (ABL & 65536) ? 0 : args.spin_limit;
     auto wait_all = [&](int* ctr) {
       if (lane == 0) {
-        for (int spin = 0; spin < kSpinLimit; ++spin) {
+        for (int spin = 0;; ++spin) {
           if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= NW) break;
+          if (spin >= spin_limit) {
+            if (args.fault) __hip_atomic_store(args.fault, kFaultSpin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+          }
           __builtin_amdgcn_s_sleep(1);
         }
       }

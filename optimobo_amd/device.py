@@ -65,6 +65,11 @@ class AcqContext:
     def synchronize(self):
         self._check(self.lib.omb_synchronize(self._h), "omb_synchronize")
 
+    def debug_set(self, what, value):
+        """omb_debug_set: e.g. ("spin_limit", polls) bounds the posterior's LDS-counter waits."""
+        code = {"spin_limit": _lib.DEBUG_SPIN_LIMIT}[what]
+        self._check(self.lib.omb_debug_set(self._h, code, int(value)), "omb_debug_set")
+
     # ------------------------------------------------------------------ GP state
     def set_gp(self, obj, X, lengthscale, variance, alpha, Linv, kernel="matern52"):
         """Upload one fitted GP (see optimobo_amd.gp.GPState) for objective ``obj``."""
@@ -90,8 +95,17 @@ class AcqContext:
         self.set_gp(obj, state.X, state.lengthscale, state.variance, state.alpha, state.Linv, state.kernel)
 
     # ------------------------------------------------------------------ posterior
+    def _check_width(self, Xc, obj=0):
+        """The C-ABI takes no candidate width: the kernels read Xc (N, d) with the installed GP's d."""
+        info = self.gp_info.get(obj)
+        if Xc.dim() != 2:
+            raise ValueError(f"candidates must be (N, d), got shape {tuple(Xc.shape)}")
+        if info is not None and Xc.shape[1] != info["d"]:
+            raise ValueError(f"candidates have {Xc.shape[1]} columns but objective {obj}'s GP has n_var={info['d']}")
+
     def kernel_block(self, obj, Xc, out=None):
         Xc = _dev_f64(Xc, self.device)
+        self._check_width(Xc, obj)
         n = self.gp_info[obj]["n"]
         N = Xc.shape[0]
         K = out if out is not None else torch.empty((n, N), dtype=torch.float64, device=self.device)
@@ -102,8 +116,7 @@ class AcqContext:
     def posterior(self, Xc, n_obj=None, out=None):
         """μ, σ² (n_obj, N) of objectives 0..n_obj-1 at candidates Xc (N, d)."""
         Xc = _dev_f64(Xc, self.device)
-        if Xc.dim() != 2:
-            raise ValueError("candidates must be (N, d)")
+        self._check_width(Xc)
         n_obj = n_obj if n_obj is not None else len(self.gp_info)
         N = Xc.shape[0]
         if out is None:
@@ -257,6 +270,7 @@ class AcqContext:
 
     def eval(self, Xc, out=None):
         Xc = _dev_f64(Xc, self.device)
+        self._check_width(Xc)
         N = Xc.shape[0]
         out = out if out is not None else torch.empty(N, dtype=torch.float64, device=self.device)
         self._stream()
@@ -265,6 +279,7 @@ class AcqContext:
 
     def eval_argmax(self, Xc, offset=0, out=None):
         Xc = _dev_f64(Xc, self.device)
+        self._check_width(Xc)
         out = out if out is not None else torch.empty(2, dtype=torch.float64, device=self.device)
         self._stream()
         self._check(self.lib.omb_eval_argmax(self._h, _ptr(Xc), Xc.shape[0], int(offset), _ptr(out)),
@@ -315,6 +330,7 @@ class AcqContext:
     def posterior_cov(self, obj, Xc, out=None):
         """μ (N,), Σ (N, N): GPy predict(Xc, full_cov=True) of objective ``obj`` (σ_n² = 0)."""
         Xc = _dev_f64(Xc, self.device)
+        self._check_width(Xc, obj)
         N = Xc.shape[0]
         mu, cov = out if out is not None else (torch.empty(N, dtype=torch.float64, device=self.device),
                                                torch.empty((N, N), dtype=torch.float64, device=self.device))
@@ -338,6 +354,7 @@ class AcqContext:
 
         Returns (Y, j) with j the absolute jitter that made Σ + jI factorisable."""
         Xc = _dev_f64(Xc, self.device)
+        self._check_width(Xc, obj)
         Zt = _dev_f64(Zt, self.device)
         N = Xc.shape[0]
         B = Zt.shape[0]

@@ -43,6 +43,28 @@ def reduce_pairs(pairs):
     return torch.stack([best, i])
 
 
+def agree_host_rng(seed=None):
+    """Make every rank draw the same host randomness; returns the seed every rank uses.
+
+    The drivers draw from numpy's global generator (LHS initial design, reference directions,
+    ``np.random.randint`` in the reference's loops) and derive the Sobol candidate seed and the
+    MC sample cache from ``seed``.  With several ranks each of those must agree, or the ranks
+    would score different candidate sets and the global arg-max index would name a point the
+    winning rank never scored.  Rank 0's numpy state and seed (drawn there when ``seed`` is
+    None) are broadcast; with one rank nothing changes.
+    """
+    import numpy as np
+    w, rank = world()
+    if w == 1:
+        return seed
+    if rank == 0 and seed is None:
+        seed = int(np.random.randint(0, 2 ** 31 - 1))
+    box = [seed, np.random.get_state()] if rank == 0 else [None, None]
+    dist.broadcast_object_list(box, src=0)
+    np.random.set_state(box[1])
+    return box[0]
+
+
 def global_argmax(local_pair, group=None):
     """All-gather each rank's {value, global index} pair and reduce it identically everywhere."""
     w, _ = world()

@@ -161,6 +161,63 @@ def make_ehvi2d(rng, uf):
                             ehvi_reference=ref, ehvi_textbook=tb)
 
 
+def make_ehvi2d_pos(rng, uf, seed=1):
+    """Reference-mode EHVI in the positive cross-covariance regime.
+
+    The reference passes the flattened sample covariance as σ (util_functions.py:163-167), so
+    σB = σ²₀·s01 and its sign is the sign of the cache's s01.  The cache is unseeded in the
+    reference (optimisers.py:133); Sobol seed 1 gives s01 = +0.070 (seed 0, used by
+    ``ehvi2d_P*.npz``, gives −0.028 and hence EHVI ≤ 0).  The candidates' means are drawn around
+    the front so that most values are strictly positive.
+    """
+    cache = cached_samples(2, 5, seed=seed)
+    c = np.cov(cache[:, 0], cache[:, 1])
+    assert c[0, 1] > 0, "positive-regime fixture needs a cache with s01 > 0"
+    for P in [1, 3, 9, 30]:
+        pf = random_pf(rng, P)
+        r = pf.max(axis=0) + 0.1 * (pf.max(axis=0) - pf.min(axis=0) + 0.1)
+        N = 128
+        # means near and below the front (improving region) plus some beyond r; variances wide
+        t = rng.uniform(0, 1, N)
+        base = np.column_stack([np.interp(t, np.linspace(0, 1, P), np.sort(pf[:, 0])),
+                                np.interp(t, np.linspace(0, 1, P), np.sort(pf[:, 1])[::-1])]).T
+        mu = base + rng.normal(0, 0.15, (2, N))
+        mu[:, -8:] = r[:, None] + rng.uniform(0.0, 0.3, (2, 8))      # beyond the reference point
+        var = np.vstack([10 ** rng.uniform(-4, -0.5, N), 10 ** rng.uniform(-4, -0.5, N)])
+        ref = np.empty(N)
+        for i in range(N):
+            models = [ConstModel(mu[0, i], var[0, i]), ConstModel(mu[1, i], var[1, i])]
+            ref[i] = np.asarray(uf.EHVI(np.zeros(2), models, r, pf, cache)).reshape(-1)[0]
+        np.savez_compressed(os.path.join(HERE, f"ehvi2d_P{P}_pos.npz"), pf=pf, r=r, cache=cache, mu=mu, var=var,
+                            ehvi_reference=ref, cache_seed=np.int64(seed))
+
+
+def make_ehvi3d_pos(rng, uf, seed=1):
+    """EHVI_3D (util_functions.py:170-214) with candidates mostly inside the box and improving on
+    the front, so most values are strictly positive (``ehvi3d.npz`` has 3 positive of 48)."""
+    cache = cached_samples(3, 5, seed=seed)
+    pf = random_pf(rng, 10, k=3)
+    r = pf.max(axis=0) + 0.3
+    N = 64
+    # means pulled towards the ideal corner (dominating part of the front), small spread
+    lam = rng.uniform(0.3, 1.0, N)
+    mu = (pf[rng.integers(0, len(pf), N)].T * lam) + rng.normal(0, 0.02, (3, N))
+    var = np.vstack([10 ** rng.uniform(-5, -2.2, N)] * 3)
+    var[1] = 10 ** rng.uniform(-5, -2.2, N)     # only var[0] matters (change() quirk); vary the rest anyway
+    mu[:, :4] = r[:, None] + 0.05                # beyond r: every sample leaves the box → pygmo raises
+    ref = np.full(N, np.nan)
+    raises = np.zeros(N, bool)
+    for i in range(N):
+        models = [ConstModel(mu[j, i], var[j, i]) for j in range(3)]
+        try:
+            ref[i] = uf.EHVI_3D(np.zeros(3), models, r, pf, cache)
+        except ValueError:
+            raises[i] = True
+    np.savez_compressed(os.path.join(HERE, "ehvi3d_pos.npz"), pf=pf, r=r, cache=cache, mu=mu, var=var,
+                        hv_pf=opareto.hypervolume(pf, r), ehvi_reference=ref, raises=raises,
+                        cache_seed=np.int64(seed))
+
+
 def make_ehvi3d(rng, uf):
     cache = cached_samples(3, 5, seed=0)
     pf = random_pf(rng, 12, k=3)
@@ -508,6 +565,9 @@ def main():
         make_turbo(np.random.default_rng(20261017), turbo_mod)
     if not only or "cparego" in only:
         make_cparego(np.random.default_rng(20261018), cparego_mod, sc)
+    if not only or "ehvi_pos" in only:
+        make_ehvi2d_pos(np.random.default_rng(20261019), uf)
+        make_ehvi3d_pos(np.random.default_rng(20261020), uf)
     print("golden fixtures written to", HERE)
 
 

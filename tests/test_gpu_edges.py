@@ -27,6 +27,40 @@ def _gp(ctx, obj, X, y, ls, var=1.0):
     ctx.set_gp_state(obj, GPState(X, y, ls, var))
 
 
+def test_counter_ring_timeout_is_reported(ctx):
+    """A posterior counter-ring wait that runs out marks the fault word and the next call returns
+    OMB_EHIP (once).  omb_debug_set(SPIN_LIMIT, 0) lets every wait poll only once, which forces
+    the path in practice (a wave reaching a counter before the other 7 waves signal it)."""
+    from optimobo_amd import _lib
+    rng = np.random.default_rng(8)
+    n, d, N = 300, 4, 1 << 15          # 128 < n ≤ 1024: the counter-synchronised ring
+    X = rng.uniform(0, 1, (n, d))
+    Y = np.column_stack([np.sin(3 * X).sum(1), np.cos(2 * X).prod(1)])
+    ls = np.array([0.4, 0.8, 1.1, 0.6])
+    for o in range(2):
+        _gp(ctx, o, X, Y[:, o], ls, float(np.var(Y[:, o])))
+    Xc = dev(rng.uniform(0, 1, (N, d)))
+    ctx.posterior(Xc, n_obj=2)
+    ctx.synchronize()                                   # default bound: no fault
+    ctx.debug_set("spin_limit", 0)
+    with pytest.raises(_lib.OMBError) as e:
+        for _ in range(3):
+            ctx.posterior(Xc, n_obj=2)
+            ctx.synchronize()
+    assert e.value.code == _lib.OMB_EHIP and "counter-ring" in str(e.value)
+    ctx.synchronize()                                   # reported once; the word is clear again
+    ctx.debug_set("spin_limit", 1 << 22)
+    mu, var = ctx.posterior(Xc[:500], n_obj=2)
+    ctx.synchronize()
+    for o in range(2):
+        m, v = ogp.ExactGP(X, Y[:, o], ls, float(np.var(Y[:, o]))).predict(Xc[:500].cpu().numpy())
+        np.testing.assert_allclose(mu[o].cpu().numpy(), m[:, 0], rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(var[o].cpu().numpy(), v[:, 0], rtol=1e-6, atol=1e-9)
+    with pytest.raises(_lib.OMBError) as e:
+        ctx.debug_set("spin_limit", -1)
+    assert e.value.code == _lib.OMB_EINVAL
+
+
 def test_error_codes(ctx):
     from optimobo_amd import _lib
     with pytest.raises(_lib.OMBError) as e:

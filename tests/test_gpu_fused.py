@@ -163,6 +163,34 @@ def test_fused_chain_matches_kernels_and_oracle(ctx, gp3):
         assert (pair[0], int(pair[1])) == (v, i), name
 
 
+@pytest.mark.parametrize("n", [100, 200, 600])
+def test_fused_chain_n_var_64(n):
+    """The fused chain (device Sobol → posterior → EI → arg-max) at the widest n_var (DP = 64)."""
+    from optimobo_amd.device import AcqContext
+    from optimobo_amd.gp import GPState
+    ctx = AcqContext(0)          # its own context: the module's ctx holds the gp3 objectives
+    rng = np.random.default_rng(n)
+    d = 64
+    X = rng.uniform(0, 1, (n, d))
+    y = np.sin(3 * X[:, :8]).sum(1) + 0.1 * X.sum(1)
+    ls = rng.uniform(0.5, 2.0, d) * 4.0
+    var_f = float(np.var(y))
+    ctx.set_gp_state(0, GPState(X, y, ls, var_f))
+    ctx.plan_ei(float(y.min()), 1e-6)
+    lo, hi = np.zeros(d), np.ones(d)
+    ctx.set_sobol(d, lo, hi, seed=5)
+    start, N = 77, 4099
+    pair = ctx.eval_argmax_sobol(start, N).cpu().numpy()
+    U = host_points(d, 5, True, lo, hi, start, N)
+    m, v = ogp.ExactGP(X, y, ls, var_f).predict(U)
+    ref = oacq.ei(m[:, 0], v[:, 0], float(y.min()), 1e-6)
+    vals = ctx.eval(dev(U)).cpu().numpy()
+    np.testing.assert_allclose(vals, ref, rtol=1e-6, atol=1e-12 * np.sqrt(var_f))
+    ov, oi = oacq.argmax(vals, offset=start)
+    assert (pair[0], int(pair[1])) == (ov, oi)
+    ctx.close()
+
+
 def test_eval_argmax_sobol_indices(ctx, gp3):
     Y = gp3[0]
     name, k, plan, separate, _ = _plans(ctx, Y)[1]          # textbook EHVI-2D

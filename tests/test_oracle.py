@@ -79,6 +79,27 @@ def test_ehvi3d_reference(golden_dir):
     assert abs(pareto.hypervolume(z["pf"], z["r"]) - float(z["hv_pf"])) < 1e-14
 
 
+@pytest.mark.parametrize("P", [1, 3, 9, 30])
+def test_ehvi2d_reference_mode_positive_cov(golden_dir, P):
+    """Reference-mode EHVI with a cache whose s01 > 0 (σB = σ²₀·s01 > 0): mostly positive values."""
+    z = load(golden_dir, f"ehvi2d_P{P}_pos.npz")
+    s00, s01 = acq.cache_stats(z["cache"])
+    assert s01 > 0
+    got = acq.ehvi2d(z["mu"], z["var"], z["pf"], z["r"], z["cache"], mode="reference")
+    ref = z["ehvi_reference"]
+    assert np.isfinite(ref).all() and (ref > 0).sum() >= 0.4 * len(ref) and (ref >= 0).all()
+    np.testing.assert_allclose(got, ref, rtol=1e-10, atol=1e-15)
+
+
+def test_ehvi3d_reference_positive(golden_dir):
+    z = load(golden_dir, "ehvi3d_pos.npz")
+    val, raises = acq.ehvi3d_reference(z["mu"], z["var"], float(z["hv_pf"]), z["r"], z["cache"])
+    assert np.array_equal(raises, z["raises"])
+    ok = ~z["raises"]
+    assert (z["ehvi_reference"][ok] > 0).sum() >= 30
+    np.testing.assert_allclose(val[ok], z["ehvi_reference"][ok], rtol=1e-10, atol=1e-15)
+
+
 def test_cells_and_hvpoi(golden_dir):
     z = load(golden_dir, "cells_hvpoi.npz")
     for t in range(4):

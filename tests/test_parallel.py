@@ -55,6 +55,45 @@ def _free_port():
         return s.getsockname()[1]
 
 
+class _Prob:
+    n_var, n_obj = 3, 2
+    xl = np.zeros(3)
+    xu = np.ones(3)
+
+
+def _rng_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from optimobo_amd.algorithms.optimisers import MultiSurrogateOptimiser
+        np.random.seed(1000 + rank)                     # ranks start out of step
+        opt = MultiSurrogateOptimiser(_Prob(), seed=None)
+        cache = opt._get_cached_samples(2, 4)
+        from optimobo_amd import util_functions      # the LHS initial design draws from the global generator
+        lhs = util_functions.generate_latin_hypercube_samples(5, list(zip(_Prob.xl, _Prob.xu)))
+        q.put((rank, opt.seed, cache.tolist(), lhs.tolist(), int(np.random.randint(0, 1 << 30))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_drivers_agree_on_host_randomness_across_ranks():
+    """with seed=None every rank must use the same Sobol seed, MC cache and numpy stream."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rng_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, s0, c0, l0, r0), (_, s1, c1, l1, r1) = sorted(got, key=lambda t: t[0])
+    assert s0 is not None and s0 == s1
+    assert c0 == c1 and l0 == l1 and r0 == r1
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_global_argmax_matches_single_process(world):
     rng = np.random.default_rng(world)

@@ -192,6 +192,152 @@ __global__ __launch_bounds__(256) void kernel_block_mfma_kernel(GPDev g, int d, 
   }
 }
 
+// Exchange of two doubles between 16-lane groups: v_permlane16_swap on both dwords.  Afterwards
+// x holds [x.g0, y.g0, x.g2, y.g2] and y holds [x.g1, y.g1, x.g3, y.g3] (g = 16-lane group).
+__device__ __forceinline__ void permlane16_swap_f64(double& x, double& y) {
+  const unsigned long long xi = __builtin_bit_cast(unsigned long long, x);
+  const unsigned long long yi = __builtin_bit_cast(unsigned long long, y);
+  const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)xi, (unsigned)yi, false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(xi >> 32), (unsigned)(yi >> 32), false, false);
+  x = __builtin_bit_cast(double, ((unsigned long long)hi[0] << 32) | lo[0]);
+  y = __builtin_bit_cast(double, ((unsigned long long)hi[1] << 32) | lo[1]);
+}
+
+// K block, store-stream friendly.  kernel_block_mfma_kernel loaded each row tile's Xf fragment (and,
+// for n_var > 8, ‖x/ℓ‖²) from global memory inside its loop; on gfx950 one counter (vmcnt) tracks
+// loads AND stores, and the compiler's wait for such a load inside a loop with stores is vmcnt(0), so
+// every iteration drained the wave's store queue.  Here the workgroup stages its rows' fragments in
+// LDS once, the loop issues only stores, and the store queue stays full.  Store addresses are one
+// per-lane base pointer plus wave-uniform row offsets (no 64-bit multiplies per store); interior tiles
+// (16 rows < n, every candidate < N) store without per-lane guards.  512 threads: wave w owns the
+// 16-candidate tile w of the workgroup's 128 candidates and sweeps kblock_rows(DP) training rows.
+constexpr bool kKBlockSwap = false;   // 2 × 256-B store rows (see kSwap below); set from the ablation
+constexpr int kblock_rows(int DP) {
+  return (((DP + 5) / 4 + 1) / 2) <= 3 ? 256 : ((((DP + 5) / 4 + 1) / 2) <= 5 ? 128 : 64);
+}
+
+// kSwap: wave w computes the two adjacent candidate tiles 2(w&3), 2(w&3)+1 of the row tiles of parity
+// w>>2, and one v_permlane16_swap per value (permlane16_swap_f64) turns the two accumulators (lane
+// group g: row 4e+g of 16 candidates) into 2 rows × 32 consecutive candidates per register, so each
+// store instruction writes 2 × 256 contiguous bytes instead of 4 × 128 (tools/microbench/mb_write:
+// 5.9-6.0 vs 5.3-5.4 TB/s for the bare store streams).
+template <int DP, int KIND, bool kNT = true, bool kSwap = false>
+__global__ __launch_bounds__(512) void kernel_block_pipe_kernel(GPDev g, int d, const double* __restrict__ Xc,
+                                                                int64_t N, double* __restrict__ K, ExpCoef ec) {
+  constexpr bool kAug = DP <= 8;
+  constexpr int KSD = kAug ? (DP + 5) / 4 : (DP + 3) / 4;
+  constexpr int KSDP = ((DP + 5) / 4 + 1) / 2;   // = packed_X_pairs(DP)
+  constexpr int NA = (KSD + 1) / 2;
+  constexpr int TPW = kblock_rows(DP) / 16;      // row tiles per workgroup
+  constexpr int NCT = kSwap ? 2 : 1;             // candidate tiles per wave
+  constexpr bool kTab256 = KIND == OMB_KERNEL_MATERN52;
+  __shared__ double etab[kTab256 ? 256 : 64];
+  __shared__ double xfs[TPW * KSDP * 128];
+  __shared__ double xsqs[kAug ? 1 : TPW * 16];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int T0 = blockIdx.y * TPW;
+  const int T1 = min((g.n + 15) / 16, T0 + TPW);
+  if (tid < (kTab256 ? 256 : 64)) etab[tid] = kTab256 ? kExp2Tab256[tid] : kExp2Tab64[tid];
+  for (int i = tid; i < (T1 - T0) * KSDP * 128; i += 512) xfs[i] = g.Xf[(int64_t)T0 * KSDP * 128 + i];
+  if constexpr (!kAug)
+    for (int i = tid; i < (T1 - T0) * 16; i += 512) xsqs[i] = g.xsq[16 * T0 + i];
+  // candidate tiles of this wave: 16·(wave·NCT + t) within the workgroup's 128 candidates (kSwap: wave&3)
+  const int64_t cb = (int64_t)blockIdx.x * 128 + 16 * NCT * (kSwap ? (wave & 3) : wave);
+  double csq[NCT], bfr[NCT][KSD];
+#pragma unroll
+  for (int t = 0; t < NCT; ++t) {
+    const int64_t c = cb + 16 * t + (lane & 15);
+    const int64_t ci = c < N ? c : N - 1;
+    double s2 = 0.0;
+#pragma unroll
+    for (int j = 0; j < DP; ++j) {
+      const double x = (j < d) ? Xc[ci * d + j] / g.ls[j] : 0.0;
+      s2 = fma(x, x, s2);
+    }
+    csq[t] = s2;
+#pragma unroll
+    for (int s = 0; s < KSD; ++s) {
+      const int j = 4 * s + (lane >> 4);
+      const double x = (j < d) ? Xc[ci * d + j] / g.ls[j] : 0.0;
+      if constexpr (kAug)
+        bfr[t][s] = (j < d) ? -2.0 * x : (j == d ? 1.0 : (j == d + 1 ? s2 : 0.0));
+      else
+        bfr[t][s] = x;
+    }
+  }
+  const double pm[3] = {g.variance, kSqrt5 * g.variance, kFiveThirds * g.variance};
+  const bool cols_full = (int64_t)(blockIdx.x + 1) * 128 <= N;     // workgroup-uniform
+  const int full_tiles = g.n / 16;                                  // tiles with all 16 rows < n
+  // stored element e of a tile: row 16T + 4e + rsub, column col
+  //   plain: rsub = lane>>4, col = cb + (lane&15);  swap: rsub = 2(lane>>5) (+1 for the second register),
+  //   col = cb + (lane&31)
+  const int rsub = kSwap ? 2 * (lane >> 5) : (lane >> 4);
+  const int64_t col = cb + (kSwap ? (lane & 31) : (lane & 15));
+  double* Kl = K + (int64_t)rsub * N + col;
+  const int64_t N4 = 4 * N;
+  auto st = [&](double* p, double v) {
+    if constexpr (kNT)
+      __builtin_nontemporal_store(v, p);
+    else
+      *p = v;
+  };
+  __syncthreads();
+  const int Tstart = T0 + (kSwap ? (wave >> 2) : 0);
+  for (int T = Tstart; T < T1; T += (kSwap ? 2 : 1)) {
+    const d2* xa = reinterpret_cast<const d2*>(xfs + (T - T0) * (KSDP * 128) + 2 * lane);
+    d2 a[NA];
+#pragma unroll
+    for (int p = 0; p < NA; ++p) a[p] = xa[64 * p];
+    double v[NCT][4];
+#pragma unroll
+    for (int t = 0; t < NCT; ++t) {
+      d4 cr = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s = 0; s < KSD; ++s)
+        cr = __builtin_amdgcn_mfma_f64_16x16x4f64((s & 1) ? a[s >> 1].y : a[s >> 1].x, bfr[t][s], cr, 0, 0, 0);
+#pragma unroll
+      for (int e = 0; e < 4; e += 2) {
+        const int l0 = 16 * (T - T0) + 4 * e + (lane >> 4), l1 = l0 + 4;
+        const double r2a = kAug ? cr[e] : fma(-2.0, cr[e], xsqs[kAug ? 0 : l0] + csq[t]);
+        const double r2b = kAug ? cr[e + 1] : fma(-2.0, cr[e + 1], xsqs[kAug ? 0 : l1] + csq[t]);
+        if constexpr (kTab256)
+          matern_r2_tab256_x2(r2a, r2b, pm, ec, etab, v[t][e], v[t][e + 1]);
+        else
+          kernel_of_r2_tab_x2<KIND>(r2a, r2b, pm, ec, etab, v[t][e], v[t][e + 1]);
+      }
+    }
+    double* p = Kl + (int64_t)T * (4 * N4);
+    if constexpr (kSwap) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) permlane16_swap_f64(v[0][e], v[1][e]);
+      if (cols_full && T < full_tiles) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          st(p + e * N4, v[0][e]);
+          st(p + e * N4 + N, v[1][e]);
+        }
+      } else if (col < N) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int k = 16 * T + 4 * e + rsub;
+          if (k < g.n) st(p + e * N4, v[0][e]);
+          if (k + 1 < g.n) st(p + e * N4 + N, v[1][e]);
+        }
+      }
+    } else {
+      if (cols_full && T < full_tiles) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) st(p + e * N4, v[0][e]);
+      } else if (col < N) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (16 * T + 4 * e + rsub < g.n) st(p + e * N4, v[0][e]);
+      }
+    }
+  }
+}
+
 // ----------------------------------------------------------------------------- posterior
 // ABL (ablation, tools/ablate only; the library instantiates ABL = 0): bit 1 replaces the Matern
 // transform by the raw dot product, bit 2 skips the MFMA phase, bit 4 feeds a constant A
@@ -604,19 +750,424 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
   }
 }
 
+// ----------------------------------------------------------------------------- posterior, n ≤ 256
+// Whole-tile variant for small training sets (BASELINE configs 2 and 4): the complete K* tile of the
+// workgroup (16·RMAX rows × BN = 16·CT candidates, 64 KiB) is generated into LDS in one pass, one
+// barrier, then V = L⁻¹K* runs with no further synchronisation.  With only 2-4 chunks of 64 rows the
+// chunk pipeline of posterior_kernel spent a large share of each workgroup in its prologue and in
+// per-chunk barriers, and its per-chunk MFMA split left SIMDs idle (at n = 128: 48 units on the
+// busiest SIMD against 36 on average).  Here the multiply is balanced exactly: SIMD s owns row-tile
+// pairs (q, RMAX−1−q), q ≡ s (mod 4), whose k-step counts 4(q+1) + 4(RMAX−q) are the same for every
+// pair; the two waves of a SIMD split the candidate tiles.  Two 64-KiB workgroups share a CU, so one
+// workgroup's generation (VALU) runs while the other multiplies (MFMA).
+//   gen:  wave w takes candidate tile w mod CT and row tiles w/CT + (8/CT)·i (RMAX·CT/8 tiles).
+//   K* in LDS in B-fragment order: element (row k, candidate c) at ((k/4)·CT + c/16)·64 + (k%4)·16 + c%16.
+// ABL (tools/ablate only): bit 2 skips the multiply, bit 4 feeds a constant A operand.
+template <int RMAX, int CT, int DP, int KIND, int ABL = 0>
+__global__ __launch_bounds__(512, 2) void posterior_tile_kernel(GPArgs args, const double* __restrict__ Xc,
+                                                                int64_t N, double* __restrict__ mu_out,
+                                                                double* __restrict__ var_out) {
+  constexpr int NW = 8, NT = 512;
+  constexpr int BN = 16 * CT;
+  constexpr int TILE = 4 * RMAX * CT * 64;          // doubles: 16·RMAX rows × BN candidates
+  constexpr bool kAug = DP <= 8;
+  constexpr int KSD = kAug ? (DP + 5) / 4 : (DP + 3) / 4;
+  constexpr int KSDP = ((DP + 5) / 4 + 1) / 2;      // = packed_X_pairs(DP)
+  constexpr bool kCandLds = DP > 8;
+  constexpr bool kTab256 = KIND == OMB_KERNEL_MATERN52;
+  constexpr int kTabN = kTab256 ? 256 : 64;
+  constexpr int GT = RMAX * CT / NW;                 // generated tiles per wave
+  constexpr int PPS = RMAX / 8;                      // row-tile pairs per SIMD
+  constexpr int CPW = CT / 2;                        // candidate tiles per wave in the multiply
+  static_assert(RMAX % 8 == 0 && CT % 2 == 0 && NW % CT == 0 && GT >= 1, "tile shape");
+  static_assert(TILE >= 4 * BN + NW * 16, "reduction scratch must fit in the K* tile");
+  __shared__ double kbuf[TILE + (kCandLds ? DP * BN : 0) + kTabN];
+
+  const int obj = blockIdx.y;
+  const GPDev g = args.gp[obj];
+  const int d = args.d;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t c0 = (int64_t)blockIdx.x * BN;
+  double* cand = kbuf + TILE;
+  double* etab = cand + (kCandLds ? DP * BN : 0);
+  for (int i = tid; i < kTabN; i += NT) etab[i] = kTab256 ? kExp2Tab256[i] : kExp2Tab64[i];
+  if constexpr (kCandLds) {
+    for (int e = tid; e < DP * BN; e += NT) {
+      const int j = e / BN, c = e % BN;
+      const int64_t cc = min(c0 + c, N - 1);
+      cand[e] = (j < d) ? Xc[cc * d + j] / g.ls[j] : 0.0;
+    }
+  }
+
+  // ---- generation operands: this wave's candidate tile as the B fragment [−2·x*/ℓ, 1, ‖x*/ℓ‖²]
+  const int ct_g = wave % CT;
+  const int64_t ci = min(c0 + 16 * ct_g + (lane & 15), N - 1);
+  if constexpr (kCandLds) __syncthreads();
+  auto coord = [&](int j) -> double {
+    if constexpr (kCandLds) return cand[j * BN + 16 * ct_g + (lane & 15)];
+    return (j < d) ? Xc[ci * d + j] / g.ls[j] : 0.0;
+  };
+  double csq = 0.0;
+#pragma unroll
+  for (int j = 0; j < DP; ++j) {
+    const double c = coord(j);
+    csq = fma(c, c, csq);
+  }
+  double bfr[KSD];
+#pragma unroll
+  for (int s = 0; s < KSD; ++s) {
+    const int j = 4 * s + (lane >> 4);
+    if constexpr (kAug)
+      bfr[s] = (j < d) ? -2.0 * coord(j) : (j == d ? 1.0 : (j == d + 1 ? csq : 0.0));
+    else
+      bfr[s] = (j < d) ? coord(j) : 0.0;
+  }
+  const double pm[3] = {g.variance, kSqrt5 * g.variance, kFiveThirds * g.variance};
+  if constexpr (!kCandLds) __syncthreads();          // etab
+
+  double mu_part = 0.0;
+#pragma unroll
+  for (int i = 0; i < GT; ++i) {
+    const int T = wave / CT + (NW / CT) * i;
+    if (T < g.R) {
+      const d2* xa = reinterpret_cast<const d2*>(g.Xf + (int64_t)T * (KSDP * 128) + 2 * lane);
+      d2 a[(KSD + 1) / 2];
+#pragma unroll
+      for (int p = 0; p < (KSD + 1) / 2; ++p) a[p] = xa[64 * p];
+      d4 cr = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s = 0; s < KSD; ++s)
+        cr = __builtin_amdgcn_mfma_f64_16x16x4f64((s & 1) ? a[s >> 1].y : a[s >> 1].x, bfr[s], cr, 0, 0, 0);
+#pragma unroll
+      for (int e = 0; e < 4; e += 2) {
+        const int k0 = 16 * T + 4 * e + (lane >> 4), k1 = k0 + 4;
+        const double r2a = kAug ? cr[e] : fma(-2.0, cr[e], g.xsq[k0] + csq);
+        const double r2b = kAug ? cr[e + 1] : fma(-2.0, cr[e + 1], g.xsq[k1] + csq);
+        double v0, v1;
+        if constexpr (kTab256)
+          matern_r2_tab256_x2(r2a, r2b, pm, args.ec, etab, v0, v1);
+        else
+          kernel_of_r2_tab_x2<KIND>(r2a, r2b, pm, args.ec, etab, v0, v1);
+        if constexpr (!kAug) {
+          v0 = (k0 < g.n) ? v0 : 0.0;
+          v1 = (k1 < g.n) ? v1 : 0.0;
+        }
+        mu_part = fma(g.alpha[k0], v0, mu_part);
+        mu_part = fma(g.alpha[k1], v1, mu_part);
+        kbuf[((4 * T + e) * CT + ct_g) * 64 + lane] = v0;
+        kbuf[((4 * T + e + 1) * CT + ct_g) * 64 + lane] = v1;
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- V = L⁻¹ K*: SIMD s owns the row-tile pairs (q, RMAX−1−q), q = s + 4p; wave h of the SIMD the
+  // candidate tiles h·CPW .. h·CPW + CPW − 1.  A (L⁻¹) k-step pairs stream from the packed copy two
+  // pairs ahead of their MFMAs.
+  const int simd = wave & 3, h = wave >> 2;
+  d4 acc[2 * PPS][CPW];
+#pragma unroll
+  for (int j = 0; j < 2 * PPS; ++j)
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) acc[j][c] = d4{0.0, 0.0, 0.0, 0.0};
+  if constexpr (!(ABL & 2)) {
+#pragma unroll
+    for (int j = 0; j < 2 * PPS; ++j) {
+      const int q = simd + 4 * (j >> 1);
+      const int r = (j & 1) ? RMAX - 1 - q : q;
+      if (r >= g.R) continue;                              // wave-uniform
+      const int nP = 2 * (r + 1);                          // k-step pairs of row tile r
+      const d2* A = reinterpret_cast<const d2*>(g.Lp + 128ll * r * (r + 1)) + lane;
+      auto ld = [&](int P) -> d2 {
+        if constexpr (ABL & 4) return d2{1e-3 * lane + P, 2e-3 * j};
+        return A[64 * min(P, nP - 1)];
+      };
+      d2 a0 = ld(0), a1 = ld(1), n0 = ld(2), n1 = ld(3);
+      for (int P = 0; P < nP; P += 2) {
+        const d2 f0 = ld(P + 4), f1 = ld(P + 5);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const d2 a = u ? a1 : a0;
+          const int S = 2 * (P + u);
+          double b0[CPW], b1[CPW];
+#pragma unroll
+          for (int c = 0; c < CPW; ++c) {
+            b0[c] = kbuf[(S * CT + h * CPW + c) * 64 + lane];
+            b1[c] = kbuf[((S + 1) * CT + h * CPW + c) * 64 + lane];
+          }
+#pragma unroll
+          for (int c = 0; c < CPW; ++c) {
+            acc[j][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(a.x, b0[c], acc[j][c], 0, 0, 0);
+            acc[j][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(a.y, b1[c], acc[j][c], 0, 0, 0);
+          }
+        }
+        a0 = n0; a1 = n1; n0 = f0; n1 = f1;
+      }
+    }
+  }
+
+  // ---- σ² = σ_f² − Σ rows V²: registers, lanes {l, l^16, l^32, l^48}, then the 4 SIMDs in a fixed
+  // order; μ: the NW/CT generating waves of each candidate tile, in a fixed order.
+  double part[CPW];
+#pragma unroll
+  for (int c = 0; c < CPW; ++c) {
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < 2 * PPS; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) s = fma(acc[j][c][i], acc[j][c][i], s);
+    s += __shfl_xor(s, 16);
+    s += __shfl_xor(s, 32);
+    part[c] = s;
+  }
+  double mp = mu_part;
+  mp += __shfl_xor(mp, 16);
+  mp += __shfl_xor(mp, 32);
+  __syncthreads();                                  // every wave is done reading K*
+  double* red = kbuf;                               // [4 SIMDs][BN]
+  double* redmu = kbuf + 4 * BN;                    // [NW waves][16]
+  if (lane < 16) {
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) red[simd * BN + (h * CPW + c) * 16 + lane] = part[c];
+    redmu[wave * 16 + lane] = mp;
+  }
+  __syncthreads();
+  if (tid < BN) {
+    const double s = ((red[tid] + red[BN + tid]) + red[2 * BN + tid]) + red[3 * BN + tid];
+    double m = 0.0;
+    for (int w = tid >> 4; w < NW; w += CT) m += redmu[w * 16 + (tid & 15)];
+    const int64_t c = c0 + tid;
+    if (c < N) {
+      mu_out[(int64_t)obj * N + c] = m;
+      var_out[(int64_t)obj * N + c] = g.variance - s;
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------- posterior, n ≤ 128, persistent
+// BASELINE config 2 (n = 128, 2^16 candidates): here generating K* costs as much as multiplying it
+// (tile kernel at n = 128: 77 µs whole, 35 µs generation alone), and most of the generation time was
+// latency — candidate loads at workgroup start, the training rows and α fetched from L2 per tile, the
+// exp table refilled per workgroup.  This variant keeps two workgroups per CU resident for the whole
+// launch: each stages the training rows (fragment-packed), α and the exp table in LDS once, then
+// loops over candidate blocks; the next block's candidate coordinates are loaded while the current
+// block multiplies, so generation reads only LDS and registers.  Per block: generate (VALU + r² MFMA)
+// → barrier → multiply (balanced as in posterior_tile_kernel) + partial sums → barrier → 64 outputs.
+// LDS: 64 KiB K* + Xf + α + table + reduction scratch ≈ 78 KiB (n_var ≤ 8).
+template <int CT, int DP, int KIND, int ABL = 0>
+__global__ __launch_bounds__(512, 2) void posterior_small_kernel(GPArgs args, const double* __restrict__ Xc,
+                                                                 int64_t N, double* __restrict__ mu_out,
+                                                                 double* __restrict__ var_out) {
+  constexpr int RMAX = 8;                            // n ≤ 128
+  constexpr int NW = 8, NT = 512;
+  constexpr int BN = 16 * CT;
+  constexpr int TILE = 4 * RMAX * CT * 64;
+  static_assert(DP <= 8, "the persistent variant keeps candidate coordinates in registers (n_var <= 8)");
+  constexpr int KSD = (DP + 5) / 4;                  // augmented r² MFMA k-steps
+  constexpr int KSDP = (KSD + 1) / 2;
+  constexpr bool kTab256 = KIND == OMB_KERNEL_MATERN52;
+  constexpr int kTabN = kTab256 ? 256 : 64;
+  constexpr int GT = RMAX * CT / NW;
+  constexpr int CPW = CT / 2;
+  constexpr int XF = RMAX * KSDP * 128;              // doubles of the packed training rows
+  static_assert(CT % 2 == 0 && NW % CT == 0 && GT >= 1, "tile shape");
+  __shared__ double kbuf[TILE + XF + 16 * RMAX + kTabN + 4 * BN + NW * 16];
+  double* xf = kbuf + TILE;
+  double* al = xf + XF;
+  double* etab = al + 16 * RMAX;
+  double* red = etab + kTabN;                        // [4 SIMDs][BN]
+  double* redmu = red + 4 * BN;                      // [NW waves][16]
+
+  const int obj = blockIdx.y;
+  const GPDev g = args.gp[obj];
+  const int d = args.d;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t nblk = (N + BN - 1) / BN;
+  int64_t b = blockIdx.x;
+  if (b >= nblk) return;                             // workgroup-uniform
+
+  for (int i = tid; i < kTabN; i += NT) etab[i] = kTab256 ? kExp2Tab256[i] : kExp2Tab64[i];
+  for (int i = tid; i < g.R * KSDP * 128; i += NT) xf[i] = g.Xf[i];
+  for (int i = tid; i < 16 * RMAX; i += NT) al[i] = (i < 16 * g.R) ? g.alpha[i] : 0.0;
+
+  const int ct_g = wave % CT;
+  const int simd = wave & 3, h = wave >> 2;
+  // this lane's candidate coordinates for block bb (raw, loaded one block ahead)
+  double xr[DP];
+  auto load_cand = [&](int64_t bb) {
+    const int64_t ci = min(bb * BN + 16 * ct_g + (lane & 15), N - 1);
+#pragma unroll
+    for (int j = 0; j < DP; ++j) xr[j] = (j < d) ? Xc[ci * d + j] : 0.0;
+  };
+  double bfr[KSD];
+  auto make_bfr = [&]() {
+    double csq = 0.0;
+    double cs[DP];
+#pragma unroll
+    for (int j = 0; j < DP; ++j) {
+      // x*/ℓ by division, as GPy and the other kernels do (bit-identical K*)
+      cs[j] = (j < d) ? xr[j] / g.ls[j] : 0.0;
+      csq = fma(cs[j], cs[j], csq);
+    }
+#pragma unroll
+    for (int s = 0; s < KSD; ++s) {
+      const int j = 4 * s + (lane >> 4);
+      double v = 0.0;
+#pragma unroll
+      for (int jj = 0; jj < DP; ++jj) v = (jj == j) ? cs[jj] : v;    // static register select
+      bfr[s] = (j < d) ? -2.0 * v : (j == d ? 1.0 : (j == d + 1 ? csq : 0.0));
+    }
+  };
+  load_cand(b);
+  make_bfr();
+  const double pm[3] = {g.variance, kSqrt5 * g.variance, kFiveThirds * g.variance};
+  __syncthreads();
+
+  for (; b < nblk; b += gridDim.x) {
+    const int64_t c0 = b * BN;
+    // ---- generate the whole K* tile of this block from LDS and registers
+    double mu_part = 0.0;
+#pragma unroll
+    for (int i = 0; i < GT; ++i) {
+      const int T = wave / CT + (NW / CT) * i;
+      if (T < g.R) {
+        const d2* xa = reinterpret_cast<const d2*>(xf + T * (KSDP * 128) + 2 * lane);
+        d2 a[KSDP];
+#pragma unroll
+        for (int p = 0; p < KSDP; ++p) a[p] = xa[64 * p];
+        d4 cr = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s = 0; s < KSD; ++s)
+          cr = __builtin_amdgcn_mfma_f64_16x16x4f64((s & 1) ? a[s >> 1].y : a[s >> 1].x, bfr[s], cr, 0, 0, 0);
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {
+          const int k0 = 16 * T + 4 * e + (lane >> 4), k1 = k0 + 4;
+          double v0, v1;
+          if constexpr (kTab256)
+            matern_r2_tab256_x2(cr[e], cr[e + 1], pm, args.ec, etab, v0, v1);
+          else
+            kernel_of_r2_tab_x2<KIND>(cr[e], cr[e + 1], pm, args.ec, etab, v0, v1);
+          mu_part = fma(al[k0], v0, mu_part);
+          mu_part = fma(al[k1], v1, mu_part);
+          kbuf[((4 * T + e) * CT + ct_g) * 64 + lane] = v0;
+          kbuf[((4 * T + e + 1) * CT + ct_g) * 64 + lane] = v1;
+        }
+      }
+    }
+    __syncthreads();                                  // A: the tile is complete
+    const int64_t bn = b + gridDim.x;
+    if (bn < nblk) load_cand(bn);                     // in flight during the multiply
+
+    // ---- V = L⁻¹ K*, SIMD s: row tiles s and 7 − s, wave h: candidate tiles h·CPW ..
+    d4 acc[2][CPW];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int c = 0; c < CPW; ++c) acc[j][c] = d4{0.0, 0.0, 0.0, 0.0};
+    if constexpr (!(ABL & 2)) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = j ? RMAX - 1 - simd : simd;
+        if (r >= g.R) continue;
+        const int nP = 2 * (r + 1);
+        const d2* A = reinterpret_cast<const d2*>(g.Lp + 128ll * r * (r + 1)) + lane;
+        auto ld = [&](int P) -> d2 { return A[64 * min(P, nP - 1)]; };
+        d2 a0 = ld(0), a1 = ld(1), n0 = ld(2), n1 = ld(3);
+        for (int P = 0; P < nP; P += 2) {
+          const d2 f0 = ld(P + 4), f1 = ld(P + 5);
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const d2 a = u ? a1 : a0;
+            const int S = 2 * (P + u);
+            double b0[CPW], b1[CPW];
+#pragma unroll
+            for (int c = 0; c < CPW; ++c) {
+              b0[c] = kbuf[(S * CT + h * CPW + c) * 64 + lane];
+              b1[c] = kbuf[((S + 1) * CT + h * CPW + c) * 64 + lane];
+            }
+#pragma unroll
+            for (int c = 0; c < CPW; ++c) {
+              acc[j][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(a.x, b0[c], acc[j][c], 0, 0, 0);
+              acc[j][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(a.y, b1[c], acc[j][c], 0, 0, 0);
+            }
+          }
+          a0 = n0; a1 = n1; n0 = f0; n1 = f1;
+        }
+      }
+    }
+    double part[CPW];
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) {
+      double s = 0.0;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s = fma(acc[j][c][i], acc[j][c][i], s);
+      s += __shfl_xor(s, 16);
+      s += __shfl_xor(s, 32);
+      part[c] = s;
+    }
+    double mp = mu_part;
+    mp += __shfl_xor(mp, 16);
+    mp += __shfl_xor(mp, 32);
+    if (lane < 16) {
+#pragma unroll
+      for (int c = 0; c < CPW; ++c) red[simd * BN + (h * CPW + c) * 16 + lane] = part[c];
+      redmu[wave * 16 + lane] = mp;
+    }
+    __syncthreads();                                  // B: partials complete, K* free
+    if (tid < BN) {
+      const double s = ((red[tid] + red[BN + tid]) + red[2 * BN + tid]) + red[3 * BN + tid];
+      double m = 0.0;
+      for (int w = tid >> 4; w < NW; w += CT) m += redmu[w * 16 + (tid & 15)];
+      const int64_t c = c0 + tid;
+      if (c < N) {
+        mu_out[(int64_t)obj * N + c] = m;
+        var_out[(int64_t)obj * N + c] = g.variance - s;
+      }
+    }
+    if (bn < nblk) make_bfr();
+  }
+}
+
 // ----------------------------------------------------------------------------- dispatch
+// Compute units of the current device (cached per device).
+static int cu_count() {
+  static int cached[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cached[dev]) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    cached[dev] = v;
+  }
+  return cached[dev];
+}
+
 template <int DP, int KIND>
 static hipError_t launch_posterior_dp(hipStream_t stream, const GPArgs& args, int n_obj, int max_R,
                                       const double* Xc, int64_t N, double* mu, double* var) {
   const int Q = (max_R + 3) / 4;
   const int RTneed = (Q + 1) / 2;
   if (RTneed <= 1) {
-    dim3 grid((unsigned)((N + 63) / 64), n_obj);
-    // n ≤ 256: two 64-KiB workgroups per CU beat the 96-KiB counter ring
-    hipLaunchKernelGGL((posterior_kernel<1, 4, DP, KIND, 8, 32>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var);
+    const int64_t nblk = (N + 63) / 64;
+    if constexpr (DP <= 8) {
+      // n ≤ 128, n_var ≤ 8: two persistent workgroups per CU loop over 64-candidate blocks
+      // (tools/ablate at n = 128, 2 objectives, 2^16 candidates: see DESIGN.md §4)
+      const int64_t per_obj = std::max<int64_t>(1, (2 * (int64_t)cu_count()) / n_obj);
+      dim3 grid((unsigned)std::min<int64_t>(nblk, per_obj), n_obj);
+      hipLaunchKernelGGL((posterior_small_kernel<4, DP, KIND>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var);
+    } else {
+      // n ≤ 128, wide inputs: the whole 128 × 64 K* tile in LDS, one barrier, balanced multiply
+      dim3 grid((unsigned)nblk, n_obj);
+      hipLaunchKernelGGL((posterior_tile_kernel<8, 4, DP, KIND>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var);
+    }
   } else if (RTneed <= 2) {
     // 128 < n ≤ 256: 32-candidate blocks on the counter ring (48 KiB, several workgroups per CU);
-    // tools/ablate at n = 256, 3 objectives, 2^17 candidates: 0.709 ms (CT 4, barrier) → 0.600 ms
+    // tools/ablate at n = 256, 3 objectives, 2^17 candidates: 0.709 ms (CT 4, barrier) → 0.641 ms;
+    // the whole-tile kernel (RMAX 16, CT 2) takes 0.688 ms there (profiles/r02_v2_ablate_c4.txt)
     dim3 grid((unsigned)((N + 31) / 32), n_obj);
     hipLaunchKernelGGL((posterior_kernel<2, 2, DP, KIND, 8, 0>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var);
   } else if (RTneed <= 4) {
@@ -658,12 +1209,20 @@ template <int KIND>
 static hipError_t launch_kblock_kind(hipStream_t stream, const GPArgs& args, int obj, const double* Xc, int64_t N,
                                      double* K) {
   const GPDev& g = args.gp[obj];
-  dim3 grid((unsigned)((N + 63) / 64), (unsigned)((g.n + kKBlockRows - 1) / kKBlockRows));
+  // n_var ≤ 8: LDS-staged fragments, 128 candidates per workgroup (kernel_block_pipe_kernel);
+  // wider inputs keep kernel_block_mfma_kernel (faster there: profiles/r02_v4_ablate_kblock_c5.txt)
+  auto pipe_grid = [&](int DP) {
+    return dim3((unsigned)((N + 127) / 128), (unsigned)((g.n + kblock_rows(DP) - 1) / kblock_rows(DP)));
+  };
+  const dim3 grid((unsigned)((N + 63) / 64), (unsigned)((g.n + kKBlockRows - 1) / kKBlockRows));
   switch (args.DP) {
+#define OMB_KBP(DPV) \
+  case DPV: hipLaunchKernelGGL((kernel_block_pipe_kernel<DPV, KIND, true, kKBlockSwap>), pipe_grid(DPV), dim3(512), 0, stream, g, args.d, Xc, N, K, exp_coef()); break;
 #define OMB_KB(DPV) \
   case DPV: hipLaunchKernelGGL((kernel_block_mfma_kernel<DPV, KIND>), grid, dim3(256), 0, stream, g, args.d, Xc, N, K, exp_coef()); break;
-    OMB_KB(2) OMB_KB(4) OMB_KB(6) OMB_KB(8) OMB_KB(16) OMB_KB(32) OMB_KB(64)
+    OMB_KBP(2) OMB_KBP(4) OMB_KBP(6) OMB_KBP(8) OMB_KB(16) OMB_KB(32) OMB_KB(64)
 #undef OMB_KB
+#undef OMB_KBP
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -1,5 +1,6 @@
-// K block: VALU dot products (kernel_block_kernel) vs r² on MFMA (kernel_block_mfma_kernel), same
-// data, interleaved (tools only).
+// K block variants on the same data, interleaved (tools only): VALU dot products (kernel_block_kernel,
+// the r01 baseline), r² on MFMA with 4 × 128-B store segments (kernel_block_mfma_kernel) and with the
+// permlane16 swap to 2 × 256-B segments (kernel_block_swap_kernel), non-temporal and plain stores.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/ablate/ablate_kblock2 tools/ablate/ablate_kblock2.hip
 // Run on the GPU box: ./tools/ablate/ablate_kblock2 [n] [N] [d]   (d = 6 or 30)
 #include <cstdio>
@@ -92,25 +93,44 @@ void bench(int n, int64_t N, int d) {
   dim3 g1((unsigned)((N + 511) / 512), (unsigned)((n + kKBlockRows - 1) / kKBlockRows));
   dim3 g2((unsigned)((N + 63) / 64), (unsigned)((n + kKBlockRows - 1) / kKBlockRows));
   auto old_k = [&] { hipLaunchKernelGGL((kernel_block_kernel<DP, 0>), g1, dim3(256), 0, 0, g, d, Xc, N, K1, ec); };
-  auto new_k = [&] { hipLaunchKernelGGL((kernel_block_mfma_kernel<DP, 0>), g2, dim3(256), 0, 0, g, d, Xc, N, K2, ec); };
-  auto plain_k = [&] {
-    hipLaunchKernelGGL((kernel_block_mfma_kernel<DP, 0, false>), g2, dim3(256), 0, 0, g, d, Xc, N, K2, ec);
-  };
-  float t1 = 0, t2 = 0, t3 = 0;
+  auto mfma_nt = [&] { hipLaunchKernelGGL((kernel_block_mfma_kernel<DP, 0>), g2, dim3(256), 0, 0, g, d, Xc, N, K2, ec); };
+  auto mfma_pl = [&] { hipLaunchKernelGGL((kernel_block_mfma_kernel<DP, 0, false>), g2, dim3(256), 0, 0, g, d, Xc, N, K2, ec); };
+  dim3 g3((unsigned)((N + 127) / 128), (unsigned)((n + kblock_rows(DP) - 1) / kblock_rows(DP)));
+  auto pipe_nt = [&] { hipLaunchKernelGGL((kernel_block_pipe_kernel<DP, 0>), g3, dim3(512), 0, 0, g, d, Xc, N, K1, ec); };
+  auto pipe_pl = [&] { hipLaunchKernelGGL((kernel_block_pipe_kernel<DP, 0, false>), g3, dim3(512), 0, 0, g, d, Xc, N, K1, ec); };
+  auto swap_nt = [&] { hipLaunchKernelGGL((kernel_block_pipe_kernel<DP, 0, true, true>), g3, dim3(512), 0, 0, g, d, Xc, N, K1, ec); };
+  auto swap_pl = [&] { hipLaunchKernelGGL((kernel_block_pipe_kernel<DP, 0, false, true>), g3, dim3(512), 0, 0, g, d, Xc, N, K1, ec); };
+  float t[7] = {0, 0, 0, 0, 0, 0, 0};
   for (int r = 0; r < 3; ++r) {
-    t1 += time_ms(old_k, 5);
-    t2 += time_ms(new_k, 5);
-    t3 += time_ms(plain_k, 5);
+    t[0] += time_ms(old_k, 5);
+    t[1] += time_ms(mfma_nt, 5);
+    t[2] += time_ms(mfma_pl, 5);
+    t[3] += time_ms(swap_nt, 5);
+    t[4] += time_ms(swap_pl, 5);
+    t[5] += time_ms(pipe_nt, 5);
+    t[6] += time_ms(pipe_pl, 5);
   }
-  printf("MFMA r2 with plain stores %.3f ms (%.0f GB/s)\n", t3 / 3, 8.0 * (n + d) * N / (t3 / 3 * 1e6));
+  const char* names[7] = {"VALU dots (r01 baseline)", "MFMA r2, 4x128-B rows, nt (r01 library)", "MFMA r2, 4x128-B rows, plain",
+                          "LDS-staged + permlane16 swap, 2x256-B rows, nt", "LDS-staged + permlane16 swap, 2x256-B rows, plain",
+                          "Xf staged in LDS + base-pointer stores, nt", "Xf staged in LDS + base-pointer stores, plain"};
+  const double bytes = 8.0 * (n + d) * N + 8.0 * n * (d + 1);
+  for (int i = 0; i < 7; ++i)
+    printf("n=%d N=%lld d=%d  %-48s %.3f ms  %.0f GB/s  (%.3f of 8 TB/s)\n", n, (long long)N, d, names[i], t[i] / 3,
+           bytes / (t[i] / 3 * 1e6), bytes / (t[i] / 3 * 1e6) / 8000.0);
   std::vector<double> h1((size_t)n * N), h2((size_t)n * N);
-  CK(hipMemcpy(h1.data(), K1, h1.size() * 8, hipMemcpyDeviceToHost));
+  mfma_nt();
+  CK(hipDeviceSynchronize());
   CK(hipMemcpy(h2.data(), K2, h2.size() * 8, hipMemcpyDeviceToHost));
-  double md = 0;
-  for (size_t i = 0; i < h1.size(); ++i) md = std::max(md, std::abs(h1[i] - h2[i]) / (std::abs(h1[i]) + 1e-300));
-  const double bytes = 8.0 * (n + d) * N;
-  printf("n=%d N=%lld d=%d  VALU dots %.3f ms (%.0f GB/s)  MFMA r2 %.3f ms (%.0f GB/s)  max rel diff %.2e\n", n,
-         (long long)N, d, t1 / 3, bytes / (t1 / 3 * 1e6), t2 / 3, bytes / (t2 / 3 * 1e6), md);
+  for (int v = 0; v < 2; ++v) {
+    CK(hipMemset(K1, 0, h1.size() * 8));
+    if (v == 0) swap_nt(); else pipe_nt();
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(h1.data(), K1, h1.size() * 8, hipMemcpyDeviceToHost));
+    size_t ndiff = 0;
+    for (size_t i = 0; i < h1.size(); ++i) ndiff += (h1[i] != h2[i]);
+    printf("%s vs r01 kernel: %zu of %zu elements differ (must be 0: same arithmetic)\n", v ? "pipe" : "swap", ndiff,
+           h1.size());
+  }
 }
 
 int main(int argc, char** argv) {
@@ -119,6 +139,7 @@ int main(int argc, char** argv) {
   const int d = argc > 3 ? atoi(argv[3]) : 6;
   if (d == 6) bench<6>(n, N, d);
   else if (d == 30) bench<32>(n, N, d);
-  else printf("d must be 6 or 30\n");
+  else if (d == 2) bench<2>(n, N, d);
+  else printf("d must be 2, 6 or 30\n");
   return 0;
 }

@@ -43,6 +43,46 @@ float run(const Bench& b, int reps) {
   return ms / reps;
 }
 
+template <int RMAX, int CT, int ABL, int DP = 6>
+float run_tile(const Bench& b, int reps) {
+  dim3 grid((unsigned)((b.N + 16 * CT - 1) / (16 * CT)), b.n_obj);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  hipLaunchKernelGGL((posterior_tile_kernel<RMAX, CT, DP, 0, ABL>), grid, dim3(512), 0, 0, b.a, b.Xc, b.N, b.mu, b.var);
+  CK(hipEventRecord(e0));
+  for (int i = 0; i < reps; ++i)
+    hipLaunchKernelGGL((posterior_tile_kernel<RMAX, CT, DP, 0, ABL>), grid, dim3(512), 0, 0, b.a, b.Xc, b.N, b.mu,
+                       b.var);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
+  return ms / reps;
+}
+
+template <int CT, int ABL, int DP = 6>
+float run_small(const Bench& b, int reps) {
+  const int64_t nblk = (b.N + 16 * CT - 1) / (16 * CT);
+  dim3 grid((unsigned)std::min<int64_t>(nblk, 512 / b.n_obj), b.n_obj);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  hipLaunchKernelGGL((posterior_small_kernel<CT, DP, 0, ABL>), grid, dim3(512), 0, 0, b.a, b.Xc, b.N, b.mu, b.var);
+  CK(hipEventRecord(e0));
+  for (int i = 0; i < reps; ++i)
+    hipLaunchKernelGGL((posterior_small_kernel<CT, DP, 0, ABL>), grid, dim3(512), 0, 0, b.a, b.Xc, b.N, b.mu, b.var);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
+  return ms / reps;
+}
+
 // Accuracy of the table-driven Matern transforms against a long-double host reference.
 __global__ void matern_acc_kernel(const double* r2, int M, ExpCoef ec, double* out) {
   __shared__ double t64[64], t256[256];
@@ -137,6 +177,7 @@ int main(int argc, char** argv) {
   b.a.d = d;
   b.a.DP = DP;
   b.a.ec = exp_coef();
+  b.a.spin_limit = kDefaultSpinLimit;
   b.Xc = Xc;
   b.N = N;
   b.n_obj = n_obj;
@@ -179,6 +220,23 @@ int main(int argc, char** argv) {
       {"no sigma_f^2 mul (256)", run<4, 4, 8, 256>},
   };
   // n ≤ 256 (configs 2 and 4): the library launches RT = 2 (n ≤ 256) or 1 (n ≤ 128), CT = 4, barrier pipeline
+  const Variant small128[] = {
+      {"persistent CT4 (library n<=128)", run_small<4, 0>},
+      {"persistent CT4 gen only (2)", run_small<4, 2>},
+      {"tile RMAX8 CT4 (library, d>8)", run_tile<8, 4, 0>},
+      {"RT1 CT4 barrier (r01 library)", run<1, 4, 8, 32>},
+      {"tile RMAX8 CT4 gen only (2)", run_tile<8, 4, 2>},
+      {"tile RMAX8 CT4 const A (4)", run_tile<8, 4, 4>},
+      {"tile RMAX16 CT2", run_tile<16, 2, 0>},
+      {"RT1 CT2 counter ring", run<1, 2, 8, 0>},
+  };
+  const Variant small256[] = {
+      {"tile RMAX16 CT2 (library n<=256)", run_tile<16, 2, 0>},
+      {"RT2 CT2 counter ring (r01 library)", run<2, 2, 8, 0>},
+      {"tile RMAX16 CT2 gen only (2)", run_tile<16, 2, 2>},
+      {"tile RMAX16 CT2 const A (4)", run_tile<16, 2, 4>},
+      {"RT2 CT4 barrier", run<2, 4, 8, 32>},
+  };
   const Variant small[] = {
       {"RT2 CT4 barrier (library n<=256)", run<2, 4, 8, 32>},
       {"RT2 CT4 counter ring", run<2, 4, 8, 0>},
@@ -193,8 +251,10 @@ int main(int argc, char** argv) {
   };
   matern_accuracy();
   const bool is_small = d == 6 && n <= 256;
-  const Variant* vs = is_small ? small : (d == 6 ? narrow : wide);
-  const int NV = is_small ? (int)(sizeof(small) / sizeof(small[0]))
+  (void)small;
+  const Variant* vs = is_small ? (n <= 128 ? small128 : small256) : (d == 6 ? narrow : wide);
+  const int NV = is_small ? (n <= 128 ? (int)(sizeof(small128) / sizeof(small128[0]))
+                                      : (int)(sizeof(small256) / sizeof(small256[0])))
                           : (d == 6 ? (int)(sizeof(narrow) / sizeof(narrow[0])) : (int)(sizeof(wide) / sizeof(wide[0])));
   std::vector<float> t(NV, 0.f);
   for (int round = 0; round < 3; ++round)

@@ -1,14 +1,17 @@
 #!/bin/bash
-# Collect PMC counters for the bench workload, one counter group per rocprofv3 pass
-# (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950).  Run from the repo root on the GPU box.
+# Collect PMC counters for a bench workload, one counter group per rocprofv3 pass (FETCH_SIZE and
+# WRITE_SIZE cannot share a pass on gfx950; each pass stays within the per-block counter limits).
+# Run from the repo root on the GPU box:  PMC_BENCH_ARGS="--config 2" bash tools/pmc_run.sh gpurun_out/pmc_c2
 set -e
 OUT=${1:-gpurun_out/pmc}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 ARGS="bench.py --steps 3 --warmup 1 --no-cpu-baseline ${PMC_BENCH_ARGS:-}"
 i=0
-for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "TCC_HIT_sum TCC_MISS_sum"; do
+for grp in "FETCH_SIZE" "WRITE_SIZE" \
+           "SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE" \
+           "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp -d "$GRAFT_REPO_ROOT/$OUT" -o pass$i --output-format csv -- python3 $ARGS > "$OUT/pass$i.log" 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc $grp -d "$GRAFT_REPO_ROOT/$OUT" -o pass$i --output-format csv -- python3 $ARGS > "$OUT/pass$i.log" 2>&1
 done
 echo done

@@ -285,6 +285,23 @@ def run_thompson(args, cfg, world_size, rank, device, backend):
     ctx.close()
 
 
+def reference_cpu(config):
+    """The reference's own per-candidate path timed in the build container (tools/ref_cpu_baseline.py,
+    committed as profiles/r02_ref_cpu_baseline.jsonl): 1 thread, as differential_evolution calls it."""
+    path = os.path.join(REPO, "profiles", "r02_ref_cpu_baseline.jsonl")
+    try:
+        with open(path) as f:
+            recs = [json.loads(line) for line in f if line.strip()]
+    except (OSError, ValueError):
+        return None
+    for r in recs:
+        if r.get("config") == config:
+            return {"value": r["value"], "unit": r["unit"], "cores": r["cores"], "kind": "reference",
+                    "what": r["what"], "measured_in": "build container (8 vCPU Xeon), tools/ref_cpu_baseline.py",
+                    "source": "profiles/r02_ref_cpu_baseline.jsonl"}
+    return None
+
+
 def load_traffic(n, N, kernel="posterior"):
     """HBM bytes per launch of the posterior ("posterior") or K-block ("kblock") kernel from the
     committed rocprofv3 PMC summary (profiles/traffic.json, tools/pmc_summary.py), if present."""
@@ -470,7 +487,7 @@ def main():
         ctx.kernel_block(0, Xc, out=K)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        reps = 5
+        reps = 20
         e0.record()
         for _ in range(reps):
             ctx.kernel_block(0, Xc, out=K)
@@ -554,6 +571,7 @@ def main():
             "roofline": roofline,
             "roofline_kblock": kblock,
             "cpu_baseline": cpu,
+            "reference_cpu_per_candidate": reference_cpu(args.config),
             "chain": args.chain,
             "stage_ms": stage_ms,
             "state_install_ms": state_ms,

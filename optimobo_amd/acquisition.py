@@ -137,15 +137,58 @@ class AcquisitionEngine:
         self.ctx.plan_ei_ext("constrained", self.n_obj, float(best), float(var_eps), float(pof_eps))
 
     # ------------------------------------------------------------------ maximiser
-    def maximise(self, acq_fn, lower, upper, n_candidates=1 << 16, seed=0, refine_rounds=2, shrink=0.1):
+    def score(self, acq_fn, X):
+        """Acquisition values at host points X (m, d) → numpy (m,); NaN reads as −inf."""
+        Xd = self._dev(np.atleast_2d(X))
+        v = (self.ctx.eval(Xd) if acq_fn is None else acq_fn(Xd)).cpu().numpy().astype(np.float64)
+        return np.where(np.isnan(v), -np.inf, v)
+
+    def polish(self, acq_fn, x0, v0, lower, upper, maxiter=100):
+        """Local L-BFGS-B finish from (x0, v0) — what ``differential_evolution(polish=True)`` does to its
+        best member (scipy's default; optimisers.py:87,118 use it).  The objective and its central-
+        difference gradient come from ONE batched device evaluation of the (2d+1)-point stencil per
+        L-BFGS-B step (one-sided at the bounds).  Keeps x0 unless the polished point scores higher."""
+        from scipy.optimize import minimize
+        lower = np.asarray(lower, np.float64)
+        upper = np.asarray(upper, np.float64)
+        d = lower.size
+        h = 1e-6 * np.maximum(upper - lower, 1e-12)
+
+        def fg(x):
+            x = np.clip(x, lower, upper)
+            P = np.repeat(x[None, :], 2 * d + 1, axis=0)
+            for j in range(d):
+                P[1 + 2 * j, j] = min(x[j] + h[j], upper[j])
+                P[2 + 2 * j, j] = max(x[j] - h[j], lower[j])
+            v = self.score(acq_fn, P)
+            if not np.isfinite(v[0]):
+                return np.inf, np.zeros(d)
+            g = np.zeros(d)
+            for j in range(d):
+                a, b = v[1 + 2 * j], v[2 + 2 * j]
+                step = P[1 + 2 * j, j] - P[2 + 2 * j, j]
+                if np.isfinite(a) and np.isfinite(b) and step > 0:
+                    g[j] = (a - b) / step
+            return -v[0], -g
+
+        res = minimize(fg, np.asarray(x0, np.float64), jac=True, method="L-BFGS-B",
+                       bounds=list(zip(lower, upper)), options={"maxiter": int(maxiter)})
+        x1 = np.clip(res.x, lower, upper)
+        v1 = float(self.score(acq_fn, x1[None, :])[0])
+        return (x1, v1) if v1 > v0 else (np.asarray(x0, np.float64), float(v0))
+
+    def maximise(self, acq_fn, lower, upper, n_candidates=1 << 16, seed=0, refine_rounds=2, shrink=0.1,
+                 polish=True):
         """Arg-max of the acquisition over [lower, upper]^d.
 
         ``acq_fn`` is None for the current plan (fused chain, one C call per batch) or a callable
         ``acq_fn(Xc_tensor (N, d)) -> (N,) tensor``.  Round 0 scores the first ``n_candidates``
         points of a scrambled Sobol sequence generated on the device (seeded, so every rank sees
         the same sequence and owns one contiguous shard).  Each refinement round re-centres a box
-        ``shrink`` times smaller on the incumbent and keeps it if it improves — a batched
-        stand-in for DE's final polish.  Returns (x_best (d,), value).
+        ``shrink`` times smaller on the incumbent and keeps it if it improves.  ``polish`` then
+        finishes with L-BFGS-B from the incumbent, as scipy's differential_evolution does by
+        default (``polish``); with several ranks rank 0 polishes and broadcasts the point.
+        Returns (x_best (d,), value).
         """
         lower = np.asarray(lower, np.float64)
         upper = np.asarray(upper, np.float64)
@@ -173,6 +216,16 @@ class AcquisitionEngine:
         if best_x is None:   # every candidate was NaN/−inf: fall back to the first Sobol point
             self.ctx.set_sobol(d, lower, upper, seed=seed)
             best_x = self.ctx.sobol(0, 1).cpu().numpy()[0]
+            return best_x, best_v
+        if polish:
+            if W == 1:
+                best_x, best_v = self.polish(acq_fn, best_x, best_v, lower, upper)
+            else:
+                box = [None]
+                if rank == 0:
+                    box[0] = self.polish(acq_fn, best_x, best_v, lower, upper)
+                torch.distributed.broadcast_object_list(box, src=0)
+                best_x, best_v = np.asarray(box[0][0], np.float64), float(box[0][1])
         return best_x, best_v
 
 

@@ -945,225 +945,18 @@ __global__ __launch_bounds__(512, 2) void posterior_tile_kernel(GPArgs args, con
   }
 }
 
-// ----------------------------------------------------------------------------- posterior, n ≤ 128, persistent
-// BASELINE config 2 (n = 128, 2^16 candidates): here generating K* costs as much as multiplying it
-// (tile kernel at n = 128: 77 µs whole, 35 µs generation alone), and most of the generation time was
-// latency — candidate loads at workgroup start, the training rows and α fetched from L2 per tile, the
-// exp table refilled per workgroup.  This variant keeps two workgroups per CU resident for the whole
-// launch: each stages the training rows (fragment-packed), α and the exp table in LDS once, then
-// loops over candidate blocks; the next block's candidate coordinates are loaded while the current
-// block multiplies, so generation reads only LDS and registers.  Per block: generate (VALU + r² MFMA)
-// → barrier → multiply (balanced as in posterior_tile_kernel) + partial sums → barrier → 64 outputs.
-// LDS: 64 KiB K* + Xf + α + table + reduction scratch ≈ 78 KiB (n_var ≤ 8).
-template <int CT, int DP, int KIND, int ABL = 0>
-__global__ __launch_bounds__(512, 2) void posterior_small_kernel(GPArgs args, const double* __restrict__ Xc,
-                                                                 int64_t N, double* __restrict__ mu_out,
-                                                                 double* __restrict__ var_out) {
-  constexpr int RMAX = 8;                            // n ≤ 128
-  constexpr int NW = 8, NT = 512;
-  constexpr int BN = 16 * CT;
-  constexpr int TILE = 4 * RMAX * CT * 64;
-  static_assert(DP <= 8, "the persistent variant keeps candidate coordinates in registers (n_var <= 8)");
-  constexpr int KSD = (DP + 5) / 4;                  // augmented r² MFMA k-steps
-  constexpr int KSDP = (KSD + 1) / 2;
-  constexpr bool kTab256 = KIND == OMB_KERNEL_MATERN52;
-  constexpr int kTabN = kTab256 ? 256 : 64;
-  constexpr int GT = RMAX * CT / NW;
-  constexpr int CPW = CT / 2;
-  constexpr int XF = RMAX * KSDP * 128;              // doubles of the packed training rows
-  static_assert(CT % 2 == 0 && NW % CT == 0 && GT >= 1, "tile shape");
-  __shared__ double kbuf[TILE + XF + 16 * RMAX + kTabN + 4 * BN + NW * 16];
-  double* xf = kbuf + TILE;
-  double* al = xf + XF;
-  double* etab = al + 16 * RMAX;
-  double* red = etab + kTabN;                        // [4 SIMDs][BN]
-  double* redmu = red + 4 * BN;                      // [NW waves][16]
-
-  const int obj = blockIdx.y;
-  const GPDev g = args.gp[obj];
-  const int d = args.d;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t nblk = (N + BN - 1) / BN;
-  int64_t b = blockIdx.x;
-  if (b >= nblk) return;                             // workgroup-uniform
-
-  for (int i = tid; i < kTabN; i += NT) etab[i] = kTab256 ? kExp2Tab256[i] : kExp2Tab64[i];
-  for (int i = tid; i < g.R * KSDP * 128; i += NT) xf[i] = g.Xf[i];
-  for (int i = tid; i < 16 * RMAX; i += NT) al[i] = (i < 16 * g.R) ? g.alpha[i] : 0.0;
-
-  const int ct_g = wave % CT;
-  const int simd = wave & 3, h = wave >> 2;
-  // this lane's candidate coordinates for block bb (raw, loaded one block ahead)
-  double xr[DP];
-  auto load_cand = [&](int64_t bb) {
-    const int64_t ci = min(bb * BN + 16 * ct_g + (lane & 15), N - 1);
-#pragma unroll
-    for (int j = 0; j < DP; ++j) xr[j] = (j < d) ? Xc[ci * d + j] : 0.0;
-  };
-  double bfr[KSD];
-  auto make_bfr = [&]() {
-    double csq = 0.0;
-    double cs[DP];
-#pragma unroll
-    for (int j = 0; j < DP; ++j) {
-      // x*/ℓ by division, as GPy and the other kernels do (bit-identical K*)
-      cs[j] = (j < d) ? xr[j] / g.ls[j] : 0.0;
-      csq = fma(cs[j], cs[j], csq);
-    }
-#pragma unroll
-    for (int s = 0; s < KSD; ++s) {
-      const int j = 4 * s + (lane >> 4);
-      double v = 0.0;
-#pragma unroll
-      for (int jj = 0; jj < DP; ++jj) v = (jj == j) ? cs[jj] : v;    // static register select
-      bfr[s] = (j < d) ? -2.0 * v : (j == d ? 1.0 : (j == d + 1 ? csq : 0.0));
-    }
-  };
-  load_cand(b);
-  make_bfr();
-  const double pm[3] = {g.variance, kSqrt5 * g.variance, kFiveThirds * g.variance};
-  __syncthreads();
-
-  for (; b < nblk; b += gridDim.x) {
-    const int64_t c0 = b * BN;
-    // ---- generate the whole K* tile of this block from LDS and registers
-    double mu_part = 0.0;
-#pragma unroll
-    for (int i = 0; i < GT; ++i) {
-      const int T = wave / CT + (NW / CT) * i;
-      if (T < g.R) {
-        const d2* xa = reinterpret_cast<const d2*>(xf + T * (KSDP * 128) + 2 * lane);
-        d2 a[KSDP];
-#pragma unroll
-        for (int p = 0; p < KSDP; ++p) a[p] = xa[64 * p];
-        d4 cr = d4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int s = 0; s < KSD; ++s)
-          cr = __builtin_amdgcn_mfma_f64_16x16x4f64((s & 1) ? a[s >> 1].y : a[s >> 1].x, bfr[s], cr, 0, 0, 0);
-#pragma unroll
-        for (int e = 0; e < 4; e += 2) {
-          const int k0 = 16 * T + 4 * e + (lane >> 4), k1 = k0 + 4;
-          double v0, v1;
-          if constexpr (kTab256)
-            matern_r2_tab256_x2(cr[e], cr[e + 1], pm, args.ec, etab, v0, v1);
-          else
-            kernel_of_r2_tab_x2<KIND>(cr[e], cr[e + 1], pm, args.ec, etab, v0, v1);
-          mu_part = fma(al[k0], v0, mu_part);
-          mu_part = fma(al[k1], v1, mu_part);
-          kbuf[((4 * T + e) * CT + ct_g) * 64 + lane] = v0;
-          kbuf[((4 * T + e + 1) * CT + ct_g) * 64 + lane] = v1;
-        }
-      }
-    }
-    __syncthreads();                                  // A: the tile is complete
-    const int64_t bn = b + gridDim.x;
-    if (bn < nblk) load_cand(bn);                     // in flight during the multiply
-
-    // ---- V = L⁻¹ K*, SIMD s: row tiles s and 7 − s, wave h: candidate tiles h·CPW ..
-    d4 acc[2][CPW];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int c = 0; c < CPW; ++c) acc[j][c] = d4{0.0, 0.0, 0.0, 0.0};
-    if constexpr (!(ABL & 2)) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int r = j ? RMAX - 1 - simd : simd;
-        if (r >= g.R) continue;
-        const int nP = 2 * (r + 1);
-        const d2* A = reinterpret_cast<const d2*>(g.Lp + 128ll * r * (r + 1)) + lane;
-        auto ld = [&](int P) -> d2 { return A[64 * min(P, nP - 1)]; };
-        d2 a0 = ld(0), a1 = ld(1), n0 = ld(2), n1 = ld(3);
-        for (int P = 0; P < nP; P += 2) {
-          const d2 f0 = ld(P + 4), f1 = ld(P + 5);
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            const d2 a = u ? a1 : a0;
-            const int S = 2 * (P + u);
-            double b0[CPW], b1[CPW];
-#pragma unroll
-            for (int c = 0; c < CPW; ++c) {
-              b0[c] = kbuf[(S * CT + h * CPW + c) * 64 + lane];
-              b1[c] = kbuf[((S + 1) * CT + h * CPW + c) * 64 + lane];
-            }
-#pragma unroll
-            for (int c = 0; c < CPW; ++c) {
-              acc[j][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(a.x, b0[c], acc[j][c], 0, 0, 0);
-              acc[j][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(a.y, b1[c], acc[j][c], 0, 0, 0);
-            }
-          }
-          a0 = n0; a1 = n1; n0 = f0; n1 = f1;
-        }
-      }
-    }
-    double part[CPW];
-#pragma unroll
-    for (int c = 0; c < CPW; ++c) {
-      double s = 0.0;
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) s = fma(acc[j][c][i], acc[j][c][i], s);
-      s += __shfl_xor(s, 16);
-      s += __shfl_xor(s, 32);
-      part[c] = s;
-    }
-    double mp = mu_part;
-    mp += __shfl_xor(mp, 16);
-    mp += __shfl_xor(mp, 32);
-    if (lane < 16) {
-#pragma unroll
-      for (int c = 0; c < CPW; ++c) red[simd * BN + (h * CPW + c) * 16 + lane] = part[c];
-      redmu[wave * 16 + lane] = mp;
-    }
-    __syncthreads();                                  // B: partials complete, K* free
-    if (tid < BN) {
-      const double s = ((red[tid] + red[BN + tid]) + red[2 * BN + tid]) + red[3 * BN + tid];
-      double m = 0.0;
-      for (int w = tid >> 4; w < NW; w += CT) m += redmu[w * 16 + (tid & 15)];
-      const int64_t c = c0 + tid;
-      if (c < N) {
-        mu_out[(int64_t)obj * N + c] = m;
-        var_out[(int64_t)obj * N + c] = g.variance - s;
-      }
-    }
-    if (bn < nblk) make_bfr();
-  }
-}
-
 // ----------------------------------------------------------------------------- dispatch
-// Compute units of the current device (cached per device).
-static int cu_count() {
-  static int cached[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (!cached[dev]) {
-    int v = 0;
-    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
-    cached[dev] = v;
-  }
-  return cached[dev];
-}
-
 template <int DP, int KIND>
 static hipError_t launch_posterior_dp(hipStream_t stream, const GPArgs& args, int n_obj, int max_R,
                                       const double* Xc, int64_t N, double* mu, double* var) {
   const int Q = (max_R + 3) / 4;
   const int RTneed = (Q + 1) / 2;
   if (RTneed <= 1) {
-    const int64_t nblk = (N + 63) / 64;
-    if constexpr (DP <= 8) {
-      // n ≤ 128, n_var ≤ 8: two persistent workgroups per CU loop over 64-candidate blocks
-      // (tools/ablate at n = 128, 2 objectives, 2^16 candidates: see DESIGN.md §4)
-      const int64_t per_obj = std::max<int64_t>(1, (2 * (int64_t)cu_count()) / n_obj);
-      dim3 grid((unsigned)std::min<int64_t>(nblk, per_obj), n_obj);
-      hipLaunchKernelGGL((posterior_small_kernel<4, DP, KIND>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var);
-    } else {
-      // n ≤ 128, wide inputs: the whole 128 × 64 K* tile in LDS, one barrier, balanced multiply
-      dim3 grid((unsigned)nblk, n_obj);
-      hipLaunchKernelGGL((posterior_tile_kernel<8, 4, DP, KIND>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var);
-    }
+    // n ≤ 128: the whole 128 × 64 K* tile in LDS, one barrier, balanced multiply (tools/ablate at
+    // n = 128, 2 objectives, 2^16 candidates: 0.083 ms for the r01 chunk pipeline → 0.074 ms;
+    // profiles/r02_v11_ablate_c2.txt)
+    dim3 grid((unsigned)((N + 63) / 64), n_obj);
+    hipLaunchKernelGGL((posterior_tile_kernel<8, 4, DP, KIND>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var);
   } else if (RTneed <= 2) {
     // 128 < n ≤ 256: 32-candidate blocks on the counter ring (48 KiB, several workgroups per CU);
     // tools/ablate at n = 256, 3 objectives, 2^17 candidates: 0.709 ms (CT 4, barrier) → 0.641 ms;

@@ -218,6 +218,57 @@ def make_ehvi3d_pos(rng, uf, seed=1):
                         cache_seed=np.int64(seed))
 
 
+def make_de_proposals(opt_mod, uf, sc):
+    """The reference's maximiser on fixed surrogates: ``MultiSurrogateOptimiser._get_proposed_EHVI``
+    (optimisers.py:91-119) and ``_get_proposed_scalarisation`` (:62-88), i.e. scipy
+    ``differential_evolution(obj, bounds)`` with its defaults (best1bin, popsize 15, tol 0.01,
+    polish=True: an L-BFGS-B finish), seeded through numpy's global state (scipy's DE draws from it
+    when no rng is given).  The fitted GPy models are the oracle's GPy restatement (oracle/gp.py),
+    duck-typed.  Stored: the surrogate data and the proposal x_DE with its acquisition value."""
+    class Prob:
+        def __init__(self, d, xl, xu):
+            self.n_var, self.n_obj = d, 2
+            self.xl, self.xu = np.asarray(xl, np.float64), np.asarray(xu, np.float64)
+
+    out = {}
+    cases = [("ehvi", 2, 20, 3), ("ehvi", 3, 40, 4), ("ehvi", 6, 64, 5), ("ehvi", 4, 30, 6),
+             ("tch", 2, 25, 7), ("tch", 5, 50, 8)]
+    for c, (kind, d, n, seed) in enumerate(cases):
+        rng = np.random.default_rng(100 + seed)
+        xl, xu = np.zeros(d), np.ones(d)
+        X = rng.uniform(0, 1, (n, d))
+        Y = zdt1(X) if d > 1 else X
+        ls = rng.uniform(0.3, 1.5, d)
+        variances = np.array([float(np.var(Y[:, o])) for o in range(2)])
+        models = [ogp.ExactGP(X, Y[:, o], ls, variances[o]) for o in range(2)]
+        opt = opt_mod.MultiSurrogateOptimiser(Prob(d, xl, xu))
+        cache = cached_samples(2, 5 if kind == "ehvi" else 3, seed=1)
+        pf = opareto.calc_pf(Y)
+        r = Y.max(0) + 0.1 * (Y.max(0) - Y.min(0))
+        np.random.seed(seed)
+        if kind == "ehvi":
+            x_de, fun = opt._get_proposed_EHVI(uf.EHVI, models, Y.min(0), r, pf, cache)
+            val = float(np.asarray(uf.EHVI(x_de, models, r, pf, cache)).reshape(-1)[0])
+            extra = {}
+        else:
+            tch = sc.Tchebicheff(Y.min(0), Y.max(0))
+            w = np.array([0.4, 0.6])
+            agg_min = float(np.min([tch(y, w) for y in Y]))
+            x_de, fun, _ = opt._get_proposed_scalarisation(uf.expected_decomposition, models, agg_min, tch, w, cache)
+            val = float(uf.expected_decomposition(x_de, models, w, tch, agg_min, cache))
+            extra = {"w": w, "agg_min": np.float64(agg_min), "ideal": Y.min(0), "max": Y.max(0)}
+        key = f"c{c}"
+        out.update({f"{key}_kind": np.array(kind), f"{key}_X": X, f"{key}_Y": Y, f"{key}_ls": ls,
+                    f"{key}_variances": variances, f"{key}_pf": pf, f"{key}_r": r, f"{key}_cache": cache,
+                    f"{key}_xl": xl, f"{key}_xu": xu, f"{key}_x_de": np.asarray(x_de, np.float64),
+                    f"{key}_fun_de": np.float64(fun), f"{key}_value_de": np.float64(val),
+                    f"{key}_np_seed": np.int64(seed)})
+        out.update({f"{key}_{k}": v for k, v in extra.items()})
+        print(f"DE proposal {key} ({kind}, d={d}, n={n}): x={np.round(x_de, 4)} value={val:.6g}", flush=True)
+    out["n_cases"] = np.int64(len(cases))
+    np.savez_compressed(os.path.join(HERE, "de_proposals.npz"), **out)
+
+
 def make_ehvi3d(rng, uf):
     cache = cached_samples(3, 5, seed=0)
     pf = random_pf(rng, 12, k=3)
@@ -565,6 +616,8 @@ def main():
         make_turbo(np.random.default_rng(20261017), turbo_mod)
     if not only or "cparego" in only:
         make_cparego(np.random.default_rng(20261018), cparego_mod, sc)
+    if not only or "de" in only:
+        make_de_proposals(opt_mod, uf, sc)
     if not only or "ehvi_pos" in only:
         make_ehvi2d_pos(np.random.default_rng(20261019), uf)
         make_ehvi3d_pos(np.random.default_rng(20261020), uf)

@@ -63,26 +63,6 @@ float run_tile(const Bench& b, int reps) {
   return ms / reps;
 }
 
-template <int CT, int ABL, int DP = 6>
-float run_small(const Bench& b, int reps) {
-  const int64_t nblk = (b.N + 16 * CT - 1) / (16 * CT);
-  dim3 grid((unsigned)std::min<int64_t>(nblk, 512 / b.n_obj), b.n_obj);
-  hipEvent_t e0, e1;
-  CK(hipEventCreate(&e0));
-  CK(hipEventCreate(&e1));
-  hipLaunchKernelGGL((posterior_small_kernel<CT, DP, 0, ABL>), grid, dim3(512), 0, 0, b.a, b.Xc, b.N, b.mu, b.var);
-  CK(hipEventRecord(e0));
-  for (int i = 0; i < reps; ++i)
-    hipLaunchKernelGGL((posterior_small_kernel<CT, DP, 0, ABL>), grid, dim3(512), 0, 0, b.a, b.Xc, b.N, b.mu, b.var);
-  CK(hipEventRecord(e1));
-  CK(hipEventSynchronize(e1));
-  float ms;
-  CK(hipEventElapsedTime(&ms, e0, e1));
-  CK(hipEventDestroy(e0));
-  CK(hipEventDestroy(e1));
-  return ms / reps;
-}
-
 // Accuracy of the table-driven Matern transforms against a long-double host reference.
 __global__ void matern_acc_kernel(const double* r2, int M, ExpCoef ec, double* out) {
   __shared__ double t64[64], t256[256];
@@ -221,9 +201,7 @@ int main(int argc, char** argv) {
   };
   // n ≤ 256 (configs 2 and 4): the library launches RT = 2 (n ≤ 256) or 1 (n ≤ 128), CT = 4, barrier pipeline
   const Variant small128[] = {
-      {"persistent CT4 (library n<=128)", run_small<4, 0>},
-      {"persistent CT4 gen only (2)", run_small<4, 2>},
-      {"tile RMAX8 CT4 (library, d>8)", run_tile<8, 4, 0>},
+      {"tile RMAX8 CT4 (library n<=128)", run_tile<8, 4, 0>},
       {"RT1 CT4 barrier (r01 library)", run<1, 4, 8, 32>},
       {"tile RMAX8 CT4 gen only (2)", run_tile<8, 4, 2>},
       {"tile RMAX8 CT4 const A (4)", run_tile<8, 4, 4>},

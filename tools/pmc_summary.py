@@ -38,7 +38,7 @@ def main():
         with open(out) as fh:
             res = json.load(fh)
     for kern in kernels:
-        if ("posterior_kernel" not in kern) and ("kernel_block" not in kern):
+        if ("posterior" not in kern) and ("kernel_block" not in kern):
             continue
         f = m.get((kern, "FETCH_SIZE"), 0.0) * 1024
         w = m.get((kern, "WRITE_SIZE"), 0.0) * 1024
@@ -60,7 +60,7 @@ def main():
             entry["valu_busy_frac_per_cu"] = valu / 256 / (gui / 8)
         if wcyc and gui:
             entry["occupancy_frac"] = 4 * wcyc / (gui / 8) / 256 / 32
-        if "posterior_kernel" in kern:
+        if "posterior" in kern:
             res[f"posterior_n{n}_N{N}"] = entry
         else:
             entry["algorithmic_bytes"] = 8.0 * (n + d) * N + 8.0 * n * (d + 1)

@@ -169,6 +169,17 @@ def _device_available():
 
 
 # ----------------------------------------------------------------------------- GPRegression
+def _logexp(p):
+    """GPy's Logexp transform θ = log(1 + e^p) (stable for large |p|), floored away from 0."""
+    return np.maximum(np.logaddexp(0.0, np.asarray(p, np.float64)), 1e-300)
+
+
+def _logexp_inv(theta):
+    """p = log(e^θ − 1) (GPy Logexp.finv), stable for large θ."""
+    th = np.asarray(theta, np.float64)
+    return np.where(th > 36.0, th, np.log(np.expm1(np.minimum(th, 36.0))))
+
+
 class _Noise:
     def __init__(self):
         self.variance = _Param(1.0)
@@ -268,13 +279,25 @@ class GPRegression:
         return -lml, -np.asarray(g)
 
     def optimize(self, messages=False, max_f_eval=1000, max_iters=None):
-        theta0 = self._get_free()
-        bounds = [(np.log(1e-10), np.log(1e10))] * len(theta0)
+        """GPy model.optimize (optimisers.py:231): L-BFGS-B over GPy's free parameters.
+
+        GPy constrains σ_f², ℓ (and a free noise variance) positive with its Logexp transform,
+        θ = log(1 + e^p), and runs L-BFGS-B on p without bounds; this does the same, with the
+        log-marginal-likelihood gradient (taken w.r.t. log θ) carried to p by the chain factor
+        dθ/dp = 1 − e^(−θ)."""
+        theta0 = self._get_free()                       # log θ
+        p0 = _logexp_inv(np.exp(theta0))
         on_device = self.device_fit and self.Gaussian_noise.variance.fixed
-        fun = self._neg_lml_and_grad_device if on_device else self._neg_lml_and_grad
-        res = optimize.minimize(fun, theta0, jac=True, method="L-BFGS-B", bounds=bounds,
+        inner = self._neg_lml_and_grad_device if on_device else self._neg_lml_and_grad
+
+        def fun(p):
+            th = _logexp(p)
+            f, g_log = inner(np.log(th))
+            return f, g_log * (-np.expm1(-th)) / th     # ∂f/∂p = (∂f/∂log θ)/θ · (1 − e^(−θ))
+
+        res = optimize.minimize(fun, p0, jac=True, method="L-BFGS-B",
                                 options={"maxfun": int(max_f_eval), "maxiter": int(max_iters or max_f_eval)})
-        self._set_free(res.x)
+        self._set_free(np.log(_logexp(res.x)))
         return res
 
     def optimize_restarts(self, num_restarts=10, robust=True, verbose=False, **kw):

@@ -956,13 +956,14 @@ static hipError_t cov_build(omb_ctx* ctx, const ObjState& s, const double* Xc, i
 
 // In-place lower Cholesky of A + jitter·I; synchronises and returns LAPACK's info in *info.
 static int run_cholesky(omb_ctx* ctx, double* A, int64_t N, int64_t lda, double jitter, int* info) {
-  const size_t steps = (size_t)((N + 63) / 64);
-  int rc = grow_dev(ctx, &ctx->ichol, &ctx->ichol_cap, sizeof(int) * (steps + 1), "Cholesky counters");
+  // [info int | pad to 16 B | factor workspace (kCholWsDoubles)]
+  int rc = grow_dev(ctx, &ctx->ichol, &ctx->ichol_cap, 16 + sizeof(double) * kCholWsDoubles, "Cholesky workspace");
   if (rc) return rc;
   int* dinfo = static_cast<int*>(ctx->ichol);
-  OMB_HIP(ctx, hipMemsetAsync(dinfo, 0, sizeof(int) * (steps + 1), ctx->stream));
+  double* ws = reinterpret_cast<double*>(static_cast<char*>(ctx->ichol) + 16);
+  OMB_HIP(ctx, hipMemsetAsync(dinfo, 0, sizeof(int), ctx->stream));
   OMB_HIP(ctx, launch_add_diag(ctx->stream, A, N, lda, jitter));
-  OMB_HIP(ctx, launch_cholesky(ctx->stream, A, N, lda, dinfo, dinfo + 1));
+  OMB_HIP(ctx, launch_cholesky(ctx->stream, A, N, lda, dinfo, ws));
   int h = 0;
   OMB_HIP(ctx, hipMemcpyAsync(&h, dinfo, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   OMB_HIP(ctx, hipStreamSynchronize(ctx->stream));

@@ -13,12 +13,7 @@
 //                      (SYRK-shaped Σ update, Cholesky trailing update) and "op(B)(k, j) = 0 for k > j"
 //                      (a lower-triangular factor read transposed: the samples μ + L z).
 //   cand_cov_kernel    lower triangle of K(X*, X*) (GPy _unscaled_dist: diagonal forced to 0).
-//   chol_panel_kernel  one step of a blocked right-looking Cholesky: every workgroup factors the
-//                      64×64 diagonal block with its first wave (lane r keeps row r in registers,
-//                      pivots by v_readlane, multipliers by LDS broadcast), the last workgroup to finish
-//                      writes it back, and each thread solves one row of the panel below (the row in
-//                      64 registers, L_kk read from LDS as a broadcast).  The
-//                      trailing update A22 −= L21 L21ᵀ is the lower-triangle GEMM.
+//   chol_*_kernel      blocked right-looking Cholesky in 64-column steps (see "Cholesky, fused steps").
 //   select_kernel      the greedy per-sample arg-min (np.argmin order) with an LDS exclusion bitmap.
 // The factor is chol(Σ + jitter·I): numpy factors Σ by SVD instead; both draw from N(μ, Σ) up to
 // the jitter, which the caller bounds (omb_posterior_samples).
@@ -222,80 +217,150 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
-// Step `step` (columns c0 = 64·step ..) of the lower Cholesky of the N×N matrix A (row-major,
-// lower triangle read and written, upper untouched).  info (1-based column of the first
-// non-positive pivot, LAPACK dpotrf convention) is set once and stops later steps.
-// ABL (tools/ablate only; the library uses 0): bit 1 skips the diagonal factorisation (identity
-// factor), bit 2 skips the panel solve.
-// VEC: every panel row starts 16-byte aligned (even lda, aligned A): 16-byte row loads and stores.
-template <int ABL = 0, bool VEC = false>
-__global__ __launch_bounds__(256) void chol_panel_kernel(double* __restrict__ A, int64_t N, int64_t lda, int step,
-                                                         int* __restrict__ info, int* __restrict__ done_ctr) {
-  __shared__ __attribute__((aligned(16))) double LsT[kNB][kNB + 2];   // LsT[c][r] = L_kk[r][c]
-  __shared__ double rinv[kNB];
-  __shared__ __attribute__((aligned(16))) double col[kNB];
-  if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
-  const int64_t c0 = (int64_t)step * kNB;
-  const int nb = (int)((N - c0) < kNB ? (N - c0) : kNB);
-  const int tid = threadIdx.x;
-  if (tid < 64) {
-    // ---- factor the diagonal block with one wave: lane r keeps row r in 64 registers (identity
-    // rows pad a short block); column j's pivot comes by v_readlane, its multipliers through LDS.
-    const int r = tid;
-    double a[kNB];
+// ----------------------------------------------------------------------------- Cholesky, fused steps
+// The blocked factorisation as three pieces per 64-column step k (launch_cholesky):
+//   chol_trsm_kernel    the panel below the diagonal block, x · L_kkᵀ = b, one row per thread, the
+//                       factor's columns (Lt = L_kkᵀ) and 1/L_jj staged from a workspace into LDS;
+//   chol_update_kernel  the trailing update A22 −= L21 L21ᵀ (lower triangle, 64×64 MFMA tiles) whose
+//                       workgroup owning the next diagonal tile factors it right after its update
+//                       (chol64_block) and writes L_{k+1,k+1}, Lt and 1/L_jj for the next panel;
+//   chol_diag_kernel    step 0's diagonal block (nothing precedes it).
+// chol_panel_kernel factored the diagonal block redundantly in every panel workgroup with a 64-step
+// right-looking loop whose every column step updated all 63 − j remaining columns (about 18 µs of the
+// 45 µs step at N = 3000, tools/ablate/ablate_chol) and solved the panel from LDS broadcast reads
+// (about 20 µs).  chol64_block updates only the 16-column sub-block inside the column loop and the
+// trailing sub-blocks in bulk after every 16 columns (the later waves in parallel).
+
+// Factor a 64×64 SPD block with the 4 waves of a 256-thread workgroup: thread (wave w, lane r) holds
+// a[q] = A[r][16w + q] (only 16w + q ≤ r is meaningful; rows past the block are identity rows).
+// Sub-block b (columns 16b..16b+15) is factored by wave b alone — 16 column steps, each updating only
+// the rest of the sub-block — and published to LDS (Lb[b]: 64 rows × 16); then every later wave
+// subtracts its contribution from its own columns in bulk (L[r][16w+q] −= Σ_j L[r][j] L[16w+q][j]).
+// The serial chain is 64 short column steps plus three 256-fma bulk updates, and a thread keeps 16
+// values, not a 64-value row (the trailing-update kernel that hosts it stays at its occupancy).
+// On return a[q] = L[r][16w+q], my_inv = 1/L[r][r] on the thread with 16w ≤ r < 16w+16 (else 1),
+// bad = 1-based first non-positive pivot column or 0 (valid on every thread).
+// LDS: col (4 × 64), Lb (4 × 64 × 16); the caller synchronises before reusing them.
+__device__ __forceinline__ void chol64_block(double (&a)[16], int w, int r, double* col, double* Lb, double& my_inv,
+                                             int* bad_lds) {
+  my_inv = 1.0;
+  int bad = 0;
+  static_for<0, 4>([&](auto bc) {
+    constexpr int b = decltype(bc)::value;
+    if (w == b) {
+      double* cw = col + 64 * b;
+      static_for<0, 16>([&](auto jc) {
+        constexpr int jj = decltype(jc)::value;
+        constexpr int j = 16 * b + jj;
+        double dj = readlane_f64(a[jj], j);            // pivot (wave-uniform)
+        if (!(dj > 0.0)) {
+          if (bad == 0) bad = j + 1;
+          dj = 1.0;                                    // continue without NaNs; flagged
+        }
+        const double y0 = __builtin_amdgcn_rsq(dj);
+        const double hd = 0.5 * dj;
+        const double y1 = fma(y0, fma(-hd * y0, y0, 0.5), y0);
+        const double inv = fma(y1, fma(-hd * y1, y1, 0.5), y1);
+        if (r == j) my_inv = inv;
+        const double lrj = (r > j) ? a[jj] * inv : (r == j ? dj * inv : 0.0);
+        a[jj] = lrj;
+        if constexpr (jj < 15) {
+          cw[r] = lrj;                                 // column j to every lane of the wave
+          __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int c = 0; c < kNB; ++c) {
-      double v = (c == r) ? 1.0 : 0.0;
-      if (r < nb && c <= r) v = A[(c0 + r) * lda + c0 + c];
-      a[c] = v;
+          for (int q = jj + 1; q < 16; ++q) a[q] = fma(-lrj, cw[16 * b + q], a[q]);
+          __builtin_amdgcn_wave_barrier();
+        }
+      });
+#pragma unroll
+      for (int q = 0; q < 16; ++q) Lb[(b * 64 + r) * 16 + q] = a[q];
+      if (r == 0 && bad) bad_lds[0] = bad;
     }
-    int bad = 0;
-    double my_inv = 1.0;
-    static_for<0, ((ABL & 1) ? 0 : kNB)>([&](auto jc) {
-      constexpr int j = decltype(jc)::value;
-      double dj = readlane_f64(a[j], j);               // pivot (wave-uniform)
-      if (!(dj > 0.0)) {
-        if (bad == 0) bad = j + 1;
-        dj = 1.0;                                      // continue without NaNs; flagged
+    __syncthreads();
+    if constexpr (b < 3) {
+      if (w > b) {
+        // own row's sub-block-b values, then one dot product per owned column
+        const double2* mine = reinterpret_cast<const double2*>(Lb + (b * 64 + r) * 16);
+        double lr[16];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const double2 v = mine[q];
+          lr[2 * q] = v.x;
+          lr[2 * q + 1] = v.y;
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const double2* other = reinterpret_cast<const double2*>(Lb + (b * 64 + 16 * w + q) * 16);
+          double s = 0.0;
+#pragma unroll
+          for (int h = 0; h < 8; ++h) {
+            const double2 v = other[h];
+            s = fma(lr[2 * h], v.x, s);
+            s = fma(lr[2 * h + 1], v.y, s);
+          }
+          a[q] -= s;
+        }
       }
-      // 1/sqrt(d) by v_rsq_f64 and two Newton steps (y ← y + y·(½ − ½ d y²)), then sqrt(d) = d·y:
-      // the shortest dependent chain for both (the column step is latency-bound)
-      const double y0 = __builtin_amdgcn_rsq(dj);
-      const double hd = 0.5 * dj;
-      const double y1 = fma(y0, fma(-hd * y0, y0, 0.5), y0);
-      const double inv = fma(y1, fma(-hd * y1, y1, 0.5), y1);
-      const double ljj = dj * inv;
-      if (r == j) my_inv = inv;
-      const double lrj = (r > j) ? a[j] * inv : (r == j ? ljj : 0.0);
-      a[j] = lrj;
-      // column j to every lane through LDS (one store, then same-address broadcast reads; the
-      // wave's LDS accesses complete in order).  The update runs on every row unmasked: entries
-      // above the diagonal (k > r) collect junk that nothing reads.
-      col[r] = lrj;
-      __builtin_amdgcn_wave_barrier();
-      axpy_tail<j>(a, -lrj, col);
-      __builtin_amdgcn_wave_barrier();
-    });
-#pragma unroll
-    for (int c = 0; c < kNB; ++c) LsT[c][r] = a[c];
-    rinv[r] = my_inv;
-    // the last workgroup to finish factoring writes L_kk back: every other one has consumed its
-    // loads of A_kk by then (they fed the factorization before its counter increment)
-    int old = 0;
-    if (r == 0) old = atomicAdd(done_ctr + step, 1);
-    if (__builtin_amdgcn_readfirstlane(old) == (int)gridDim.x - 1) {
-      if (r < nb)
-        for (int c = 0; c <= r; ++c) A[(c0 + r) * lda + c0 + c] = LsT[c][r];
-      if (r == 0 && bad) atomicCAS(info, 0, (int)(c0 + bad));
     }
+  });
+}
+
+// Writes the factored block (threads (w, r), rows r < nb of block c0) back into A's lower triangle,
+// its transpose Lt (row j = column j of L) and 1/L_jj into the workspace, and the first bad pivot.
+__device__ __forceinline__ void chol64_store(const double (&a)[16], int w, int r, int nb, double my_inv, int bad,
+                                             double* __restrict__ A, int64_t lda, int64_t c0,
+                                             double* __restrict__ ws, int* __restrict__ info) {
+  if (r < nb) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      if (16 * w + q <= r) A[(c0 + r) * lda + c0 + 16 * w + q] = a[q];
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) ws[(16 * w + q) * kNB + r] = a[q];
+  if (r >= 16 * w && r < 16 * w + 16) ws[kNB * kNB + r] = my_inv;
+  if (w == 0 && r == 0 && bad) atomicCAS(info, 0, (int)(c0 + bad));
+}
+
+__global__ __launch_bounds__(256) void chol_diag_kernel(double* __restrict__ A, int64_t N, int64_t lda,
+                                                         double* __restrict__ ws, int* __restrict__ info) {
+  __shared__ double col[4 * kNB];
+  __shared__ __attribute__((aligned(16))) double Lb[4 * kNB * 16];
+  __shared__ int bad_lds[1];
+  const int nb = (int)(N < kNB ? N : kNB);
+  const int r = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (threadIdx.x == 0) bad_lds[0] = 0;
+  double a[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int c = 16 * w + q;
+    double v = (c == r) ? 1.0 : 0.0;
+    if (r < nb && c <= r) v = A[(int64_t)r * lda + c];
+    a[q] = v;
   }
   __syncthreads();
-  // ---- panel: rows below the block solve x · L_kkᵀ = b (forward substitution)
-  const int64_t row = c0 + nb + (int64_t)blockIdx.x * blockDim.x + tid;
-  if ((ABL & 2) || row >= N) return;
+  double inv;
+  chol64_block(a, w, r, col, Lb, inv, bad_lds);
+  chol64_store(a, w, r, nb, inv, bad_lds[0], A, lda, 0, ws, info);
+}
+
+// Panel of step `step`: rows c0+64 .. N−1 solve x · L_kkᵀ = b by column-oriented substitution, one
+// row per thread (the row in 64 registers), the factor's columns (Lt = L_kkᵀ) staged from the
+// workspace into LDS and read as broadcasts.  (Reading them through the scalar cache instead —
+// s_load into SGPR operands of every fma — measured 33.7 µs per panel at N = 3000 against about
+// 20 µs: the loads' latency is exposed at every column step; profiles/r02_v15_chol_kernel_stats.csv.)
+template <bool VEC, int NT>
+__global__ __launch_bounds__(NT) void chol_trsm_kernel(double* __restrict__ A, int64_t N, int64_t lda, int step,
+                                                        const double* __restrict__ ws, const int* __restrict__ info) {
+  __shared__ __attribute__((aligned(16))) double LsT[kNB * kNB];   // LsT[j·64 + k] = L_kk[k][j]
+  __shared__ double rinv[kNB];
+  if (*info != 0) return;
+  for (int i = threadIdx.x; i < kNB * kNB; i += NT) LsT[i] = ws[i];
+  if (threadIdx.x < kNB) rinv[threadIdx.x] = ws[kNB * kNB + threadIdx.x];
+  __syncthreads();
+  const int64_t c0 = (int64_t)step * kNB;
+  const int64_t row = c0 + kNB + (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (row >= N) return;
   double* rp = A + row * lda + c0;
-  // rows below the block exist only while a full block remains (nb == 64): unconditional
-  // accesses keep x[] in registers (a per-column guard makes the compiler spill it)
   double x[kNB];
   if constexpr (VEC) {
 #pragma unroll
@@ -308,13 +373,11 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(double* __restrict__ A,
 #pragma unroll
     for (int c = 0; c < kNB; ++c) x[c] = rp[c];
   }
-  // column-oriented (right-looking) substitution: after x_j is final, every later x_k is updated
-  // independently — 63 independent fmas per step instead of one 2016-long dependent chain
   static_for<0, kNB>([&](auto jc) {
     constexpr int j = decltype(jc)::value;
     const double xj = x[j] * rinv[j];
     x[j] = xj;
-    axpy_tail<j>(x, -xj, LsT[j]);
+    axpy_tail<j>(x, -xj, LsT + j * kNB);
   });
   if constexpr (VEC) {
 #pragma unroll
@@ -323,6 +386,112 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(double* __restrict__ A,
 #pragma unroll
     for (int c = 0; c < kNB; ++c) rp[c] = x[c];
   }
+}
+
+// Trailing update of step `step` (A22 −= L21 L21ᵀ, lower 64×64 tiles, gemm_kernel's MFMA tiling with
+// K = 64) fused with the factorisation of the next diagonal block by the workgroup that owns it.
+__global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A, int64_t N, int64_t lda, int step,
+                                                          double* __restrict__ ws, int* __restrict__ info) {
+  if (blockIdx.x > blockIdx.y) return;                      // tile strictly above the diagonal
+  if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+  const int64_t c0 = (int64_t)step * kNB;
+  const int64_t r0 = c0 + kNB;                              // first row / column of A22
+  const int64_t M = N - r0;
+  const int64_t m0 = (int64_t)blockIdx.y * kGT, n0 = (int64_t)blockIdx.x * kGT;
+  // As and Bs are contiguous (one array) so the diagonal workgroup can reuse them as the 64 × 65
+  // staging tile D and then as the factorisation's Lb (4096 doubles of the 4224)
+  __shared__ __attribute__((aligned(16))) double ABs[2][2][kGK][kGP];
+  auto& As = ABs[0];   // As[buf][k][m] = L21(m0 + m, k0 + k)
+  auto& Bs = ABs[1];   // Bs[buf][k][n] = L21(n0 + n, k0 + k)
+  __shared__ double col[4 * kNB];
+  __shared__ int bad_lds[1];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const double* L21 = A + r0 * lda + c0;
+  double ra[4], rb[4];
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int idx = tid + 256 * e;
+      const int am = idx >> 4, ak = idx & 15;
+      ra[e] = (m0 + am < M) ? L21[(m0 + am) * lda + k0 + ak] : 0.0;
+      rb[e] = (n0 + am < M) ? L21[(n0 + am) * lda + k0 + ak] : 0.0;
+    }
+  };
+  auto stash = [&](int buf) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int idx = tid + 256 * e;
+      As[buf][idx & 15][idx >> 4] = ra[e];
+      Bs[buf][idx & 15][idx >> 4] = rb[e];
+    }
+  };
+  d4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+  fetch(0);
+  stash(0);
+  __syncthreads();
+  int buf = 0;
+#pragma unroll
+  for (int k0 = 0; k0 < kNB; k0 += kGK) {
+    const bool more = k0 + kGK < kNB;
+    if (more) fetch(k0 + kGK);
+#pragma unroll
+    for (int ks = 0; ks < kGK / 4; ++ks) {
+      const int kk = 4 * ks + (lane >> 4);
+      const double a0 = As[buf][kk][32 * wm + (lane & 15)];
+      const double a1 = As[buf][kk][32 * wm + 16 + (lane & 15)];
+      const double b0 = Bs[buf][kk][32 * wn + (lane & 15)];
+      const double b1 = Bs[buf][kk][32 * wn + 16 + (lane & 15)];
+      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    if (more) stash(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  const bool diag = (blockIdx.x == 0 && blockIdx.y == 0);  // the next diagonal block: A22's first tile
+  double* D = &As[0][0][0];                                  // 64 × 65 staging of that tile (fits As+Bs)
+  // C/D map of v_mfma_f64_16x16x4f64: col = lane & 15, row = (lane >> 4) + 4·i
+#pragma unroll
+  for (int rb2 = 0; rb2 < 2; ++rb2)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int lr = 32 * wm + 16 * rb2 + (lane >> 4) + 4 * i;
+        const int lc = 32 * wn + 16 * cb + (lane & 15);
+        const int64_t row = m0 + lr, col_g = n0 + lc;
+        if (row < M && col_g < M && col_g <= row) {
+          double* p = A + (r0 + row) * lda + r0 + col_g;
+          const double v = *p - acc[rb2][cb][i];
+          if (diag)
+            D[lr * 65 + lc] = v;
+          else
+            *p = v;
+        }
+      }
+  if (!diag) return;
+  __syncthreads();
+  const int nb = (int)(M < kNB ? M : kNB);
+  const int r = lane, w = wave;
+  double a[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int c = 16 * w + q;
+    a[q] = (r < nb && c <= r) ? D[r * 65 + c] : (c == r ? 1.0 : 0.0);
+  }
+  if (tid == 0) bad_lds[0] = 0;
+  __syncthreads();                                           // D consumed: As/Bs become Lb
+  double inv;
+  chol64_block(a, w, r, col, &As[0][0][0], inv, bad_lds);
+  chol64_store(a, w, r, nb, inv, bad_lds[0], A, lda, r0, ws, info);
 }
 
 // ----------------------------------------------------------------------------- triangular inverse
@@ -858,29 +1027,33 @@ hipError_t launch_add_diag(hipStream_t stream, double* S, int64_t N, int64_t lds
   return hipGetLastError();
 }
 
-hipError_t launch_cholesky(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, int* done_ctr) {
+#ifndef OMB_TRSM_THREADS
+#define OMB_TRSM_THREADS 64
+#endif
+constexpr int kTrsmThreads = OMB_TRSM_THREADS;   // threads per panel workgroup (tools/ablate: 64 vs 256)
+
+hipError_t launch_cholesky(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws) {
+  if (N <= 0) return hipSuccess;
   const int steps = (int)((N + kNB - 1) / kNB);
   const bool vec = (lda % 2 == 0) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
-  for (int k = 0; k < steps; ++k) {
-    const int64_t c0 = (int64_t)k * kNB;
-    const int64_t nb = (N - c0) < kNB ? (N - c0) : kNB;
-    const int64_t rest = N - c0 - nb;
-    const unsigned blocks = (unsigned)(rest > 0 ? (rest + 255) / 256 : 1);
+  hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), 0, stream, A, N, lda, ws, info);
+  hipError_t e = hipGetLastError();
+  for (int k = 0; k + 1 < steps && e == hipSuccess; ++k) {
+    const int64_t rest = N - (int64_t)(k + 1) * kNB;      // rows below the diagonal block
+    // one wave per workgroup: the broadcast reads of L_kk are per-CU LDS traffic, so spreading the
+    // panel's waves over more CUs shortens every wave's solve
+    const unsigned pblocks = (unsigned)((rest + kTrsmThreads - 1) / kTrsmThreads);
     if (vec)
-      hipLaunchKernelGGL((chol_panel_kernel<0, true>), dim3(blocks), dim3(256), 0, stream, A, N, lda, k, info, done_ctr);
+      hipLaunchKernelGGL((chol_trsm_kernel<true, kTrsmThreads>), dim3(pblocks), dim3(kTrsmThreads), 0, stream, A, N, lda, k, ws, info);
     else
-      hipLaunchKernelGGL((chol_panel_kernel<0, false>), dim3(blocks), dim3(256), 0, stream, A, N, lda, k, info, done_ctr);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    if (rest > 0) {
-      // A22 −= L21 L21ᵀ (lower triangle): op(A) = L21, op(B) = L21ᵀ
-      double* L21 = A + (c0 + nb) * lda + c0;
-      e = gemm<false, true, false, true>(stream, rest, rest, nb, -1.0, L21, lda, L21, lda, 1.0,
-                                         A + (c0 + nb) * lda + c0 + nb, lda, nullptr);
-      if (e != hipSuccess) return e;
-    }
+      hipLaunchKernelGGL((chol_trsm_kernel<false, kTrsmThreads>), dim3(pblocks), dim3(kTrsmThreads), 0, stream, A, N, lda, k, ws, info);
+    e = hipGetLastError();
+    if (e != hipSuccess) break;
+    const unsigned t = (unsigned)((rest + kGT - 1) / kGT);
+    hipLaunchKernelGGL(chol_update_kernel, dim3(t, t), dim3(256), 0, stream, A, N, lda, k, ws, info);
+    e = hipGetLastError();
   }
-  return hipSuccess;
+  return e;
 }
 
 hipError_t launch_chol_samples(hipStream_t stream, const double* L, int64_t N, int64_t ldl, const double* mu,

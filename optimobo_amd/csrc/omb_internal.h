@@ -118,8 +118,9 @@ hipError_t launch_cand_cov(hipStream_t stream, const GPDev& g, int d, int DP, co
 hipError_t launch_mirror_lower(hipStream_t stream, double* S, int64_t N, int64_t lds);
 hipError_t launch_add_diag(hipStream_t stream, double* S, int64_t N, int64_t lds, double v);
 // in-place lower Cholesky; info (device int, zeroed by the caller) = first bad column (1-based);
-// ws: kCholWsDoubles device doubles of workspace (the current diagonal block's factor).
-constexpr int kCholWsDoubles = 64 * 64 + 64;
+// ws: kCholWsDoubles device doubles of workspace (the inverse of the current diagonal block, as MFMA
+// fragments for the panel product).
+constexpr int kCholWsDoubles = 64 * 64;
 hipError_t launch_cholesky(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws);
 // Y (B, N) = μ + Zt Lᵀ (L lower, N×N): row b of Y is the sample μ + L z_b.
 hipError_t launch_chol_samples(hipStream_t stream, const double* L, int64_t N, int64_t ldl, const double* mu,

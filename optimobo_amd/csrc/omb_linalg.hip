@@ -185,6 +185,11 @@ __global__ void add_diag_kernel(double* __restrict__ S, int64_t N, int64_t lds, 
 // ----------------------------------------------------------------------------- Cholesky
 constexpr int kNB = 64;
 
+// Phase timestamps of the diagonal-block factorisation for tools/ablate/ablate_chol (empty here).
+#ifndef OMB_CHOL_TRACE
+#define OMB_CHOL_TRACE(id, cond)
+#endif
+
 __device__ __forceinline__ double readlane_f64(double v, int l) {
   const long long b = __builtin_bit_cast(long long, v);
   const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(b & 0xffffffffll), l);
@@ -218,37 +223,38 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 // ----------------------------------------------------------------------------- Cholesky, fused steps
-// The blocked factorisation as three pieces per 64-column step k (launch_cholesky):
-//   chol_trsm_kernel    the panel below the diagonal block, x · L_kkᵀ = b, one row per thread, the
-//                       factor's columns (Lt = L_kkᵀ) and 1/L_jj staged from a workspace into LDS;
+// The blocked factorisation as two kernels per 64-column step k (launch_cholesky):
+//   chol_panel_kernel   the panel below the diagonal block, L21 = A21 · W_kkᵀ with W_kk = L_kk⁻¹, on
+//                       MFMA (16 rows per 2-wave workgroup; W_kk's B fragments read from the workspace);
 //   chol_update_kernel  the trailing update A22 −= L21 L21ᵀ (lower triangle, 64×64 MFMA tiles) whose
 //                       workgroup owning the next diagonal tile factors it right after its update
-//                       (chol64_block) and writes L_{k+1,k+1}, Lt and 1/L_jj for the next panel;
+//                       (chol64_block), inverts the factor and writes L_{k+1,k+1} and the fragments of
+//                       W_{k+1,k+1} for the next panel (chol64_finish);
 //   chol_diag_kernel    step 0's diagonal block (nothing precedes it).
-// chol_panel_kernel factored the diagonal block redundantly in every panel workgroup with a 64-step
-// right-looking loop whose every column step updated all 63 − j remaining columns (about 18 µs of the
-// 45 µs step at N = 3000, tools/ablate/ablate_chol) and solved the panel from LDS broadcast reads
-// (about 20 µs).  chol64_block updates only the 16-column sub-block inside the column loop and the
-// trailing sub-blocks in bulk after every 16 columns (the later waves in parallel).
+// The serial chain of a step is the diagonal workgroup's factor + inverse.  Round 2's panel solved
+// x · L_kkᵀ = b by substitution, a 64-step dependent chain per row with an LDS broadcast read at every
+// step (29.5 µs per step at N = 3000, profiles/r02_v20_c6_top_kernels.txt), and the factor broadcast each
+// column through LDS (29.9 µs for the update kernel's diagonal workgroup).  Solving with the explicit
+// inverse of the 64×64 diagonal block is the usual GPU TRSM; its error grows with cond(L_kk), which
+// the jitter of omb_posterior_samples bounds.
 
 // Factor a 64×64 SPD block with the 4 waves of a 256-thread workgroup: thread (wave w, lane r) holds
 // a[q] = A[r][16w + q] (only 16w + q ≤ r is meaningful; rows past the block are identity rows).
 // Sub-block b (columns 16b..16b+15) is factored by wave b alone — 16 column steps, each updating only
-// the rest of the sub-block — and published to LDS (Lb[b]: 64 rows × 16); then every later wave
-// subtracts its contribution from its own columns in bulk (L[r][16w+q] −= Σ_j L[r][j] L[16w+q][j]).
-// The serial chain is 64 short column steps plus three 256-fma bulk updates, and a thread keeps 16
-// values, not a 64-value row (the trailing-update kernel that hosts it stays at its occupancy).
-// On return a[q] = L[r][16w+q], my_inv = 1/L[r][r] on the thread with 16w ≤ r < 16w+16 (else 1),
-// bad = 1-based first non-positive pivot column or 0 (valid on every thread).
-// LDS: col (4 × 64), Lb (4 × 64 × 16); the caller synchronises before reusing them.
-__device__ __forceinline__ void chol64_block(double (&a)[16], int w, int r, double* col, double* Lb, double& my_inv,
+// the rest of the sub-block, the column's entries L[16b+q][j] taken from lane 16b+q by v_readlane
+// (scalar operands of the fmas: no LDS round trip on the chain) — and published to LDS (Lb[b]: 64
+// rows × 16); then every later wave subtracts its contribution from its own columns in bulk
+// (L[r][16w+q] −= Σ_j L[r][j] L[16w+q][j]).
+// On return (after a barrier) a[q] = L[r][16w+q], Lb holds L, my_inv = 1/L[r][r] on the thread with
+// 16w ≤ r < 16w+16 (else 1), bad_lds[0] = 1-based first non-positive pivot column or 0.
+__device__ __forceinline__ void chol64_block(double (&a)[16], int w, int r, double* Lb, double& my_inv,
                                              int* bad_lds) {
   my_inv = 1.0;
   int bad = 0;
   static_for<0, 4>([&](auto bc) {
     constexpr int b = decltype(bc)::value;
     if (w == b) {
-      double* cw = col + 64 * b;
+      OMB_CHOL_TRACE(2 + 2 * b, r == 0);
       static_for<0, 16>([&](auto jc) {
         constexpr int jj = decltype(jc)::value;
         constexpr int j = 16 * b + jj;
@@ -264,14 +270,10 @@ __device__ __forceinline__ void chol64_block(double (&a)[16], int w, int r, doub
         if (r == j) my_inv = inv;
         const double lrj = (r > j) ? a[jj] * inv : (r == j ? dj * inv : 0.0);
         a[jj] = lrj;
-        if constexpr (jj < 15) {
-          cw[r] = lrj;                                 // column j to every lane of the wave
-          __builtin_amdgcn_wave_barrier();
 #pragma unroll
-          for (int q = jj + 1; q < 16; ++q) a[q] = fma(-lrj, cw[16 * b + q], a[q]);
-          __builtin_amdgcn_wave_barrier();
-        }
+        for (int q = jj + 1; q < 16; ++q) a[q] = fma(-lrj, readlane_f64(lrj, 16 * b + q), a[q]);
       });
+      OMB_CHOL_TRACE(3 + 2 * b, r == 0);
 #pragma unroll
       for (int q = 0; q < 16; ++q) Lb[(b * 64 + r) * 16 + q] = a[q];
       if (r == 0 && bad) bad_lds[0] = bad;
@@ -300,34 +302,94 @@ __device__ __forceinline__ void chol64_block(double (&a)[16], int w, int r, doub
           }
           a[q] -= s;
         }
+        OMB_CHOL_TRACE(10 + b, w == 3 && r == 0);
       }
     }
   });
 }
 
-// Writes the factored block (threads (w, r), rows r < nb of block c0) back into A's lower triangle,
-// its transpose Lt (row j = column j of L) and 1/L_jj into the workspace, and the first bad pivot.
-__device__ __forceinline__ void chol64_store(const double (&a)[16], int w, int r, int nb, double my_inv, int bad,
-                                             double* __restrict__ A, int64_t lda, int64_t c0,
-                                             double* __restrict__ ws, int* __restrict__ info) {
+// After chol64_block: writes L (rows r < nb of the block at c0) into A's lower triangle, the first bad
+// pivot into info, and W = L⁻¹ as the MFMA B fragments of chol_panel_kernel:
+//   Wf[(jb·16 + s)·64 + l] = W[16jb + (l & 15)][m(s, l >> 4)],   m(s, g) = 16(s >> 2) + 4g + (s & 3)
+// (k-step s of the panel's output column block jb; only s < 4(jb + 1) is read — the rest of that row
+// block of W is zero — so the panel skips W's upper triangle in whole k-steps).
+// Phase 1: wave i inverts its diagonal 16×16 block by column-oriented substitution (lane l → column
+// l & 15, the factor's entries by v_readlane) and leaves W_ii in place of L_ii in Lb.  Phase 2: wave j
+// forms its column block, W_ij = −W_ii Σ_{k=j}^{i−1} L_ik W_kj for i = j+1..3, on MFMA: a product's
+// accumulator layout (lane l: rows 4e + (l >> 4), column l & 15) is the next product's B operand
+// layout, so the W_kj (k > j) stay in registers and only L and the W_ii are read from LDS.
+__device__ __forceinline__ void chol64_finish(const double (&a)[16], int w, int r, int nb, double my_inv, int bad,
+                                              double* Lb, double* __restrict__ A, int64_t lda, int64_t c0,
+                                              double* __restrict__ Wf, int* __restrict__ info) {
   if (r < nb) {
 #pragma unroll
     for (int q = 0; q < 16; ++q)
       if (16 * w + q <= r) A[(c0 + r) * lda + c0 + 16 * w + q] = a[q];
   }
-#pragma unroll
-  for (int q = 0; q < 16; ++q) ws[(16 * w + q) * kNB + r] = a[q];
-  if (r >= 16 * w && r < 16 * w + 16) ws[kNB * kNB + r] = my_inv;
   if (w == 0 && r == 0 && bad) atomicCAS(info, 0, (int)(c0 + bad));
+  OMB_CHOL_TRACE(13, w == 0 && r == 0);
+  const int c = r & 15, g = r >> 4;
+  // phase 1: x[m] = W_ww[m][c]
+  double x[16];
+#pragma unroll
+  for (int m = 0; m < 16; ++m) x[m] = (m == c) ? 1.0 : 0.0;
+  static_for<0, 16>([&](auto pc) {
+    constexpr int p = decltype(pc)::value;
+    x[p] *= readlane_f64(my_inv, 16 * w + p);
+#pragma unroll
+    for (int m = p + 1; m < 16; ++m) x[m] = fma(-readlane_f64(a[p], 16 * w + m), x[p], x[m]);
+  });
+  if (r < 16) {
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      Lb[(w * 64 + 16 * w + m) * 16 + c] = x[m];
+      // W[16w + m][16w + c]: jb = w, s = 4w + (c & 3), lane m + 16 (c >> 2)
+      Wf[(w * 16 + 4 * w + (c & 3)) * 64 + m + 16 * (c >> 2)] = x[m];
+    }
+  }
+  OMB_CHOL_TRACE(14, w == 0 && r == 0);
+  __syncthreads();
+  OMB_CHOL_TRACE(15, w == 0 && r == 0);
+  // phase 2
+  d4 Wc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) Wc[i] = d4{0.0, 0.0, 0.0, 0.0};
+  static_for<1, 4>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+    if (i > w) {
+      d4 T = d4{0.0, 0.0, 0.0, 0.0};
+      static_for<0, i>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        if (k >= w) {
+          static_for<0, 4>([&](auto sc) {
+            constexpr int s = decltype(sc)::value;
+            const double av = Lb[(k * 64 + 16 * i + c) * 16 + 4 * s + g];   // L[16i + c][16k + 4s + g]
+            // B operand W_kj[4s + g][c]: W_ww from LDS (phase 1), the others from registers
+            const double bv = (k == w) ? Lb[(k * 64 + 16 * k + 4 * s + g) * 16 + c] : Wc[k][s];
+            T = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, T, 0, 0, 0);
+          });
+        }
+      });
+      d4 R = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        R = __builtin_amdgcn_mfma_f64_16x16x4f64(Lb[(i * 64 + 16 * i + c) * 16 + 4 * s + g], T[s], R, 0, 0, 0);
+      Wc[i] = -R;
+      // W[16i + 4e + g][16w + c]: jb = i, s = 4w + (c & 3), lane 4e + g + 16 (c >> 2)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Wf[(i * 16 + 4 * w + (c & 3)) * 64 + 4 * e + g + 16 * (c >> 2)] = Wc[i][e];
+    }
+  });
+  OMB_CHOL_TRACE(16, w == 0 && r == 0);
 }
 
 __global__ __launch_bounds__(256) void chol_diag_kernel(double* __restrict__ A, int64_t N, int64_t lda,
                                                          double* __restrict__ ws, int* __restrict__ info) {
-  __shared__ double col[4 * kNB];
   __shared__ __attribute__((aligned(16))) double Lb[4 * kNB * 16];
   __shared__ int bad_lds[1];
   const int nb = (int)(N < kNB ? N : kNB);
-  const int r = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  OMB_CHOL_TRACE(0, threadIdx.x == 0);
   if (threadIdx.x == 0) bad_lds[0] = 0;
   double a[16];
 #pragma unroll
@@ -338,58 +400,72 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(double* __restrict__ A, 
     a[q] = v;
   }
   __syncthreads();
+  OMB_CHOL_TRACE(1, threadIdx.x == 0);
   double inv;
-  chol64_block(a, w, r, col, Lb, inv, bad_lds);
-  chol64_store(a, w, r, nb, inv, bad_lds[0], A, lda, 0, ws, info);
+  chol64_block(a, w, r, Lb, inv, bad_lds);
+  chol64_finish(a, w, r, nb, inv, bad_lds[0], Lb, A, lda, 0, ws, info);
 }
 
-// Panel of step `step`: rows c0+64 .. N−1 solve x · L_kkᵀ = b by column-oriented substitution, one
-// row per thread (the row in 64 registers), the factor's columns (Lt = L_kkᵀ) staged from the
-// workspace into LDS and read as broadcasts.  (Reading them through the scalar cache instead —
-// s_load into SGPR operands of every fma — measured 33.7 µs per panel at N = 3000 against about
-// 20 µs: the loads' latency is exposed at every column step; profiles/r02_v15_chol_kernel_stats.csv.)
-template <bool VEC, int NT>
-__global__ __launch_bounds__(NT) void chol_trsm_kernel(double* __restrict__ A, int64_t N, int64_t lda, int step,
-                                                        const double* __restrict__ ws, const int* __restrict__ info) {
-  __shared__ __attribute__((aligned(16))) double LsT[kNB * kNB];   // LsT[j·64 + k] = L_kk[k][j]
-  __shared__ double rinv[kNB];
+// Panel of step `step`: rows c0+64 .. N−1, L21 = A21 · Wᵀ (W = L_kk⁻¹ from chol64_finish's fragments).
+// Workgroup = 16 rows, 2 waves: wave 0 the output column blocks 0 and 3, wave 1 blocks 1 and 2 (20
+// MFMAs each).  The k index is permuted as m(s, g) = 16(s >> 2) + 4g + (s & 3) so a lane's A operands
+// are 4 contiguous doubles per 16-column group; the barrier separates both waves' reads of the rows
+// from the in-place writes.
+template <bool VEC>
+__global__ __launch_bounds__(128) void chol_panel_kernel(double* __restrict__ A, int64_t N, int64_t lda, int step,
+                                                         const double* __restrict__ Wf, const int* __restrict__ info) {
   if (*info != 0) return;
-  for (int i = threadIdx.x; i < kNB * kNB; i += NT) LsT[i] = ws[i];
-  if (threadIdx.x < kNB) rinv[threadIdx.x] = ws[kNB * kNB + threadIdx.x];
-  __syncthreads();
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t c0 = (int64_t)step * kNB;
-  const int64_t row = c0 + kNB + (int64_t)blockIdx.x * NT + threadIdx.x;
-  if (row >= N) return;
-  double* rp = A + row * lda + c0;
-  double x[kNB];
-  if constexpr (VEC) {
+  const int64_t r0 = c0 + kNB + (int64_t)blockIdx.x * 16;
+  const int64_t row = r0 + c;
+  const int ngroups = wave == 0 ? 4 : 3;            // 16-column groups of A21 this wave reads
+  double x[16];                                       // x[4sg + u] = A21[row][16sg + 4g + u]
+  const double* rp = A + row * lda + c0 + 4 * g;
 #pragma unroll
-    for (int c = 0; c < kNB; c += 2) {
-      const double2 v = reinterpret_cast<const double2*>(rp)[c >> 1];
-      x[c] = v.x;
-      x[c + 1] = v.y;
+  for (int sg = 0; sg < 4; ++sg) {
+    if (sg < ngroups && row < N) {
+      if constexpr (VEC) {
+        const double2 v0 = reinterpret_cast<const double2*>(rp + 16 * sg)[0];
+        const double2 v1 = reinterpret_cast<const double2*>(rp + 16 * sg)[1];
+        x[4 * sg] = v0.x;
+        x[4 * sg + 1] = v0.y;
+        x[4 * sg + 2] = v1.x;
+        x[4 * sg + 3] = v1.y;
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) x[4 * sg + u] = rp[16 * sg + u];
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) x[4 * sg + u] = 0.0;
     }
-  } else {
-#pragma unroll
-    for (int c = 0; c < kNB; ++c) x[c] = rp[c];
   }
-  static_for<0, kNB>([&](auto jc) {
-    constexpr int j = decltype(jc)::value;
-    const double xj = x[j] * rinv[j];
-    x[j] = xj;
-    axpy_tail<j>(x, -xj, LsT + j * kNB);
-  });
-  if constexpr (VEC) {
+  d4 acc[2];
+  int jbs[2] = {wave == 0 ? 0 : 1, wave == 0 ? 3 : 2};
 #pragma unroll
-    for (int c = 0; c < kNB; c += 2) reinterpret_cast<double2*>(rp)[c >> 1] = double2{x[c], x[c + 1]};
-  } else {
+  for (int h = 0; h < 2; ++h) {
+    acc[h] = d4{0.0, 0.0, 0.0, 0.0};
+    const int jb = jbs[h];
+    const double* wf = Wf + (int64_t)jb * 16 * 64 + lane;
 #pragma unroll
-    for (int c = 0; c < kNB; ++c) rp[c] = x[c];
+    for (int s = 0; s < 16; ++s)
+      if (s < 4 * (jb + 1)) acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[s], wf[s * 64], acc[h], 0, 0, 0);
   }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t orow = r0 + 4 * e + g;
+      if (orow < N) A[orow * lda + c0 + 16 * jbs[h] + c] = acc[h][e];
+    }
 }
 
 // Trailing update of step `step` (A22 −= L21 L21ᵀ, lower 64×64 tiles, gemm_kernel's MFMA tiling with
-// K = 64) fused with the factorisation of the next diagonal block by the workgroup that owns it.
+// K = 64) fused with the factorisation and inversion of the next diagonal block by the workgroup that
+// owns it.
 __global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A, int64_t N, int64_t lda, int step,
                                                           double* __restrict__ ws, int* __restrict__ info) {
   if (blockIdx.x > blockIdx.y) return;                      // tile strictly above the diagonal
@@ -403,7 +479,6 @@ __global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A
   __shared__ __attribute__((aligned(16))) double ABs[2][2][kGK][kGP];
   auto& As = ABs[0];   // As[buf][k][m] = L21(m0 + m, k0 + k)
   auto& Bs = ABs[1];   // Bs[buf][k][n] = L21(n0 + n, k0 + k)
-  __shared__ double col[4 * kNB];
   __shared__ int bad_lds[1];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -490,8 +565,8 @@ __global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A
   if (tid == 0) bad_lds[0] = 0;
   __syncthreads();                                           // D consumed: As/Bs become Lb
   double inv;
-  chol64_block(a, w, r, col, &As[0][0][0], inv, bad_lds);
-  chol64_store(a, w, r, nb, inv, bad_lds[0], A, lda, r0, ws, info);
+  chol64_block(a, w, r, &As[0][0][0], inv, bad_lds);
+  chol64_finish(a, w, r, nb, inv, bad_lds[0], &As[0][0][0], A, lda, r0, ws, info);
 }
 
 // ----------------------------------------------------------------------------- triangular inverse
@@ -1027,11 +1102,6 @@ hipError_t launch_add_diag(hipStream_t stream, double* S, int64_t N, int64_t lds
   return hipGetLastError();
 }
 
-#ifndef OMB_TRSM_THREADS
-#define OMB_TRSM_THREADS 64
-#endif
-constexpr int kTrsmThreads = OMB_TRSM_THREADS;   // threads per panel workgroup (tools/ablate: 64 vs 256)
-
 hipError_t launch_cholesky(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws) {
   if (N <= 0) return hipSuccess;
   const int steps = (int)((N + kNB - 1) / kNB);
@@ -1040,13 +1110,11 @@ hipError_t launch_cholesky(hipStream_t stream, double* A, int64_t N, int64_t lda
   hipError_t e = hipGetLastError();
   for (int k = 0; k + 1 < steps && e == hipSuccess; ++k) {
     const int64_t rest = N - (int64_t)(k + 1) * kNB;      // rows below the diagonal block
-    // one wave per workgroup: the broadcast reads of L_kk are per-CU LDS traffic, so spreading the
-    // panel's waves over more CUs shortens every wave's solve
-    const unsigned pblocks = (unsigned)((rest + kTrsmThreads - 1) / kTrsmThreads);
+    const unsigned pblocks = (unsigned)((rest + 15) / 16);
     if (vec)
-      hipLaunchKernelGGL((chol_trsm_kernel<true, kTrsmThreads>), dim3(pblocks), dim3(kTrsmThreads), 0, stream, A, N, lda, k, ws, info);
+      hipLaunchKernelGGL((chol_panel_kernel<true>), dim3(pblocks), dim3(128), 0, stream, A, N, lda, k, ws, info);
     else
-      hipLaunchKernelGGL((chol_trsm_kernel<false, kTrsmThreads>), dim3(pblocks), dim3(kTrsmThreads), 0, stream, A, N, lda, k, ws, info);
+      hipLaunchKernelGGL((chol_panel_kernel<false>), dim3(pblocks), dim3(128), 0, stream, A, N, lda, k, ws, info);
     e = hipGetLastError();
     if (e != hipSuccess) break;
     const unsigned t = (unsigned)((rest + kGT - 1) / kGT);

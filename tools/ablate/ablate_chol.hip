@@ -1,4 +1,4 @@
-// Timing of the blocked Cholesky (launch_cholesky: chol_diag / chol_trsm / chol_update kernels) on an
+// Timing of the blocked Cholesky (launch_cholesky: chol_diag / chol_panel / chol_update kernels) on an
 // SPD matrix (tools only; not part of the library).  Correctness is tests/test_gpu_turbo.py.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/ablate/ablate_chol tools/ablate/ablate_chol.hip
 // Run on the GPU box: ./tools/ablate/ablate_chol [N ...]
@@ -7,13 +7,52 @@
 #include <cstdlib>
 #include <vector>
 
+// phase timestamps of chol_diag_kernel: shader clock (s_memtime) and the 100 MHz constant clock
+__device__ unsigned long long g_trace[2][32];
+#define OMB_CHOL_TRACE(id, cond)                                  \
+  do {                                                            \
+    if (cond) {                                                   \
+      g_trace[0][id] = __builtin_readcyclecounter();              \
+      g_trace[1][id] = __builtin_amdgcn_s_memrealtime();          \
+    }                                                             \
+  } while (0)
+
 #include "../../optimobo_amd/csrc/omb_linalg.hip"
 
 using namespace omb;
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); exit(1);} } while (0)
 
+static void trace_diag() {
+  const int N = 64;
+  std::vector<double> h(N * N);
+  for (int i = 0; i < N; ++i)
+    for (int j = 0; j < N; ++j) h[i * N + j] = (i == j) ? N : 1.0 / (1.0 + std::abs((double)(i - j)));
+  double *A, *ws;
+  int* info;
+  CK(hipMalloc(&A, N * N * 8));
+  CK(hipMalloc(&ws, kCholWsDoubles * 8));
+  CK(hipMalloc(&info, 64));
+  const char* names[17] = {"start", "loaded", "b0 begin", "b0 factored", "b1 begin", "b1 factored", "b2 begin",
+                           "b2 factored", "b3 begin", "b3 factored", "bulk0 (w3)", "bulk1 (w3)", "bulk2 (w3)",
+                           "L stored", "W_ii done", "barrier", "W done"};
+  for (int rep = 0; rep < 3; ++rep) {
+    CK(hipMemcpy(A, h.data(), N * N * 8, hipMemcpyHostToDevice));
+    CK(hipMemset(info, 0, 4));
+    hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), 0, 0, A, (int64_t)N, (int64_t)N, ws, info);
+    CK(hipDeviceSynchronize());
+    unsigned long long t[2][32];
+    CK(hipMemcpyFromSymbol(t, HIP_SYMBOL(g_trace), sizeof(t)));
+    if (rep < 2) continue;
+    printf("chol_diag_kernel phases (cycles of s_memtime from start; us from the 100 MHz clock)\n");
+    for (int i = 0; i < 17; ++i)
+      printf("  %-12s %8lld cyc  %7.2f us\n", names[i], (long long)(t[0][i] - t[0][0]), (t[1][i] - t[1][0]) / 100.0);
+  }
+  CK(hipFree(A)); CK(hipFree(ws)); CK(hipFree(info));
+}
+
 int main(int argc, char** argv) {
+  trace_diag();
   std::vector<int64_t> sizes;
   for (int i = 1; i < argc; ++i) sizes.push_back(atoll(argv[i]));
   if (sizes.empty()) sizes = {512, 1024, 3000};

@@ -66,6 +66,9 @@ struct omb_ctx {
   size_t tws_cap = 0;
   void* ichol = nullptr;
   size_t ichol_cap = 0;
+  // Thompson selection: per-sample sorted heads (select_sort_kernel)
+  void* sws = nullptr;
+  size_t sws_cap = 0;
   // GP fit: Ky | L⁻¹ | Ky⁻¹ | scratch workspace
   void* fws = nullptr;
   size_t fws_cap = 0;
@@ -449,6 +452,7 @@ int omb_destroy(omb_ctx* ctx) {
   if (ctx->sob) (void)hipFree(ctx->sob);
   if (ctx->tws) (void)hipFree(ctx->tws);
   if (ctx->ichol) (void)hipFree(ctx->ichol);
+  if (ctx->sws) (void)hipFree(ctx->sws);
   if (ctx->fws) (void)hipFree(ctx->fws);
   if (ctx->dws) (void)hipFree(ctx->dws);
   if (ctx->fault_host) (void)hipHostFree(ctx->fault_host);
@@ -931,7 +935,9 @@ static int check_cov_n(omb_ctx* ctx, int64_t N) {
   return OMB_OK;
 }
 
-// μ (N) and σ² (N) by the posterior kernel, K* (n, N) by the K block, V = L⁻¹K* (n, N) by GEMM.
+// K* (n, N) by the K block, V = L⁻¹K* (n, N) by GEMM, μ = K*ᵀα and σ² = σ_f² − Σ V² by the column
+// reduction over those two (the fused posterior kernel would recompute K* and V; at TuRBO's ≤ 5,000
+// candidates it also runs on a few dozen workgroups: 90 µs of a 3 ms step, profiles/r02_v21_c6_kernel_stats.csv).
 static hipError_t cov_prepare(omb_ctx* ctx, const ObjState& s, const double* Xc, int64_t N, double* Kst, double* V,
                               double* mu, double* var) {
   GPArgs args;
@@ -939,17 +945,17 @@ static hipError_t cov_prepare(omb_ctx* ctx, const ObjState& s, const double* Xc,
   args.gp[0] = s.dev;
   args.d = s.d;
   args.DP = s.DP;
-  const double* Ld[1] = {s.Ld};
-  hipError_t e = posterior_any(ctx, args, Ld, 1, s.R, Xc, N, mu, var);
-  if (e == hipSuccess) e = launch_kernel_block(ctx->stream, args, 0, Xc, N, Kst);
+  hipError_t e = launch_kernel_block(ctx->stream, args, 0, Xc, N, Kst);
   if (e == hipSuccess) e = launch_gemm_nn(ctx->stream, s.n, N, s.n, 1.0, s.Ld, s.n, Kst, N, 0.0, V, N);
+  if (e == hipSuccess) e = launch_post_colreduce(ctx->stream, Kst, V, s.n, N, s.dev.alpha, s.dev.variance, mu, var);
   return e;
 }
 
-// lower triangle of Σ = K(X*, X*) − VᵀV (GPy PosteriorExact._raw_predict, full_cov=True).
+// lower triangle of Σ = K(X*, X*) − VᵀV (GPy PosteriorExact._raw_predict, full_cov=True); cws:
+// cand_cov_ws_doubles(N, DP) doubles.
 static hipError_t cov_build(omb_ctx* ctx, const ObjState& s, const double* Xc, int64_t N, const double* V, double* S,
-                            int64_t lds) {
-  hipError_t e = launch_cand_cov(ctx->stream, s.dev, s.d, s.DP, Xc, N, S, lds);
+                            int64_t lds, double* cws) {
+  hipError_t e = launch_cand_cov(ctx->stream, s.dev, s.d, s.DP, Xc, N, S, lds, cws);
   if (e == hipSuccess) e = launch_gemm_tn_lower(ctx->stream, N, s.n, -1.0, V, N, 1.0, S, lds);
   return e;
 }
@@ -979,12 +985,15 @@ int omb_posterior_cov(omb_ctx* ctx, int obj, const double* Xc_dev, int64_t N, do
   if (N == 0) return OMB_OK;
   const ObjState& s = ctx->obj[obj];
   const size_t nN = (size_t)s.n * N;
-  if ((rc = grow_dev(ctx, &ctx->tws, &ctx->tws_cap, sizeof(double) * (2 * nN + N), "covariance workspace"))) return rc;
+  const size_t cw = (size_t)cand_cov_ws_doubles(N, s.DP);
+  if ((rc = grow_dev(ctx, &ctx->tws, &ctx->tws_cap, sizeof(double) * (2 * nN + N + cw), "covariance workspace")))
+    return rc;
   double* Kst = static_cast<double*>(ctx->tws);
   double* V = Kst + nN;
   double* var = V + nN;
+  double* cws = var + N;
   hipError_t e = cov_prepare(ctx, s, Xc_dev, N, Kst, V, mu_dev, var);
-  if (e == hipSuccess) e = cov_build(ctx, s, Xc_dev, N, V, cov_dev, N);
+  if (e == hipSuccess) e = cov_build(ctx, s, Xc_dev, N, V, cov_dev, N, cws);
   if (e == hipSuccess) e = launch_mirror_lower(ctx->stream, cov_dev, N, N);
   if (e != hipSuccess) return hip_fail(ctx, e, "posterior_cov");
   return OMB_OK;
@@ -1012,26 +1021,30 @@ int omb_posterior_samples(omb_ctx* ctx, int obj, const double* Xc_dev, int64_t N
     return fail(ctx, OMB_EINVAL, "jitter_rel=%g must be >= 0 and max_tries=%d in [1, 32]", jitter_rel, max_tries);
   const ObjState& s = ctx->obj[obj];
   const size_t nN = (size_t)s.n * N;
-  const size_t doubles = 2 * nN + 2 * (size_t)N + (size_t)N * N;
+  const size_t cw = (size_t)cand_cov_ws_doubles(N, s.DP);
+  const size_t sw = (size_t)chol_samples_ws_doubles(N, B);
+  const size_t doubles = 2 * nN + 2 * (size_t)N + (size_t)N * N + (cw > sw ? cw : sw);
   if ((rc = grow_dev(ctx, &ctx->tws, &ctx->tws_cap, sizeof(double) * doubles, "sampling workspace"))) return rc;
   double* Kst = static_cast<double*>(ctx->tws);
   double* V = Kst + nN;
   double* mu = V + nN;
   double* var = mu + N;
   double* S = var + N;
+  double* cws = S + (size_t)N * N;
   hipError_t e = cov_prepare(ctx, s, Xc_dev, N, Kst, V, mu, var);
   if (e != hipSuccess) return hip_fail(ctx, e, "posterior_samples (posterior)");
   double jit = jitter_rel * s.variance;
   int info = -1, t = 0;
   for (; t < max_tries; ++t, jit *= 10.0) {
-    if ((e = cov_build(ctx, s, Xc_dev, N, V, S, N)) != hipSuccess) return hip_fail(ctx, e, "posterior_samples (cov)");
+    if ((e = cov_build(ctx, s, Xc_dev, N, V, S, N, cws)) != hipSuccess)
+      return hip_fail(ctx, e, "posterior_samples (cov)");
     if ((rc = run_cholesky(ctx, S, N, N, jit, &info))) return rc;
     if (info == 0) break;
   }
   if (info != 0)
     return fail(ctx, OMB_ENOTPD, "posterior covariance + %g I is not positive definite (column %d) after %d tries",
                 jit / 10.0, info, max_tries);
-  if ((e = launch_chol_samples(ctx->stream, S, N, N, mu, Zt_dev, B, Y_dev)) != hipSuccess)
+  if ((e = launch_chol_samples(ctx->stream, S, N, N, mu, Zt_dev, B, Y_dev, cws)) != hipSuccess)
     return hip_fail(ctx, e, "posterior_samples (samples)");
   if (jitter_used) *jitter_used = jit;
   return OMB_OK;
@@ -1044,7 +1057,10 @@ int omb_thompson_select(omb_ctx* ctx, const double* Y_dev, int B, int64_t N, int
   if (N > kSelectMaxN) return fail(ctx, OMB_EUNSUP, "N=%lld candidates exceed %lld", (long long)N,
                                    (long long)kSelectMaxN);
   if (B > 0 && (!Y_dev || !idx_dev)) return fail(ctx, OMB_EINVAL, "null device pointer");
-  hipError_t e = launch_select(ctx->stream, Y_dev, B, N, idx_dev);
+  if (B == 0) return OMB_OK;
+  const size_t sw = (size_t)select_ws_bytes(B, N);
+  if (sw && (rc = grow_dev(ctx, &ctx->sws, &ctx->sws_cap, sw, "selection workspace"))) return rc;
+  hipError_t e = launch_select(ctx->stream, Y_dev, B, N, idx_dev, ctx->sws);
   if (e != hipSuccess) return hip_fail(ctx, e, "thompson_select");
   return OMB_OK;
 }
@@ -1063,6 +1079,7 @@ struct GPFactor {
   double* ls;      // (DP)
   double* part;    // gp_grad_blocks(n)·(DP+1)
   double* out;     // DP + 3
+  double* cws;     // cand_cov_ws_doubles(n, DP): X/ℓ and its squared norms for K(X, X)
   double jitter;   // jitter added by jitchol (0 when the first factorisation succeeded)
 };
 
@@ -1073,7 +1090,7 @@ static int gp_factor(omb_ctx* ctx, int kernel, int n, int d, const double* X, co
   const int DP = pad_dim(d);
   const size_t nn = (size_t)n * n;
   const size_t doubles = 3 * nn + 64 * (size_t)n + 2 * (size_t)n + DP +
-                         (size_t)gp_grad_blocks(n) * (DP + 1) + DP + 3;
+                         (size_t)gp_grad_blocks(n) * (DP + 1) + DP + 3 + (size_t)cand_cov_ws_doubles(n, DP);
   int rc = grow_dev(ctx, &ctx->fws, &ctx->fws_cap, sizeof(double) * doubles, "GP fit workspace");
   if (rc) return rc;
   double* p = static_cast<double*>(ctx->fws);
@@ -1085,7 +1102,8 @@ static int gp_factor(omb_ctx* ctx, int kernel, int n, int d, const double* X, co
   f->v = p; p += n;
   f->ls = p; p += DP;
   f->part = p; p += (size_t)gp_grad_blocks(n) * (DP + 1);
-  f->out = p;
+  f->out = p; p += DP + 3;
+  f->cws = p;
   void* h = nullptr;
   if ((rc = stage_begin(ctx, sizeof(double) * DP, &h))) return rc;
   for (int j = 0; j < DP; ++j) static_cast<double*>(h)[j] = (j < d) ? ls_host[j] : 1.0;
@@ -1100,7 +1118,7 @@ static int gp_factor(omb_ctx* ctx, int kernel, int n, int d, const double* X, co
   f->jitter = 0.0;
   for (int t = -1; t < 5; ++t) {
     const double jit = (t < 0) ? 0.0 : mean_diag * 1e-6 * pow(10.0, (double)t);
-    OMB_HIP(ctx, launch_cand_cov(ctx->stream, g, d, DP, X, n, f->Ky, n));
+    OMB_HIP(ctx, launch_cand_cov(ctx->stream, g, d, DP, X, n, f->Ky, n, f->cws));
     if ((rc = run_cholesky(ctx, f->Ky, n, n, base + jit, &info))) return rc;
     if (info == 0) {
       f->jitter = jit;

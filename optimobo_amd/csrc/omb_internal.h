@@ -112,9 +112,11 @@ hipError_t launch_gemm_nn(hipStream_t s, int64_t M, int64_t Nc, int64_t K, doubl
 // lower triangle of C (N, N) = β C + α AᵀA, A (K, N).
 hipError_t launch_gemm_tn_lower(hipStream_t s, int64_t N, int64_t K, double alpha, const double* A, int64_t lda,
                                 double beta, double* C, int64_t ldc);
-// lower triangle of K(X*, X*) of one GP's kernel (ℓ, σ_f² from g) at Xc (N, d).
+// lower triangle of K(X*, X*) of one GP's kernel (ℓ, σ_f² from g) at Xc (N, d); ws: cand_cov_ws_doubles
+// device doubles (X*/ℓ and its squared norms).
+int64_t cand_cov_ws_doubles(int64_t N, int DP);
 hipError_t launch_cand_cov(hipStream_t stream, const GPDev& g, int d, int DP, const double* Xc, int64_t N, double* S,
-                           int64_t lds);
+                           int64_t lds, double* ws);
 hipError_t launch_mirror_lower(hipStream_t stream, double* S, int64_t N, int64_t lds);
 hipError_t launch_add_diag(hipStream_t stream, double* S, int64_t N, int64_t lds, double v);
 // in-place lower Cholesky; info (device int, zeroed by the caller) = first bad column (1-based);
@@ -123,9 +125,15 @@ hipError_t launch_add_diag(hipStream_t stream, double* S, int64_t N, int64_t lds
 constexpr int kCholWsDoubles = 64 * 64;
 hipError_t launch_cholesky(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws);
 // Y (B, N) = μ + Zt Lᵀ (L lower, N×N): row b of Y is the sample μ + L z_b.
+// ws: chol_samples_ws_doubles(N, B) device doubles (split-K partial products; 0 when unsplit).
+int64_t chol_samples_ws_doubles(int64_t N, int B);
 hipError_t launch_chol_samples(hipStream_t stream, const double* L, int64_t N, int64_t ldl, const double* mu,
-                               const double* Zt, int B, double* Y);
-hipError_t launch_select(hipStream_t stream, const double* Y, int B, int64_t N, int64_t* idx);
+                               const double* Zt, int B, double* Y, double* ws);
+// greedy per-sample arg-min (TuRBO select_candidates); ws: select_ws_bytes(B, N) bytes of device memory
+// (the sorted heads of every sample when N ≤ kSelectSortN; 0 otherwise).
+constexpr int64_t kSelectSortN = 8192;
+int64_t select_ws_bytes(int B, int64_t N);
+hipError_t launch_select(hipStream_t stream, const double* Y, int B, int64_t N, int64_t* idx, void* ws);
 // C (M, Nc) = β C + α AᵀB, A (K, M), B (K, Nc).
 hipError_t launch_gemm_tn(hipStream_t s, int64_t M, int64_t Nc, int64_t K, double alpha, const double* A, int64_t lda,
                           const double* B, int64_t ldb, double beta, double* C, int64_t ldc);

@@ -36,7 +36,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t Nc, int64_
                                                    const double* __restrict__ A, int64_t lda,
                                                    const double* __restrict__ B, int64_t ldb, double beta,
                                                    double* __restrict__ C, int64_t ldc,
-                                                   const double* __restrict__ col_bias) {
+                                                   const double* __restrict__ col_bias, int64_t kchunk,
+                                                   int64_t zstride) {
   const int64_t m0 = (int64_t)blockIdx.y * kGT, n0 = (int64_t)blockIdx.x * kGT;
   if (LOWER && n0 > m0) return;   // tile strictly above the diagonal
   __shared__ double As[2][kGK][kGP];   // As[k][m] = op(A)(m0 + m, k0 + k)
@@ -45,7 +46,13 @@ __global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t Nc, int64_
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   // with BTRI, slabs past the tile's last column are all zero in op(B)
-  const int64_t kend = BTRI ? (K < n0 + kGT ? K : n0 + kGT) : K;
+  int64_t kend = BTRI ? (K < n0 + kGT ? K : n0 + kGT) : K;
+  // split K (gridDim.z > 1): slice z covers [z·kchunk, (z+1)·kchunk) into its own partial C + z·zstride
+  const int64_t kbeg = (int64_t)blockIdx.z * kchunk;
+  if (gridDim.z > 1) {
+    kend = kend < kbeg + kchunk ? kend : kbeg + kchunk;
+    C += (int64_t)blockIdx.z * zstride;
+  }
 
   // 1024 elements of each operand per slab, 4 per thread; consecutive threads walk the
   // contiguous dimension of the stored matrix (coalesced), LDS stores land conflict-free.
@@ -78,13 +85,13 @@ __global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t Nc, int64_
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
 
-  if (kend > 0) {
-    fetch(0);
+  if (kend > kbeg) {
+    fetch(kbeg);
     stash(0);
   }
   __syncthreads();
   int buf = 0;
-  for (int64_t k0 = 0; k0 < kend; k0 += kGK) {
+  for (int64_t k0 = kbeg; k0 < kend; k0 += kGK) {
     const bool more = k0 + kGK < kend;
     if (more) fetch(k0 + kGK);      // in flight while this slab multiplies
 #pragma unroll
@@ -130,34 +137,99 @@ static hipError_t gemm(hipStream_t stream, int64_t M, int64_t Nc, int64_t K, dou
   if (M <= 0 || Nc <= 0) return hipSuccess;
   dim3 grid((unsigned)((Nc + kGT - 1) / kGT), (unsigned)((M + kGT - 1) / kGT));
   hipLaunchKernelGGL((gemm_kernel<TA, TB, BTRI, LOWER>), grid, dim3(256), 0, stream, M, Nc, K, alpha, A, lda, B, ldb,
-                     beta, C, ldc, col_bias);
+                     beta, C, ldc, col_bias, (int64_t)0, (int64_t)0);
   return hipGetLastError();
+}
+
+// C (M, Nc) = bias + Σ_z P[z] in slice order (deterministic), P[z] (M, Nc) dense at P + z·zstride.
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const double* __restrict__ P, int S, int64_t zstride,
+                                                            int64_t M, int64_t Nc, const double* __restrict__ bias,
+                                                            double* __restrict__ C, int64_t ldc) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * Nc) return;
+  const int64_t r = i / Nc, c = i - r * Nc;
+  double v = 0.0;
+  for (int z = 0; z < S; ++z) v += P[z * zstride + i];
+  C[r * ldc + c] = v + (bias ? bias[c] : 0.0);
 }
 
 // ----------------------------------------------------------------------------- K(X*, X*)
 // GPy Stationary._unscaled_dist(X) on X/ℓ: r² = −2·(aᵢ·aⱼ) + (‖aᵢ‖² + ‖aⱼ‖²), diagonal forced
-// to 0, clipped at 0; then K_of_r.  Lower triangle only (j ≤ i), 16×16 tiles.
-template <int DP, int KIND>
-__global__ __launch_bounds__(256) void cand_cov_kernel(const double* __restrict__ Xc, int d, int64_t N,
-                                                       const double* __restrict__ ls, double variance,
-                                                       double* __restrict__ S, int64_t lds) {
-  if (blockIdx.x > blockIdx.y) return;
-  const int64_t i = (int64_t)blockIdx.y * 16 + (threadIdx.x >> 4);
-  const int64_t j = (int64_t)blockIdx.x * 16 + (threadIdx.x & 15);
-  if (i >= N || j > i) return;
-  double aa = 0.0, bb = 0.0, dot = 0.0;
+// to 0, clipped at 0; then K_of_r.  Lower triangle only (j ≤ i).
+//   cand_scale_kernel  a = X/ℓ (GPy divides; once per element, not per pair) into rows of KP = ⌈DP/4⌉·4
+//                      doubles (zero padded) and ‖a‖² in coordinate order;
+//   cand_cov_kernel    one 64×64 lower tile per 256-thread workgroup (4 waves × 32×32, gemm_kernel's
+//                      tiling), the cross term aᵢ·aⱼ on v_mfma_f64_16x16x4f64 over KP/4 k-steps from LDS,
+//                      the kernel transform fused into the store.
+// Round 2's kernel divided by ℓ inside every pair and read both rows per thread (203 µs for the
+// lower triangle at N = 3000, d = 30: profiles/r02_v21_c6_kernel_stats.csv).
+template <int DP>
+__global__ __launch_bounds__(256) void cand_scale_kernel(const double* __restrict__ Xc, int d, int64_t N,
+                                                         const double* __restrict__ ls, double* __restrict__ Xs,
+                                                         double* __restrict__ xsq) {
+  constexpr int KP = (DP + 3) / 4 * 4;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  double s = 0.0;
 #pragma unroll
-  for (int k = 0; k < DP; ++k) {
-    if (k < d) {
-      const double a = Xc[i * d + k] / ls[k];
-      const double b = Xc[j * d + k] / ls[k];
-      aa += a * a;
-      bb += b * b;
-      dot = fma(a, b, dot);
-    }
+  for (int k = 0; k < KP; ++k) {
+    double a = 0.0;
+    if (k < d) a = Xc[i * d + k] / ls[k];
+    s = fma(a, a, s);
+    Xs[i * KP + k] = a;
   }
-  const double r2 = (i == j) ? 0.0 : fma(-2.0, dot, aa + bb);
-  S[i * lds + j] = kernel_of_r2<KIND>(r2, variance);
+  xsq[i] = s;
+}
+
+template <int DP, int KIND>
+__global__ __launch_bounds__(256) void cand_cov_kernel(const double* __restrict__ Xs, const double* __restrict__ xsq,
+                                                       int64_t N, double variance, double* __restrict__ S,
+                                                       int64_t lds) {
+  constexpr int KP = (DP + 3) / 4 * 4;
+  if (blockIdx.x > blockIdx.y) return;
+  const int64_t m0 = (int64_t)blockIdx.y * 64, n0 = (int64_t)blockIdx.x * 64;
+  __shared__ double As[KP][65], Bs[KP][65];   // As[k][m] = a_{m0+m}[k]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  for (int idx = tid; idx < 64 * KP; idx += 256) {
+    const int m = idx / KP, k = idx % KP;
+    As[k][m] = (m0 + m < N) ? Xs[(m0 + m) * KP + k] : 0.0;
+    Bs[k][m] = (n0 + m < N) ? Xs[(n0 + m) * KP + k] : 0.0;
+  }
+  __syncthreads();
+  d4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int ks = 0; ks < KP / 4; ++ks) {
+    const int kk = 4 * ks + (lane >> 4);
+    const double a0 = As[kk][32 * wm + (lane & 15)];
+    const double a1 = As[kk][32 * wm + 16 + (lane & 15)];
+    const double b0 = Bs[kk][32 * wn + (lane & 15)];
+    const double b1 = Bs[kk][32 * wn + 16 + (lane & 15)];
+    acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+    acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+    acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+    acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+  }
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb) {
+    const int64_t col = n0 + 32 * wn + 16 * cb + (lane & 15);
+    const double bsq = col < N ? xsq[col] : 0.0;
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t row = m0 + 32 * wm + 16 * rb + (lane >> 4) + 4 * e;
+        if (row < N && col <= row) {
+          const double r2 = (row == col) ? 0.0 : fma(-2.0, acc[rb][cb][e], xsq[row] + bsq);
+          S[row * lds + col] = kernel_of_r2<KIND>(r2, variance);
+        }
+      }
+  }
 }
 
 __global__ __launch_bounds__(256) void mirror_lower_kernel(double* __restrict__ S, int64_t N, int64_t lds) {
@@ -238,23 +310,35 @@ __device__ __forceinline__ void static_for(F&& f) {
 // inverse of the 64×64 diagonal block is the usual GPU TRSM; its error grows with cond(L_kk), which
 // the jitter of omb_posterior_samples bounds.
 
+// LDS of the diagonal-block factorisation (diagonal workgroups of chol_update_kernel, chol_diag_kernel):
+//   Lb    4 sub-blocks × 64 rows × kLbP doubles: Lb[(b·64 + r)·kLbP + q] = L[r][16b + q]; the 144-B row
+//         pitch keeps 16 lanes reading 16 different rows (the bulk updates, the L store) conflict-free;
+//   cbuf  2 × 64: the current column, double buffered;  dinv  64: 1/L_jj.
+constexpr int kLbP = 18;
+constexpr int kLbDoubles = 4 * kNB * kLbP;
+constexpr int kCholAux = 2 * kNB + kNB;
+
 // Factor a 64×64 SPD block with the 4 waves of a 256-thread workgroup: thread (wave w, lane r) holds
 // a[q] = A[r][16w + q] (only 16w + q ≤ r is meaningful; rows past the block are identity rows).
 // Sub-block b (columns 16b..16b+15) is factored by wave b alone — 16 column steps, each updating only
-// the rest of the sub-block, the column's entries L[16b+q][j] taken from lane 16b+q by v_readlane
-// (scalar operands of the fmas: no LDS round trip on the chain) — and published to LDS (Lb[b]: 64
-// rows × 16); then every later wave subtracts its contribution from its own columns in bulk
-// (L[r][16w+q] −= Σ_j L[r][j] L[16w+q][j]).
-// On return (after a barrier) a[q] = L[r][16w+q], Lb holds L, my_inv = 1/L[r][r] on the thread with
-// 16w ≤ r < 16w+16 (else 1), bad_lds[0] = 1-based first non-positive pivot column or 0.
-__device__ __forceinline__ void chol64_block(double (&a)[16], int w, int r, double* Lb, double& my_inv,
-                                             int* bad_lds) {
-  my_inv = 1.0;
+// the rest of the sub-block: the next column's entry L[j+1][j] by v_readlane (the serial chain), the
+// others as LDS broadcasts of the column (their latency hides behind the next pivot) — and published to
+// Lb; then every later wave subtracts its contribution from its own columns in bulk
+// (L[r][16w+q] −= Σ_j L[r][j] L[16w+q][j]).  Round 2 measured 300 cycles per column with every entry
+// by v_readlane (two 4-cycle VALU ops per entry, profiles/r02_v22_chol_diag_trace.txt).
+// Entries above the diagonal are not kept at zero (a[jj] is scaled on every row, no selects); they
+// only ever feed entries above the diagonal of the same row, which nothing reads.
+// On return (after a barrier) Lb holds L, dinv[j] = 1/L_jj, bad_lds[0] = 1-based first non-positive
+// pivot column or 0.
+__device__ __forceinline__ void chol64_block(double (&a)[16], int w, int r, double* Lb, double* aux, int* bad_lds) {
+  double* dinv = aux + 2 * kNB;
   int bad = 0;
   static_for<0, 4>([&](auto bc) {
     constexpr int b = decltype(bc)::value;
     if (w == b) {
       OMB_CHOL_TRACE(2 + 2 * b, r == 0);
+      double pl = 0.0;   // the previous column's entry of this row
+      double pv[16];     // the previous column's entries L[16b+q][j−1] (q ≥ jj+1), from LDS
       static_for<0, 16>([&](auto jc) {
         constexpr int jj = decltype(jc)::value;
         constexpr int j = 16 * b + jj;
@@ -267,22 +351,36 @@ __device__ __forceinline__ void chol64_block(double (&a)[16], int w, int r, doub
         const double hd = 0.5 * dj;
         const double y1 = fma(y0, fma(-hd * y0, y0, 0.5), y0);
         const double inv = fma(y1, fma(-hd * y1, y1, 0.5), y1);
-        if (r == j) my_inv = inv;
-        const double lrj = (r > j) ? a[jj] * inv : (r == j ? dj * inv : 0.0);
+        if (r == j) dinv[j] = inv;
+        const double lrj = a[jj] * inv;                // row j: dj·inv = √dj
         a[jj] = lrj;
+        // the chain: column j's entry of the next pivot's row
+        if constexpr (jj < 15) a[jj + 1] = fma(-lrj, readlane_f64(lrj, j + 1), a[jj + 1]);
+        // software pipeline: column j−1's other updates, its entries loaded one column ago
+        if constexpr (jj >= 1) {
 #pragma unroll
-        for (int q = jj + 1; q < 16; ++q) a[q] = fma(-lrj, readlane_f64(lrj, 16 * b + q), a[q]);
+          for (int q = jj + 1; q < 16; ++q) a[q] = fma(-pl, pv[q], a[q]);
+        }
+        if constexpr (jj < 14) {
+          double* cb = aux + kNB * (jj & 1);
+          cb[r] = lrj;
+#pragma unroll
+          for (int q = jj + 2; q < 16; ++q) pv[q] = cb[16 * b + q];
+          pl = lrj;
+        }
+        __builtin_amdgcn_sched_barrier(0);
       });
       OMB_CHOL_TRACE(3 + 2 * b, r == 0);
 #pragma unroll
-      for (int q = 0; q < 16; ++q) Lb[(b * 64 + r) * 16 + q] = a[q];
+      for (int q = 0; q < 16; q += 2)
+        *reinterpret_cast<double2*>(Lb + (b * 64 + r) * kLbP + q) = double2{a[q], a[q + 1]};
       if (r == 0 && bad) bad_lds[0] = bad;
     }
     __syncthreads();
     if constexpr (b < 3) {
       if (w > b) {
         // own row's sub-block-b values, then one dot product per owned column
-        const double2* mine = reinterpret_cast<const double2*>(Lb + (b * 64 + r) * 16);
+        const double2* mine = reinterpret_cast<const double2*>(Lb + (b * 64 + r) * kLbP);
         double lr[16];
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
@@ -292,15 +390,15 @@ __device__ __forceinline__ void chol64_block(double (&a)[16], int w, int r, doub
         }
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-          const double2* other = reinterpret_cast<const double2*>(Lb + (b * 64 + 16 * w + q) * 16);
-          double s = 0.0;
+          const double2* other = reinterpret_cast<const double2*>(Lb + (b * 64 + 16 * w + q) * kLbP);
+          double s0 = 0.0, s1 = 0.0;
 #pragma unroll
           for (int h = 0; h < 8; ++h) {
             const double2 v = other[h];
-            s = fma(lr[2 * h], v.x, s);
-            s = fma(lr[2 * h + 1], v.y, s);
+            s0 = fma(lr[2 * h], v.x, s0);
+            s1 = fma(lr[2 * h + 1], v.y, s1);
           }
-          a[q] -= s;
+          a[q] -= s0 + s1;
         }
         OMB_CHOL_TRACE(10 + b, w == 3 && r == 0);
       }
@@ -308,48 +406,62 @@ __device__ __forceinline__ void chol64_block(double (&a)[16], int w, int r, doub
   });
 }
 
-// After chol64_block: writes L (rows r < nb of the block at c0) into A's lower triangle, the first bad
-// pivot into info, and W = L⁻¹ as the MFMA B fragments of chol_panel_kernel:
+// After chol64_block: writes L (rows < nb of the block at c0) into A's lower triangle (coalesced rows
+// from Lb), the first bad pivot into info, and W = L⁻¹ as the MFMA B fragments of chol_panel_kernel:
 //   Wf[(jb·16 + s)·64 + l] = W[16jb + (l & 15)][m(s, l >> 4)],   m(s, g) = 16(s >> 2) + 4g + (s & 3)
 // (k-step s of the panel's output column block jb; only s < 4(jb + 1) is read — the rest of that row
 // block of W is zero — so the panel skips W's upper triangle in whole k-steps).
-// Phase 1: wave i inverts its diagonal 16×16 block by column-oriented substitution (lane l → column
-// l & 15, the factor's entries by v_readlane) and leaves W_ii in place of L_ii in Lb.  Phase 2: wave j
-// forms its column block, W_ij = −W_ii Σ_{k=j}^{i−1} L_ik W_kj for i = j+1..3, on MFMA: a product's
-// accumulator layout (lane l: rows 4e + (l >> 4), column l & 15) is the next product's B operand
-// layout, so the W_kj (k > j) stay in registers and only L and the W_ii are read from LDS.
-__device__ __forceinline__ void chol64_finish(const double (&a)[16], int w, int r, int nb, double my_inv, int bad,
-                                              double* Lb, double* __restrict__ A, int64_t lda, int64_t c0,
+// Phase 1: wave i inverts its diagonal 16×16 block by substitution, lane l → column c = l & 15:
+// x[m] = (δ_mc − Σ_{p<m} L_ii[m][p] x[p]) / L_ii[m][m], the rows of L_ii as LDS broadcasts, and leaves
+// W_ii in place of L_ii in Lb.  Phase 2: wave j forms its column block, W_ij = −W_ii Σ_{k=j}^{i−1} L_ik W_kj
+// for i = j+1..3, on MFMA: a product's accumulator layout (lane l: rows 4e + (l >> 4), column l & 15) is
+// the next product's B operand layout, so the W_kj (k > j) stay in registers and only L and the W_ii
+// are read from LDS.
+__device__ __forceinline__ void chol64_finish(int w, int r, int nb, int bad, double* Lb, const double* aux,
+                                              double* __restrict__ A, int64_t lda, int64_t c0,
                                               double* __restrict__ Wf, int* __restrict__ info) {
-  if (r < nb) {
+  const double* dinv = aux + 2 * kNB;
+  double lv[16];
 #pragma unroll
-    for (int q = 0; q < 16; ++q)
-      if (16 * w + q <= r) A[(c0 + r) * lda + c0 + 16 * w + q] = a[q];
+  for (int i = 0; i < 16; ++i) lv[i] = Lb[((r >> 4) * 64 + w + 4 * i) * kLbP + (r & 15)];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int row = w + 4 * i, col = r;
+    if (row < nb && col <= row) A[(c0 + row) * lda + c0 + col] = lv[i];
   }
   if (w == 0 && r == 0 && bad) atomicCAS(info, 0, (int)(c0 + bad));
   OMB_CHOL_TRACE(13, w == 0 && r == 0);
   const int c = r & 15, g = r >> 4;
   // phase 1: x[m] = W_ww[m][c]
+  const double* Ld = Lb + (w * 64 + 16 * w) * kLbP;   // L_ww row m at Ld + m·kLbP
   double x[16];
+  static_for<0, 16>([&](auto mc) {
+    constexpr int m = decltype(mc)::value;
+    // row m's offset passes through an empty asm that consumes x[m−2]: its reads issue one row ahead
+    // of their use, not all 120 at once (which took the kernel to 256 VGPRs)
+    int off = m * kLbP;
+    if constexpr (m >= 2) asm volatile("" : "+v"(off) : "v"(x[m - 2]));
+    double s0 = (m == c) ? 1.0 : 0.0, s1 = 0.0;
 #pragma unroll
-  for (int m = 0; m < 16; ++m) x[m] = (m == c) ? 1.0 : 0.0;
-  static_for<0, 16>([&](auto pc) {
-    constexpr int p = decltype(pc)::value;
-    x[p] *= readlane_f64(my_inv, 16 * w + p);
-#pragma unroll
-    for (int m = p + 1; m < 16; ++m) x[m] = fma(-readlane_f64(a[p], 16 * w + m), x[p], x[m]);
+    for (int p = 0; p + 1 < m; p += 2) {
+      const double2 l = *reinterpret_cast<const double2*>(Ld + off + p);
+      s0 = fma(-l.x, x[p], s0);
+      s1 = fma(-l.y, x[p + 1], s1);
+    }
+    if constexpr (m & 1) s0 = fma(-Ld[off + m - 1], x[m - 1], s0);
+    x[m] = (s0 + s1) * dinv[16 * w + m];
   });
+  __syncthreads();                                     // every wave's phase-1 reads of Lb are done
   if (r < 16) {
 #pragma unroll
-    for (int m = 0; m < 16; ++m) {
-      Lb[(w * 64 + 16 * w + m) * 16 + c] = x[m];
-      // W[16w + m][16w + c]: jb = w, s = 4w + (c & 3), lane m + 16 (c >> 2)
-      Wf[(w * 16 + 4 * w + (c & 3)) * 64 + m + 16 * (c >> 2)] = x[m];
-    }
+    for (int m = 0; m < 16; ++m) Lb[(w * 64 + 16 * w + m) * kLbP + c] = x[m];
   }
   OMB_CHOL_TRACE(14, w == 0 && r == 0);
   __syncthreads();
   OMB_CHOL_TRACE(15, w == 0 && r == 0);
+  // W_ww's fragments: rows jb = w, k-steps s = 4w + u: W[16w + c][16w + 4g + u]
+#pragma unroll
+  for (int u = 0; u < 4; ++u) Wf[(w * 16 + 4 * w + u) * 64 + r] = Lb[(w * 64 + 16 * w + c) * kLbP + 4 * g + u];
   // phase 2
   d4 Wc[4];
 #pragma unroll
@@ -363,9 +475,9 @@ __device__ __forceinline__ void chol64_finish(const double (&a)[16], int w, int 
         if (k >= w) {
           static_for<0, 4>([&](auto sc) {
             constexpr int s = decltype(sc)::value;
-            const double av = Lb[(k * 64 + 16 * i + c) * 16 + 4 * s + g];   // L[16i + c][16k + 4s + g]
+            const double av = Lb[(k * 64 + 16 * i + c) * kLbP + 4 * s + g];   // L[16i + c][16k + 4s + g]
             // B operand W_kj[4s + g][c]: W_ww from LDS (phase 1), the others from registers
-            const double bv = (k == w) ? Lb[(k * 64 + 16 * k + 4 * s + g) * 16 + c] : Wc[k][s];
+            const double bv = (k == w) ? Lb[(k * 64 + 16 * k + 4 * s + g) * kLbP + c] : Wc[k][s];
             T = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, T, 0, 0, 0);
           });
         }
@@ -373,7 +485,7 @@ __device__ __forceinline__ void chol64_finish(const double (&a)[16], int w, int 
       d4 R = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int s = 0; s < 4; ++s)
-        R = __builtin_amdgcn_mfma_f64_16x16x4f64(Lb[(i * 64 + 16 * i + c) * 16 + 4 * s + g], T[s], R, 0, 0, 0);
+        R = __builtin_amdgcn_mfma_f64_16x16x4f64(Lb[(i * 64 + 16 * i + c) * kLbP + 4 * s + g], T[s], R, 0, 0, 0);
       Wc[i] = -R;
       // W[16i + 4e + g][16w + c]: jb = i, s = 4w + (c & 3), lane 4e + g + 16 (c >> 2)
 #pragma unroll
@@ -385,7 +497,8 @@ __device__ __forceinline__ void chol64_finish(const double (&a)[16], int w, int 
 
 __global__ __launch_bounds__(256) void chol_diag_kernel(double* __restrict__ A, int64_t N, int64_t lda,
                                                          double* __restrict__ ws, int* __restrict__ info) {
-  __shared__ __attribute__((aligned(16))) double Lb[4 * kNB * 16];
+  __shared__ __attribute__((aligned(16))) double Lb[kLbDoubles];
+  __shared__ double aux[kCholAux];
   __shared__ int bad_lds[1];
   const int nb = (int)(N < kNB ? N : kNB);
   const int r = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -401,9 +514,8 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(double* __restrict__ A, 
   }
   __syncthreads();
   OMB_CHOL_TRACE(1, threadIdx.x == 0);
-  double inv;
-  chol64_block(a, w, r, Lb, inv, bad_lds);
-  chol64_finish(a, w, r, nb, inv, bad_lds[0], Lb, A, lda, 0, ws, info);
+  chol64_block(a, w, r, Lb, aux, bad_lds);
+  chol64_finish(w, r, nb, bad_lds[0], Lb, aux, A, lda, 0, ws, info);
 }
 
 // Panel of step `step`: rows c0+64 .. N−1, L21 = A21 · Wᵀ (W = L_kk⁻¹ from chol64_finish's fragments).
@@ -474,11 +586,13 @@ __global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A
   const int64_t r0 = c0 + kNB;                              // first row / column of A22
   const int64_t M = N - r0;
   const int64_t m0 = (int64_t)blockIdx.y * kGT, n0 = (int64_t)blockIdx.x * kGT;
-  // As and Bs are contiguous (one array) so the diagonal workgroup can reuse them as the 64 × 65
-  // staging tile D and then as the factorisation's Lb (4096 doubles of the 4224)
-  __shared__ __attribute__((aligned(16))) double ABs[2][2][kGK][kGP];
-  auto& As = ABs[0];   // As[buf][k][m] = L21(m0 + m, k0 + k)
-  auto& Bs = ABs[1];   // Bs[buf][k][n] = L21(n0 + n, k0 + k)
+  // one array: the GEMM's As and Bs, then (the diagonal workgroup) the 64 × 65 staging tile D, then
+  // the factorisation's Lb
+  static_assert(2 * 2 * kGK * kGP <= kLbDoubles && kNB * (kNB + 1) <= kLbDoubles, "LDS carve-up");
+  __shared__ __attribute__((aligned(16))) double smem[kLbDoubles];
+  __shared__ double aux[kCholAux];
+  auto& As = *reinterpret_cast<double (*)[2][kGK][kGP]>(smem);                      // As[buf][k][m] = L21(m0 + m, k0 + k)
+  auto& Bs = *reinterpret_cast<double (*)[2][kGK][kGP]>(smem + 2 * kGK * kGP);      // Bs[buf][k][n] = L21(n0 + n, k0 + k)
   __shared__ int bad_lds[1];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -532,7 +646,7 @@ __global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A
     buf ^= 1;
   }
   const bool diag = (blockIdx.x == 0 && blockIdx.y == 0);  // the next diagonal block: A22's first tile
-  double* D = &As[0][0][0];                                  // 64 × 65 staging of that tile (fits As+Bs)
+  double* D = smem;                                          // 64 × 65 staging of that tile
   // C/D map of v_mfma_f64_16x16x4f64: col = lane & 15, row = (lane >> 4) + 4·i
 #pragma unroll
   for (int rb2 = 0; rb2 < 2; ++rb2)
@@ -563,10 +677,9 @@ __global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A
     a[q] = (r < nb && c <= r) ? D[r * 65 + c] : (c == r ? 1.0 : 0.0);
   }
   if (tid == 0) bad_lds[0] = 0;
-  __syncthreads();                                           // D consumed: As/Bs become Lb
-  double inv;
-  chol64_block(a, w, r, &As[0][0][0], inv, bad_lds);
-  chol64_finish(a, w, r, nb, inv, bad_lds[0], &As[0][0][0], A, lda, r0, ws, info);
+  __syncthreads();                                           // D consumed: smem becomes Lb
+  chol64_block(a, w, r, smem, aux, bad_lds);
+  chol64_finish(w, r, nb, bad_lds[0], smem, aux, A, lda, r0, ws, info);
 }
 
 // ----------------------------------------------------------------------------- triangular inverse
@@ -1058,6 +1171,101 @@ __global__ __launch_bounds__(1024) void select_kernel(const double* __restrict__
   }
 }
 
+// Sorted path (N ≤ kSelectSortN): sample b's pick is the first entry of its row in np.argmin order
+// that no earlier sample took, and at most b entries are taken, so the first min(B, N) entries of
+// every row in that order decide all picks.
+//   select_sort_kernel    one workgroup per sample: the row as (key, index) pairs in LDS, bitonic sort,
+//                         the head written out (index, bit 62 set when the value is +inf);
+//   select_greedy_kernel  one wave walks the samples in order over the heads with an LDS bitmap of
+//                         taken candidates (a ballot per 64 entries).
+// key: NaN → 0 (np.argmin returns the first NaN), else the order-preserving map of the IEEE bits
+// (−0 folded onto +0, which compare equal); ties resolve by index.  A taken candidate reads as +inf
+// (turbo.py:151, :381): when the first free entry is +inf, the pick is the lowest index among it and
+// the taken ones.
+constexpr int kSelThreads = 1024;
+constexpr unsigned long long kSelKeyInf = 0xFFF0000000000000ull;
+constexpr long long kSelInfFlag = 1ll << 62;
+
+__device__ __forceinline__ unsigned long long sel_key(double v) {
+  if (v != v) return 0ull;
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v + 0.0);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+__global__ __launch_bounds__(kSelThreads) void select_sort_kernel(const double* __restrict__ Y, int64_t N, int N2,
+                                                                  int K, long long* __restrict__ heads) {
+  __shared__ unsigned long long key[kSelectSortN];
+  __shared__ unsigned short ix[kSelectSortN];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const double* y = Y + (int64_t)b * N;
+  for (int i = tid; i < N2; i += kSelThreads) {
+    key[i] = i < N ? sel_key(y[i]) : ~0ull;
+    ix[i] = (unsigned short)i;
+  }
+  __syncthreads();
+  for (int k = 2; k <= N2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int t = tid; t < (N2 >> 1); t += kSelThreads) {
+        // t-th compare-exchange of this stage: i has bit j clear, partner i + j
+        const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
+        const int p = i + j;
+        const unsigned long long ki = key[i], kp = key[p];
+        const unsigned short xi = ix[i], xp = ix[p];
+        const bool gt = ki > kp || (ki == kp && xi > xp);
+        if (((i & k) == 0) == gt) {
+          key[i] = kp;
+          key[p] = ki;
+          ix[i] = xp;
+          ix[p] = xi;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = tid; i < K; i += kSelThreads)
+    heads[(int64_t)b * K + i] = (long long)ix[i] | (key[i] == kSelKeyInf ? kSelInfFlag : 0ll);
+}
+
+constexpr int kSelHeadLds = 4096;   // staged head entries (64 per sample, samples 0..63)
+__global__ __launch_bounds__(256) void select_greedy_kernel(const long long* __restrict__ heads, int B, int64_t N,
+                                                            int K, int64_t* __restrict__ idx_out) {
+  __shared__ unsigned taken[kSelectSortN / 32];
+  __shared__ long long hl[kSelHeadLds];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int H = K < 64 ? K : 64;                      // staged entries per sample
+  const int Bs = B < kSelHeadLds / 64 ? B : kSelHeadLds / 64;
+  for (int w = tid; w < kSelectSortN / 32; w += 256) taken[w] = 0u;
+  for (int i = tid; i < Bs * H; i += 256) hl[i] = heads[(int64_t)(i / H) * K + i % H];
+  __syncthreads();
+  if (tid >= 64) return;
+  long long min_taken = N;
+  for (int b = 0; b < B; ++b) {
+    long long pick = -1;
+    for (int c0 = 0; c0 < K && pick < 0; c0 += 64) {
+      long long e = -1;
+      if (c0 + lane < K) e = (c0 == 0 && b < Bs) ? hl[b * H + lane] : heads[(int64_t)b * K + c0 + lane];
+      const long long i = e >= 0 ? (e & (kSelInfFlag - 1)) : 0;
+      const bool free_ = e >= 0 && !((taken[i >> 5] >> (i & 31)) & 1u);
+      const unsigned long long m = __ballot(free_);
+      if (m) {
+        const int f = __builtin_ctzll(m);
+        const long long ef = __shfl(e, f);
+        const long long fi = ef & (kSelInfFlag - 1);
+        pick = (ef & kSelInfFlag) ? (fi < min_taken ? fi : min_taken) : fi;
+      }
+    }
+    if (pick < 0) pick = min_taken;   // every candidate taken: all read +inf, the lowest index wins
+    if (lane == 0) {
+      idx_out[b] = pick;
+      taken[pick >> 5] |= 1u << (pick & 31);
+    }
+    min_taken = pick < min_taken ? pick : min_taken;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
 // ----------------------------------------------------------------------------- launchers
 hipError_t launch_gemm_nn(hipStream_t s, int64_t M, int64_t Nc, int64_t K, double alpha, const double* A, int64_t lda,
                           const double* B, int64_t ldb, double beta, double* C, int64_t ldc) {
@@ -1069,18 +1277,26 @@ hipError_t launch_gemm_tn_lower(hipStream_t s, int64_t N, int64_t K, double alph
   return gemm<true, false, false, true>(s, N, N, K, alpha, A, lda, A, lda, beta, C, ldc, nullptr);
 }
 
+int64_t cand_cov_ws_doubles(int64_t N, int DP) { return N * ((DP + 3) / 4 * 4) + N; }
+
 hipError_t launch_cand_cov(hipStream_t stream, const GPDev& g, int d, int DP, const double* Xc, int64_t N, double* S,
-                           int64_t lds) {
-  const unsigned nt = (unsigned)((N + 15) / 16);
+                           int64_t lds, double* ws) {
+  if (N <= 0) return hipSuccess;
+  const int KP = (DP + 3) / 4 * 4;
+  double* Xs = ws;
+  double* xsq = ws + N * KP;
+  const unsigned sb = (unsigned)((N + 255) / 256);
+  const unsigned nt = (unsigned)((N + 63) / 64);
   dim3 grid(nt, nt);
-#define OMB_COV(DPV)                                                                                        \
-  case DPV:                                                                                                 \
-    if (g.kind == OMB_KERNEL_RBF)                                                                           \
-      hipLaunchKernelGGL((cand_cov_kernel<DPV, OMB_KERNEL_RBF>), grid, dim3(256), 0, stream, Xc, d, N, g.ls, \
-                         g.variance, S, lds);                                                               \
-    else                                                                                                    \
-      hipLaunchKernelGGL((cand_cov_kernel<DPV, OMB_KERNEL_MATERN52>), grid, dim3(256), 0, stream, Xc, d, N,  \
-                         g.ls, g.variance, S, lds);                                                         \
+#define OMB_COV(DPV)                                                                                          \
+  case DPV:                                                                                                   \
+    hipLaunchKernelGGL((cand_scale_kernel<DPV>), dim3(sb), dim3(256), 0, stream, Xc, d, N, g.ls, Xs, xsq);    \
+    if (g.kind == OMB_KERNEL_RBF)                                                                             \
+      hipLaunchKernelGGL((cand_cov_kernel<DPV, OMB_KERNEL_RBF>), grid, dim3(256), 0, stream, Xs, xsq, N,      \
+                         g.variance, S, lds);                                                                 \
+    else                                                                                                      \
+      hipLaunchKernelGGL((cand_cov_kernel<DPV, OMB_KERNEL_MATERN52>), grid, dim3(256), 0, stream, Xs, xsq, N, \
+                         g.variance, S, lds);                                                                 \
     break;
   switch (DP) {
     OMB_COV(2) OMB_COV(4) OMB_COV(6) OMB_COV(8) OMB_COV(16) OMB_COV(32) OMB_COV(64)
@@ -1124,10 +1340,39 @@ hipError_t launch_cholesky(hipStream_t stream, double* A, int64_t N, int64_t lda
   return e;
 }
 
+// K slices of the sample product: enough (tile, slice) workgroups to fill the chip (≥ 1024), slices of
+// ≥ 256 columns.  At B = 64 draws of N = 3000 candidates the unsplit product has 47 workgroups
+// (208 µs, profiles/r02_v21_c6_kernel_stats.csv).
+static int samples_split(int64_t N, int B) {
+  const int64_t tiles = ((B + kGT - 1) / kGT) * ((N + kGT - 1) / kGT);
+  int64_t S = (1024 + tiles - 1) / tiles;
+  const int64_t smax = (N + 255) / 256;
+  if (S > smax) S = smax;
+  if (S > 16) S = 16;
+  return S < 1 ? 1 : (int)S;
+}
+
+int64_t chol_samples_ws_doubles(int64_t N, int B) {
+  const int S = samples_split(N, B);
+  return S > 1 ? (int64_t)S * B * N : 0;
+}
+
 hipError_t launch_chol_samples(hipStream_t stream, const double* L, int64_t N, int64_t ldl, const double* mu,
-                               const double* Zt, int B, double* Y) {
+                               const double* Zt, int B, double* Y, double* ws) {
   // Y (B, N) = Zt · Lᵀ + μ  with  op(B)(k, j) = L[j][k] for k ≤ j (the factor's upper part is ignored)
-  return gemm<false, true, true, false>(stream, B, N, N, 1.0, Zt, N, L, ldl, 0.0, Y, N, mu);
+  const int S = samples_split(N, B);
+  if (S == 1) return gemm<false, true, true, false>(stream, B, N, N, 1.0, Zt, N, L, ldl, 0.0, Y, N, mu);
+  const int64_t kchunk = ((N + S - 1) / S + kGK - 1) / kGK * kGK;
+  const int64_t zstride = (int64_t)B * N;
+  dim3 grid((unsigned)((N + kGT - 1) / kGT), (unsigned)((B + kGT - 1) / kGT), (unsigned)S);
+  hipLaunchKernelGGL((gemm_kernel<false, true, true, false>), grid, dim3(256), 0, stream, (int64_t)B, N, N, 1.0, Zt,
+                     N, L, ldl, 0.0, ws, N, (const double*)nullptr, kchunk, zstride);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int64_t tot = (int64_t)B * N;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, ws, S, zstride,
+                     (int64_t)B, N, mu, Y, N);
+  return hipGetLastError();
 }
 
 hipError_t launch_gemm_tn(hipStream_t s, int64_t M, int64_t Nc, int64_t K, double alpha, const double* A, int64_t lda,
@@ -1182,34 +1427,73 @@ hipError_t launch_gp_grad(hipStream_t stream, int kind, int DP, const double* X,
   return hipGetLastError();
 }
 
-// Dense posterior path (n_train > OMB_MAX_TRAIN): μ_c = Σ_k α_k K*_kc, σ²_c = σ_f² − Σ_k V_kc² for the
-// columns of one candidate chunk; one thread per candidate, rows walked in order (coalesced).
-__global__ __launch_bounds__(256) void post_colreduce_kernel(const double* __restrict__ Kst,
-                                                             const double* __restrict__ V, int64_t n, int64_t Nc,
-                                                             const double* __restrict__ alpha, double variance,
-                                                             double* __restrict__ mu, double* __restrict__ var) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= Nc) return;
+// μ_c = Σ_k α_k K*_kc, σ²_c = σ_f² − Σ_k V_kc² for the columns of one candidate chunk (the dense
+// posterior path, n_train > OMB_MAX_TRAIN, and the Thompson-sampling mean).  Workgroup = 64 candidates
+// × 16 row slices (coalesced 512-B row segments); the slices' partial sums are added in slice order.
+// One thread per candidate over all rows ran 12 workgroups at N = 3000 (142 µs,
+// profiles/r02_v23_c6_kernel_stats.csv).
+constexpr int kColSlices = 16;
+__global__ __launch_bounds__(64 * kColSlices) void post_colreduce_kernel(const double* __restrict__ Kst,
+                                                                          const double* __restrict__ V, int64_t n,
+                                                                          int64_t Nc, const double* __restrict__ alpha,
+                                                                          double variance, double* __restrict__ mu,
+                                                                          double* __restrict__ var) {
+  __shared__ double pm[kColSlices][64], ps[kColSlices][64];
+  const int lane = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t rs = (n + kColSlices - 1) / kColSlices;
+  const int64_t k0 = sl * rs, k1 = (k0 + rs) < n ? (k0 + rs) : n;
   double m = 0.0, s = 0.0;
-  for (int64_t k = 0; k < n; ++k) {
-    m = fma(alpha[k], Kst[k * Nc + c], m);
-    const double v = V[k * Nc + c];
-    s = fma(v, v, s);
+  if (c < Nc) {
+    for (int64_t k = k0; k < k1; ++k) {
+      m = fma(alpha[k], Kst[k * Nc + c], m);
+      const double v = V[k * Nc + c];
+      s = fma(v, v, s);
+    }
   }
-  mu[c] = m;
-  var[c] = variance - s;
+  pm[sl][lane] = m;
+  ps[sl][lane] = s;
+  __syncthreads();
+  if (sl == 0 && c < Nc) {
+#pragma unroll
+    for (int j = 1; j < kColSlices; ++j) {
+      m += pm[j][lane];
+      s += ps[j][lane];
+    }
+    mu[c] = m;
+    var[c] = variance - s;
+  }
 }
 
 hipError_t launch_post_colreduce(hipStream_t stream, const double* Kst, const double* V, int64_t n, int64_t Nc,
                                  const double* alpha, double variance, double* mu, double* var) {
   if (Nc <= 0) return hipSuccess;
-  hipLaunchKernelGGL(post_colreduce_kernel, dim3((unsigned)((Nc + 255) / 256)), dim3(256), 0, stream, Kst, V, n, Nc,
-                     alpha, variance, mu, var);
+  hipLaunchKernelGGL(post_colreduce_kernel, dim3((unsigned)((Nc + 63) / 64)), dim3(64 * kColSlices), 0, stream, Kst, V,
+                     n, Nc, alpha, variance, mu, var);
   return hipGetLastError();
 }
 
-hipError_t launch_select(hipStream_t stream, const double* Y, int B, int64_t N, int64_t* idx) {
+static bool select_sorted(int B, int64_t N) { return N <= kSelectSortN && B >= 1; }
+
+int64_t select_ws_bytes(int B, int64_t N) {
+  if (!select_sorted(B, N)) return 0;
+  const int64_t K = B < N ? B : N;
+  return (int64_t)B * K * (int64_t)sizeof(long long);
+}
+
+hipError_t launch_select(hipStream_t stream, const double* Y, int B, int64_t N, int64_t* idx, void* ws) {
   if (B <= 0) return hipSuccess;
+  if (select_sorted(B, N)) {
+    int N2 = 2;
+    while (N2 < N) N2 <<= 1;
+    const int K = (int)(B < N ? B : N);
+    long long* heads = static_cast<long long*>(ws);
+    hipLaunchKernelGGL(select_sort_kernel, dim3((unsigned)B), dim3(kSelThreads), 0, stream, Y, N, N2, K, heads);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(select_greedy_kernel, dim3(1), dim3(256), 0, stream, heads, B, N, K, idx);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(select_kernel, dim3(1), dim3(1024), 0, stream, Y, B, N, idx);
   return hipGetLastError();
 }

@@ -221,7 +221,11 @@ constexpr int kblock_rows(int DP) {
 // group g: row 4e+g of 16 candidates) into 2 rows × 32 consecutive candidates per register, so each
 // store instruction writes 2 × 256 contiguous bytes instead of 4 × 128 (tools/microbench/mb_write:
 // 5.9-6.0 vs 5.3-5.4 TB/s for the bare store streams).
-template <int DP, int KIND, bool kNT = true, bool kSwap = false>
+// kTrans: the 8 waves' 16×16 tiles of a row tile go through LDS (tb, double buffered, one barrier per
+// row tile) and wave w stores rows 2w, 2w+1 of the workgroup's 128 candidates, one 1-KB row segment
+// per store instruction (b128 per lane), instead of 4 × 128 B.
+constexpr int kTransPitch = 144;   // tb row pitch (doubles): the 4 row groups of a tile write land on disjoint banks
+template <int DP, int KIND, bool kNT = true, bool kSwap = false, bool kTrans = false>
 __global__ __launch_bounds__(512) void kernel_block_pipe_kernel(GPDev g, int d, const double* __restrict__ Xc,
                                                                 int64_t N, double* __restrict__ K, ExpCoef ec) {
   constexpr bool kAug = DP <= 8;
@@ -234,6 +238,7 @@ __global__ __launch_bounds__(512) void kernel_block_pipe_kernel(GPDev g, int d, 
   __shared__ double etab[kTab256 ? 256 : 64];
   __shared__ double xfs[TPW * KSDP * 128];
   __shared__ double xsqs[kAug ? 1 : TPW * 16];
+  __shared__ __attribute__((aligned(16))) double tb[kTrans ? 2 * 16 * kTransPitch : 1];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int T0 = blockIdx.y * TPW;
@@ -268,6 +273,8 @@ __global__ __launch_bounds__(512) void kernel_block_pipe_kernel(GPDev g, int d, 
   }
   const double pm[3] = {g.variance, kSqrt5 * g.variance, kFiveThirds * g.variance};
   const bool cols_full = (int64_t)(blockIdx.x + 1) * 128 <= N;     // workgroup-uniform
+  // kTrans row segments are 16-B aligned when K is and N is even
+  const bool wide = cols_full && ((reinterpret_cast<uintptr_t>(K) & 15) == 0) && (N % 2 == 0);
   const int full_tiles = g.n / 16;                                  // tiles with all 16 rows < n
   // stored element e of a tile: row 16T + 4e + rsub, column col
   //   plain: rsub = lane>>4, col = cb + (lane&15);  swap: rsub = 2(lane>>5) (+1 for the second register),
@@ -326,7 +333,22 @@ __global__ __launch_bounds__(512) void kernel_block_pipe_kernel(GPDev g, int d, 
         }
       }
     } else {
-      if (cols_full && T < full_tiles) {
+      if (kTrans && wide && T < full_tiles) {
+        double* B = tb + (T & 1) * (16 * kTransPitch);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) B[(4 * e + (lane >> 4)) * kTransPitch + 16 * wave + (lane & 15)] = v[0][e];
+        __syncthreads();
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int row = 2 * wave + h;
+          const d2 val = *reinterpret_cast<const d2*>(B + row * kTransPitch + 2 * lane);
+          d2* dst = reinterpret_cast<d2*>(K + (int64_t)(16 * T + row) * N + (int64_t)blockIdx.x * 128 + 2 * lane);
+          if constexpr (kNT)
+            __builtin_nontemporal_store(val, dst);
+          else
+            *dst = val;
+        }
+      } else if (cols_full && T < full_tiles) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) st(p + e * N4, v[0][e]);
       } else if (col < N) {
@@ -750,6 +772,11 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
   }
 }
 
+// Per-workgroup phase timestamps of posterior_tile_kernel for tools/ablate/ablate_posterior (empty here).
+#ifndef OMB_POST_TRACE
+#define OMB_POST_TRACE(id)
+#endif
+
 // ----------------------------------------------------------------------------- posterior, n ≤ 256
 // Whole-tile variant for small training sets (BASELINE configs 2 and 4): the complete K* tile of the
 // workgroup (16·RMAX rows × BN = 16·CT candidates, 64 KiB) is generated into LDS in one pass, one
@@ -758,11 +785,17 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
 // per-chunk barriers, and its per-chunk MFMA split left SIMDs idle (at n = 128: 48 units on the
 // busiest SIMD against 36 on average).  Here the multiply is balanced exactly: SIMD s owns row-tile
 // pairs (q, RMAX−1−q), q ≡ s (mod 4), whose k-step counts 4(q+1) + 4(RMAX−q) are the same for every
-// pair; the two waves of a SIMD split the candidate tiles.  Two 64-KiB workgroups share a CU, so one
-// workgroup's generation (VALU) runs while the other multiplies (MFMA).
+// pair; the two waves of a SIMD split the candidate tiles.  At n_var ≤ 8 two 66-KiB workgroups share a
+// CU; at n_var > 8 the staged candidates (DP·BN doubles) take a workgroup to 82–98 KiB and one per CU.
+// The two workgroups do not overlap generation with multiply: FP64 VALU and FP64 MFMA share one pipe,
+// and the per-workgroup timeline (tools/ablate/ablate_posterior trace, profiles/r02_v28_ablate_c2_tile_trace.txt,
+// n = 128, 2^16 candidates, 2 objectives) shows a new workgroup's prologue (median 7.3 µs) waiting behind
+// its neighbour's multiply (5.6 µs), then generation 2.7 µs: one workgroup leaves a CU every 8.7 µs
+// against ≈ 5.8 µs of FP64-pipe work (144 MFMAs per SIMD for V, 16 for r², ≈ 640 transform VALU issues).
 //   gen:  wave w takes candidate tile w mod CT and row tiles w/CT + (8/CT)·i (RMAX·CT/8 tiles).
 //   K* in LDS in B-fragment order: element (row k, candidate c) at ((k/4)·CT + c/16)·64 + (k%4)·16 + c%16.
-// ABL (tools/ablate only): bit 2 skips the multiply, bit 4 feeds a constant A operand.
+// ABL (tools/ablate only): bit 2 skips the multiply, bit 4 feeds a constant A operand, bit 8 scales the
+// candidates by v_rcp_f64(ℓ) instead of dividing (timing only: not the GPy quotient).
 template <int RMAX, int CT, int DP, int KIND, int ABL = 0>
 __global__ __launch_bounds__(512, 2) void posterior_tile_kernel(GPArgs args, const double* __restrict__ Xc,
                                                                 int64_t N, double* __restrict__ mu_out,
@@ -783,6 +816,7 @@ __global__ __launch_bounds__(512, 2) void posterior_tile_kernel(GPArgs args, con
   static_assert(TILE >= 4 * BN + NW * 16, "reduction scratch must fit in the K* tile");
   __shared__ double kbuf[TILE + (kCandLds ? DP * BN : 0) + kTabN];
 
+  OMB_POST_TRACE(0);
   const int obj = blockIdx.y;
   const GPDev g = args.gp[obj];
   const int d = args.d;
@@ -806,6 +840,7 @@ __global__ __launch_bounds__(512, 2) void posterior_tile_kernel(GPArgs args, con
   if constexpr (kCandLds) __syncthreads();
   auto coord = [&](int j) -> double {
     if constexpr (kCandLds) return cand[j * BN + 16 * ct_g + (lane & 15)];
+    if constexpr (ABL & 8) return (j < d) ? Xc[ci * d + j] * __builtin_amdgcn_rcp(g.ls[j]) : 0.0;
     return (j < d) ? Xc[ci * d + j] / g.ls[j] : 0.0;
   };
   double csq = 0.0;
@@ -825,6 +860,7 @@ __global__ __launch_bounds__(512, 2) void posterior_tile_kernel(GPArgs args, con
   }
   const double pm[3] = {g.variance, kSqrt5 * g.variance, kFiveThirds * g.variance};
   if constexpr (!kCandLds) __syncthreads();          // etab
+  OMB_POST_TRACE(1);
 
   double mu_part = 0.0;
 #pragma unroll
@@ -860,7 +896,9 @@ __global__ __launch_bounds__(512, 2) void posterior_tile_kernel(GPArgs args, con
       }
     }
   }
+  OMB_POST_TRACE(2);
   __syncthreads();
+  OMB_POST_TRACE(3);
 
   // ---- V = L⁻¹ K*: SIMD s owns the row-tile pairs (q, RMAX−1−q), q = s + 4p; wave h of the SIMD the
   // candidate tiles h·CPW .. h·CPW + CPW − 1.  A (L⁻¹) k-step pairs stream from the packed copy two
@@ -924,6 +962,7 @@ __global__ __launch_bounds__(512, 2) void posterior_tile_kernel(GPArgs args, con
   double mp = mu_part;
   mp += __shfl_xor(mp, 16);
   mp += __shfl_xor(mp, 32);
+  OMB_POST_TRACE(4);
   __syncthreads();                                  // every wave is done reading K*
   double* red = kbuf;                               // [4 SIMDs][BN]
   double* redmu = kbuf + 4 * BN;                    // [NW waves][16]
@@ -943,6 +982,7 @@ __global__ __launch_bounds__(512, 2) void posterior_tile_kernel(GPArgs args, con
       var_out[(int64_t)obj * N + c] = g.variance - s;
     }
   }
+  OMB_POST_TRACE(5);
 }
 
 // ----------------------------------------------------------------------------- dispatch

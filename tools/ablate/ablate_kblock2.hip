@@ -100,7 +100,9 @@ void bench(int n, int64_t N, int d) {
   auto pipe_pl = [&] { hipLaunchKernelGGL((kernel_block_pipe_kernel<DP, 0, false>), g3, dim3(512), 0, 0, g, d, Xc, N, K1, ec); };
   auto swap_nt = [&] { hipLaunchKernelGGL((kernel_block_pipe_kernel<DP, 0, true, true>), g3, dim3(512), 0, 0, g, d, Xc, N, K1, ec); };
   auto swap_pl = [&] { hipLaunchKernelGGL((kernel_block_pipe_kernel<DP, 0, false, true>), g3, dim3(512), 0, 0, g, d, Xc, N, K1, ec); };
-  float t[7] = {0, 0, 0, 0, 0, 0, 0};
+  auto trans_nt = [&] { hipLaunchKernelGGL((kernel_block_pipe_kernel<DP, 0, true, false, true>), g3, dim3(512), 0, 0, g, d, Xc, N, K1, ec); };
+  auto trans_pl = [&] { hipLaunchKernelGGL((kernel_block_pipe_kernel<DP, 0, false, false, true>), g3, dim3(512), 0, 0, g, d, Xc, N, K1, ec); };
+  float t[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   for (int r = 0; r < 3; ++r) {
     t[0] += time_ms(old_k, 5);
     t[1] += time_ms(mfma_nt, 5);
@@ -109,26 +111,29 @@ void bench(int n, int64_t N, int d) {
     t[4] += time_ms(swap_pl, 5);
     t[5] += time_ms(pipe_nt, 5);
     t[6] += time_ms(pipe_pl, 5);
+    t[7] += time_ms(trans_nt, 5);
+    t[8] += time_ms(trans_pl, 5);
   }
-  const char* names[7] = {"VALU dots (r01 baseline)", "MFMA r2, 4x128-B rows, nt (r01 library)", "MFMA r2, 4x128-B rows, plain",
+  const char* names[9] = {"VALU dots (r01 baseline)", "MFMA r2, 4x128-B rows, nt (r01 library)", "MFMA r2, 4x128-B rows, plain",
                           "LDS-staged + permlane16 swap, 2x256-B rows, nt", "LDS-staged + permlane16 swap, 2x256-B rows, plain",
-                          "Xf staged in LDS + base-pointer stores, nt", "Xf staged in LDS + base-pointer stores, plain"};
+                          "Xf staged in LDS + base-pointer stores, nt", "Xf staged in LDS + base-pointer stores, plain",
+                          "LDS transpose, 1-KB row stores (b128), nt", "LDS transpose, 1-KB row stores (b128), plain"};
   const double bytes = 8.0 * (n + d) * N + 8.0 * n * (d + 1);
-  for (int i = 0; i < 7; ++i)
+  for (int i = 0; i < 9; ++i)
     printf("n=%d N=%lld d=%d  %-48s %.3f ms  %.0f GB/s  (%.3f of 8 TB/s)\n", n, (long long)N, d, names[i], t[i] / 3,
            bytes / (t[i] / 3 * 1e6), bytes / (t[i] / 3 * 1e6) / 8000.0);
   std::vector<double> h1((size_t)n * N), h2((size_t)n * N);
   mfma_nt();
   CK(hipDeviceSynchronize());
   CK(hipMemcpy(h2.data(), K2, h2.size() * 8, hipMemcpyDeviceToHost));
-  for (int v = 0; v < 2; ++v) {
+  for (int v = 0; v < 3; ++v) {
     CK(hipMemset(K1, 0, h1.size() * 8));
-    if (v == 0) swap_nt(); else pipe_nt();
+    if (v == 0) swap_nt(); else if (v == 1) pipe_nt(); else trans_nt();
     CK(hipDeviceSynchronize());
     CK(hipMemcpy(h1.data(), K1, h1.size() * 8, hipMemcpyDeviceToHost));
     size_t ndiff = 0;
     for (size_t i = 0; i < h1.size(); ++i) ndiff += (h1[i] != h2[i]);
-    printf("%s vs r01 kernel: %zu of %zu elements differ (must be 0: same arithmetic)\n", v ? "pipe" : "swap", ndiff,
+    printf("%s vs r01 kernel: %zu of %zu elements differ (must be 0: same arithmetic)\n", v == 2 ? "trans" : (v ? "pipe" : "swap"), ndiff,
            h1.size());
   }
 }

@@ -7,7 +7,26 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <vector>
+
+// phase timestamps (100 MHz constant clock) and hardware id of every workgroup of posterior_tile_kernel
+__device__ unsigned long long g_ptrace[4096][8];
+#define OMB_POST_TRACE(id)                                                              \
+  do {                                                                                  \
+    if (threadIdx.x == 0) {                                                             \
+      const unsigned wg_ = blockIdx.y * gridDim.x + blockIdx.x;                         \
+      if (wg_ < 4096) {                                                                 \
+        g_ptrace[wg_][id] = __builtin_amdgcn_s_memrealtime();                           \
+        if ((id) == 0) {                                                                \
+          unsigned hw_, xcc_;                                                           \
+          asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));             \
+          asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));           \
+          g_ptrace[wg_][7] = ((unsigned long long)xcc_ << 32) | hw_;                    \
+        }                                                                               \
+      }                                                                                 \
+    }                                                                                   \
+  } while (0)
 
 #include "../../optimobo_amd/csrc/omb_posterior.hip"
 
@@ -114,6 +133,44 @@ void matern_accuracy() {
   CK(hipFree(dr2)); CK(hipFree(dout));
 }
 
+// Phase timeline of the library's n ≤ 128 tile kernel: per-workgroup durations of prologue, generation,
+// barrier wait, multiply and reduction, and how many workgroups are resident per CU over time.
+void trace_tile(const Bench& b) {
+  dim3 grid((unsigned)((b.N + 63) / 64), b.n_obj);
+  const unsigned nwg = grid.x * grid.y;
+  if (nwg > 4096) { printf("trace: too many workgroups\n"); return; }
+  for (int rep = 0; rep < 3; ++rep)
+    hipLaunchKernelGGL((posterior_tile_kernel<8, 4, 6, 0, 0>), grid, dim3(512), 0, 0, b.a, b.Xc, b.N, b.mu, b.var);
+  CK(hipDeviceSynchronize());
+  std::vector<unsigned long long> t(4096 * 8);
+  CK(hipMemcpyFromSymbol(t.data(), HIP_SYMBOL(g_ptrace), t.size() * 8));
+  unsigned long long t0 = ~0ull, t1 = 0;
+  for (unsigned w = 0; w < nwg; ++w) { t0 = std::min(t0, t[w * 8]); t1 = std::max(t1, t[w * 8 + 5]); }
+  const char* ph[5] = {"prologue (etab, candidates)", "generation", "barrier wait", "multiply", "reduction + store"};
+  printf("tile kernel trace: %u workgroups, span %.2f us (first start to last end)\n", nwg, (t1 - t0) / 100.0);
+  for (int p = 0; p < 5; ++p) {
+    std::vector<double> d;
+    for (unsigned w = 0; w < nwg; ++w) d.push_back((t[w * 8 + p + 1] - t[w * 8 + p]) / 100.0);
+    std::sort(d.begin(), d.end());
+    double s = 0; for (double x : d) s += x;
+    printf("  %-28s mean %6.2f us  p10 %6.2f  p50 %6.2f  p90 %6.2f\n", ph[p], s / d.size(), d[d.size() / 10], d[d.size() / 2],
+           d[d.size() * 9 / 10]);
+  }
+  std::vector<double> life;
+  for (unsigned w = 0; w < nwg; ++w) life.push_back((t[w * 8 + 5] - t[w * 8]) / 100.0);
+  std::sort(life.begin(), life.end());
+  printf("  workgroup lifetime p50 %.2f us; sum of lifetimes / span = %.1f workgroups resident on average\n",
+         life[life.size() / 2], [&] { double s = 0; for (double x : life) s += x; return s; }() / ((t1 - t0) / 100.0));
+  // start-time histogram in 2-us bins
+  printf("  starts per 2-us bin:");
+  for (unsigned long long s = t0; s < t1; s += 200) {
+    int c = 0;
+    for (unsigned w = 0; w < nwg; ++w) c += (t[w * 8] >= s && t[w * 8] < s + 200);
+    printf(" %d", c);
+  }
+  printf("\n");
+}
+
 struct Variant {
   const char* name;
   float (*fn)(const Bench&, int);
@@ -205,6 +262,8 @@ int main(int argc, char** argv) {
       {"RT1 CT4 barrier (r01 library)", run<1, 4, 8, 32>},
       {"tile RMAX8 CT4 gen only (2)", run_tile<8, 4, 2>},
       {"tile RMAX8 CT4 const A (4)", run_tile<8, 4, 4>},
+      {"tile RMAX8 CT4 rcp candidates (8)", run_tile<8, 4, 8>},
+      {"tile RMAX8 CT4 rcp, gen only (10)", run_tile<8, 4, 10>},
       {"tile RMAX16 CT2", run_tile<16, 2, 0>},
       {"RT1 CT2 counter ring", run<1, 2, 8, 0>},
   };
@@ -228,6 +287,7 @@ int main(int argc, char** argv) {
       {"RT1 CT2 barrier", run<1, 2, 8, 32>},
   };
   matern_accuracy();
+  if (d == 6 && n <= 128) trace_tile(b);
   const bool is_small = d == 6 && n <= 256;
   (void)small;
   const Variant* vs = is_small ? (n <= 128 ? small128 : small256) : (d == 6 ? narrow : wide);

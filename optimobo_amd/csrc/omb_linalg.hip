@@ -300,8 +300,8 @@ __device__ __forceinline__ void static_for(F&& f) {
 //                       MFMA (16 rows per 2-wave workgroup; W_kk's B fragments read from the workspace);
 //   chol_update_kernel  the trailing update A22 −= L21 L21ᵀ (lower triangle, 64×64 MFMA tiles) whose
 //                       workgroup owning the next diagonal tile factors it right after its update
-//                       (chol64_block), inverts the factor and writes L_{k+1,k+1} and the fragments of
-//                       W_{k+1,k+1} for the next panel (chol64_finish);
+//                       (chol64_factor), inverts the factor and writes L_{k+1,k+1} and the fragments of
+//                       W_{k+1,k+1} for the next panel (chol64_factor, chol64_inverse);
 //   chol_diag_kernel    step 0's diagonal block (nothing precedes it).
 // The serial chain of a step is the diagonal workgroup's factor + inverse.  Round 2's panel solved
 // x · L_kkᵀ = b by substitution, a 64-step dependent chain per row with an LDS broadcast read at every
@@ -312,157 +312,165 @@ __device__ __forceinline__ void static_for(F&& f) {
 
 // LDS of the diagonal-block factorisation (diagonal workgroups of chol_update_kernel, chol_diag_kernel):
 //   Lb    4 sub-blocks × 64 rows × kLbP doubles: Lb[(b·64 + r)·kLbP + q] = L[r][16b + q]; the 144-B row
-//         pitch keeps 16 lanes reading 16 different rows (the bulk updates, the L store) conflict-free;
-//   cbuf  2 × 64: the current column, double buffered;  dinv  64: 1/L_jj.
+//         pitch keeps 16 lanes reading 16 different rows conflict-free;
+//   aux   cbuf (2 × 64: the current column, double buffered) | dinv (64: 1/L_jj);
+//   prog  4 ints: columns of sub-block b published to Lb so far.
 constexpr int kLbP = 18;
 constexpr int kLbDoubles = 4 * kNB * kLbP;
 constexpr int kCholAux = 2 * kNB + kNB;
 
 // Factor a 64×64 SPD block with the 4 waves of a 256-thread workgroup: thread (wave w, lane r) holds
 // a[q] = A[r][16w + q] (only 16w + q ≤ r is meaningful; rows past the block are identity rows).
-// Sub-block b (columns 16b..16b+15) is factored by wave b alone — 16 column steps, each updating only
-// the rest of the sub-block: the next column's entry L[j+1][j] by v_readlane (the serial chain), the
-// others as LDS broadcasts of the column (their latency hides behind the next pivot) — and published to
-// Lb; then every later wave subtracts its contribution from its own columns in bulk
-// (L[r][16w+q] −= Σ_j L[r][j] L[16w+q][j]).  Round 2 measured 300 cycles per column with every entry
-// by v_readlane (two 4-cycle VALU ops per entry, profiles/r02_v22_chol_diag_trace.txt).
+// Wave b factors sub-block b (columns 16b..16b+15).  Before its turn it applies every earlier
+// sub-block's columns to its own 16 columns as they are published (a progress counter per sub-block
+// in LDS; L[r][j]·L[16w+q][j] from Lb), so when the previous wave finishes, the next one starts at once
+// — round 2's bulk update after every 16 columns took ≈ 2 µs each (profiles/r02_v24_ablate_chol.txt).
+// Column j of the own sub-block:
+//   * the serial chain runs on wave-uniform values: d_{j+1} = A'_{j+1,j+1} − (a_{j+1,j}·inv_j)², where
+//     A' and a_{j+1,j} were read (v_readlane) before inv_j is known — 9 dependent FP64 ops per column
+//     (rsq, two Newton steps, one mul, one fma);
+//   * the next two rows' entries of column j are applied at once (uniform scalars a_{j+k,j}·inv_j), the
+//     rest one column later from an LDS broadcast of the column (software pipeline);
+//   * the column goes to Lb for the later waves, then the progress counter moves (release order).
 // Entries above the diagonal are not kept at zero (a[jj] is scaled on every row, no selects); they
 // only ever feed entries above the diagonal of the same row, which nothing reads.
-// On return (after a barrier) Lb holds L, dinv[j] = 1/L_jj, bad_lds[0] = 1-based first non-positive
-// pivot column or 0.
-__device__ __forceinline__ void chol64_block(double (&a)[16], int w, int r, double* Lb, double* aux, int* bad_lds) {
+// When its sub-block is done, the wave stores its 16 columns of L into A (rows < nb), then inverts its
+// 16×16 diagonal block by substitution (x[m] = (δ_mc − Σ_{p<m} L_ww[m][p] x[p]) / L_ww[m][m], lane l →
+// column l & 15, rows of L_ww as LDS broadcasts), leaves W_ww in place of L_ww in Lb and writes W_ww's
+// fragments to Wf (see chol64_inverse) — while the later waves are still factoring.
+// bad_lds[0] = 1-based first non-positive pivot column or 0 (valid after the caller's barrier).
+__device__ __forceinline__ void chol64_factor(double (&a)[16], int w, int r, int nb, double* Lb, double* aux,
+                                              int* prog, int* bad_lds, double* __restrict__ A, int64_t lda,
+                                              int64_t c0, double* __restrict__ Wf) {
   double* dinv = aux + 2 * kNB;
-  int bad = 0;
+  // ---- earlier sub-blocks' columns, as they appear
+#pragma unroll 1
+  for (int b = 0; b < w; ++b) {
+#pragma unroll 1   // rolled: unrolled, the column reads were merged and hoisted (512 VGPRs + spills)
+    for (int jj = 0; jj < 16; ++jj) {
+      while (__hip_atomic_load(&prog[b], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= jj)
+        __builtin_amdgcn_s_sleep(1);
+      const double lr = Lb[(b * 64 + r) * kLbP + jj];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) a[q] = fma(-lr, Lb[(b * 64 + 16 * w + q) * kLbP + jj], a[q]);
+    }
+  }
+  // ---- own sub-block
   static_for<0, 4>([&](auto bc) {
     constexpr int b = decltype(bc)::value;
-    if (w == b) {
-      OMB_CHOL_TRACE(2 + 2 * b, r == 0);
-      double pl = 0.0;   // the previous column's entry of this row
-      double pv[16];     // the previous column's entries L[16b+q][j−1] (q ≥ jj+1), from LDS
-      static_for<0, 16>([&](auto jc) {
-        constexpr int jj = decltype(jc)::value;
-        constexpr int j = 16 * b + jj;
-        double dj = readlane_f64(a[jj], j);            // pivot (wave-uniform)
-        if (!(dj > 0.0)) {
-          if (bad == 0) bad = j + 1;
-          dj = 1.0;                                    // continue without NaNs; flagged
-        }
-        const double y0 = __builtin_amdgcn_rsq(dj);
-        const double hd = 0.5 * dj;
-        const double y1 = fma(y0, fma(-hd * y0, y0, 0.5), y0);
-        const double inv = fma(y1, fma(-hd * y1, y1, 0.5), y1);
-        if (r == j) dinv[j] = inv;
-        const double lrj = a[jj] * inv;                // row j: dj·inv = √dj
-        a[jj] = lrj;
-        // the chain: column j's entry of the next pivot's row
-        if constexpr (jj < 15) a[jj + 1] = fma(-lrj, readlane_f64(lrj, j + 1), a[jj + 1]);
-        // software pipeline: column j−1's other updates, its entries loaded one column ago
-        if constexpr (jj >= 1) {
+    if (w != b) return;
+    OMB_CHOL_TRACE(2 + 2 * b, r == 0);
+    int bad = 0;
+    double dj = readlane_f64(a[0], 16 * b);          // first pivot (every earlier column applied)
+    double pl = 0.0;   // the previous column's entry of this row
+    double pv[16];     // the previous column's entries L[16b+q][j−1] (q ≥ jj+2), from LDS
+    // order within column j: chain (pre-read entries, inv, next pivot), scale + the next two rows,
+    // publish (Lb, progress), then column j−1's deferred updates, then column j's broadcast loads —
+    // the loads' LDS latency hides behind the next column's chain
+    static_for<0, 16>([&](auto jc) {
+      constexpr int jj = decltype(jc)::value;
+      constexpr int j = 16 * b + jj;
+      // entries for the chain and the next two rows (column j−1's deferred updates never touch them)
+      double a1 = 0.0, a2 = 0.0, ap = 0.0;
+      if constexpr (jj < 15) {
+        a1 = readlane_f64(a[jj], j + 1);
+        ap = readlane_f64(a[jj + 1], j + 1);
+      }
+      if constexpr (jj < 14) a2 = readlane_f64(a[jj], j + 2);
+      if (!(dj > 0.0)) {
+        if (bad == 0) bad = j + 1;
+        dj = 1.0;                                      // continue without NaNs; flagged
+      }
+      const double y0 = __builtin_amdgcn_rsq(dj);
+      const double hd = 0.5 * dj;
+      const double y1 = fma(y0, fma(-hd * y0, y0, 0.5), y0);
+      const double inv = fma(y1, fma(-hd * y1, y1, 0.5), y1);
+      double s1 = 0.0, s2 = 0.0;
+      if constexpr (jj < 15) {
+        s1 = a1 * inv;                                 // L[j+1][j]
+        dj = fma(-s1, s1, ap);                         // next pivot
+      }
+      if constexpr (jj < 14) s2 = a2 * inv;            // L[j+2][j]
+      const double lrj = a[jj] * inv;                  // row j: dj·inv = √dj
+      a[jj] = lrj;
+      if constexpr (jj < 15) a[jj + 1] = fma(-lrj, s1, a[jj + 1]);
+      if constexpr (jj < 14) a[jj + 2] = fma(-lrj, s2, a[jj + 2]);
+      // publish the column, then release it to the later waves (before any new LDS load is queued)
+      if (r == j) dinv[j] = inv;
+      Lb[(b * 64 + r) * kLbP + jj] = lrj;
+      if constexpr (b < 3) {
+        if (r == 0) __hip_atomic_store(&prog[b], jj + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      // column j−1's remaining updates (q ≥ jj+2; loaded one column ago, their latency behind the chain)
+      if constexpr (jj >= 1) {
 #pragma unroll
-          for (int q = jj + 1; q < 16; ++q) a[q] = fma(-pl, pv[q], a[q]);
-        }
-        if constexpr (jj < 14) {
-          double* cb = aux + kNB * (jj & 1);
-          cb[r] = lrj;
+        for (int q = jj + 2; q < 16; ++q) a[q] = fma(-pl, pv[q], a[q]);
+      }
+      if constexpr (jj < 13) {
+        double* cb = aux + kNB * (jj & 1);
+        cb[r] = lrj;
 #pragma unroll
-          for (int q = jj + 2; q < 16; ++q) pv[q] = cb[16 * b + q];
-          pl = lrj;
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      });
-      OMB_CHOL_TRACE(3 + 2 * b, r == 0);
+        for (int q = jj + 3; q < 16; ++q) pv[q] = cb[16 * b + q];
+        pl = lrj;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    OMB_CHOL_TRACE(3 + 2 * b, r == 0);
+    if (r == 0 && bad) bad_lds[0] = bad;
+    // ---- this sub-block's 16 columns of L into A: lane → (row 4i + (r >> 4), column r & 15)
+    {
+      const int q = r & 15;
+      double lv[16];
 #pragma unroll
-      for (int q = 0; q < 16; q += 2)
-        *reinterpret_cast<double2*>(Lb + (b * 64 + r) * kLbP + q) = double2{a[q], a[q + 1]};
-      if (r == 0 && bad) bad_lds[0] = bad;
-    }
-    __syncthreads();
-    if constexpr (b < 3) {
-      if (w > b) {
-        // own row's sub-block-b values, then one dot product per owned column
-        const double2* mine = reinterpret_cast<const double2*>(Lb + (b * 64 + r) * kLbP);
-        double lr[16];
+      for (int i = 0; i < 16; ++i) lv[i] = Lb[(b * 64 + 4 * i + (r >> 4)) * kLbP + q];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const double2 v = mine[q];
-          lr[2 * q] = v.x;
-          lr[2 * q + 1] = v.y;
-        }
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const double2* other = reinterpret_cast<const double2*>(Lb + (b * 64 + 16 * w + q) * kLbP);
-          double s0 = 0.0, s1 = 0.0;
-#pragma unroll
-          for (int h = 0; h < 8; ++h) {
-            const double2 v = other[h];
-            s0 = fma(lr[2 * h], v.x, s0);
-            s1 = fma(lr[2 * h + 1], v.y, s1);
-          }
-          a[q] -= s0 + s1;
-        }
-        OMB_CHOL_TRACE(10 + b, w == 3 && r == 0);
+      for (int i = 0; i < 16; ++i) {
+        const int row = 4 * i + (r >> 4);
+        if (row < nb && 16 * b + q <= row) A[(c0 + row) * lda + c0 + 16 * b + q] = lv[i];
       }
     }
+    // ---- W_bb = L_bb⁻¹, column c = r & 15 per lane
+    const int c = r & 15, g = r >> 4;
+    const double* Ld = Lb + (b * 64 + 16 * b) * kLbP;   // L_bb row m at Ld + m·kLbP
+    double x[16];
+    static_for<0, 16>([&](auto mc) {
+      constexpr int m = decltype(mc)::value;
+      // row m's offset passes through an empty asm that consumes x[m−2]: its reads issue one row
+      // ahead of their use, not all 120 at once (which took the kernel to 256 VGPRs)
+      int off = m * kLbP;
+      if constexpr (m >= 2) asm volatile("" : "+v"(off) : "v"(x[m - 2]));
+      double t0 = (m == c) ? 1.0 : 0.0, t1 = 0.0;
+#pragma unroll
+      for (int p = 0; p + 1 < m; p += 2) {
+        const double2 l = *reinterpret_cast<const double2*>(Ld + off + p);
+        t0 = fma(-l.x, x[p], t0);
+        t1 = fma(-l.y, x[p + 1], t1);
+      }
+      if constexpr (m & 1) t0 = fma(-Ld[off + m - 1], x[m - 1], t0);
+      x[m] = (t0 + t1) * dinv[16 * b + m];
+    });
+    // every lane's reads of L_bb precede the overwrite (LDS operations of a wave complete in order)
+    if (r < 16) {
+#pragma unroll
+      for (int m = 0; m < 16; ++m) Lb[(b * 64 + 16 * b + m) * kLbP + c] = x[m];
+    }
+    // W_bb's fragments: rows jb = b, k-steps s = 4b + u: W[16b + c][16b + 4g + u]
+#pragma unroll
+    for (int u = 0; u < 4; ++u) Wf[(b * 16 + 4 * b + u) * 64 + r] = Lb[(b * 64 + 16 * b + c) * kLbP + 4 * g + u];
+    OMB_CHOL_TRACE(10 + b, r == 0);
   });
 }
 
-// After chol64_block: writes L (rows < nb of the block at c0) into A's lower triangle (coalesced rows
-// from Lb), the first bad pivot into info, and W = L⁻¹ as the MFMA B fragments of chol_panel_kernel:
+// After chol64_factor and a barrier: the off-diagonal blocks of W = L⁻¹ into Wf, the MFMA B fragments
+// of chol_panel_kernel:
 //   Wf[(jb·16 + s)·64 + l] = W[16jb + (l & 15)][m(s, l >> 4)],   m(s, g) = 16(s >> 2) + 4g + (s & 3)
 // (k-step s of the panel's output column block jb; only s < 4(jb + 1) is read — the rest of that row
 // block of W is zero — so the panel skips W's upper triangle in whole k-steps).
-// Phase 1: wave i inverts its diagonal 16×16 block by substitution, lane l → column c = l & 15:
-// x[m] = (δ_mc − Σ_{p<m} L_ii[m][p] x[p]) / L_ii[m][m], the rows of L_ii as LDS broadcasts, and leaves
-// W_ii in place of L_ii in Lb.  Phase 2: wave j forms its column block, W_ij = −W_ii Σ_{k=j}^{i−1} L_ik W_kj
-// for i = j+1..3, on MFMA: a product's accumulator layout (lane l: rows 4e + (l >> 4), column l & 15) is
-// the next product's B operand layout, so the W_kj (k > j) stay in registers and only L and the W_ii
-// are read from LDS.
-__device__ __forceinline__ void chol64_finish(int w, int r, int nb, int bad, double* Lb, const double* aux,
-                                              double* __restrict__ A, int64_t lda, int64_t c0,
-                                              double* __restrict__ Wf, int* __restrict__ info) {
-  const double* dinv = aux + 2 * kNB;
-  double lv[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) lv[i] = Lb[((r >> 4) * 64 + w + 4 * i) * kLbP + (r & 15)];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int row = w + 4 * i, col = r;
-    if (row < nb && col <= row) A[(c0 + row) * lda + c0 + col] = lv[i];
-  }
-  if (w == 0 && r == 0 && bad) atomicCAS(info, 0, (int)(c0 + bad));
-  OMB_CHOL_TRACE(13, w == 0 && r == 0);
+// Wave j forms its column block, W_ij = −W_ii Σ_{k=j}^{i−1} L_ik W_kj for i = j+1..3, on MFMA: a product's
+// accumulator layout (lane l: rows 4e + (l >> 4), column l & 15) is the next product's B operand
+// layout, so the W_kj (k > j) stay in registers and only L and the W_ii are read from LDS.
+__device__ __forceinline__ void chol64_inverse(int w, int r, const double* Lb, double* __restrict__ Wf) {
   const int c = r & 15, g = r >> 4;
-  // phase 1: x[m] = W_ww[m][c]
-  const double* Ld = Lb + (w * 64 + 16 * w) * kLbP;   // L_ww row m at Ld + m·kLbP
-  double x[16];
-  static_for<0, 16>([&](auto mc) {
-    constexpr int m = decltype(mc)::value;
-    // row m's offset passes through an empty asm that consumes x[m−2]: its reads issue one row ahead
-    // of their use, not all 120 at once (which took the kernel to 256 VGPRs)
-    int off = m * kLbP;
-    if constexpr (m >= 2) asm volatile("" : "+v"(off) : "v"(x[m - 2]));
-    double s0 = (m == c) ? 1.0 : 0.0, s1 = 0.0;
-#pragma unroll
-    for (int p = 0; p + 1 < m; p += 2) {
-      const double2 l = *reinterpret_cast<const double2*>(Ld + off + p);
-      s0 = fma(-l.x, x[p], s0);
-      s1 = fma(-l.y, x[p + 1], s1);
-    }
-    if constexpr (m & 1) s0 = fma(-Ld[off + m - 1], x[m - 1], s0);
-    x[m] = (s0 + s1) * dinv[16 * w + m];
-  });
-  __syncthreads();                                     // every wave's phase-1 reads of Lb are done
-  if (r < 16) {
-#pragma unroll
-    for (int m = 0; m < 16; ++m) Lb[(w * 64 + 16 * w + m) * kLbP + c] = x[m];
-  }
-  OMB_CHOL_TRACE(14, w == 0 && r == 0);
-  __syncthreads();
-  OMB_CHOL_TRACE(15, w == 0 && r == 0);
-  // W_ww's fragments: rows jb = w, k-steps s = 4w + u: W[16w + c][16w + 4g + u]
-#pragma unroll
-  for (int u = 0; u < 4; ++u) Wf[(w * 16 + 4 * w + u) * 64 + r] = Lb[(w * 64 + 16 * w + c) * kLbP + 4 * g + u];
-  // phase 2
   d4 Wc[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) Wc[i] = d4{0.0, 0.0, 0.0, 0.0};
@@ -476,7 +484,7 @@ __device__ __forceinline__ void chol64_finish(int w, int r, int nb, int bad, dou
           static_for<0, 4>([&](auto sc) {
             constexpr int s = decltype(sc)::value;
             const double av = Lb[(k * 64 + 16 * i + c) * kLbP + 4 * s + g];   // L[16i + c][16k + 4s + g]
-            // B operand W_kj[4s + g][c]: W_ww from LDS (phase 1), the others from registers
+            // B operand W_kj[4s + g][c]: W_ww from LDS, the others from registers
             const double bv = (k == w) ? Lb[(k * 64 + 16 * k + 4 * s + g) * kLbP + c] : Wc[k][s];
             T = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, T, 0, 0, 0);
           });
@@ -499,11 +507,13 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(double* __restrict__ A, 
                                                          double* __restrict__ ws, int* __restrict__ info) {
   __shared__ __attribute__((aligned(16))) double Lb[kLbDoubles];
   __shared__ double aux[kCholAux];
+  __shared__ int prog[4];
   __shared__ int bad_lds[1];
   const int nb = (int)(N < kNB ? N : kNB);
   const int r = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   OMB_CHOL_TRACE(0, threadIdx.x == 0);
   if (threadIdx.x == 0) bad_lds[0] = 0;
+  if (threadIdx.x < 4) prog[threadIdx.x] = 0;
   double a[16];
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
@@ -514,11 +524,15 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(double* __restrict__ A, 
   }
   __syncthreads();
   OMB_CHOL_TRACE(1, threadIdx.x == 0);
-  chol64_block(a, w, r, Lb, aux, bad_lds);
-  chol64_finish(w, r, nb, bad_lds[0], Lb, aux, A, lda, 0, ws, info);
+  chol64_factor(a, w, r, nb, Lb, aux, prog, bad_lds, A, lda, 0, ws);
+  __syncthreads();
+  OMB_CHOL_TRACE(15, threadIdx.x == 0);
+  if (threadIdx.x == 0 && bad_lds[0]) atomicCAS(info, 0, bad_lds[0]);
+  chol64_inverse(w, r, Lb, ws);
 }
 
-// Panel of step `step`: rows c0+64 .. N−1, L21 = A21 · Wᵀ (W = L_kk⁻¹ from chol64_finish's fragments).
+// Panel of step `step`: rows c0+64 .. N−1, L21 = A21 · Wᵀ (W = L_kk⁻¹ from the fragments of chol64_factor /
+// chol64_inverse).
 // Workgroup = 16 rows, 2 waves: wave 0 the output column blocks 0 and 3, wave 1 blocks 1 and 2 (20
 // MFMAs each).  The k index is permuted as m(s, g) = 16(s >> 2) + 4g + (s & 3) so a lane's A operands
 // are 4 contiguous doubles per 16-column group; the barrier separates both waves' reads of the rows
@@ -591,6 +605,7 @@ __global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A
   static_assert(2 * 2 * kGK * kGP <= kLbDoubles && kNB * (kNB + 1) <= kLbDoubles, "LDS carve-up");
   __shared__ __attribute__((aligned(16))) double smem[kLbDoubles];
   __shared__ double aux[kCholAux];
+  __shared__ int prog[4];
   auto& As = *reinterpret_cast<double (*)[2][kGK][kGP]>(smem);                      // As[buf][k][m] = L21(m0 + m, k0 + k)
   auto& Bs = *reinterpret_cast<double (*)[2][kGK][kGP]>(smem + 2 * kGK * kGP);      // Bs[buf][k][n] = L21(n0 + n, k0 + k)
   __shared__ int bad_lds[1];
@@ -677,9 +692,12 @@ __global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A
     a[q] = (r < nb && c <= r) ? D[r * 65 + c] : (c == r ? 1.0 : 0.0);
   }
   if (tid == 0) bad_lds[0] = 0;
+  if (tid < 4) prog[tid] = 0;
   __syncthreads();                                           // D consumed: smem becomes Lb
-  chol64_block(a, w, r, smem, aux, bad_lds);
-  chol64_finish(w, r, nb, bad_lds[0], smem, aux, A, lda, r0, ws, info);
+  chol64_factor(a, w, r, nb, smem, aux, prog, bad_lds, A, lda, r0, ws);
+  __syncthreads();
+  if (tid == 0 && bad_lds[0]) atomicCAS(info, 0, (int)(r0 + bad_lds[0]));
+  chol64_inverse(w, r, smem, ws);
 }
 
 // ----------------------------------------------------------------------------- triangular inverse

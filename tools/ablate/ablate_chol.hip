@@ -34,8 +34,8 @@ static void trace_diag() {
   CK(hipMalloc(&ws, kCholWsDoubles * 8));
   CK(hipMalloc(&info, 64));
   const char* names[17] = {"start", "loaded", "b0 begin", "b0 factored", "b1 begin", "b1 factored", "b2 begin",
-                           "b2 factored", "b3 begin", "b3 factored", "bulk0 (w3)", "bulk1 (w3)", "bulk2 (w3)",
-                           "L stored", "W_ii done", "barrier", "W done"};
+                           "b2 factored", "b3 begin", "b3 factored", "w0 L + W_00", "w1 L + W_11", "w2 L + W_22",
+                           "w3 L + W_33", "(unused)", "barrier", "W done"};
   for (int rep = 0; rep < 3; ++rep) {
     CK(hipMemcpy(A, h.data(), N * N * 8, hipMemcpyHostToDevice));
     CK(hipMemset(info, 0, 4));

@@ -261,6 +261,27 @@ int omb_posterior_samples(omb_ctx* ctx, int obj, const double* Xc_dev, int64_t N
 int omb_thompson_select(omb_ctx* ctx, const double* Y_dev, int B, int64_t N, int64_t* idx_dev);
 
 /* ---------------------------------------------------------------------------------------
+ * ParEGO / KEEP evolutionary acquisition search (parego.py:223-271, keep.py:240-292): the
+ * reference's steady-state GA over a temporary population (20: mutants of archive members + Latin
+ * hypercube points), 1,000 generations of binary tournaments without replacement (parego.py:78-111),
+ * simulated binary crossover (:58-75) and ×1.05 / ×0.95 mutation (:37-56), the child replacing the
+ * first parent unless the parent is strictly fitter; the proposal is the best individual seen at the
+ * start of any generation (initially `lower` with fitness 0).  Fitness of objective 0's model:
+ *   OMB_EA_EI         EI(μ0, σ = sqrt(σ²0 + var_eps))                  ParEGO (var_eps 1e-6)
+ *   OMB_EA_PARETO_EI  μ1 · EI(μ0, ...) with objective 1 the Pareto-membership model   KEEP
+ * The random draws come as a tape replayed on the host in the reference's call order (see
+ * optimobo_amd/ea.py): sel_dev (iters, 4) int32 — tournament 1's random.sample over range(1, P),
+ * tournament 2's over range(1, P − 1) (indices into the population without the first winner; the
+ * caller guarantees these ranges); cross_dev (iters) int8 crossover flags; beta_dev (iters, d) the
+ * crossover β per gene; mut_dev (iters, d) int8 mutation codes (0 none, 1 ×1.05, 2 ×0.95).
+ * pop_dev (P, d), lower_dev / upper_dev (d), out_dev (d + 1) = best x, best fitness.  3 ≤ P ≤ 32,
+ * n_train ≤ 2048.  One workgroup runs the search.  Asynchronous. */
+enum { OMB_EA_EI = 0, OMB_EA_PARETO_EI = 1 };
+int omb_ea_search(omb_ctx* ctx, int mode, double best, double var_eps, const double* pop_dev, int P, int iters,
+                  const int32_t* sel_dev, const int8_t* cross_dev, const double* beta_dev, const int8_t* mut_dev,
+                  const double* lower_dev, const double* upper_dev, double* out_dev);
+
+/* ---------------------------------------------------------------------------------------
  * GP fit on the device — GPy GPRegression(X, y, Matern52(d, ARD=True)) with the noise variance
  * fixed (optimisers.py:223-231 and every other driver's fit): exact inference with GPy's jitchol
  * (Ky = K + (σ_n² + 1e-8) I; on failure + mean(diag Ky)·1e-6·10^t, t < 5), the log marginal

@@ -17,6 +17,7 @@ ERROR_NAMES = {OMB_EINVAL: "OMB_EINVAL", OMB_EHIP: "OMB_EHIP", OMB_ENOMEM: "OMB_
 KERNEL_MATERN52, KERNEL_RBF = 0, 1
 EHVI_REFERENCE, EHVI_TEXTBOOK, EHVI_SIGMA = 0, 1, 2
 EI_PLAIN, EI_PARETO, EI_CONSTRAINED = 0, 1, 2
+EA_EI, EA_PARETO_EI = 0, 1
 DEBUG_SPIN_LIMIT = 1
 MAX_OBJ, MAX_DIM, MAX_TRAIN, MAX_TRAIN_DENSE = 8, 64, 1024, 16384
 
@@ -68,6 +69,7 @@ SIGNATURES = {
     "omb_cholesky": (_i, [_p, _p, _i64, _i64, _d, ctypes.POINTER(_i)]),
     "omb_posterior_samples": (_i, [_p, _i, _p, _i64, _p, _i, _d, _i, _p, _dp]),
     "omb_thompson_select": (_i, [_p, _p, _i, _i64, _p]),
+    "omb_ea_search": (_i, [_p, _i, _d, _d, _p, _i, _i, _p, _p, _p, _p, _p, _p, _p]),
     # GP fit on the device
     "omb_gp_lml_grad": (_i, [_p, _i, _i, _i, _p, _p, _dp, _d, _d, _dp, _dp, _dp]),
     "omb_gp_fit_state": (_i, [_p, _i, _i, _i, _i, _p, _p, _dp, _d, _d, _dp]),

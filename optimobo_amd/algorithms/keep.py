@@ -4,18 +4,20 @@ KEEP is ParEGO with a second GP: besides the model of the scalarised archive it 
 of Pareto-set membership (1 for archive points in the current front, 0 otherwise,
 keep.py:227-238) and ranks candidates by μ_pareto(x) · EI(x) with σ = sqrt(σ² + 1e-6)
 (pareto_expected_improvement, keep.py:142-151).  The host loop follows the reference; the
-20-member evolutionary search with 1,000 sequential re-mutations (keep.py:240-287) is
-replaced by the batched device arg-max of the same fitness (omb_plan_ei_ext, kind "pareto":
-both posteriors and the product in one fused chain).
+acquisition search is the reference's 20-member evolutionary search with 1,000 generations
+(keep.py:240-287) run on the device (omb_ea_search mode OMB_EA_PARETO_EI, draws from the global
+generators in the reference's order).  `acq_search = "batch"` uses the batched device arg-max of the
+same fitness instead (omb_plan_ei_ext, kind "pareto": both posteriors and the product in one chain).
 """
 import numpy as np
 
-from .. import pareto
+from .. import ea, pareto
 from ..refdirs import get_reference_directions
 from ._base import BODriver
 
 
 class KEEP(BODriver):
+    acq_search = "ea"
     def _expected_improvement(self, X, model, opt_value, kappa=0.01):
         """keep.py:118-137 (σ = sqrt(σ² + 1e-6)); X (d,) → (1,), X (N, d) → (N,)."""
         from ..acquisition import engine_for
@@ -30,9 +32,15 @@ class KEEP(BODriver):
         out = engine_for([scalarised_model, pareto_model], self.device).pareto_ei(Xb, opt_value).cpu().numpy()
         return out[:1] if np.ndim(X) == 1 else out
 
-    def _get_proposed(self, pareto_model, scalar_model, current_best):
+    def _get_proposed(self, pareto_model, scalar_model, current_best, Xsample=None):
         from ..acquisition import engine_for
         eng = engine_for([scalar_model, pareto_model], self.device)
+        if self.acq_search == "ea" and Xsample is not None:
+            lower = np.asarray(self.test_problem.xl, np.float64)
+            upper = np.asarray(self.test_problem.xu, np.float64)
+            pop = ea.initial_population(Xsample, lower, upper)           # keep.py:246-252
+            tape = ea.ea_tape(len(pop), Xsample.shape[1])               # keep.py:256-290
+            return eng.ctx.ea_search(pop, tape, current_best, lower, upper, mode=1)
         eng.plan_pareto_ei(current_best)
         return self._maximise([scalar_model, pareto_model], None)
 
@@ -59,7 +67,7 @@ class KEEP(BODriver):
             scalar_model = self._fit(Xsample, aggregated)
             pareto_model = self._fit(Xsample, self._membership(Xsample, ysample))
             current_best = aggregated[np.argmin(aggregated)]
-            next_X, _ = self._get_proposed(pareto_model, scalar_model, current_best)
+            next_X, _ = self._get_proposed(pareto_model, scalar_model, current_best, Xsample)
             next_y = self._objective_function(problem, next_X)
             ysample = np.vstack((ysample, next_y))
             Xsample = np.vstack((Xsample, next_X))

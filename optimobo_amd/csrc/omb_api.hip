@@ -69,6 +69,9 @@ struct omb_ctx {
   // Thompson selection: per-sample sorted heads (select_sort_kernel)
   void* sws = nullptr;
   size_t sws_cap = 0;
+  // evolutionary search: L0⁻¹ transposed
+  void* ews = nullptr;
+  size_t ews_cap = 0;
   // GP fit: Ky | L⁻¹ | Ky⁻¹ | scratch workspace
   void* fws = nullptr;
   size_t fws_cap = 0;
@@ -453,6 +456,7 @@ int omb_destroy(omb_ctx* ctx) {
   if (ctx->tws) (void)hipFree(ctx->tws);
   if (ctx->ichol) (void)hipFree(ctx->ichol);
   if (ctx->sws) (void)hipFree(ctx->sws);
+  if (ctx->ews) (void)hipFree(ctx->ews);
   if (ctx->fws) (void)hipFree(ctx->fws);
   if (ctx->dws) (void)hipFree(ctx->dws);
   if (ctx->fault_host) (void)hipHostFree(ctx->fault_host);
@@ -1196,6 +1200,52 @@ int omb_gp_fit_state(omb_ctx* ctx, int obj, int kernel, int n, int d, const doub
   if ((rc = gp_factor(ctx, kernel, n, d, X_dev, y_dev, lengthscale_host, variance, noise, &f))) return rc;
   if (jitter_used) *jitter_used = f.jitter;
   return omb_set_gp(ctx, obj, kernel, n, d, X_dev, lengthscale_host, variance, f.alpha, f.Linv);
+}
+
+// ---------------------------------------------------------------------------------------
+// ParEGO / KEEP evolutionary acquisition search: parego.py:223-271, keep.py:240-292.
+int omb_ea_search(omb_ctx* ctx, int mode, double best, double var_eps, const double* pop_dev, int P, int iters,
+                  const int32_t* sel_dev, const int8_t* cross_dev, const double* beta_dev, const int8_t* mut_dev,
+                  const double* lower_dev, const double* upper_dev, double* out_dev) {
+  int rc = enter(ctx);
+  if (rc) return rc;
+  if (mode != OMB_EA_EI && mode != OMB_EA_PARETO_EI) return fail(ctx, OMB_EINVAL, "unknown search mode %d", mode);
+  if ((rc = check_obj(ctx, 0))) return rc;
+  if (mode == OMB_EA_PARETO_EI && (rc = check_obj(ctx, 1))) return rc;
+  const ObjState& s0 = ctx->obj[0];
+  if (mode == OMB_EA_PARETO_EI && ctx->obj[1].d != s0.d)
+    return fail(ctx, OMB_EINVAL, "objectives 0 and 1 disagree on n_var (%d vs %d)", s0.d, ctx->obj[1].d);
+  if (P < 3 || P > kEAMaxPop) return fail(ctx, OMB_EINVAL, "population size %d outside [3, %d]", P, kEAMaxPop);
+  if (iters < 0) return fail(ctx, OMB_EINVAL, "iters=%d must be >= 0", iters);
+  if (s0.n > kEAMaxTrain || (mode == OMB_EA_PARETO_EI && ctx->obj[1].n > kEAMaxTrain))
+    return fail(ctx, OMB_EUNSUP, "n_train above %d", kEAMaxTrain);
+  if (!(var_eps >= 0.0)) return fail(ctx, OMB_EINVAL, "var_eps=%g must be >= 0", var_eps);
+  if (!pop_dev || !lower_dev || !upper_dev || !out_dev || (iters > 0 && (!sel_dev || !cross_dev || !beta_dev || !mut_dev)))
+    return fail(ctx, OMB_EINVAL, "null device pointer");
+  if ((rc = grow_dev(ctx, &ctx->ews, &ctx->ews_cap, sizeof(double) * (size_t)s0.n * s0.n, "search workspace")))
+    return rc;
+  EASearch es{};
+  es.g0 = s0.dev;
+  es.g1 = (mode == OMB_EA_PARETO_EI) ? ctx->obj[1].dev : s0.dev;
+  es.Ld0 = s0.Ld;
+  es.mode = mode;
+  es.d = s0.d;
+  es.DP = s0.DP;
+  es.P = P;
+  es.iters = iters;
+  es.best = best;
+  es.var_eps = var_eps;
+  es.pop = pop_dev;
+  es.sel = sel_dev;
+  es.cross = cross_dev;
+  es.beta = beta_dev;
+  es.mut = mut_dev;
+  es.lower = lower_dev;
+  es.upper = upper_dev;
+  es.out = out_dev;
+  hipError_t e = launch_ea_search(ctx->stream, es, static_cast<double*>(ctx->ews));
+  if (e != hipSuccess) return hip_fail(ctx, e, "ea_search");
+  return OMB_OK;
 }
 
 }  // extern "C"

@@ -156,6 +156,26 @@ hipError_t launch_gp_grad(hipStream_t stream, int kind, int DP, const double* X,
                           double variance, const double* alpha, const double* Kinv, int64_t ldk, double* partials,
                           const double* L, int64_t lda, const double* y, double* out);
 
+// ParEGO / KEEP evolutionary acquisition search (omb_ea.hip): one workgroup runs the whole search from a
+// host-replayed tape of the reference's random draws.  ldt_ws: n0·n0 doubles (L0⁻¹ transposed).
+constexpr int kEAMaxPop = 32;
+constexpr int kEAMaxTrain = 2048;
+struct EASearch {
+  GPDev g0, g1;          // g0: the EI model; g1: KEEP's Pareto-membership model (mode 1)
+  const double* Ld0;     // dense row-major L0⁻¹ (n0, n0)
+  int mode, d, DP, P, iters;
+  double best, var_eps;
+  const double* pop;
+  const int* sel;
+  const int8_t* cross;
+  const double* beta;
+  const int8_t* mut;
+  const double* lower;
+  const double* upper;
+  double* out;
+};
+hipError_t launch_ea_search(hipStream_t stream, const EASearch& s, double* ldt_ws);
+
 // Packed-L^-1 size in doubles for R row tiles: Σ_{r<R} 4(r+1)·64 = 128·R·(R+1).
 inline int64_t packed_L_size(int R) { return 128ll * R * (R + 1); }
 // k-step pairs of the training-row A fragments [x/ℓ, ‖x/ℓ‖², 1]: ⌈⌈(DP+2)/4⌉/2⌉

@@ -377,6 +377,38 @@ class AcqContext:
         self._check(self.lib.omb_thompson_select(self._h, _ptr(Y), B, N, _ptr(idx)), "omb_thompson_select")
         return idx
 
+    def ea_search(self, pop, tape, best, lower, upper, mode=0, var_eps=1e-6):
+        """ParEGO (mode 0: EI of objective 0) / KEEP (mode 1: μ of objective 1 · EI of objective 0)
+        evolutionary acquisition search (omb_ea_search) from the temporary population `pop` (P, d) and
+        a tape of the reference's random draws (optimobo_amd.ea.ea_tape) → (best x (d,), best fitness),
+        host numpy.  Synchronises."""
+        pop = np.ascontiguousarray(pop, np.float64)
+        P, d = pop.shape
+        if tape.beta.shape[1:] != (d,) or tape.mut.shape[1:] != (d,) or tape.sel.shape[1:] != (4,):
+            raise ValueError("tape does not match the population width")
+        sel = tape.sel
+        if len(sel) and (sel[:, :2].min() < 1 or sel[:, :2].max() > P - 1 or sel[:, 2:].min() < 1
+                         or sel[:, 2:].max() > P - 2):
+            raise ValueError("tournament samples outside range(1, P) / range(1, P - 1)")
+        dv = self.device
+        t_pop = torch.as_tensor(pop, device=dv)
+        self._check_width(t_pop)
+        if mode == _lib.EA_PARETO_EI:
+            self._check_width(t_pop, 1)
+        t_sel = torch.as_tensor(np.ascontiguousarray(sel, np.int32), device=dv)
+        t_cross = torch.as_tensor(np.ascontiguousarray(tape.cross, np.int8), device=dv)
+        t_beta = torch.as_tensor(np.ascontiguousarray(tape.beta, np.float64), device=dv)
+        t_mut = torch.as_tensor(np.ascontiguousarray(tape.mut, np.int8), device=dv)
+        t_lo = torch.as_tensor(np.ascontiguousarray(lower, np.float64).reshape(d), device=dv)
+        t_hi = torch.as_tensor(np.ascontiguousarray(upper, np.float64).reshape(d), device=dv)
+        out = torch.empty(d + 1, dtype=torch.float64, device=dv)
+        self._stream()
+        self._check(self.lib.omb_ea_search(self._h, int(mode), float(best), float(var_eps), _ptr(t_pop), P,
+                                           int(tape.iters), _ptr(t_sel), _ptr(t_cross), _ptr(t_beta), _ptr(t_mut),
+                                           _ptr(t_lo), _ptr(t_hi), _ptr(out)), "omb_ea_search")
+        o = out.cpu().numpy()
+        return o[:d].copy(), float(o[d])
+
     def timing(self, level=2):
         """0 off, 1 posterior only, 2 every stage of the fused chain (see omb_timing)."""
         self._stream()

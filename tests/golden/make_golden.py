@@ -577,6 +577,101 @@ def make_cparego(rng, cparego_mod, sc):
     np.savez_compressed(os.path.join(HERE, "cparego.npz"), **out)
 
 
+class _ZDT1Box:
+    """ZDT1 on [0, 1]^d (optimobo/problem.py:924-936), the problem object the EA fixtures run on."""
+
+    def __init__(self, d):
+        self.n_var, self.n_obj = d, 2
+        self.xl, self.xu = np.zeros(d), np.ones(d)
+
+    def evaluate(self, x):
+        return zdt1(np.atleast_2d(np.asarray(x, np.float64)))[0]
+
+
+def make_ea(parego_mod, keep_mod, sc):
+    """ParEGO / KEEP evolutionary acquisition search (parego.py:223-271, keep.py:240-292) run by the
+    reference's own solve() for one BO iteration.  GPy double: GPRegression = the oracle's GPy restatement
+    (oracle/gp.py) with GPy's default Matern52 ARD hyperparameters (ℓ = 1, σ_f² = 1; noise fixed to 0,
+    optimize a no-op).  A hook on the binary tournament records, at its first call (generation 0, after
+    which every random draw of the search follows), the temporary population, the numpy and `random`
+    generator states, the training set of the model(s) and the incumbent; the proposal is the x that
+    solve() evaluates after the search."""
+    import random
+
+    class DuckGP:
+        def __init__(self, X, Y, kern=None):
+            self.X, self.Y = np.array(X, np.float64), np.array(Y, np.float64)
+            self.gp = ogp.ExactGP(self.X, self.Y[:, 0], 1.0, 1.0)
+            self.Gaussian_noise = types.SimpleNamespace(variance=types.SimpleNamespace(fix=lambda *a: None))
+
+        def optimize(self, **kw):
+            pass
+
+        def predict(self, X):
+            return self.gp.predict(X)
+
+    sys.modules["GPy"].models.GPRegression = DuckGP
+    sys.modules["GPy"].kern.Matern52 = lambda *a, **k: None
+
+    class HV:
+        def __init__(self, ref_point):
+            self.r = np.asarray(ref_point, np.float64)
+
+        def __call__(self, Y):
+            return opareto.hypervolume(Y, self.r)
+    for mod in (parego_mod, keep_mod):
+        mod.get_reference_directions = lambda name, n_dim, n_partitions=None: _das_dennis(n_dim, n_partitions)
+        mod.HV = HV
+
+    out = {}
+    cases = [("parego", 1, 3, 12), ("parego", 2, 6, 20), ("keep", 3, 2, 12), ("keep", 4, 5, 16)]
+    out["n_cases"] = np.int64(len(cases))
+    for c, (kind, seed, d, n_init) in enumerate(cases):
+        cls = parego_mod.ParEGO if kind == "parego" else keep_mod.KEEP
+        tname = ("parego_binary_tournament_selection_without_replacment" if kind == "parego"
+                 else "KEEP_binary_tournament_selection_without_replacment")
+        orig = getattr(cls, tname)
+        rec = {}
+
+        def hook(self, population, *args, _orig=orig, _rec=rec):
+            if not _rec:
+                st = np.random.get_state()
+                _rec["pop"] = np.array(population, np.float64)
+                _rec["np_keys"], _rec["np_pos"] = np.array(st[1], np.uint32), np.int64(st[2])
+                _rec["np_has_gauss"], _rec["np_gauss"] = np.int64(st[3]), np.float64(st[4])
+                pst = random.getstate()
+                _rec["py_version"], _rec["py_state"] = np.int64(pst[0]), np.array(pst[1], np.int64)
+                models = args[:-1]
+                _rec["best"] = np.float64(np.asarray(args[-1]).reshape(-1)[0])
+                _rec["X"] = models[-1].X                     # scalar model (the last model argument)
+                _rec["y0"] = models[-1].Y[:, 0]
+                if len(models) == 2:
+                    _rec["y1"] = models[0].Y[:, 0]           # KEEP: the Pareto-membership model
+            return _orig(self, population, *args)
+        setattr(cls, tname, hook)
+        evaluated = []
+        inst = cls(_ZDT1Box(d))
+        orig_obj = inst._objective_function
+
+        def obj_fn(problem, x, _o=orig_obj, _e=evaluated):
+            _e.append(np.array(x, np.float64))
+            return _o(problem, x)
+        inst._objective_function = obj_fn
+        np.random.seed(seed)
+        random.seed(seed)
+        inst.solve(sc.Tchebicheff(), budget=1, n_init_samples=n_init)
+        setattr(cls, tname, orig)
+        k = f"c{c}"
+        out[f"{k}_kind"] = np.array(kind)
+        out[f"{k}_seed"], out[f"{k}_d"] = np.int64(seed), np.int64(d)
+        for key, v in rec.items():
+            out[f"{k}_{key}"] = v
+        out[f"{k}_next_x"] = evaluated[-1]
+        out[f"{k}_lower"], out[f"{k}_upper"] = np.zeros(d), np.ones(d)
+        print(f"  ea case {c}: {kind} d={d} n={len(rec['X'])} next_x={evaluated[-1]}")
+    np.savez_compressed(os.path.join(HERE, "ea.npz"), **out)
+
+
 def make_calc_pf(rng, uf):
     out = {}
     for t, (n, k) in enumerate([(1, 2), (40, 2), (60, 3)]):
@@ -618,6 +713,8 @@ def main():
         make_cparego(np.random.default_rng(20261018), cparego_mod, sc)
     if not only or "de" in only:
         make_de_proposals(opt_mod, uf, sc)
+    if not only or "ea" in only:
+        make_ea(parego_mod, keep_mod, sc)
     if not only or "ehvi_pos" in only:
         make_ehvi2d_pos(np.random.default_rng(20261019), uf)
         make_ehvi3d_pos(np.random.default_rng(20261020), uf)

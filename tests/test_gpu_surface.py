@@ -137,10 +137,15 @@ def test_solve_mono_emo_parego():
     r1 = MonoSurrogateOptimiser(p, [0, 0], [700, 12], n_candidates=2048, seed=3).solve(
         sc.Tchebicheff([0, 0], [700, 12]), budget=2, n_init_samples=8)
     r2 = EMO(p, [0, 0], [700, 12], n_candidates=2048, seed=4).solve(budget=2, n_init_samples=8)
+    # the evolutionary search (the reference's) samples 10 archive members: n_init ≥ 10, as in the reference
     r3 = ParEGO(p, [0, 0], [700, 12], n_candidates=2048, seed=5).solve(sc.Tchebicheff([0, 0], [700, 12]), budget=2,
-                                                                        n_init_samples=8)
-    for r in (r1, r2, r3):
+                                                                        n_init_samples=10)
+    for r in (r1, r2):
         assert r.ysample.shape == (10, 2)
+    assert r3.ysample.shape == (12, 2) and np.all(np.abs(r3.Xsample) <= 2 + 1e-12)
+    r4 = ParEGO(p, [0, 0], [700, 12], n_candidates=2048, seed=5)
+    r4.acq_search = "batch"
+    assert r4.solve(sc.Tchebicheff([0, 0], [700, 12]), budget=2, n_init_samples=8).ysample.shape == (10, 2)
 
 
 def test_keep_solve_and_fitness(fitted):
@@ -149,8 +154,8 @@ def test_keep_solve_and_fitness(fitted):
     np.random.seed(3)
     p = _myproblem()
     keep = KEEP(p, [0, 0], [700, 12], n_candidates=2048, seed=6)
-    r = keep.solve(sc.Tchebicheff([0, 0], [700, 12]), budget=2, n_init_samples=8)
-    assert r.ysample.shape == (10, 2) and np.all(np.abs(r.Xsample) <= 2 + 1e-12)
+    r = keep.solve(sc.Tchebicheff([0, 0], [700, 12]), budget=2, n_init_samples=10)
+    assert r.ysample.shape == (12, 2) and np.all(np.abs(r.Xsample) <= 2 + 1e-12)
     # the fitness KEEP maximises, batched and single, against the oracle chain
     X, Y, ls, models = fitted
     Xc = np.random.default_rng(4).uniform(0, 1, (500, 4))

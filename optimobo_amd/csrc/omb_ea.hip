@@ -12,8 +12,9 @@
 // (optimobo_amd/ea.py: tournament samples, crossover flag and β, mutation codes) and one 256-thread
 // workgroup runs all generations: the population and its fitness stay in LDS (the reference recomputes
 // the same fitness every generation), and each generation evaluates one child — its K* row on all
-// threads, L⁻¹k* with a thread per row over a transposed copy of L⁻¹ (coalesced column reads), μ and
-// ‖L⁻¹k*‖² by fixed-order reductions.  Child arithmetic uses unfused IEEE ops in numpy's order, so with
+// threads, L⁻¹k* with a thread per row (L⁻¹ packed in LDS for n ≤ 128, else a transposed global copy
+// read column-wise), μ and ‖L⁻¹k*‖² by fixed-order reductions (wave shuffles, then the 4 waves).
+// Child arithmetic uses unfused IEEE ops in numpy's order, so with
 // the same tape the device search makes the reference's choices.
 #include "omb_internal.h"
 #include "omb_math.h"
@@ -38,10 +39,13 @@ struct EAArgs {
   double* out;           // (d + 1): best x, best fitness
 };
 
-// μ and (with LdT) σ² of one point x (LDS, d values) under model g; every thread returns the result.
+// μ and (with L) σ² of one point x (LDS, d values) under model g; every thread returns the result.
+// L⁻¹k* with a thread per row: Lds (n ≤ kEALdsN) is the packed lower L⁻¹ by columns in LDS — element
+// (i, j) at j·n − j(j−1)/2 + (i − j), consecutive rows at consecutive addresses; otherwise LdT (global,
+// transposed) is read over each row's columns, two accumulators.
 template <int DP>
-__device__ double ea_moments(const GPDev& g, const double* __restrict__ LdT, int d, const double* x, double* ab,
-                             double* kst, double* red, double* var_out) {
+__device__ double ea_moments(const GPDev& g, const double* __restrict__ LdT, const double* Lds, int d,
+                             const double* x, double* ab, double* kst, double* red, double* var_out) {
   const int tid = threadIdx.x;
   if (tid < DP) ab[tid] = (tid < d) ? x[tid] / g.ls[tid] : 0.0;     // GPy divides by ℓ
   __syncthreads();
@@ -61,24 +65,49 @@ __device__ double ea_moments(const GPDev& g, const double* __restrict__ LdT, int
   }
   __syncthreads();
   double vp = 0.0;
-  if (LdT) {
-    for (int i = tid; i < g.n; i += kEAThreads) {
-      double v = 0.0;
-      for (int j = 0; j <= i; ++j) v = fma(LdT[(int64_t)j * g.n + i], kst[j], v);
+  const int n = g.n;
+  if (Lds) {
+    for (int i = tid; i < n; i += kEAThreads) {
+      double v0 = 0.0, v1 = 0.0;
+      int addr = i;                                                  // column 0, row i
+      int j = 0;
+      for (; j + 1 <= i; j += 2) {
+        v0 = fma(Lds[addr], kst[j], v0);
+        addr += n - j - 1;
+        v1 = fma(Lds[addr], kst[j + 1], v1);
+        addr += n - j - 2;
+      }
+      if (j <= i) v0 = fma(Lds[addr], kst[j], v0);
+      const double v = v0 + v1;
+      vp = fma(v, v, vp);
+    }
+  } else if (LdT) {
+    for (int i = tid; i < n; i += kEAThreads) {
+      double v0 = 0.0, v1 = 0.0;
+      int j = 0;
+      for (; j + 1 <= i; j += 2) {
+        v0 = fma(LdT[(int64_t)j * n + i], kst[j], v0);
+        v1 = fma(LdT[(int64_t)(j + 1) * n + i], kst[j + 1], v1);
+      }
+      if (j <= i) v0 = fma(LdT[(int64_t)j * n + i], kst[j], v0);
+      const double v = v0 + v1;
       vp = fma(v, v, vp);
     }
   }
-  red[tid] = mp;
-  red[kEAThreads + tid] = vp;
+  // fixed-order reduction: within each wave by xor shuffles, then the 4 waves in order
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    mp += __shfl_xor(mp, off);
+    vp += __shfl_xor(vp, off);
+  }
+  if ((tid & 63) == 0) {
+    red[tid >> 6] = mp;
+    red[4 + (tid >> 6)] = vp;
+  }
   __syncthreads();
   if (tid == 0) {
-    double m = 0.0, s = 0.0;
-    for (int t = 0; t < kEAThreads; ++t) {
-      m += red[t];
-      s += red[kEAThreads + t];
-    }
-    red[2 * kEAThreads] = m;
-    red[2 * kEAThreads + 1] = g.variance - s;
+    red[2 * kEAThreads] = (red[0] + red[1]) + (red[2] + red[3]);
+    red[2 * kEAThreads + 1] = g.variance - ((red[4] + red[5]) + (red[6] + red[7]));
   }
   __syncthreads();
   const double mu = red[2 * kEAThreads];
@@ -88,13 +117,14 @@ __device__ double ea_moments(const GPDev& g, const double* __restrict__ LdT, int
 }
 
 template <int DP>
-__device__ double ea_fitness(const EAArgs& A, const double* x, double* ab, double* kst, double* red) {
+__device__ double ea_fitness(const EAArgs& A, const double* Lds, const double* x, double* ab, double* kst,
+                             double* red) {
   double var0;
-  const double mu0 = ea_moments<DP>(A.g0, A.LdT, A.d, x, ab, kst, red, &var0);
+  const double mu0 = ea_moments<DP>(A.g0, A.LdT, Lds, A.d, x, ab, kst, red, &var0);
   const double sigma = sqrt(var0 + A.var_eps);
   const double gamma = (A.best - mu0) / (sigma + 1e-10);
   double v = sigma * (gamma * ndtr(gamma) + npdf(gamma));
-  if (A.mode == 1) v = ea_moments<DP>(A.g1, nullptr, A.d, x, ab, kst, red, nullptr) * v;
+  if (A.mode == 1) v = ea_moments<DP>(A.g1, nullptr, nullptr, A.d, x, ab, kst, red, nullptr) * v;
   return v;
 }
 
@@ -108,7 +138,15 @@ __global__ __launch_bounds__(kEAThreads) void ea_search_kernel(EAArgs A) {
   __shared__ double kst[kEAMaxTrain];
   __shared__ double red[2 * kEAThreads + 2];
   __shared__ int ctl[4];                                            // w1, w2, replace
+  __shared__ double lds_l[kEALdsN * (kEALdsN + 1) / 2];             // packed L0⁻¹ (n0 ≤ kEALdsN)
   const int tid = threadIdx.x, d = A.d, P = A.P;
+  const int n0 = A.g0.n;
+  const double* Lds = nullptr;
+  if (n0 <= kEALdsN) {
+    for (int j = 0, off = 0; j < n0; off += n0 - j, ++j)
+      for (int i = j + tid; i < n0; i += kEAThreads) lds_l[off + i - j] = A.LdT[(int64_t)j * n0 + i];
+    Lds = lds_l;
+  }
   for (int i = tid; i < P * DP; i += kEAThreads) {
     const int p = i / DP, j = i % DP;
     pop[i] = (j < d) ? A.pop[p * d + j] : 0.0;
@@ -116,7 +154,7 @@ __global__ __launch_bounds__(kEAThreads) void ea_search_kernel(EAArgs A) {
   if (tid < DP) bestx[tid] = (tid < d) ? A.lower[tid] : 0.0;      // best_solution_found = self.lower
   __syncthreads();
   for (int p = 0; p < P; ++p) {
-    const double f = ea_fitness<DP>(A, pop + p * DP, ab, kst, red);
+    const double f = ea_fitness<DP>(A, Lds, pop + p * DP, ab, kst, red);
     if (tid == 0) F[p] = f;
   }
   double best_f = 0.0;                                              // best_EI = 0 (thread 0's copy)
@@ -160,7 +198,7 @@ __global__ __launch_bounds__(kEAThreads) void ea_search_kernel(EAArgs A) {
       child[tid] = 0.0;
     }
     __syncthreads();
-    const double fc = ea_fitness<DP>(A, child, ab, kst, red);
+    const double fc = ea_fitness<DP>(A, Lds, child, ab, kst, red);
     if (!(F[w1] > fc)) {                                            // the parent stays only if strictly fitter
       if (tid < DP) pop[w1 * DP + tid] = child[tid];
       if (tid == 0) F[w1] = fc;
@@ -171,19 +209,18 @@ __global__ __launch_bounds__(kEAThreads) void ea_search_kernel(EAArgs A) {
   if (tid == 0) A.out[d] = best_f;
 }
 
-// LdT[j·n + i] = Ld[i·n + j] for j ≤ i (32×32 tiles through LDS; tiles above the diagonal skipped).
+// LdT[j·n + i] = Ld[i·n + j] for j ≤ i, 0 above the diagonal (32×32 tiles through LDS).
 __global__ __launch_bounds__(256) void lower_transpose_kernel(const double* __restrict__ Ld, int64_t n,
                                                               double* __restrict__ LdT) {
-  if (blockIdx.x > blockIdx.y) return;
   __shared__ double t[32][33];
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   const int64_t r0 = (int64_t)blockIdx.y * 32, c0 = (int64_t)blockIdx.x * 32;   // source tile rows r0.., cols c0..
   for (int r = ty; r < 32; r += 8)
-    if (r0 + r < n && c0 + tx < n) t[r][tx] = Ld[(r0 + r) * n + c0 + tx];
+    if (r0 + r < n && c0 + tx < n) t[r][tx] = (c0 + tx <= r0 + r) ? Ld[(r0 + r) * n + c0 + tx] : 0.0;
   __syncthreads();
   for (int r = ty; r < 32; r += 8) {
     const int64_t j = c0 + r, i = r0 + tx;                          // destination row j (= source column)
-    if (j < n && i < n && j <= i) LdT[j * n + i] = t[tx][r];
+    if (j < n && i < n) LdT[j * n + i] = t[tx][r];
   }
 }
 

@@ -160,6 +160,7 @@ hipError_t launch_gp_grad(hipStream_t stream, int kind, int DP, const double* X,
 // host-replayed tape of the reference's random draws.  ldt_ws: n0·n0 doubles (L0⁻¹ transposed).
 constexpr int kEAMaxPop = 32;
 constexpr int kEAMaxTrain = 2048;
+constexpr int kEALdsN = 128;      // L0⁻¹ kept in LDS (packed lower) up to this n_train
 struct EASearch {
   GPDev g0, g1;          // g0: the EI model; g1: KEEP's Pareto-membership model (mode 1)
   const double* Ld0;     // dense row-major L0⁻¹ (n0, n0)

@@ -360,6 +360,11 @@ __global__ __launch_bounds__(512) void kernel_block_pipe_kernel(GPDev g, int d, 
   }
 }
 
+// Per-workgroup phase timestamps of the posterior kernels for tools/ablate/ablate_posterior (empty here).
+#ifndef OMB_POST_TRACE
+#define OMB_POST_TRACE(id)
+#endif
+
 // ----------------------------------------------------------------------------- posterior
 // ABL (ablation, tools/ablate only; the library instantiates ABL = 0): bit 1 replaces the Matern
 // transform by the raw dot product, bit 2 skips the MFMA phase, bit 4 feeds a constant A
@@ -396,6 +401,7 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
   constexpr int kTabN = kTab256 ? 256 : 64;
   __shared__ double kbuf[NBUF * CHUNK + kCtrDoubles + (kCandLds ? DP * BN : 0) + kTabN];
 
+  OMB_POST_TRACE(0);
   const int obj = blockIdx.y;
   const GPDev g = args.gp[obj];
   const int d = args.d;
@@ -693,6 +699,7 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     };
+    OMB_POST_TRACE(1);
     generate(0, kbuf);
     signal(&ready[0]);
     if (Q > 1) {
@@ -709,7 +716,9 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
         signal(&ready[kc + 2]);
       }
     }
+    OMB_POST_TRACE(2);
     __syncthreads();
+    OMB_POST_TRACE(3);
   } else {
     generate(0, kbuf);
     __syncthreads();
@@ -770,12 +779,8 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
       var_out[(int64_t)obj * N + c] = g.variance - s;
     }
   }
+  OMB_POST_TRACE(4);
 }
-
-// Per-workgroup phase timestamps of posterior_tile_kernel for tools/ablate/ablate_posterior (empty here).
-#ifndef OMB_POST_TRACE
-#define OMB_POST_TRACE(id)
-#endif
 
 // ----------------------------------------------------------------------------- posterior, n ≤ 256
 // Whole-tile variant for small training sets (BASELINE configs 2 and 4): the complete K* tile of the

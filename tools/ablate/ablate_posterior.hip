@@ -171,6 +171,53 @@ void trace_tile(const Bench& b) {
   printf("\n");
 }
 
+// Phase timeline of the library's counter-ring kernel (n > 256): prologue, chunk pipeline, final
+// barrier, reduction; gaps between consecutive workgroups on the same CU (XCC + SE/SH/CU id).
+template <int RT, int CT>
+void trace_ring(const Bench& b) {
+  dim3 grid((unsigned)((b.N + 16 * CT - 1) / (16 * CT)), b.n_obj);
+  const unsigned nwg = grid.x * grid.y;
+  if (nwg > 4096) { printf("trace: too many workgroups (%u)\n", nwg); return; }
+  for (int rep = 0; rep < 3; ++rep)
+    hipLaunchKernelGGL((posterior_kernel<RT, CT, 6, 0, 8, 0>), grid, dim3(512), 0, 0, b.a, b.Xc, b.N, b.mu, b.var);
+  CK(hipDeviceSynchronize());
+  std::vector<unsigned long long> t(4096 * 8);
+  CK(hipMemcpyFromSymbol(t.data(), HIP_SYMBOL(g_ptrace), t.size() * 8));
+  unsigned long long t0 = ~0ull, t1 = 0;
+  for (unsigned w = 0; w < nwg; ++w) { t0 = std::min(t0, t[w * 8]); t1 = std::max(t1, t[w * 8 + 4]); }
+  const char* ph[4] = {"prologue (table, candidates, counters)", "chunk pipeline", "final barrier", "reduction + store"};
+  printf("ring kernel RT%d CT%d trace: %u workgroups, span %.2f us\n", RT, CT, nwg, (t1 - t0) / 100.0);
+  for (int p = 0; p < 4; ++p) {
+    std::vector<double> d;
+    for (unsigned w = 0; w < nwg; ++w) d.push_back((t[w * 8 + p + 1] - t[w * 8 + p]) / 100.0);
+    std::sort(d.begin(), d.end());
+    double s = 0; for (double x : d) s += x;
+    printf("  %-40s mean %7.2f us  p10 %7.2f  p50 %7.2f  p90 %7.2f\n", ph[p], s / d.size(), d[d.size() / 10],
+           d[d.size() / 2], d[d.size() * 9 / 10]);
+  }
+  // per CU: sort its workgroups by start, gap = next start − previous end
+  std::vector<std::pair<unsigned long long, unsigned>> byc;
+  for (unsigned w = 0; w < nwg; ++w) {
+    const unsigned long long hw = t[w * 8 + 7];
+    const unsigned cu = (unsigned)((hw >> 8) & 0xf), sh = (unsigned)((hw >> 12) & 1), se = (unsigned)((hw >> 13) & 7);
+    const unsigned xcc = (unsigned)(hw >> 32) & 0xf;
+    byc.push_back({((unsigned long long)((xcc << 8) | (se << 5) | (sh << 4) | cu) << 40) | (t[w * 8] - t0), w});
+  }
+  std::sort(byc.begin(), byc.end());
+  std::vector<double> gaps;
+  unsigned ncu = 0;
+  for (size_t i = 0; i < byc.size(); ++i) {
+    if (i == 0 || (byc[i].first >> 40) != (byc[i - 1].first >> 40)) { ++ncu; continue; }
+    const unsigned prev = byc[i - 1].second, cur = byc[i].second;
+    gaps.push_back(((double)t[cur * 8] - (double)t[prev * 8 + 4]) / 100.0);
+  }
+  std::sort(gaps.begin(), gaps.end());
+  double s = 0; for (double x : gaps) s += x;
+  if (!gaps.empty())
+    printf("  %u CUs seen; start of next minus end of previous workgroup on a CU: mean %.2f us p10 %.2f p50 %.2f p90 %.2f\n",
+           ncu, s / gaps.size(), gaps[gaps.size() / 10], gaps[gaps.size() / 2], gaps[gaps.size() * 9 / 10]);
+}
+
 struct Variant {
   const char* name;
   float (*fn)(const Bench&, int);
@@ -288,6 +335,8 @@ int main(int argc, char** argv) {
   };
   matern_accuracy();
   if (d == 6 && n <= 128) trace_tile(b);
+  if (d == 6 && n > 256) trace_ring<4, 4>(b);
+  if (d == 6 && n > 128 && n <= 256) trace_ring<2, 2>(b);
   const bool is_small = d == 6 && n <= 256;
   (void)small;
   const Variant* vs = is_small ? (n <= 128 ? small128 : small256) : (d == 6 ? narrow : wide);

@@ -613,75 +613,126 @@ __global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const double* L21 = A + r0 * lda + c0;
-  double ra[4], rb[4];
-  auto fetch = [&](int k0) {
+  // the next diagonal block (A22's first tile) belongs to workgroup (0, 0)
+  if (!(blockIdx.x == 0 && blockIdx.y == 0)) {
+    double ra[4], rb[4];
+    auto fetch = [&](int k0) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int idx = tid + 256 * e;
-      const int am = idx >> 4, ak = idx & 15;
-      ra[e] = (m0 + am < M) ? L21[(m0 + am) * lda + k0 + ak] : 0.0;
-      rb[e] = (n0 + am < M) ? L21[(n0 + am) * lda + k0 + ak] : 0.0;
-    }
-  };
-  auto stash = [&](int buf) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int idx = tid + 256 * e;
-      As[buf][idx & 15][idx >> 4] = ra[e];
-      Bs[buf][idx & 15][idx >> 4] = rb[e];
-    }
-  };
-  d4 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
-  fetch(0);
-  stash(0);
-  __syncthreads();
-  int buf = 0;
-#pragma unroll
-  for (int k0 = 0; k0 < kNB; k0 += kGK) {
-    const bool more = k0 + kGK < kNB;
-    if (more) fetch(k0 + kGK);
-#pragma unroll
-    for (int ks = 0; ks < kGK / 4; ++ks) {
-      const int kk = 4 * ks + (lane >> 4);
-      const double a0 = As[buf][kk][32 * wm + (lane & 15)];
-      const double a1 = As[buf][kk][32 * wm + 16 + (lane & 15)];
-      const double b0 = Bs[buf][kk][32 * wn + (lane & 15)];
-      const double b1 = Bs[buf][kk][32 * wn + 16 + (lane & 15)];
-      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
-    }
-    if (more) stash(buf ^ 1);
-    __syncthreads();
-    buf ^= 1;
-  }
-  const bool diag = (blockIdx.x == 0 && blockIdx.y == 0);  // the next diagonal block: A22's first tile
-  double* D = smem;                                          // 64 × 65 staging of that tile
-  // C/D map of v_mfma_f64_16x16x4f64: col = lane & 15, row = (lane >> 4) + 4·i
-#pragma unroll
-  for (int rb2 = 0; rb2 < 2; ++rb2)
-#pragma unroll
-    for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int lr = 32 * wm + 16 * rb2 + (lane >> 4) + 4 * i;
-        const int lc = 32 * wn + 16 * cb + (lane & 15);
-        const int64_t row = m0 + lr, col_g = n0 + lc;
-        if (row < M && col_g < M && col_g <= row) {
-          double* p = A + (r0 + row) * lda + r0 + col_g;
-          const double v = *p - acc[rb2][cb][i];
-          if (diag)
-            D[lr * 65 + lc] = v;
-          else
-            *p = v;
-        }
+      for (int e = 0; e < 4; ++e) {
+        const int idx = tid + 256 * e;
+        const int am = idx >> 4, ak = idx & 15;
+        ra[e] = (m0 + am < M) ? L21[(m0 + am) * lda + k0 + ak] : 0.0;
+        rb[e] = (n0 + am < M) ? L21[(n0 + am) * lda + k0 + ak] : 0.0;
       }
-  if (!diag) return;
+    };
+    auto stash = [&](int buf) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int idx = tid + 256 * e;
+        As[buf][idx & 15][idx >> 4] = ra[e];
+        Bs[buf][idx & 15][idx >> 4] = rb[e];
+      }
+    };
+    d4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+    fetch(0);
+    stash(0);
+    __syncthreads();
+    int buf = 0;
+#pragma unroll
+    for (int k0 = 0; k0 < kNB; k0 += kGK) {
+      const bool more = k0 + kGK < kNB;
+      if (more) fetch(k0 + kGK);
+#pragma unroll
+      for (int ks = 0; ks < kGK / 4; ++ks) {
+        const int kk = 4 * ks + (lane >> 4);
+        const double a0 = As[buf][kk][32 * wm + (lane & 15)];
+        const double a1 = As[buf][kk][32 * wm + 16 + (lane & 15)];
+        const double b0 = Bs[buf][kk][32 * wn + (lane & 15)];
+        const double b1 = Bs[buf][kk][32 * wn + 16 + (lane & 15)];
+        acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+      }
+      if (more) stash(buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+    }
+    // C/D map of v_mfma_f64_16x16x4f64: col = lane & 15, row = (lane >> 4) + 4·i
+#pragma unroll
+    for (int rb2 = 0; rb2 < 2; ++rb2)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int lr = 32 * wm + 16 * rb2 + (lane >> 4) + 4 * i;
+          const int lc = 32 * wn + 16 * cb + (lane & 15);
+          const int64_t row = m0 + lr, col_g = n0 + lc;
+          if (row < M && col_g < M && col_g <= row) {
+            double* p = A + (r0 + row) * lda + r0 + col_g;
+            *p = *p - acc[rb2][cb][i];
+          }
+        }
+    return;
+  }
+  // Diagonal workgroup: the tile's 64 L21 rows and its A22 values are loaded at once (one load latency
+  // instead of one per 16-column slab of the pipeline above), the product runs from one LDS copy
+  // (A and B are the same rows), and D = A22 − L21 L21ᵀ is formed in place for the factorisation.
+  double* D = smem;                                          // 64 × 65: first T[k·65 + m] = L21(m, k), then D
+  {
+    double lv[16], av[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int idx = tid + 256 * e, m = idx >> 6, k = idx & 63;
+      lv[e] = (m < M) ? L21[m * lda + k] : 0.0;
+      av[e] = (m < M && k <= m) ? A[(r0 + m) * lda + r0 + k] : 0.0;
+    }
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int idx = tid + 256 * e;
+      D[(idx & 63) * 65 + (idx >> 6)] = lv[e];
+    }
+    __syncthreads();
+    d4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+    if (wm >= wn) {                                          // the upper-right quadrant is not needed
+#pragma unroll
+      for (int ks = 0; ks < kNB / 4; ++ks) {
+        const int kk = 4 * ks + (lane >> 4);
+        const double a0 = D[kk * 65 + 32 * wm + (lane & 15)];
+        const double a1 = D[kk * 65 + 32 * wm + 16 + (lane & 15)];
+        const double b0 = D[kk * 65 + 32 * wn + (lane & 15)];
+        const double b1 = D[kk * 65 + 32 * wn + 16 + (lane & 15)];
+        acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+      }
+    }
+    __syncthreads();                                         // T consumed
+    if (wm >= wn) {
+#pragma unroll
+      for (int rb2 = 0; rb2 < 2; ++rb2)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            D[(32 * wm + 16 * rb2 + (lane >> 4) + 4 * i) * 65 + 32 * wn + 16 * cb + (lane & 15)] = acc[rb2][cb][i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int idx = tid + 256 * e, m = idx >> 6, k = idx & 63;
+      if (k <= m) D[m * 65 + k] = av[e] - D[m * 65 + k];
+    }
+  }
   __syncthreads();
   const int nb = (int)(M < kNB ? M : kNB);
   const int r = lane, w = wave;

@@ -281,13 +281,14 @@ __device__ __forceinline__ void kernel_of_r2_k_x2(double r2a, double r2b, double
 //     correction of sqrt_nonneg only settles round-to-nearest ties).  r² is clamped to ≥ 1e-300 in
 //     place of the zero test: r = 1e-150 gives exactly σ_f², as r = 0 does.
 //   * Matern polynomial from r² itself: 1 + √5 r + 5/3 r² (GPy squares r; ≤ 1 ulp apart).
-// v_max_f64 without the canonicalising v_max x,x that fmax() adds for IEEE maxNum semantics (the
-// inputs here are never signalling NaNs).
-__device__ __forceinline__ double vmax_vs(double a, double b) {
-  double r;
-  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "s"(b));
-  return r;
-}
+// r² clamp: |r²| + r²_min (r²_min = 1e-300, an SGPR kernel argument) is one v_add_f64 with an abs
+// source modifier.  It equals max(r², r²_min) except for r² < 0 (rounding of the augmented dot
+// product, |r²| ~ 1e-16 where GPy clips to 0: the kernel value differs by < 1e-16 relative) and for
+// 0 < r² < 1e-284 (r < 1e-142: the value is σ_f² either way).  Round 1 used an inline-asm v_max_f64
+// here; the compiler's hazard recognizer does not see inside inline asm, and as the first reader of
+// an FP64 MFMA result it could issue before the required wait states (found in r02 when a variant
+// with more registers scheduled it straight after the r²-MFMA and returned wrong moments).
+__device__ __forceinline__ double r2_clamp(double r2, double r2min) { return fabs(r2) + r2min; }
 
 // Round-to-nearest-even of y with |y| < 2^51, as a double and as an int, from one add: the
 // 1.5·2^52 shift leaves the integer in the low word (replaces v_rndne + v_cvt_i32).
@@ -305,8 +306,8 @@ __device__ __forceinline__ void kernel_of_r2_tab_x2(double r2a, double r2b, cons
                                                     const double* tab, double& outa, double& outb) {
   double xa, xb, ka_, kb_, pa_ = pm[0], pb_ = pm[0];
   if constexpr (KIND == OMB_KERNEL_MATERN52) {
-    r2a = vmax_vs(r2a, ec.t[7]);
-    r2b = vmax_vs(r2b, ec.t[7]);
+    r2a = r2_clamp(r2a, ec.t[7]);
+    r2b = r2_clamp(r2b, ec.t[7]);
     const double ya = __builtin_amdgcn_rsq(r2a), yb = __builtin_amdgcn_rsq(r2b);
     double ga = r2a * ya, gb = r2b * yb, ha = 0.5 * ya, hb = 0.5 * yb;
     const double qa = fma(-ga, ha, 0.5), qb = fma(-gb, hb, 0.5);
@@ -323,8 +324,8 @@ __device__ __forceinline__ void kernel_of_r2_tab_x2(double r2a, double r2b, cons
     ka_ = fma(ga, ec.t[0], 6755399441055744.0);     // −√5·r·64/ln2 + 1.5·2^52
     kb_ = fma(gb, ec.t[0], 6755399441055744.0);
   } else {
-    xa = -0.5 * vmax_vs(r2a, 0.0);
-    xb = -0.5 * vmax_vs(r2b, 0.0);
+    xa = -0.5 * fabs(r2a);                        // GPy clips r² < 0 (rounding, ~1e-16) to 0
+    xb = -0.5 * fabs(r2b);
     ka_ = fma(xa, -ec.t[0] / kSqrt5, 6755399441055744.0);
     kb_ = fma(xb, -ec.t[0] / kSqrt5, 6755399441055744.0);
   }
@@ -357,8 +358,8 @@ __device__ __forceinline__ void kernel_of_r2_tab_x2(double r2a, double r2b, cons
 template <bool SHORT = false>
 __device__ __forceinline__ void matern_r2_tab256_x2(double r2a, double r2b, const double (&pm)[3], const ExpCoef& ec,
                                                     const double* tab, double& outa, double& outb) {
-  r2a = vmax_vs(r2a, ec.t[7]);
-  r2b = vmax_vs(r2b, ec.t[7]);
+  r2a = r2_clamp(r2a, ec.t[7]);
+  r2b = r2_clamp(r2b, ec.t[7]);
   const double ya = __builtin_amdgcn_rsq(r2a), yb = __builtin_amdgcn_rsq(r2b);
   double ga = r2a * ya, gb = r2b * yb, ha = 0.5 * ya, hb = 0.5 * yb;
   const double qa = fma(-ga, ha, 0.5), qb = fma(-gb, hb, 0.5);

@@ -990,15 +990,203 @@ __global__ __launch_bounds__(512, 2) void posterior_tile_kernel(GPArgs args, con
   OMB_POST_TRACE(5);
 }
 
+// ----------------------------------------------------------------------------- posterior, n ≤ 128, n_var ≤ 8
+// Persistent, barrier-free variant for BASELINE config 2 (n = 128, n_var = 6): L⁻¹ lives in LDS and
+// K* never does.  The whole-tile kernel above spends a third of each workgroup's life outside the
+// FP64 pipe (prologue behind the neighbour's multiply, one barrier, cross-wave reductions;
+// profiles/r02_v28_ablate_c2_tile_trace.txt).  Here:
+//   * each workgroup (one objective) stages the packed L⁻¹ (72 KiB at n = 128), α and the exp table
+//     in LDS once, synchronises once, and its waves then loop independently over 16-candidate tiles
+//     (wave-strided, every wave ends when the tiles run out — no further barrier);
+//   * a wave generates the K* tile of training-row tile T (16 rows × its 16 candidates) with the
+//     augmented r²-MFMA and the Matern transform; the accumulator's register e is the B fragment of
+//     k-step 4T + e, so the four values feed the MFMAs of V = L⁻¹K* straight from registers:
+//     acc[r] += L⁻¹[r, 4T..4T+3] · K*[4T..4T+3] for every row tile r ≥ T (A from LDS, 16-byte pair reads);
+//   * the 8 accumulators stay in registers for the whole tile and σ² = σ_f² − Σ acc² is reduced over
+//     the wave's 4 row groups by two shuffles; μ accumulates during generation the same way.
+// Work per tile equals the tile kernel's (144 MFMAs for V, ⌈(d+2)/4⌉·8 for r², 32 transforms per lane);
+// what goes is the idle pipe between phases.  Two 75-KiB workgroups (16 waves) share a CU; the grid is
+// sized to stay resident (G·n_obj ≈ 2·CUs).  Requires n ≤ 128 (R ≤ 8) and n_var ≤ 8.
+// RMAX (2, 4 or 8 row tiles) is a compile-time bound with no branch on the actual R: rows past n are
+// zero in the staged L⁻¹ and α, and tiles T ≥ R reuse row tile R−1's fragments (finite values that
+// meet only zeros), so the unrolled code has no wave-uniform control flow to merge around.
+// ABL (tools/ablate only): bit 1 stops after staging, bit 2 skips the multiply, bit 8 skips the
+// Matern transform (K* = r²).
+template <int RMAX, int DP, int KIND, int NW = 8, bool XL = false, int ABL = 0>
+__global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : NW / 4) void posterior_reg_kernel(
+    GPArgs args, const double* __restrict__ Xc, int64_t N, double* __restrict__ mu_out, double* __restrict__ var_out) {
+  constexpr int NT = 64 * NW;
+  static_assert(DP <= 8, "augmented r² needs n_var ≤ 8");
+  static_assert(RMAX >= 1 && RMAX <= 8, "n ≤ 128");
+  constexpr int KSD = (DP + 5) / 4;                 // k-steps of [x/ℓ, ‖x/ℓ‖², 1]
+  constexpr int KSDP = (KSD + 1) / 2;               // = packed_X_pairs(DP)
+  constexpr bool kTab256 = KIND == OMB_KERNEL_MATERN52;
+  constexpr int kTabN = kTab256 ? 256 : 64;
+  constexpr int kL2 = 64 * RMAX * (RMAX + 1);       // d2 elements of the packed L⁻¹
+  constexpr int kX2 = XL ? 64 * KSDP * RMAX : 1;    // d2 elements of the staged Xf (XL)
+  __shared__ double lds_L[2 * kL2];
+  __shared__ double lds_X[2 * kX2];
+  __shared__ double lds_alpha[16 * RMAX];
+  __shared__ double etab[kTabN];
+
+  const int obj = blockIdx.y;
+  const GPDev g = args.gp[obj];
+  const int d = args.d;
+  const int R = g.R;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t ntiles = (N + 15) / 16;
+  const int64_t stride = (int64_t)gridDim.x * NW;
+  int64_t t = (int64_t)blockIdx.x * NW + wave;
+  // the first tile's coordinates are in flight while the workgroup stages its operands
+  auto load_raw = [&](int64_t tt, double (&raw)[KSD]) {
+    const int64_t cc = min(16 * tt + (lane & 15), N - 1);
+#pragma unroll
+    for (int q = 0; q < KSD; ++q) {
+      const int j = 4 * q + (lane >> 4);
+      raw[q] = (j < d) ? Xc[cc * d + j] : 0.0;
+    }
+  };
+  double raw[KSD];
+  load_raw(t < ntiles ? t : 0, raw);
+  {
+    const int nL2 = 64 * R * (R + 1);
+    const d2* src = reinterpret_cast<const d2*>(g.Lp);
+    d2* dst = reinterpret_cast<d2*>(lds_L);
+    for (int i = tid; i < kL2; i += NT) dst[i] = i < nL2 ? src[i] : d2{0.0, 0.0};
+    if constexpr (XL) {
+      const int nX2 = 64 * KSDP * R;                // row tiles past R repeat tile R−1 (see Tl below)
+      const d2* xs2 = reinterpret_cast<const d2*>(g.Xf);
+      d2* xd2 = reinterpret_cast<d2*>(lds_X);
+      for (int i = tid; i < kX2; i += NT) xd2[i] = xs2[i < nX2 ? i : i % (64 * KSDP) + nX2 - 64 * KSDP];
+    }
+    if (tid < 16 * RMAX) lds_alpha[tid] = tid < 16 * R ? g.alpha[tid] : 0.0;
+    for (int i = tid; i < kTabN; i += NT) etab[i] = kTab256 ? kExp2Tab256[i] : kExp2Tab64[i];
+  }
+  __syncthreads();
+  if constexpr ((ABL & 1) != 0) return;
+
+  const double pm[3] = {g.variance, kSqrt5 * g.variance, kFiveThirds * g.variance};
+  const d2* xf = XL ? reinterpret_cast<const d2*>(lds_X) + lane : reinterpret_cast<const d2*>(g.Xf) + lane;
+  for (; t < ntiles; t += stride) {
+    const int64_t c = 16 * t + (lane & 15);
+    // B fragment [−2·x*/ℓ, 1, ‖x*/ℓ‖²]: lane l needs dims 4s + (l>>4) only; ‖x*/ℓ‖² from the four
+    // lane groups by two shuffles
+    double xs[KSD], csq = 0.0;
+#pragma unroll
+    for (int q = 0; q < KSD; ++q) {
+      const int j = 4 * q + (lane >> 4);
+      xs[q] = (j < d) ? raw[q] / g.ls[j] : 0.0;
+      csq = fma(xs[q], xs[q], csq);
+    }
+    if (t + stride < ntiles) load_raw(t + stride, raw);
+    csq += __shfl_xor(csq, 16);
+    csq += __shfl_xor(csq, 32);
+    double bfr[KSD];
+#pragma unroll
+    for (int s = 0; s < KSD; ++s) {
+      const int j = 4 * s + (lane >> 4);
+      bfr[s] = (j < d) ? -2.0 * xs[s] : (j == d ? 1.0 : (j == d + 1 ? csq : 0.0));
+    }
+
+    d4 acc[RMAX];
+    double mu_part = 0.0, s = 0.0;
+#pragma unroll
+    for (int T = 0; T < RMAX; ++T) {
+      const int Tl = XL ? T : min(T, R - 1);        // T ≥ R: finite stand-in rows (zero L⁻¹ / α)
+      d2 a[KSDP];
+#pragma unroll
+      for (int p = 0; p < KSDP; ++p) a[p] = xf[64 * (KSDP * Tl + p)];
+      d4 cr = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int q = 0; q < KSD; ++q)
+        cr = __builtin_amdgcn_mfma_f64_16x16x4f64((q & 1) ? a[q >> 1].y : a[q >> 1].x, bfr[q], cr, 0, 0, 0);
+      double kv[4];
+#pragma unroll
+      for (int e = 0; e < 4; e += 2) {
+        if constexpr ((ABL & 8) != 0) {
+          kv[e] = cr[e];
+          kv[e + 1] = cr[e + 1];
+        } else if constexpr (kTab256) {
+          matern_r2_tab256_x2(cr[e], cr[e + 1], pm, args.ec, etab, kv[e], kv[e + 1]);
+        } else {
+          kernel_of_r2_tab_x2<KIND>(cr[e], cr[e + 1], pm, args.ec, etab, kv[e], kv[e + 1]);
+        }
+        mu_part = fma(lds_alpha[16 * T + 4 * e + (lane >> 4)], kv[e], mu_part);
+        mu_part = fma(lds_alpha[16 * T + 4 * e + 4 + (lane >> 4)], kv[e + 1], mu_part);
+      }
+      if constexpr (!(ABL & 2)) {
+#pragma unroll
+        for (int r = T; r < RMAX; ++r) {
+          const d2* A = reinterpret_cast<const d2*>(lds_L + 128 * r * (r + 1) + 256 * T) + lane;
+          const d2 a0 = A[0], a1 = A[64];
+          d4 v = (T == 0) ? d4{0.0, 0.0, 0.0, 0.0} : acc[r];
+          v = __builtin_amdgcn_mfma_f64_16x16x4f64(a0.x, kv[0], v, 0, 0, 0);
+          v = __builtin_amdgcn_mfma_f64_16x16x4f64(a0.y, kv[1], v, 0, 0, 0);
+          v = __builtin_amdgcn_mfma_f64_16x16x4f64(a1.x, kv[2], v, 0, 0, 0);
+          acc[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1.y, kv[3], v, 0, 0, 0);
+        }
+      } else {
+        acc[T] = d4{kv[0], kv[1], kv[2], kv[3]};
+      }
+      // row tile T has all its k-steps (T' ≤ T): retire its accumulator, so at most RMAX − T are live
+#pragma unroll
+      for (int i = 0; i < 4; ++i) s = fma(acc[T][i], acc[T][i], s);
+    }
+    s += __shfl_xor(s, 16);
+    s += __shfl_xor(s, 32);
+    mu_part += __shfl_xor(mu_part, 16);
+    mu_part += __shfl_xor(mu_part, 32);
+    if (lane < 16 && c < N) {
+      mu_out[(int64_t)obj * N + c] = mu_part;
+      var_out[(int64_t)obj * N + c] = g.variance - s;
+    }
+  }
+}
+
+// Resident grid of posterior_reg_kernel: two workgroups per CU over all objectives.
+static int device_cu_count() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cached[dev] == 0) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    cached[dev] = cus;
+  }
+  return cached[dev];
+}
+
+static dim3 reg_grid(int64_t N, int n_obj, int NW = 8, int per_cu = 2) {
+  const int64_t waves_needed = (N + 15) / 16;
+  const int64_t wgs = (waves_needed + NW - 1) / NW;
+  const int64_t resident = std::max<int64_t>(1, (per_cu * (int64_t)device_cu_count()) / std::max(1, n_obj));
+  return dim3((unsigned)std::max<int64_t>(1, std::min(wgs, resident)), (unsigned)n_obj);
+}
+
 // ----------------------------------------------------------------------------- dispatch
 template <int DP, int KIND>
 static hipError_t launch_posterior_dp(hipStream_t stream, const GPArgs& args, int n_obj, int max_R,
                                       const double* Xc, int64_t N, double* mu, double* var) {
   const int Q = (max_R + 3) / 4;
   const int RTneed = (Q + 1) / 2;
-  if (RTneed <= 1) {
-    // n ≤ 128: the whole 128 × 64 K* tile in LDS, one barrier, balanced multiply (tools/ablate at
-    // n = 128, 2 objectives, 2^16 candidates: 0.083 ms for the r01 chunk pipeline → 0.074 ms;
+  if (RTneed <= 1 && DP <= 8) {
+    // n ≤ 128, n_var ≤ 8: persistent, L⁻¹ in LDS, K* in registers (posterior_reg_kernel)
+    if constexpr (DP <= 8) {
+      // 16 waves, one workgroup per CU, training rows staged in LDS: 0.062 ms at config 2 against
+      // 0.066 for two 8-wave workgroups per CU (profiles/r02_v49_ablate_c2.txt)
+      const dim3 grid = reg_grid(N, n_obj, 16, 1);
+      const dim3 block(1024);
+      if (max_R <= 2)
+        hipLaunchKernelGGL((posterior_reg_kernel<2, DP, KIND, 16, true>), grid, block, 0, stream, args, Xc, N, mu, var);
+      else if (max_R <= 4)
+        hipLaunchKernelGGL((posterior_reg_kernel<4, DP, KIND, 16, true>), grid, block, 0, stream, args, Xc, N, mu, var);
+      else
+        hipLaunchKernelGGL((posterior_reg_kernel<8, DP, KIND, 16, true>), grid, block, 0, stream, args, Xc, N, mu, var);
+    }
+  } else if (RTneed <= 1) {
+    // n ≤ 128, n_var > 8: the whole 128 × 64 K* tile in LDS, one barrier, balanced multiply (tools/ablate
+    // at n = 128, 2 objectives, 2^16 candidates: 0.083 ms for the r01 chunk pipeline → 0.074 ms;
     // profiles/r02_v11_ablate_c2.txt)
     dim3 grid((unsigned)((N + 63) / 64), n_obj);
     hipLaunchKernelGGL((posterior_tile_kernel<8, 4, DP, KIND>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var);

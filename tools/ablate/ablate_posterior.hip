@@ -82,6 +82,25 @@ float run_tile(const Bench& b, int reps) {
   return ms / reps;
 }
 
+template <int ABL, int NW = 8, bool XL = false, int DP = 6>
+float run_reg(const Bench& b, int reps) {
+  const dim3 grid = reg_grid(b.N, b.n_obj, NW, NW == 8 ? 2 : 1);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  hipLaunchKernelGGL((posterior_reg_kernel<8, DP, 0, NW, XL, ABL>), grid, dim3(64 * NW), 0, 0, b.a, b.Xc, b.N, b.mu, b.var);
+  CK(hipEventRecord(e0));
+  for (int i = 0; i < reps; ++i)
+    hipLaunchKernelGGL((posterior_reg_kernel<8, DP, 0, NW, XL, ABL>), grid, dim3(64 * NW), 0, 0, b.a, b.Xc, b.N, b.mu, b.var);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
+  return ms / reps;
+}
+
 // Accuracy of the table-driven Matern transforms against a long-double host reference.
 __global__ void matern_acc_kernel(const double* r2, int M, ExpCoef ec, double* out) {
   __shared__ double t64[64], t256[256];
@@ -307,6 +326,15 @@ int main(int argc, char** argv) {
   const Variant small128[] = {
       {"tile RMAX8 CT4 (library n<=128)", run_tile<8, 4, 0>},
       {"RT1 CT4 barrier (r01 library)", run<1, 4, 8, 32>},
+      {"reg: L^-1 in LDS, K* in registers", run_reg<0>},
+      {"reg gen only (2)", run_reg<2>},
+      {"reg staging only (1)", run_reg<1>},
+      {"reg no Matern, gen only (10)", run_reg<10>},
+      {"reg 8 waves, Xf in LDS", run_reg<0, 8, true>},
+      {"reg 12 waves 1 WG/CU", run_reg<0, 12, false>},
+      {"reg 12 waves 1 WG/CU Xf in LDS", run_reg<0, 12, true>},
+      {"reg 16 waves 1 WG/CU Xf in LDS", run_reg<0, 16, true>},
+      {"reg 12 waves gen only", run_reg<2, 12, true>},
       {"tile RMAX8 CT4 gen only (2)", run_tile<8, 4, 2>},
       {"tile RMAX8 CT4 const A (4)", run_tile<8, 4, 4>},
       {"tile RMAX8 CT4 rcp candidates (8)", run_tile<8, 4, 8>},
@@ -365,6 +393,22 @@ int main(int argc, char** argv) {
         ev = fmax(ev, fabs(v1[j] - v0[j]) / fmax(fabs(v0[j]), 1e-300));
       }
       printf("vs default: %-26s mu max rel %.2e  var max rel %.2e\n", vs[i].name, em, ev);
+      if (em > 1e-10 || ev > 1e-10) {       // where a variant disagrees: first cases, counts by lane slot
+        int64_t bad = 0, shown = 0, by16[16] = {0};
+        for (int64_t j = 0; j < n_obj * N; ++j) {
+          const bool w = fabs(m1[j] - m0[j]) > 1e-10 * fmax(fabs(m0[j]), 1e-300) ||
+                         fabs(v1[j] - v0[j]) > 1e-10 * fmax(fabs(v0[j]), 1e-300);
+          if (!w) continue;
+          ++bad;
+          ++by16[(j % N) % 16];
+          if (shown++ < 6)
+            printf("    obj %lld cand %lld (tile %lld): mu %.6e vs %.6e  var %.6e vs %.6e\n", (long long)(j / N),
+                   (long long)(j % N), (long long)((j % N) / 16), m1[j], m0[j], v1[j], v0[j]);
+        }
+        printf("    %lld of %lld disagree; by candidate %% 16:", (long long)bad, (long long)(n_obj * N));
+        for (int q = 0; q < 16; ++q) printf(" %lld", (long long)by16[q]);
+        printf("\n");
+      }
     }
   }
   double flops = (double)n_obj * N * ((double)n * (n + 1) + 2 * n + 2 * n + n * (2 * d + 2) + 10 * n);

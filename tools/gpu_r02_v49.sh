@@ -1,0 +1,13 @@
+#!/bin/bash
+# r² clamp without inline asm: ablations at configs 2 and 3, parity tests, default and config-2 bench
+set -e
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/${1:-r02_v49}
+mkdir -p "$O"
+timeout -k 10 120 ./tools/ablate/ablate_posterior 128 65536 6 2 > "$O/ablate_c2.txt" 2>&1
+timeout -k 10 120 ./tools/ablate/ablate_posterior 128 262144 6 2 > "$O/ablate_c2_N18.txt" 2>&1
+timeout -k 10 200 ./tools/ablate/ablate_posterior 512 1048576 6 2 > "$O/ablate_c3.txt" 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fused.py tests/test_gpu_edges.py tests/test_gpu_properties.py -x -v --timeout 120 --timeout-method thread > "$O/gpu_tests.txt" 2>&1
+timeout -k 10 300 python -u bench.py --no-cpu-baseline > "$O/bench.json" 2> "$O/bench.err"
+timeout -k 10 300 python -u bench.py --config 2 --steps 20 --warmup 5 --no-cpu-baseline > "$O/bench_c2.json" 2> "$O/bench_c2.err"
+echo v49-done

@@ -355,7 +355,7 @@ __device__ __forceinline__ void kernel_of_r2_tab_x2(double r2a, double r2b, cons
 // |f'| ≤ c/2, so |−√5 f'| ≤ ln2/512 and the degree-4 remainder is < 4e-17.  18 fp64 instructions
 // per element + rsq instead of 21 (no −√5 r product, one polynomial degree fewer).  SHORT drops the
 // residual correction of the sqrt (r from one Goldschmidt step on the v_rsq_f64 seed).
-template <bool SHORT = false>
+template <bool SHORT = false, bool IEXP = false>
 __device__ __forceinline__ void matern_r2_tab256_x2(double r2a, double r2b, const double (&pm)[3], const ExpCoef& ec,
                                                     const double* tab, double& outa, double& outb) {
   r2a = r2_clamp(r2a, ec.t[7]);
@@ -385,9 +385,20 @@ __device__ __forceinline__ void matern_r2_tab256_x2(double r2a, double r2b, cons
   sb = fma_vvs(sb, fb, ec.u[6]);
   const int ia = rka.ki, ib = rkb.ki;
   const double Ta = tab[ia & 255], Tb = tab[ib & 255];
-  const double ea = ldexp(fma(Ta, sa * fa, Ta), ia >> 8), eb = ldexp(fma(Tb, sb * fb, Tb), ib >> 8);
-  outa = pa_ * ea;
-  outb = pb_ * eb;
+  if constexpr (IEXP) {
+    // 2^(k>>8) applied as an integer add to the high word (integer VALU instead of v_ldexp_f64); the
+    // scale is clamped at 2^-1021 so the result stays normal (K* < 1e-300·σ_f² there instead of 0)
+    const double xa = fma(Ta, sa * fa, Ta), xb = fma(Tb, sb * fb, Tb);
+    const int ma = max(ia >> 8, -1021), mb = max(ib >> 8, -1021);
+    const double ea = __hiloint2double(__double2hiint(xa) + (ma << 20), __double2loint(xa));
+    const double eb = __hiloint2double(__double2hiint(xb) + (mb << 20), __double2loint(xb));
+    outa = pa_ * ea;
+    outb = pb_ * eb;
+  } else {
+    const double ea = ldexp(fma(Ta, sa * fa, Ta), ia >> 8), eb = ldexp(fma(Tb, sb * fb, Tb), ib >> 8);
+    outa = pa_ * ea;
+    outb = pb_ * eb;
+  }
 }
 
 // GPy Matern52.K_of_r: variance*(1+sqrt(5)*r+5/3*r**2)*exp(-sqrt(5)*r)  (r ≥ 0)

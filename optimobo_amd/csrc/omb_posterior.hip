@@ -1011,7 +1011,8 @@ __global__ __launch_bounds__(512, 2) void posterior_tile_kernel(GPArgs args, con
 // zero in the staged L⁻¹ and α, and tiles T ≥ R reuse row tile R−1's fragments (finite values that
 // meet only zeros), so the unrolled code has no wave-uniform control flow to merge around.
 // ABL (tools/ablate only): bit 1 stops after staging, bit 2 skips the multiply, bit 8 skips the
-// Matern transform (K* = r²).
+// Matern transform (K* = r²), bit 16 drops the sqrt's residual correction, bit 32 scales by 2^m with
+// an integer exponent add instead of v_ldexp_f64.
 template <int RMAX, int DP, int KIND, int NW = 8, bool XL = false, int ABL = 0>
 __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : NW / 4) void posterior_reg_kernel(
     GPArgs args, const double* __restrict__ Xc, int64_t N, double* __restrict__ mu_out, double* __restrict__ var_out) {
@@ -1037,7 +1038,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : NW / 4) void posterior_reg_k
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t ntiles = (N + 15) / 16;
   const int64_t stride = (int64_t)gridDim.x * NW;
-  int64_t t = (int64_t)blockIdx.x * NW + wave;
+  const int64_t first = (int64_t)blockIdx.x * NW + wave;
+  int64_t t = first;
   // the first tile's coordinates are in flight while the workgroup stages its operands
   auto load_raw = [&](int64_t tt, double (&raw)[KSD]) {
     const int64_t cc = min(16 * tt + (lane & 15), N - 1);
@@ -1070,6 +1072,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : NW / 4) void posterior_reg_k
   const d2* xf = XL ? reinterpret_cast<const d2*>(lds_X) + lane : reinterpret_cast<const d2*>(g.Xf) + lane;
   for (; t < ntiles; t += stride) {
     const int64_t c = 16 * t + (lane & 15);
+    if (t != first) load_raw(t, raw);
     // B fragment [−2·x*/ℓ, 1, ‖x*/ℓ‖²]: lane l needs dims 4s + (l>>4) only; ‖x*/ℓ‖² from the four
     // lane groups by two shuffles
     double xs[KSD], csq = 0.0;
@@ -1079,7 +1082,6 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : NW / 4) void posterior_reg_k
       xs[q] = (j < d) ? raw[q] / g.ls[j] : 0.0;
       csq = fma(xs[q], xs[q], csq);
     }
-    if (t + stride < ntiles) load_raw(t + stride, raw);
     csq += __shfl_xor(csq, 16);
     csq += __shfl_xor(csq, 32);
     double bfr[KSD];
@@ -1108,7 +1110,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : NW / 4) void posterior_reg_k
           kv[e] = cr[e];
           kv[e + 1] = cr[e + 1];
         } else if constexpr (kTab256) {
-          matern_r2_tab256_x2(cr[e], cr[e + 1], pm, args.ec, etab, kv[e], kv[e + 1]);
+          matern_r2_tab256_x2<(ABL & 16) != 0, (ABL & 32) != 0>(cr[e], cr[e + 1], pm, args.ec, etab, kv[e], kv[e + 1]);
         } else {
           kernel_of_r2_tab_x2<KIND>(cr[e], cr[e + 1], pm, args.ec, etab, kv[e], kv[e + 1]);
         }

@@ -100,6 +100,32 @@ def test_posterior_sizes(ctx, n, d, N):
     assert_posterior(mu.cpu().numpy(), var.cpu().numpy(), mu_o, var_o, variances)
 
 
+@pytest.mark.parametrize("n,d,N,n_obj,kernel", [
+    (5, 1, 17, 1, "matern52"), (32, 8, 100, 2, "matern52"),         # RMAX 2
+    (33, 7, 1000, 3, "matern52"), (64, 8, 77, 1, "rbf"),            # RMAX 4
+    (65, 2, 5000, 2, "rbf"), (120, 8, 300, 3, "matern52"),          # RMAX 8
+    (128, 6, 300001, 1, "matern52"), (128, 6, 131083, 2, "matern52"), (97, 5, 70000, 3, "rbf")])
+def test_posterior_small_n_persistent(ctx, n, d, N, n_obj, kernel):
+    """n ≤ 128, n_var ≤ 8: posterior_reg_kernel — each row-tile bound (RMAX 2/4/8), both kernels, 1–3
+    objectives (different resident grids) and ragged batches where every wave loops over several
+    16-candidate tiles; a sample of candidates against the oracle, the whole batch for finiteness."""
+    rng = np.random.default_rng(n * 7 + d + N)
+    X = rng.uniform(0, 1, (n, d))
+    Y = np.column_stack([np.sin(3 * X).sum(1), np.cos(2 * X).prod(1), (X ** 2).sum(1)])[:, :n_obj]
+    ls = rng.uniform(0.2, 2.0, d) * np.sqrt(d)
+    variances = [float(np.var(Y[:, o]) + 0.1) for o in range(n_obj)]
+    set_gps(ctx, X, Y, ls, variances, kernel=kernel)
+    Xc = rng.uniform(0, 1, (N, d))
+    Xc[: min(3, N)] = X[: min(3, N)]
+    mu, var = ctx.posterior(dev(Xc), n_obj=n_obj)
+    mu, var = mu.cpu().numpy(), var.cpu().numpy()
+    assert np.isfinite(mu).all() and np.isfinite(var).all()
+    idx = np.unique(np.concatenate([np.arange(min(N, 40)), np.arange(max(0, N - 40), N),
+                                    rng.choice(N, min(N, 2000), replace=False)]))
+    mu_o, var_o = oracle_posterior(X, Y, ls, variances, Xc[idx], kernel=kernel)
+    assert_posterior(mu[:, idx], var[:, idx], mu_o, var_o, variances)
+
+
 @pytest.mark.parametrize("n", [96, 200, 400, 900])   # every posterior dispatch shape (RT 1/2/4/8)
 def test_posterior_rbf_kernel(ctx, n):
     rng = np.random.default_rng(5)

@@ -330,9 +330,12 @@ int main(int argc, char** argv) {
       {"reg gen only (2)", run_reg<2>},
       {"reg staging only (1)", run_reg<1>},
       {"reg no Matern, gen only (10)", run_reg<10>},
+      {"reg16 short sqrt (16)", run_reg<16, 16, true>},
+      {"reg16 int exponent (32)", run_reg<32, 16, true>},
+      {"reg16 short sqrt + int exp (48)", run_reg<48, 16, true>},
+      {"reg16 gen only", run_reg<2, 16, true>},
       {"reg 8 waves, Xf in LDS", run_reg<0, 8, true>},
-      {"reg 12 waves 1 WG/CU", run_reg<0, 12, false>},
-      {"reg 12 waves 1 WG/CU Xf in LDS", run_reg<0, 12, true>},
+
       {"reg 16 waves 1 WG/CU Xf in LDS", run_reg<0, 16, true>},
       {"reg 12 waves gen only", run_reg<2, 12, true>},
       {"tile RMAX8 CT4 gen only (2)", run_tile<8, 4, 2>},

@@ -587,6 +587,11 @@ def main():
             out["best"]["note"] = ("reference-mode EHVI passes sigma_B = var_0*s01 (util_functions.py:163-167); this "
                                    f"cache has s01 = {s01:.4g} < 0, so the acquisition is <= 0 everywhere and the "
                                    "arg-max is the lowest index among its maxima (DESIGN.md section 2, quirk 2)")
+        if acq_kind == "ehvi3d" and args.mode == "reference" and float(best[0]) <= 0.0:
+            out["best"]["note"] = ("reference EHVI_3D credits a Monte-Carlo sample only when the hypervolume of that "
+                                   "single point exceeds the whole front's (util_functions.py:202-211); with a dense "
+                                   "256-point front no sample does, so the acquisition is 0 and the arg-max is the "
+                                   "lowest index among its maxima; --mode textbook gives the exact EHVI")
         print(json.dumps(out))
     if world_size > 1:
         dist.barrier()

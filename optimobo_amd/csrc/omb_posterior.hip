@@ -254,6 +254,28 @@ __global__ __launch_bounds__(512) void kernel_block_pipe_kernel(GPDev g, int d, 
   for (int t = 0; t < NCT; ++t) {
     const int64_t c = cb + 16 * t + (lane & 15);
     const int64_t ci = c < N ? c : N - 1;
+    if constexpr (!kSwap) {
+      // lane l needs only dims 4s + (l>>4) of its candidate (KSD divisions instead of d + KSD);
+      // ‖x*/ℓ‖² from the four lane groups by two shuffles.  At n_var = 30 the staged kernel overtook
+      // the round-1 kernel with this (1.70 → 1.44 ms, profiles/r02_v54_ablate_kblock_c5.txt); at
+      // n_var = 6 it is 0.80 → 0.78 ms (profiles/r02_v55_ablate_kblock_c3*.txt)
+      double s2 = 0.0, xs[KSD];
+#pragma unroll
+      for (int s = 0; s < KSD; ++s) {
+        const int j = 4 * s + (lane >> 4);
+        xs[s] = (j < d) ? Xc[ci * d + j] / g.ls[j] : 0.0;
+        s2 = fma(xs[s], xs[s], s2);
+      }
+      s2 += __shfl_xor(s2, 16);
+      s2 += __shfl_xor(s2, 32);
+      csq[t] = s2;
+#pragma unroll
+      for (int s = 0; s < KSD; ++s) {
+        const int j = 4 * s + (lane >> 4);
+        bfr[t][s] = kAug ? ((j < d) ? -2.0 * xs[s] : (j == d ? 1.0 : (j == d + 1 ? s2 : 0.0))) : xs[s];
+      }
+      continue;
+    }
     double s2 = 0.0;
 #pragma unroll
     for (int j = 0; j < DP; ++j) {
@@ -1237,8 +1259,11 @@ template <int KIND>
 static hipError_t launch_kblock_kind(hipStream_t stream, const GPArgs& args, int obj, const double* Xc, int64_t N,
                                      double* K) {
   const GPDev& g = args.gp[obj];
-  // n_var ≤ 8: LDS-staged fragments, 128 candidates per workgroup (kernel_block_pipe_kernel);
-  // wider inputs keep kernel_block_mfma_kernel (faster there: profiles/r02_v4_ablate_kblock_c5.txt)
+  // LDS-staged fragments, 128 candidates per workgroup (kernel_block_pipe_kernel) for every n_var.
+  // n_var > 8 first kept kernel_block_mfma_kernel (profiles/r02_v4_ablate_kblock_c5.txt: the staged
+  // kernel's per-workgroup candidate setup divided every coordinate); with each lane dividing only the
+  // coordinates of its B-fragment slots the staged kernel is faster there too (config 5, n = 1024,
+  // d = 30, N = 2^19: 1.70 → 1.44 ms, profiles/r02_v54_ablate_kblock_c5.txt)
   auto pipe_grid = [&](int DP) {
     return dim3((unsigned)((N + 127) / 128), (unsigned)((g.n + kblock_rows(DP) - 1) / kblock_rows(DP)));
   };
@@ -1248,7 +1273,7 @@ static hipError_t launch_kblock_kind(hipStream_t stream, const GPArgs& args, int
   case DPV: hipLaunchKernelGGL((kernel_block_pipe_kernel<DPV, KIND, true, kKBlockSwap>), pipe_grid(DPV), dim3(512), 0, stream, g, args.d, Xc, N, K, exp_coef()); break;
 #define OMB_KB(DPV) \
   case DPV: hipLaunchKernelGGL((kernel_block_mfma_kernel<DPV, KIND>), grid, dim3(256), 0, stream, g, args.d, Xc, N, K, exp_coef()); break;
-    OMB_KBP(2) OMB_KBP(4) OMB_KBP(6) OMB_KBP(8) OMB_KB(16) OMB_KB(32) OMB_KB(64)
+    OMB_KBP(2) OMB_KBP(4) OMB_KBP(6) OMB_KBP(8) OMB_KBP(16) OMB_KBP(32) OMB_KBP(64)
 #undef OMB_KB
 #undef OMB_KBP
     default: return hipErrorInvalidValue;

@@ -140,7 +140,8 @@ def test_posterior_rbf_kernel(ctx, n):
     assert_posterior(mu.cpu().numpy(), var.cpu().numpy(), mu_o, var_o, variances)
 
 
-@pytest.mark.parametrize("n,d,N", [(20, 2, 100), (512, 6, 4099), (100, 30, 77), (300, 64, 129)])
+@pytest.mark.parametrize("n,d,N", [(20, 2, 100), (512, 6, 4099), (100, 30, 77), (300, 64, 129), (150, 12, 333),
+                                   (257, 8, 1000), (1030, 30, 260)])
 def test_kernel_block(ctx, n, d, N):
     rng = np.random.default_rng(n + d)
     X = rng.uniform(0, 1, (n, d))

@@ -155,7 +155,7 @@ def run_solve(args, cfg, world_size, rank):
             split[name] += time.perf_counter() - t
             return r
         return w
-    opt._fit = timed("fit", opt._fit)
+    opt._fit_many = timed("fit", opt._fit_many)          # the per-objective fits (concurrent on the GPU)
     opt._maximise = timed("maximise", opt._maximise)
     t0 = time.perf_counter()
     res = opt.solve(budget=budget, n_init_samples=20, sample_exponent=3,

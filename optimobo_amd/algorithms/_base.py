@@ -11,7 +11,7 @@ import numpy as np
 from .. import pareto
 from .. import util_functions
 from ..acquisition import engine_for
-from ..gp import GPRegression, Matern52
+from ..gp import GPRegression, Matern52, fit_concurrently
 from ..parallel import agree_host_rng
 from ..result import Res
 
@@ -63,11 +63,23 @@ class BODriver:
     def _hypervolume(self, ysample):
         return pareto.hypervolume(ysample, self.max_point)
 
-    def _fit(self, X, y):
+    def _model(self, X, y):
         model = GPRegression(X, np.reshape(y, (-1, 1)), Matern52(self.n_vars, ARD=True))
         model.Gaussian_noise.variance.fix(0)
+        return model
+
+    def _fit(self, X, y):
+        model = self._model(X, y)
         model.optimize(messages=False, max_f_eval=1000)
         return model
+
+    def _fit_many(self, X, ys):
+        """One surrogate per column of ``ys`` on the same inputs, as the reference's per-objective
+        loop does (optimisers.py:186, emo.py:297-301); the independent fits run concurrently on the
+        GPU (gp.fit_concurrently), each taking the path it takes alone."""
+        models = [self._model(X, ys[:, i]) for i in range(ys.shape[1])]
+        fit_concurrently(models, device=self.device, messages=False, max_f_eval=1000)
+        return models
 
     def _maximise(self, models, acq_fn):
         """acq_fn None: the plan set on the engine (fused chain); else a batched callable."""

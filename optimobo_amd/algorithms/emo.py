@@ -52,7 +52,7 @@ class EMO(BODriver):
             if not self.is_max_known:
                 self.max_point = ysample.max(axis=0).astype(float)
             hypervolume_convergence.append(self._hypervolume(ysample))
-            models = [self._fit(Xsample, ysample[:, i]) for i in range(self.n_obj)]
+            models = self._fit_many(Xsample, ysample[:, :self.n_obj])
             cells = self.decompose_into_cells(pareto.calc_pf(ysample))
             X_next, _ = self.get_proposed(self.hypervolume_based_PoI, ysample, cells, models)
             y_next = self._objective_function(problem, X_next)

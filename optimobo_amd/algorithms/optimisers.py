@@ -51,7 +51,7 @@ class MultiSurrogateOptimiser(BODriver):
         for _ in range(budget):
             self._update_bounds(ysample, acquisition_func)
             hypervolume_convergence.append(self._hypervolume(ysample))
-            models = [self._fit(Xsample, ysample[:, i]) for i in range(problem.n_obj)]
+            models = self._fit_many(Xsample, ysample[:, :problem.n_obj])
             ref_dir = np.asarray(ref_dirs[np.random.randint(0, len(ref_dirs))])
             if acquisition_func is None:
                 pf = pareto.calc_pf(ysample)

@@ -15,6 +15,9 @@ omb_gp_fit_state.  Without a GPU (the CPU test suite) the same arithmetic runs i
 ``predict`` — the hot path — runs on the GPU through the HIP posterior kernel
 (optimobo_amd.device); there is no CPU prediction path.
 """
+import concurrent.futures
+import threading
+
 import numpy as np
 from scipy import linalg, optimize
 
@@ -168,6 +171,63 @@ def _device_available():
         return False
 
 
+# ----------------------------------------------------------------------------- concurrent fits
+# The drivers fit one surrogate per objective from the same inputs (optimisers.py:223-231, called per
+# objective at :186; emo.py:297-301).  The fits are independent and deterministic, so on the GPU they
+# run at once: each on a pool thread with its own device context and HIP stream.  An evaluation is one
+# C call that synchronises its stream (≈ 0.1 ms at the BO loop's sizes, most of it host-side: scipy,
+# ctypes, launch); ctypes drops the GIL inside the call, so one fit's host work overlaps the other's
+# device work.  Every fit takes exactly the path it takes alone (same start, same arithmetic).
+_FIT_TLS = threading.local()
+_FIT_POOL = None
+_FIT_POOL_LOCK = threading.Lock()
+_FIT_CONTEXTS = []          # the pool threads' contexts live as long as the process, like the engines
+
+
+def _fit_context():
+    ctx = getattr(_FIT_TLS, "ctx", None)
+    if ctx is not None:
+        return ctx
+    from .acquisition import engine_for
+    return engine_for([]).ctx
+
+
+def _fit_on_thread(model, device, kw):
+    import torch
+    if getattr(_FIT_TLS, "ctx", None) is None:
+        torch.cuda.set_device(device)
+        from .device import AcqContext
+        _FIT_TLS.ctx = AcqContext(device)
+        _FIT_TLS.stream = torch.cuda.Stream(device)
+        with _FIT_POOL_LOCK:
+            _FIT_CONTEXTS.append(_FIT_TLS.ctx)
+    with torch.cuda.stream(_FIT_TLS.stream):
+        res = model.optimize(**kw)
+    _FIT_TLS.stream.synchronize()
+    return res
+
+
+def fit_concurrently(models, device=None, **kw):
+    """``model.optimize(**kw)`` for every model; concurrently when they fit on the GPU."""
+    global _FIT_POOL
+    models = list(models)
+    if len(models) < 2 or not all(m.device_fit and m.Gaussian_noise.variance.fixed for m in models):
+        return [m.optimize(**kw) for m in models]
+    import torch
+    if device is None:
+        dev = torch.cuda.current_device()
+    elif isinstance(device, torch.device):
+        dev = device.index if device.index is not None else torch.cuda.current_device()
+    else:
+        dev = int(device)
+    with _FIT_POOL_LOCK:
+        if _FIT_POOL is None:
+            _FIT_POOL = concurrent.futures.ThreadPoolExecutor(max_workers=4, thread_name_prefix="omb-gp-fit")
+    torch.cuda.current_stream(dev).synchronize()       # inputs staged on the caller's stream
+    futures = [_FIT_POOL.submit(_fit_on_thread, m, dev, kw) for m in models]
+    return [f.result() for f in futures]
+
+
 # ----------------------------------------------------------------------------- GPRegression
 def _logexp(p):
     """GPy's Logexp transform θ = log(1 + e^p) (stable for large |p|), floored away from 0."""
@@ -231,8 +291,7 @@ class GPRegression:
         import torch
         from . import _lib
         self._set_free(theta)
-        from .acquisition import engine_for
-        ctx = engine_for([]).ctx          # the shared context, without installing this model
+        ctx = _fit_context()              # the shared context (or a fit thread's own), without installing this model
         if self._dev_xy is None:
             self._dev_xy = (torch.as_tensor(self.X, device=ctx.device), torch.as_tensor(self.Y[:, 0], device=ctx.device))
         Xd, yd = self._dev_xy

@@ -137,3 +137,36 @@ def test_lml_grad_small_path_deterministic(ctx):
     r1 = ctx.gp_lml_grad(X, y, ls, var)
     r2 = ctx.gp_lml_grad(X, y, ls, var)
     assert r1[0] == r2[0] and np.array_equal(r1[1], r2[1])
+
+
+@pytest.mark.parametrize("n", [20, 60, 119])
+def test_concurrent_fits_match_sequential(n):
+    """gp.fit_concurrently (the drivers' per-objective fits on pool threads, one context and stream
+    each) gives bitwise the hyperparameters of fitting the same models one after another."""
+    from optimobo_amd.gp import GPRegression, Matern52, fit_concurrently
+    rng = np.random.default_rng(n)
+    X = rng.uniform(-2, 2, (n, 2))
+    Y = np.column_stack([100 * (X ** 2).sum(1), ((X[:, 0] - 1) ** 2 + X[:, 1] ** 2), np.sin(3 * X).sum(1)])
+
+    def models():
+        out = []
+        for i in range(Y.shape[1]):
+            m = GPRegression(X, Y[:, i:i + 1], Matern52(2, ARD=True))
+            m.Gaussian_noise.variance.fix(0)
+            out.append(m)
+        return out
+
+    seq = models()
+    for m in seq:
+        m.optimize(max_f_eval=1000)
+    con = models()
+    fit_concurrently(con, max_f_eval=1000)
+    for a, b in zip(seq, con):
+        assert float(a.kern.variance) == float(b.kern.variance)
+        assert np.array_equal(a.kern.lengthscale.values, b.kern.lengthscale.values)
+    # the fitted models predict identically through the shared engine
+    Xc = rng.uniform(-2, 2, (257, 2))
+    for a, b in zip(seq, con):
+        ma, va = a.predict(Xc)
+        mb, vb = b.predict(Xc)
+        assert np.array_equal(ma, mb) and np.array_equal(va, vb)

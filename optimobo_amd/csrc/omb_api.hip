@@ -81,6 +81,10 @@ struct omb_ctx {
   // device fault word (pinned, mapped host memory): kernels mark it, enter() reports it
   int* fault_host = nullptr;
   int* fault_dev = nullptr;
+  // GP-fit results (omb_gp_lml_grad): pinned, host-mapped; the one-workgroup kernel stores into it
+  // directly (no D2H copy on the per-evaluation path), the blocked path copies into it
+  double* fit_host = nullptr;
+  double* fit_dev = nullptr;
   int spin_limit = kDefaultSpinLimit;
 };
 
@@ -430,7 +434,10 @@ int omb_create(int device, omb_ctx** out) {
       hipHostMalloc(&ctx->result_host, sizeof(double) * 2, hipHostMallocDefault) != hipSuccess ||
       hipMalloc(&ctx->sob, sobol_state_bytes(OMB_MAX_DIM, 32)) != hipSuccess ||
       hipHostMalloc(&ctx->fault_host, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
-      hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->fault_dev), ctx->fault_host, 0) != hipSuccess) {
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->fault_dev), ctx->fault_host, 0) != hipSuccess ||
+      hipHostMalloc(&ctx->fit_host, sizeof(double) * (OMB_MAX_DIM + 8), hipHostMallocMapped | hipHostMallocCoherent) !=
+          hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->fit_dev), ctx->fit_host, 0) != hipSuccess) {
     omb_destroy(ctx);
     return OMB_ENOMEM;
   }
@@ -460,6 +467,7 @@ int omb_destroy(omb_ctx* ctx) {
   if (ctx->fws) (void)hipFree(ctx->fws);
   if (ctx->dws) (void)hipFree(ctx->dws);
   if (ctx->fault_host) (void)hipHostFree(ctx->fault_host);
+  if (ctx->fit_host) (void)hipHostFree(ctx->fit_host);
   for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;
@@ -1152,14 +1160,12 @@ int omb_gp_lml_grad(omb_ctx* ctx, int kernel, int n, int d, const double* X_dev,
   if (!(variance > 0.0) || !(noise >= 0.0)) return fail(ctx, OMB_EINVAL, "variance must be > 0 and noise >= 0");
   const int DP = pad_dim(d);
   if (gp_lml_small_fits(n, DP)) {
-    // one workgroup, one launch, one synchronisation (launch_gp_lml_small)
-    if ((rc = grow_dev(ctx, &ctx->fws, &ctx->fws_cap, sizeof(double) * (DP + 5), "GP fit workspace"))) return rc;
-    double* dout = static_cast<double*>(ctx->fws);
+    // one workgroup, one launch, one synchronisation (launch_gp_lml_small); the kernel stores its
+    // DP + 5 results straight into the pinned, host-mapped fit_host (no D2H copy per evaluation)
     OMB_HIP(ctx, launch_gp_lml_small(ctx->stream, kernel, DP, X_dev, d, n, lengthscale_host, variance, noise + 1e-8,
-                                     y_dev, dout));
-    double h[OMB_MAX_DIM + 5];
-    OMB_HIP(ctx, hipMemcpyAsync(h, dout, sizeof(double) * (DP + 5), hipMemcpyDeviceToHost, ctx->stream));
+                                     y_dev, ctx->fit_dev));
     OMB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    const volatile double* h = ctx->fit_host;
     if (h[DP + 4] != 0.0)
       return fail(ctx, OMB_ENOTPD, "K + jitter is not positive definite, even with jitter (column %d)", (int)h[DP + 4]);
     *lml = -0.5 * h[DP + 2] - h[DP + 1] - 0.5 * n * log(2.0 * M_PI);
@@ -1173,9 +1179,9 @@ int omb_gp_lml_grad(omb_ctx* ctx, int kernel, int n, int d, const double* X_dev,
   OMB_HIP(ctx, launch_gemm_tn_lower(ctx->stream, n, n, 1.0, f.Linv, n, 0.0, f.Kinv, n));
   OMB_HIP(ctx, launch_gp_grad(ctx->stream, kernel, DP, X_dev, d, n, f.ls, variance, f.alpha, f.Kinv, n, f.part,
                               f.Ky, n, y_dev, f.out));
-  double h[OMB_MAX_DIM + 3];
-  OMB_HIP(ctx, hipMemcpyAsync(h, f.out, sizeof(double) * (DP + 3), hipMemcpyDeviceToHost, ctx->stream));
+  OMB_HIP(ctx, hipMemcpyAsync(ctx->fit_host, f.out, sizeof(double) * (DP + 3), hipMemcpyDeviceToHost, ctx->stream));
   OMB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  const volatile double* h = ctx->fit_host;
   // GPy: log p(y) = −½ yᵀα − Σ log L_ii − ½ n log 2π
   *lml = -0.5 * h[DP + 2] - h[DP + 1] - 0.5 * n * log(2.0 * M_PI);
   for (int q = 0; q <= d; ++q) grad[q] = h[q];

@@ -48,8 +48,10 @@ class AcqContext:
             raise _lib.OMBError(rc, f"{what}: {msg.decode() if msg else ''}")
 
     def _stream(self):
-        s = torch.cuda.current_stream(self.device)
-        self._check(self.lib.omb_set_stream(self._h, ctypes.c_void_p(s.cuda_stream)), "omb_set_stream")
+        s = torch.cuda.current_stream(self.device).cuda_stream
+        if s != getattr(self, "_cur_stream", None):     # one C call per stream change, not per call
+            self._check(self.lib.omb_set_stream(self._h, ctypes.c_void_p(s)), "omb_set_stream")
+            self._cur_stream = s
 
     def close(self):
         if getattr(self, "_h", None):

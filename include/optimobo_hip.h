@@ -293,6 +293,18 @@ int omb_ea_search(omb_ctx* ctx, int mode, double best, double var_eps, const dou
 int omb_gp_lml_grad(omb_ctx* ctx, int kernel, int n, int d, const double* X_dev, const double* y_dev,
                     const double* lengthscale_host, double variance, double noise, double* lml, double* grad_host,
                     double* jitter_used);
+/* k ≤ 4 GPs on the same inputs at once (the drivers fit one GP per objective on the same X;
+ * optimisers.py:186): problem p has targets y_dev[p] (device pointer, n), lengthscales
+ * lengthscale_host[p·d .. p·d + d − 1] and variance_host[p]; its results go to lml[p], grad_host[p·(d+1) ..],
+ * jitter_used[p] (may be NULL) and status[p] (OMB_OK or OMB_ENOTPD, per problem: one non-positive-definite
+ * problem does not fail the others).  Each problem's results are exactly omb_gp_lml_grad's: for n ≤ 96
+ * and n_var ≤ 8 they run as one launch (one workgroup each) and one synchronisation, otherwise one after
+ * another through omb_gp_lml_grad.  Replaces GPy
+ * model.optimize's per-objective evaluations (optimisers.py:231).  Returns OMB_OK unless an argument or the
+ * device call fails. */
+int omb_gp_lml_grad_batch(omb_ctx* ctx, int kernel, int k, int n, int d, const double* X_dev,
+                          const double* const* y_dev, const double* lengthscale_host, const double* variance_host,
+                          double noise, double* lml, double* grad_host, double* jitter_used, int* status);
 /* Fit the exact-inference state of objective `obj` on the device (Cholesky, L⁻¹, α) and install
  * it as omb_set_gp would — the device replacement for the host O(n³) factorisation. */
 int omb_gp_fit_state(omb_ctx* ctx, int obj, int kernel, int n, int d, const double* X_dev, const double* y_dev,

@@ -72,6 +72,7 @@ SIGNATURES = {
     "omb_ea_search": (_i, [_p, _i, _d, _d, _p, _i, _i, _p, _p, _p, _p, _p, _p, _p]),
     # GP fit on the device
     "omb_gp_lml_grad": (_i, [_p, _i, _i, _i, _p, _p, _dp, _d, _d, _dp, _dp, _dp]),
+    "omb_gp_lml_grad_batch": (_i, [_p, _i, _i, _i, _i, _p, _p, _dp, _dp, _d, _dp, _dp, _dp, _p]),
     "omb_gp_fit_state": (_i, [_p, _i, _i, _i, _i, _p, _p, _dp, _d, _d, _dp]),
 }
 

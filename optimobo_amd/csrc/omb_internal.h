@@ -149,6 +149,11 @@ int64_t gp_grad_blocks(int64_t n);
 bool gp_lml_small_fits(int n, int DP);
 hipError_t launch_gp_lml_small(hipStream_t stream, int kind, int DP, const double* X, int d, int n,
                                const double* ls_host, double variance, double base, const double* y, double* out);
+// k ≤ kFitBatchMax problems on the same X (y[p], ls_host[p·d..], variance[p] → out[p]), one workgroup each
+constexpr int kFitBatchMax = 4;
+hipError_t launch_gp_lml_small_batch(hipStream_t stream, int kind, int DP, const double* X, int d, int n, int k,
+                                     const double* const* y, const double* ls_host, const double* variance,
+                                     double base, double* const* out);
 // dense posterior path: μ, σ² of a candidate chunk from K* (n, Nc) and V = L⁻¹K* (n, Nc).
 hipError_t launch_post_colreduce(hipStream_t stream, const double* Kst, const double* V, int64_t n, int64_t Nc,
                                  const double* alpha, double variance, double* mu, double* var);

@@ -937,10 +937,9 @@ __device__ __forceinline__ void fit_pair(const double* __restrict__ a, const dou
 
 // Thread map: wave w owns rows i ≡ w (mod 16), lane l owns columns l and l + 64.
 template <int DP, int KIND>
-__global__ __launch_bounds__(kSmallFitThreads) void gp_lml_small_kernel(const double* __restrict__ X, int d, int n,
-                                                                        FitLs ls, double variance, double base,
-                                                                        const double* __restrict__ y,
-                                                                        double* __restrict__ out) {
+__device__ __forceinline__ void gp_lml_small_body(const double* __restrict__ X, int d, int n, const FitLs& ls,
+                                                  double variance, double base, const double* __restrict__ y,
+                                                  double* __restrict__ out) {
   constexpr int NW = kSmallFitThreads / 64, LD = kSmallFitLD, RPW = kSmallFitN / NW;
   __shared__ double A[kSmallFitN * LD];
   __shared__ double xs[kSmallFitXs];
@@ -1154,6 +1153,33 @@ __global__ __launch_bounds__(kSmallFitThreads) void gp_lml_small_kernel(const do
   }
 }
 
+template <int DP, int KIND>
+__global__ __launch_bounds__(kSmallFitThreads) void gp_lml_small_kernel(const double* __restrict__ X, int d, int n,
+                                                                        FitLs ls, double variance, double base,
+                                                                        const double* __restrict__ y,
+                                                                        double* __restrict__ out) {
+  gp_lml_small_body<DP, KIND>(X, d, n, ls, variance, base, y, out);
+}
+
+// Several GPs on the same inputs (the drivers' per-objective fits), one workgroup each, one launch:
+// workgroup b evaluates problem b with exactly the single-problem arithmetic.
+struct FitBatch {
+  const double* y[kFitBatchMax];
+  double* out[kFitBatchMax];
+  double ls[kFitBatchMax][8];
+  double variance[kFitBatchMax];
+};
+
+template <int DP, int KIND>
+__global__ __launch_bounds__(kSmallFitThreads) void gp_lml_small_batch_kernel(const double* __restrict__ X, int d,
+                                                                              int n, FitBatch b, double base) {
+  const int p = blockIdx.x;
+  FitLs ls;
+#pragma unroll
+  for (int j = 0; j < OMB_MAX_DIM; ++j) ls.v[j] = j < 8 ? b.ls[p][j] : 1.0;
+  gp_lml_small_body<DP, KIND>(X, d, n, ls, b.variance[p], base, b.y[p], b.out[p]);
+}
+
 // DP ≤ 8: the two candidate columns' scaled coordinates stay in registers (DP = 16 spills at 1024 threads).
 // n ≤ 96: the sweep is one CU's work, n/2 steps of n²/2 entries with a barrier each; measured per evaluation
 // (tools/bench_gpfit.py, profiles/r01_v20_gpfit.jsonl) 0.076 / 0.10 / 0.18 / 0.32 ms at n = 32 / 64 / 96 / 128
@@ -1180,6 +1206,35 @@ hipError_t launch_gp_lml_small(hipStream_t stream, int kind, int DP, const doubl
     default: return hipErrorInvalidValue;
   }
 #undef OMB_GS
+  return hipGetLastError();
+}
+
+hipError_t launch_gp_lml_small_batch(hipStream_t stream, int kind, int DP, const double* X, int d, int n, int k,
+                                     const double* const* y, const double* ls_host, const double* variance,
+                                     double base, double* const* out) {
+  if (!gp_lml_small_fits(n, DP) || d < 1 || d > DP || DP > 8 || k < 1 || k > kFitBatchMax)
+    return hipErrorInvalidValue;
+  FitBatch b{};
+  for (int p = 0; p < k; ++p) {
+    b.y[p] = y[p];
+    b.out[p] = out[p];
+    b.variance[p] = variance[p];
+    for (int j = 0; j < 8; ++j) b.ls[p][j] = (j < d) ? ls_host[p * d + j] : 1.0;
+  }
+#define OMB_GSB(DPV)                                                                                        \
+  case DPV:                                                                                                 \
+    if (kind == OMB_KERNEL_RBF)                                                                             \
+      hipLaunchKernelGGL((gp_lml_small_batch_kernel<DPV, OMB_KERNEL_RBF>), dim3(k), dim3(kSmallFitThreads), 0, \
+                         stream, X, d, n, b, base);                                                          \
+    else                                                                                                    \
+      hipLaunchKernelGGL((gp_lml_small_batch_kernel<DPV, OMB_KERNEL_MATERN52>), dim3(k),                    \
+                         dim3(kSmallFitThreads), 0, stream, X, d, n, b, base);                              \
+    break;
+  switch (DP) {
+    OMB_GSB(2) OMB_GSB(4) OMB_GSB(6) OMB_GSB(8)
+    default: return hipErrorInvalidValue;
+  }
+#undef OMB_GSB
   return hipGetLastError();
 }
 

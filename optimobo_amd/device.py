@@ -313,6 +313,31 @@ class AcqContext:
                     "omb_gp_lml_grad")
         return lml.value, np.array(grad[:]), jit.value
 
+    def gp_lml_grad_batch(self, X, ys, lengthscales, variances, noise=0.0, kernel="matern52"):
+        """omb_gp_lml_grad_batch: k ≤ 4 GPs on the same inputs in one call — (lml (k,), grad (k, d+1),
+        jitter (k,), status (k,)); status[p] is 0 or OMB_ENOTPD for problem p."""
+        X = _dev_f64(X, self.device)
+        ys = [_dev_f64(y, self.device).reshape(-1) for y in ys]
+        n, d = X.shape
+        k = len(ys)
+        if any(y.shape[0] != n for y in ys):
+            raise ValueError("gp_lml_grad_batch: every y needs one value per input row")
+        ls = np.ascontiguousarray(np.broadcast_to(np.asarray(lengthscales, np.float64), (k, d)))
+        var = np.ascontiguousarray(np.asarray(variances, np.float64).reshape(k))
+        kid = {"matern52": _lib.KERNEL_MATERN52, "rbf": _lib.KERNEL_RBF}[kernel]
+        yptr = (ctypes.c_void_p * k)(*[y.data_ptr() for y in ys])
+        lml = np.zeros(k)
+        grad = np.zeros((k, d + 1))
+        jit = np.zeros(k)
+        status = np.zeros(k, np.int32)
+        dp = ctypes.POINTER(ctypes.c_double)
+        self._stream()
+        self._check(self.lib.omb_gp_lml_grad_batch(
+            self._h, kid, k, n, d, _ptr(X), ctypes.cast(yptr, ctypes.c_void_p), ls.ctypes.data_as(dp),
+            var.ctypes.data_as(dp), float(noise), lml.ctypes.data_as(dp), grad.ctypes.data_as(dp),
+            jit.ctypes.data_as(dp), ctypes.c_void_p(status.ctypes.data)), "omb_gp_lml_grad_batch")
+        return lml, grad, jit, status
+
     def gp_fit_state(self, obj, X, y, lengthscale, variance, noise=0.0, kernel="matern52"):
         """Factorise on the device and install objective ``obj`` (omb_gp_fit_state); returns the jitter."""
         X = _dev_f64(X, self.device)

@@ -15,9 +15,6 @@ omb_gp_fit_state.  Without a GPU (the CPU test suite) the same arithmetic runs i
 ``predict`` — the hot path — runs on the GPU through the HIP posterior kernel
 (optimobo_amd.device); there is no CPU prediction path.
 """
-import concurrent.futures
-import threading
-
 import numpy as np
 from scipy import linalg, optimize
 
@@ -173,59 +170,145 @@ def _device_available():
 
 # ----------------------------------------------------------------------------- concurrent fits
 # The drivers fit one surrogate per objective from the same inputs (optimisers.py:223-231, called per
-# objective at :186; emo.py:297-301).  The fits are independent and deterministic, so on the GPU they
-# run at once: each on a pool thread with its own device context and HIP stream.  An evaluation is one
-# C call that synchronises its stream (≈ 0.1 ms at the BO loop's sizes, most of it host-side: scipy,
-# ctypes, launch); ctypes drops the GIL inside the call, so one fit's host work overlaps the other's
-# device work.  Every fit takes exactly the path it takes alone (same start, same arithmetic).
-_FIT_TLS = threading.local()
-_FIT_POOL = None
-_FIT_POOL_LOCK = threading.Lock()
-_FIT_CONTEXTS = []          # the pool threads' contexts live as long as the process, like the engines
+# objective at :186; emo.py:297-301).  The fits are independent and deterministic.  A device evaluation at
+# the BO loop's sizes is ≈ 40 µs of launch and synchronisation that host threads do not overlap
+# (tools/gpfit_threads_probe.py, profiles/r02_v64_threads_probe.txt), so the fits run in lockstep on ONE
+# thread: each keeps its own L-BFGS-B state in scipy's reverse-communication routine (the loop of
+# scipy.optimize._lbfgsb_py._minimize_lbfgsb, scipy 1.15, restated below), and every round of
+# evaluations — one per fit still running — is one C call (omb_gp_lml_grad_batch: one launch with a
+# workgroup per fit, one synchronisation).  Each fit takes exactly the path scipy.optimize.minimize takes
+# for it alone (test_concurrent_fits_match_sequential: bitwise equal hyperparameters).
+
+
+def _lbfgsb_routine():
+    try:
+        from scipy.optimize import _lbfgsb
+        return _lbfgsb.setulb
+    except Exception:  # pragma: no cover - another scipy layout: fit one after another
+        return None
+
+
+class _LbfgsbRun:
+    """scipy.optimize._lbfgsb_py._minimize_lbfgsb without bounds, driven from outside: ``advance``
+    runs the routine until it needs f and g at a point not evaluated last (returned) or it stops (None);
+    ScalarFunction's rule (re-use the last evaluation when x is unchanged) and its evaluation count
+    (the initial point counts once) are kept."""
+
+    def __init__(self, x0, f0, g0, maxfun, maxiter, m=10, ftol=2.2204460492503131e-09, gtol=1e-5, maxls=20):
+        self.setulb = _lbfgsb_routine()
+        self.m, self.maxls = m, maxls
+        self.pgtol, self.factr = gtol, ftol / np.finfo(float).eps
+        self.maxfun, self.maxiter = maxfun, maxiter
+        self.x = np.array(np.asarray(x0).ravel(), dtype=np.float64)
+        n = self.x.shape[0]
+        self.f = np.array(0.0, dtype=np.int32)
+        self.g = np.zeros((n,), dtype=np.int32)
+        self.nbd = np.zeros(n, np.int32)
+        self.low = np.zeros(n, np.float64)
+        self.up = np.zeros(n, np.float64)
+        self.wa = np.zeros(2 * m * n + 5 * n + 11 * m * m + 8 * m, np.float64)
+        self.iwa = np.zeros(3 * n, dtype=np.int32)
+        self.task = np.zeros(2, dtype=np.int32)
+        self.ln_task = np.zeros(2, dtype=np.int32)
+        self.lsave = np.zeros(4, dtype=np.int32)
+        self.isave = np.zeros(44, dtype=np.int32)
+        self.dsave = np.zeros(29, dtype=np.float64)
+        self.nit = 0
+        self.nfev = 1                                   # ScalarFunction evaluates x0 on construction
+        self.last_x, self.last_f, self.last_g = self.x.copy(), f0, g0
+
+    def advance(self):
+        while True:
+            self.g = self.g.astype(np.float64)
+            self.setulb(self.m, self.x, self.low, self.up, self.nbd, self.f, self.g, self.factr, self.pgtol,
+                        self.wa, self.iwa, self.task, self.lsave, self.isave, self.dsave, self.maxls, self.ln_task)
+            if self.task[0] == 3:
+                if np.array_equal(self.x, self.last_x):
+                    self.f, self.g = self.last_f, self.last_g
+                    continue
+                return self.x.copy()
+            if self.task[0] == 1:
+                self.nit += 1
+                if self.nit >= self.maxiter:
+                    self.task[0], self.task[1] = 5, 504
+                elif self.nfev > self.maxfun:
+                    self.task[0], self.task[1] = 5, 502
+                continue
+            return None
+
+    def supply(self, x, f, g):
+        self.nfev += 1
+        self.last_x, self.last_f, self.last_g = x, f, g
+        self.f, self.g = f, g
+
+
+def _batched_objective(ctx, X_dev, y_devs, kernel, noise, models, ps):
+    """The optimize() objective (GPy Logexp parameters p → −log p(y), ∂/∂p) of several models at once."""
+    from . import _lib
+    thetas, ths = [], []
+    for m, p in zip(models, ps):
+        th = _logexp(p)
+        theta = np.log(th)
+        m._set_free(theta)
+        thetas.append(theta)
+        ths.append(th)
+    lml, grad, _, status = ctx.gp_lml_grad_batch(X_dev, y_devs, np.stack([m.kern.ls_vector() for m in models]),
+                                                 [float(m.kern.variance) for m in models], noise, kernel)
+    out = []
+    for q, m in enumerate(models):
+        if status[q] == _lib.OMB_ENOTPD:
+            f, g_log = 1e25, np.zeros_like(thetas[q])
+        else:
+            g = grad[q]
+            nl = m.kern.lengthscale.values.size
+            gl = [g[0]] + ([float(np.sum(g[1:]))] if nl == 1 else list(g[1:1 + nl]))
+            f, g_log = -float(lml[q]), -np.asarray(gl)
+        out.append((f, g_log * (-np.expm1(-ths[q])) / ths[q]))
+    return out
+
+
+def fit_concurrently(models, device=None, max_f_eval=1000, max_iters=None, **kw):
+    """``model.optimize(max_f_eval=…)`` for every model; in lockstep with batched device evaluations when
+    they are fitted on the GPU on the same inputs, else one after another."""
+    models = list(models)
+    same_inputs = all(m.X.shape == models[0].X.shape and np.array_equal(m.X, models[0].X) for m in models)
+    if (len(models) < 2 or len(models) > 4 or not same_inputs or _lbfgsb_routine() is None or
+            not all(m.device_fit and m.Gaussian_noise.variance.fixed for m in models) or
+            len({(m.kern.kind, float(m.Gaussian_noise.variance)) for m in models}) != 1):
+        return [m.optimize(max_f_eval=max_f_eval, max_iters=max_iters) for m in models]
+    import torch
+    ctx = _fit_context()
+    X_dev = torch.as_tensor(models[0].X, device=ctx.device)
+    y_devs = [torch.as_tensor(np.ascontiguousarray(m.Y[:, 0]), device=ctx.device) for m in models]
+    kernel, noise = models[0].kern.kind, float(models[0].Gaussian_noise.variance)
+    maxfun, maxiter = int(max_f_eval), int(max_iters or max_f_eval)
+    p0 = [np.atleast_1d(_logexp_inv(np.exp(m._get_free()))).astype(np.float64) for m in models]
+    first = _batched_objective(ctx, X_dev, y_devs, kernel, noise, models, p0)
+    runs = [_LbfgsbRun(p, f, g, maxfun, maxiter) for p, (f, g) in zip(p0, first)]
+    active = list(range(len(models)))
+    while active:
+        need = []
+        for i in active:
+            x = runs[i].advance()
+            if x is not None:
+                need.append((i, x))
+        active = [i for i, _ in need]
+        if need:
+            vals = _batched_objective(ctx, X_dev, [y_devs[i] for i, _ in need], kernel, noise,
+                                      [models[i] for i, _ in need], [x for _, x in need])
+            for (i, x), (f, g) in zip(need, vals):
+                runs[i].supply(x, f, g)
+    results = []
+    for m, r in zip(models, runs):
+        m._set_free(np.log(_logexp(r.x)))
+        results.append(optimize.OptimizeResult(x=r.x.copy(), fun=r.f, nfev=r.nfev, nit=r.nit,
+                                               status=0 if r.task[0] == 4 else 1))
+    return results
 
 
 def _fit_context():
-    ctx = getattr(_FIT_TLS, "ctx", None)
-    if ctx is not None:
-        return ctx
     from .acquisition import engine_for
     return engine_for([]).ctx
-
-
-def _fit_on_thread(model, device, kw):
-    import torch
-    if getattr(_FIT_TLS, "ctx", None) is None:
-        torch.cuda.set_device(device)
-        from .device import AcqContext
-        _FIT_TLS.ctx = AcqContext(device)
-        _FIT_TLS.stream = torch.cuda.Stream(device)
-        with _FIT_POOL_LOCK:
-            _FIT_CONTEXTS.append(_FIT_TLS.ctx)
-    with torch.cuda.stream(_FIT_TLS.stream):
-        res = model.optimize(**kw)
-    _FIT_TLS.stream.synchronize()
-    return res
-
-
-def fit_concurrently(models, device=None, **kw):
-    """``model.optimize(**kw)`` for every model; concurrently when they fit on the GPU."""
-    global _FIT_POOL
-    models = list(models)
-    if len(models) < 2 or not all(m.device_fit and m.Gaussian_noise.variance.fixed for m in models):
-        return [m.optimize(**kw) for m in models]
-    import torch
-    if device is None:
-        dev = torch.cuda.current_device()
-    elif isinstance(device, torch.device):
-        dev = device.index if device.index is not None else torch.cuda.current_device()
-    else:
-        dev = int(device)
-    with _FIT_POOL_LOCK:
-        if _FIT_POOL is None:
-            _FIT_POOL = concurrent.futures.ThreadPoolExecutor(max_workers=4, thread_name_prefix="omb-gp-fit")
-    torch.cuda.current_stream(dev).synchronize()       # inputs staged on the caller's stream
-    futures = [_FIT_POOL.submit(_fit_on_thread, m, dev, kw) for m in models]
-    return [f.result() for f in futures]
 
 
 # ----------------------------------------------------------------------------- GPRegression
@@ -291,7 +374,7 @@ class GPRegression:
         import torch
         from . import _lib
         self._set_free(theta)
-        ctx = _fit_context()              # the shared context (or a fit thread's own), without installing this model
+        ctx = _fit_context()              # the shared context, without installing this model
         if self._dev_xy is None:
             self._dev_xy = (torch.as_tensor(self.X, device=ctx.device), torch.as_tensor(self.Y[:, 0], device=ctx.device))
         Xd, yd = self._dev_xy

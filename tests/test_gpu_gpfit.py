@@ -139,10 +139,11 @@ def test_lml_grad_small_path_deterministic(ctx):
     assert r1[0] == r2[0] and np.array_equal(r1[1], r2[1])
 
 
-@pytest.mark.parametrize("n", [20, 60, 119])
+@pytest.mark.parametrize("n", [20, 60, 96, 119])
 def test_concurrent_fits_match_sequential(n):
-    """gp.fit_concurrently (the drivers' per-objective fits on pool threads, one context and stream
-    each) gives bitwise the hyperparameters of fitting the same models one after another."""
+    """gp.fit_concurrently (the drivers' per-objective fits in lockstep, each round of evaluations one
+    batched C call) gives bitwise the hyperparameters and predictions of fitting the same models one
+    after another (n ≤ 96: one launch per round; n = 119: the blocked path, problem after problem)."""
     from optimobo_amd.gp import GPRegression, Matern52, fit_concurrently
     rng = np.random.default_rng(n)
     X = rng.uniform(-2, 2, (n, 2))
@@ -161,12 +162,27 @@ def test_concurrent_fits_match_sequential(n):
         m.optimize(max_f_eval=1000)
     con = models()
     fit_concurrently(con, max_f_eval=1000)
+    Xc = rng.uniform(-2, 2, (257, 2))
     for a, b in zip(seq, con):
         assert float(a.kern.variance) == float(b.kern.variance)
         assert np.array_equal(a.kern.lengthscale.values, b.kern.lengthscale.values)
-    # the fitted models predict identically through the shared engine
-    Xc = rng.uniform(-2, 2, (257, 2))
-    for a, b in zip(seq, con):
         ma, va = a.predict(Xc)
         mb, vb = b.predict(Xc)
         assert np.array_equal(ma, mb) and np.array_equal(va, vb)
+
+
+@pytest.mark.parametrize("n,d", [(20, 2), (60, 3), (96, 8), (119, 2), (40, 12)])
+def test_lml_grad_batch_matches_single(ctx, n, d):
+    """omb_gp_lml_grad_batch: every problem bitwise equal to its own omb_gp_lml_grad (one launch with a
+    workgroup per problem for n ≤ 96, n_var ≤ 8; the blocked path one problem after another)."""
+    rng = np.random.default_rng(n + d)
+    X = torch.as_tensor(rng.uniform(0, 1, (n, d)), device="cuda:0")
+    k = 3
+    ys = [torch.as_tensor(rng.normal(size=n), device="cuda:0") for _ in range(k)]
+    ls = rng.uniform(0.3, 2.0, (k, d))
+    var = rng.uniform(0.5, 2.0, k)
+    lml, grad, jit, status = ctx.gp_lml_grad_batch(X, ys, ls, var)
+    assert (status == 0).all()
+    for p in range(k):
+        l1, g1, j1 = ctx.gp_lml_grad(X, ys[p], ls[p], float(var[p]))
+        assert lml[p] == l1 and np.array_equal(grad[p], g1) and jit[p] == j1

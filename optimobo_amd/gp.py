@@ -277,7 +277,7 @@ def fit_concurrently(models, device=None, max_f_eval=1000, max_iters=None, **kw)
             len({(m.kern.kind, float(m.Gaussian_noise.variance)) for m in models}) != 1):
         return [m.optimize(max_f_eval=max_f_eval, max_iters=max_iters) for m in models]
     import torch
-    ctx = _fit_context()
+    ctx = _fit_context(device)
     X_dev = torch.as_tensor(models[0].X, device=ctx.device)
     y_devs = [torch.as_tensor(np.ascontiguousarray(m.Y[:, 0]), device=ctx.device) for m in models]
     kernel, noise = models[0].kern.kind, float(models[0].Gaussian_noise.variance)
@@ -306,9 +306,9 @@ def fit_concurrently(models, device=None, max_f_eval=1000, max_iters=None, **kw)
     return results
 
 
-def _fit_context():
+def _fit_context(device=None):
     from .acquisition import engine_for
-    return engine_for([]).ctx
+    return engine_for([], device).ctx
 
 
 # ----------------------------------------------------------------------------- GPRegression

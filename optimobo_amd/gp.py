@@ -15,6 +15,9 @@ omb_gp_fit_state.  Without a GPU (the CPU test suite) the same arithmetic runs i
 ``predict`` — the hot path — runs on the GPU through the HIP posterior kernel
 (optimobo_amd.device); there is no CPU prediction path.
 """
+import concurrent.futures
+import threading
+
 import numpy as np
 from scipy import linalg, optimize
 
@@ -242,6 +245,53 @@ class _LbfgsbRun:
         self.f, self.g = f, g
 
 
+def _one_launch(n, d):
+    """omb_gp_lml_grad_batch's one-launch case (gp_lml_small_fits: n ≤ 96, padded n_var ≤ 8)."""
+    dp = 2 if d <= 2 else (4 if d <= 4 else (6 if d <= 6 else (8 if d <= 8 else 16)))
+    return n <= 96 and dp <= 8 and n * dp <= 1024
+
+
+# Above n = 96 an evaluation is the blocked multi-launch path (≈ 0.26 ms at n = 119, mostly device time),
+# which two host threads with their own context and stream do overlap (profiles/r02_v64_threads_probe.txt:
+# 1.6× at n = 96); the round's problems then go to pool threads, each through omb_gp_lml_grad.
+_FIT_POOL = None
+_FIT_POOL_LOCK = threading.Lock()
+_FIT_TLS = threading.local()
+_FIT_CONTEXTS = []          # pool threads' contexts live as long as the process, like the engines
+
+
+def _single_on_thread(device, X_dev, y_dev, ls, var, noise, kernel):
+    import torch
+    from . import _lib
+    if getattr(_FIT_TLS, "ctx", None) is None:
+        torch.cuda.set_device(device)
+        from .device import AcqContext
+        _FIT_TLS.ctx = AcqContext(device)
+        _FIT_TLS.stream = torch.cuda.Stream(device)
+        with _FIT_POOL_LOCK:
+            _FIT_CONTEXTS.append(_FIT_TLS.ctx)
+    with torch.cuda.stream(_FIT_TLS.stream):
+        try:
+            lml, g, _ = _FIT_TLS.ctx.gp_lml_grad(X_dev, y_dev, ls, var, noise, kernel)
+            return lml, g, 0
+        except _lib.OMBError as e:
+            if e.code != _lib.OMB_ENOTPD:
+                raise
+            return 0.0, np.zeros(X_dev.shape[1] + 1), _lib.OMB_ENOTPD
+
+
+def _parallel_singles(ctx, X_dev, y_devs, lss, vs, noise, kernel):
+    global _FIT_POOL
+    with _FIT_POOL_LOCK:
+        if _FIT_POOL is None:
+            _FIT_POOL = concurrent.futures.ThreadPoolExecutor(max_workers=4, thread_name_prefix="omb-gp-fit")
+    dev = ctx.device.index
+    futs = [_FIT_POOL.submit(_single_on_thread, dev, X_dev, y, ls, v, noise, kernel)
+            for y, ls, v in zip(y_devs, lss, vs)]
+    res = [f.result() for f in futs]
+    return (np.array([r[0] for r in res]), np.stack([r[1] for r in res]), np.array([r[2] for r in res]))
+
+
 def _batched_objective(ctx, X_dev, y_devs, kernel, noise, models, ps):
     """The optimize() objective (GPy Logexp parameters p → −log p(y), ∂/∂p) of several models at once."""
     from . import _lib
@@ -252,8 +302,13 @@ def _batched_objective(ctx, X_dev, y_devs, kernel, noise, models, ps):
         m._set_free(theta)
         thetas.append(theta)
         ths.append(th)
-    lml, grad, _, status = ctx.gp_lml_grad_batch(X_dev, y_devs, np.stack([m.kern.ls_vector() for m in models]),
-                                                 [float(m.kern.variance) for m in models], noise, kernel)
+    lss = [m.kern.ls_vector() for m in models]
+    vs = [float(m.kern.variance) for m in models]
+    n, d = X_dev.shape
+    if len(models) > 1 and not _one_launch(n, d):
+        lml, grad, status = _parallel_singles(ctx, X_dev, y_devs, lss, vs, noise, kernel)
+    else:
+        lml, grad, _, status = ctx.gp_lml_grad_batch(X_dev, y_devs, np.stack(lss), vs, noise, kernel)
     out = []
     for q, m in enumerate(models):
         if status[q] == _lib.OMB_ENOTPD:
@@ -281,6 +336,7 @@ def fit_concurrently(models, device=None, max_f_eval=1000, max_iters=None, **kw)
     X_dev = torch.as_tensor(models[0].X, device=ctx.device)
     y_devs = [torch.as_tensor(np.ascontiguousarray(m.Y[:, 0]), device=ctx.device) for m in models]
     kernel, noise = models[0].kern.kind, float(models[0].Gaussian_noise.variance)
+    torch.cuda.current_stream(ctx.device).synchronize()   # inputs ready for the pool threads' streams
     maxfun, maxiter = int(max_f_eval), int(max_iters or max_f_eval)
     p0 = [np.atleast_1d(_logexp_inv(np.exp(m._get_free()))).astype(np.float64) for m in models]
     first = _batched_objective(ctx, X_dev, y_devs, kernel, noise, models, p0)

@@ -11,6 +11,8 @@ N = 2^20 unscrambled-Sobol candidates; rank g scores Sobol indices [gÂ·N, (g+1)Â
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W]
         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N  (multi-GPU)
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts its own N ranks (one child
+process per GPU, MASTER_ADDR 127.0.0.1) before anything touches the GPU, and exits with their status.
 Prints ONE JSON line on rank 0.
 """
 import argparse
@@ -315,6 +317,58 @@ def load_traffic(n, N, kernel="posterior"):
         return None
 
 
+def _free_port():
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`python bench.py --gpus N` without a launcher: start N ranks of this script as child processes with
+    torch.distributed.run's environment (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR/PORT) and wait for them.
+    Runs before torch is imported, so this process never touches the GPU.  If one rank fails, the others
+    (which would wait in a collective) are terminated; the exit status is the first failure's, else 0."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    status = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc
+                for q in live:
+                    q.terminate()
+        time.sleep(0.1)
+    return status
+
+
+def launch_check(world_size, rank, backend):
+    """--launch-check: the rank set-up alone (process group, one all-gather of the ranks), no GPU work with
+    gloo.  Rank 0 prints what torch.distributed saw."""
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group(backend=backend, init_method="env://")
+    dev = "cpu" if backend == "gloo" else torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    mine = torch.tensor([rank], dtype=torch.int64, device=dev)
+    got = [torch.empty_like(mine) for _ in range(dist.get_world_size())]
+    dist.all_gather(got, mine)
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "world_size": dist.get_world_size(), "backend": dist.get_backend(),
+                          "ranks": [int(t.item()) for t in got], "master_addr": os.environ.get("MASTER_ADDR")}))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -328,12 +382,16 @@ def main():
     ap.add_argument("--no-kblock", action="store_true")
     ap.add_argument("--chain", default="fused", choices=["fused", "separate", "sobol"])
     ap.add_argument("--stage-timing", action="store_true", help="events around every stage (adds ~5 us/stage)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="start the ranks and the process group only, print what torch.distributed saw")
     ap.add_argument("--cache-seed", type=int, default=1,
                     help="Sobol seed of the MC sample cache (optimisers.py:121-141, unseeded in the reference). "
                          "1: s01 = +0.070, reference-mode EHVI positive where it improves (default); "
                          "0: s01 = -0.028, reference-mode EHVI <= 0 everywhere (degenerate arg-max)")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))          # no launcher: this process starts the ranks
 
     import torch
     import torch.distributed as dist
@@ -342,11 +400,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus > 1 and world_size != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world_size}: launch one rank per GPU with "
-                         "python -m torch.distributed.run --nproc-per-node N bench.py --gpus N")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world_size}")
     # OMB_DIST_BACKEND=gloo rehearses the multi-rank path on a box with fewer GPUs than ranks
     # (ranks then share GPUs round-robin); the driver's multi-GPU runs use nccl (= RCCL).
     backend = os.environ.get("OMB_DIST_BACKEND", "nccl")
+    if args.launch_check:
+        return launch_check(world_size, rank, backend)
     gpu = local_rank % max(1, torch.cuda.device_count()) if backend == "gloo" else local_rank
     dist_info = {"backend": None, "world_size": 1}
     if world_size > 1:

@@ -27,7 +27,7 @@ class ParEGO(BODriver):
     def _get_proposed(self, model, current_best, Xsample=None):
         from ..acquisition import engine_for
         eng = engine_for([model], self.device)
-        if self.acq_search == "ea" and Xsample is not None:
+        if self.acq_search == "ea" and Xsample is not None and ea.device_search_fits(len(Xsample)):
             lower = np.asarray(self.test_problem.xl, np.float64)
             upper = np.asarray(self.test_problem.xu, np.float64)
             pop = ea.initial_population(Xsample, lower, upper)           # parego.py:229-235

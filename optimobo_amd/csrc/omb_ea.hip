@@ -134,10 +134,9 @@ __global__ __launch_bounds__(kEAThreads) void ea_search_kernel(EAArgs A) {
   __shared__ double F[kEAMaxPop];
   __shared__ double child[DP];
   __shared__ double ab[DP];
-  __shared__ double bestx[DP];
   __shared__ double kst[kEAMaxTrain];
   __shared__ double red[2 * kEAThreads + 2];
-  __shared__ int ctl[4];                                            // w1, w2, replace
+  __shared__ int ctl[4];                                            // w1, w2, best row (−1: none yet)
   __shared__ double lds_l[kEALdsN * (kEALdsN + 1) / 2];             // packed L0⁻¹ (n0 ≤ kEALdsN)
   const int tid = threadIdx.x, d = A.d, P = A.P;
   const int n0 = A.g0.n;
@@ -151,7 +150,7 @@ __global__ __launch_bounds__(kEAThreads) void ea_search_kernel(EAArgs A) {
     const int p = i / DP, j = i % DP;
     pop[i] = (j < d) ? A.pop[p * d + j] : 0.0;
   }
-  if (tid < DP) bestx[tid] = (tid < d) ? A.lower[tid] : 0.0;      // best_solution_found = self.lower
+  if (tid == 0) ctl[2] = -1;                                        // best_solution_found = self.lower
   __syncthreads();
   for (int p = 0; p < P; ++p) {
     const double f = ea_fitness<DP>(A, Lds, pop + p * DP, ab, kst, red);
@@ -161,12 +160,17 @@ __global__ __launch_bounds__(kEAThreads) void ea_search_kernel(EAArgs A) {
   __syncthreads();
   for (int it = 0; it < A.iters; ++it) {
     if (tid == 0) {
-      // best of the population before this generation (np.argmax: first maximum)
+      // best of the population before this generation: np.max (NaN if any fitness is NaN, and then
+      // no update) and np.argmax (the first maximum).  The reference keeps a view of that row
+      // (parego.py:248-251, keep.py:268-271), so only its index is recorded here: a later replacement
+      // of the row changes the proposal, as it does in the reference.
       int bi = 0;
-      for (int p = 1; p < P; ++p)
+      bool nan = F[0] != F[0];
+      for (int p = 1; p < P; ++p) {
+        nan |= F[p] != F[p];
         if (F[p] > F[bi]) bi = p;
-      ctl[2] = -1;
-      if (F[bi] > best_f) {
+      }
+      if (!nan && F[bi] > best_f) {
         best_f = F[bi];
         ctl[2] = bi;
       }
@@ -178,7 +182,6 @@ __global__ __launch_bounds__(kEAThreads) void ea_search_kernel(EAArgs A) {
     }
     __syncthreads();
     const int w1 = ctl[0], w2 = ctl[1];
-    if (ctl[2] >= 0 && tid < DP) bestx[tid] = pop[ctl[2] * DP + tid];
     if (tid < d) {
 #pragma clang fp contract(off)   // numpy rounds every product and sum: no fma contraction here
       const double p1 = pop[w1 * DP + tid], p2 = pop[w2 * DP + tid];
@@ -205,7 +208,8 @@ __global__ __launch_bounds__(kEAThreads) void ea_search_kernel(EAArgs A) {
     }
     __syncthreads();
   }
-  if (tid < d) A.out[tid] = bestx[tid];
+  const int br = ctl[2];
+  if (tid < d) A.out[tid] = (br >= 0) ? pop[br * DP + tid] : A.lower[tid];
   if (tid == 0) A.out[d] = best_f;
 }
 

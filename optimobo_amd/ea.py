@@ -26,6 +26,13 @@ EA_POP = 20              # 10 mutants + 10 Latin-hypercube points (parego.py:230
 EA_ITERS = 1000          # n_remutations (parego.py:241)
 EA_ETA = 2.0             # parego.py:226
 EA_CROSS_PROB = 0.2      # simulated_binary_crossover(..., crossover_prob=0.2) (parego.py:259)
+EA_MAX_TRAIN = 2048      # omb_ea_search keeps one K* row in LDS (kEAMaxTrain, omb_internal.h)
+
+
+def device_search_fits(n_train):
+    """True when omb_ea_search takes a surrogate of `n_train` points; the drivers use the batched
+    device arg-max of the same fitness above that (omb_ea_search returns OMB_EUNSUP there)."""
+    return int(n_train) <= EA_MAX_TRAIN
 
 
 class EATape:

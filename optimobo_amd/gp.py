@@ -15,6 +15,7 @@ omb_gp_fit_state.  Without a GPU (the CPU test suite) the same arithmetic runs i
 ``predict`` — the hot path — runs on the GPU through the HIP posterior kernel
 (optimobo_amd.device); there is no CPU prediction path.
 """
+import atexit
 import concurrent.futures
 import threading
 
@@ -282,22 +283,45 @@ def _one_launch(n, d):
 _FIT_POOL = None
 _FIT_POOL_LOCK = threading.Lock()
 _FIT_TLS = threading.local()
-_FIT_CONTEXTS = []          # pool threads' contexts live as long as the process, like the engines
+_FIT_CONTEXTS = []          # every pool thread's (context, stream); closed at interpreter exit
+
+
+def _close_fit_contexts():
+    with _FIT_POOL_LOCK:
+        ctxs = [c for c, _ in _FIT_CONTEXTS]
+        _FIT_CONTEXTS.clear()
+    for c in ctxs:
+        try:
+            c.close()
+        except Exception:  # pragma: no cover - the runtime may already be shutting down
+            pass
+
+
+atexit.register(_close_fit_contexts)
+
+
+def _thread_context(device):
+    """This pool thread's (context, stream) on `device` — one per device the thread has served."""
+    import torch
+    per_dev = getattr(_FIT_TLS, "by_device", None)
+    if per_dev is None:
+        per_dev = _FIT_TLS.by_device = {}
+    if device not in per_dev:
+        torch.cuda.set_device(device)
+        from .device import AcqContext
+        per_dev[device] = (AcqContext(device), torch.cuda.Stream(device))
+        with _FIT_POOL_LOCK:
+            _FIT_CONTEXTS.append(per_dev[device])
+    return per_dev[device]
 
 
 def _single_on_thread(device, X_dev, y_dev, ls, var, noise, kernel):
     import torch
     from . import _lib
-    if getattr(_FIT_TLS, "ctx", None) is None:
-        torch.cuda.set_device(device)
-        from .device import AcqContext
-        _FIT_TLS.ctx = AcqContext(device)
-        _FIT_TLS.stream = torch.cuda.Stream(device)
-        with _FIT_POOL_LOCK:
-            _FIT_CONTEXTS.append(_FIT_TLS.ctx)
-    with torch.cuda.stream(_FIT_TLS.stream):
+    ctx, stream = _thread_context(device)
+    with torch.cuda.stream(stream):
         try:
-            lml, g, _ = _FIT_TLS.ctx.gp_lml_grad(X_dev, y_dev, ls, var, noise, kernel)
+            lml, g, _ = ctx.gp_lml_grad(X_dev, y_dev, ls, var, noise, kernel)
             return lml, g, 0
         except _lib.OMBError as e:
             if e.code != _lib.OMB_ENOTPD:
@@ -343,7 +367,7 @@ def _batched_objective(ctx, X_dev, y_devs, kernel, noise, models, ps):
             nl = m.kern.lengthscale.values.size
             gl = [g[0]] + ([float(np.sum(g[1:]))] if nl == 1 else list(g[1:1 + nl]))
             f, g_log = -float(lml[q]), -np.asarray(gl)
-        out.append((f, g_log * (-np.expm1(-ths[q])) / ths[q]))
+        out.append((f, g_log * _logexp_gradfactor(ths[q]) / ths[q]))
     return out
 
 
@@ -393,15 +417,26 @@ def _fit_context(device=None):
 
 
 # ----------------------------------------------------------------------------- GPRegression
+_LOGEXP_LIM = 36.0          # paramz.transformations._lim_val
+
+
 def _logexp(p):
-    """GPy's Logexp transform θ = log(1 + e^p) (stable for large |p|), floored away from 0."""
-    return np.maximum(np.logaddexp(0.0, np.asarray(p, np.float64)), 1e-300)
+    """GPy's (paramz) Logexp transform θ = log(1 + e^p), restated as paramz writes it: p itself above 36,
+    else log1p(exp(clip(p, −36, 36)))."""
+    p = np.asarray(p, np.float64)
+    return np.where(p > _LOGEXP_LIM, p, np.log1p(np.exp(np.clip(p, -_LOGEXP_LIM, _LOGEXP_LIM))))
+
+
+def _logexp_gradfactor(theta):
+    """paramz Logexp.gradfactor: dθ/dp = 1 above 36, else −expm1(−θ)."""
+    th = np.asarray(theta, np.float64)
+    return np.where(th > _LOGEXP_LIM, 1.0, -np.expm1(-th))
 
 
 def _logexp_inv(theta):
-    """p = log(e^θ − 1) (GPy Logexp.finv), stable for large θ."""
+    """p = log(e^θ − 1) (paramz Logexp.finv), θ itself above 36."""
     th = np.asarray(theta, np.float64)
-    return np.where(th > 36.0, th, np.log(np.expm1(np.minimum(th, 36.0))))
+    return np.where(th > _LOGEXP_LIM, th, np.log(np.expm1(np.minimum(th, _LOGEXP_LIM))))
 
 
 class _Noise:
@@ -516,7 +551,7 @@ class GPRegression:
         def fun(p):
             th = _logexp(p)
             f, g_log = inner(np.log(th))
-            return f, g_log * (-np.expm1(-th)) / th     # ∂f/∂p = (∂f/∂log θ)/θ · (1 − e^(−θ))
+            return f, g_log * _logexp_gradfactor(th) / th     # ∂f/∂p = (∂f/∂log θ)/θ · dθ/dp
 
         res = optimize.minimize(fun, p0, jac=True, method="L-BFGS-B",
                                 options={"maxfun": int(max_f_eval), "maxiter": int(max_iters or max_f_eval)})

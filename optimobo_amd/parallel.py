@@ -7,6 +7,9 @@ contributes {best value, best global index} (16 bytes) to one all-gather, and ev
 reduces the gathered pairs with the same rule as the device kernel (highest value, lowest
 index on ties, index −1 = no valid candidate).  The result is identical to the single-GPU
 arg-max over the concatenated batch.
+
+The pair travels as two float64s, so the global index is exact up to 2^53 candidates (one step
+scores at most 2^20-2^22 per rank; a maximiser sweep 2^16 per round).
 """
 import torch
 import torch.distributed as dist
@@ -47,21 +50,26 @@ def agree_host_rng(seed=None):
     """Make every rank draw the same host randomness; returns the seed every rank uses.
 
     The drivers draw from numpy's global generator (LHS initial design, reference directions,
-    ``np.random.randint`` in the reference's loops) and derive the Sobol candidate seed and the
-    MC sample cache from ``seed``.  With several ranks each of those must agree, or the ranks
-    would score different candidate sets and the global arg-max index would name a point the
-    winning rank never scored.  Rank 0's numpy state and seed (drawn there when ``seed`` is
-    None) are broadcast; with one rank nothing changes.
+    ``np.random.randint`` in the reference's loops) and from Python's ``random`` (ParEGO's and KEEP's
+    evolutionary search: ``random.sample`` for the temporary population and the tournaments,
+    parego.py:91,228, keep.py:246), and derive the Sobol candidate seed and the MC sample cache from
+    ``seed``.  With several ranks each of those must agree, or the ranks would score different
+    candidate sets (or run different searches) and propose different points.  Rank 0's numpy state,
+    ``random`` state and seed (drawn there when ``seed`` is None) are broadcast; with one rank nothing
+    changes.
     """
+    import random
+
     import numpy as np
     w, rank = world()
     if w == 1:
         return seed
     if rank == 0 and seed is None:
         seed = int(np.random.randint(0, 2 ** 31 - 1))
-    box = [seed, np.random.get_state()] if rank == 0 else [None, None]
+    box = [seed, np.random.get_state(), random.getstate()] if rank == 0 else [None, None, None]
     dist.broadcast_object_list(box, src=0)
     np.random.set_state(box[1])
+    random.setstate(box[2])
     return box[0]
 
 

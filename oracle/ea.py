@@ -11,17 +11,26 @@ the reference's own solve() through tests/golden/ea.npz (tests/golden/make_golde
 import numpy as np
 
 
-def search(pop0, fitness, tape, lower, upper):
-    """→ (best_x, best_fitness).  fitness(X (m, d)) → (m,)."""
+def search(pop0, fitness, tape, lower, upper, alias=True):
+    """→ (best_x, best_fitness).  fitness(X (m, d)) → (m,).
+
+    The reference keeps ``best_solution_found = temporary_population[np.argmax(EIs)]``, a numpy *view*
+    of a population row (parego.py:248-251, keep.py:268-271), so a later
+    ``temporary_population[parent1_idx] = final`` into that row (:270 / :292) changes the proposal it
+    returns.  The search therefore tracks the best row's *index* and reads the row after the last
+    generation (``lower`` if no generation improved on best_EI = 0).  ``alias=False`` keeps a copy of the
+    row instead; it exists only so tests/golden/make_golden.py can find runs where the two differ.
+    """
     pop = np.array(pop0, np.float64, copy=True)
     lower = np.asarray(lower, np.float64)
     upper = np.asarray(upper, np.float64)
     F = np.asarray(fitness(pop), np.float64).reshape(-1)
-    best_f, best_x = 0.0, lower.copy()                 # best_EI = 0, best_solution_found = self.lower
+    best_f, best_row, best_copy = 0.0, -1, lower.copy()  # best_EI = 0, best_solution_found = self.lower
     for it in range(tape.iters):
-        i = int(np.argmax(F))                          # best of the population before this generation
-        if F[i] > best_f:
-            best_f, best_x = F[i], pop[i].copy()
+        fmax = np.max(F)                               # NaN if any fitness is NaN (np.max propagates it)
+        if fmax > best_f:
+            best_f, best_row = fmax, int(np.argmax(F))   # argmax: the first maximum
+            best_copy = pop[best_row].copy()
         s = tape.sel[it]
         w1 = s[0] if F[s[0]] > F[s[1]] else s[1]       # tournament 1 over the whole population
         a = s[2] if s[2] < w1 else s[2] + 1            # tournament 2 over the population without w1
@@ -40,7 +49,9 @@ def search(pop0, fitness, tape, lower, upper):
         if not F[w1] > fc:                             # the parent stays only if strictly better
             pop[w1] = child
             F[w1] = fc
-    return best_x, best_f
+    if not alias:
+        return best_copy, best_f
+    return (pop[best_row].copy() if best_row >= 0 else lower.copy()), best_f
 
 
 def ei_fitness(gp, best, var_eps=1e-6):

@@ -588,16 +588,8 @@ class _ZDT1Box:
         return zdt1(np.atleast_2d(np.asarray(x, np.float64)))[0]
 
 
-def make_ea(parego_mod, keep_mod, sc):
-    """ParEGO / KEEP evolutionary acquisition search (parego.py:223-271, keep.py:240-292) run by the
-    reference's own solve() for one BO iteration.  GPy double: GPRegression = the oracle's GPy restatement
-    (oracle/gp.py) with GPy's default Matern52 ARD hyperparameters (ℓ = 1, σ_f² = 1; noise fixed to 0,
-    optimize a no-op).  A hook on the binary tournament records, at its first call (generation 0, after
-    which every random draw of the search follows), the temporary population, the numpy and `random`
-    generator states, the training set of the model(s) and the incumbent; the proposal is the x that
-    solve() evaluates after the search."""
-    import random
-
+def _ea_prepare(parego_mod, keep_mod):
+    """GPy double and HV / reference-direction stand-ins for running ParEGO / KEEP solve()."""
     class DuckGP:
         def __init__(self, X, Y, kern=None):
             self.X, self.Y = np.array(X, np.float64), np.array(Y, np.float64)
@@ -623,33 +615,34 @@ def make_ea(parego_mod, keep_mod, sc):
         mod.get_reference_directions = lambda name, n_dim, n_partitions=None: _das_dennis(n_dim, n_partitions)
         mod.HV = HV
 
-    out = {}
-    cases = [("parego", 1, 3, 12), ("parego", 2, 6, 20), ("keep", 3, 2, 12), ("keep", 4, 5, 16)]
-    out["n_cases"] = np.int64(len(cases))
-    for c, (kind, seed, d, n_init) in enumerate(cases):
-        cls = parego_mod.ParEGO if kind == "parego" else keep_mod.KEEP
-        tname = ("parego_binary_tournament_selection_without_replacment" if kind == "parego"
-                 else "KEEP_binary_tournament_selection_without_replacment")
-        orig = getattr(cls, tname)
-        rec = {}
 
-        def hook(self, population, *args, _orig=orig, _rec=rec):
-            if not _rec:
-                st = np.random.get_state()
-                _rec["pop"] = np.array(population, np.float64)
-                _rec["np_keys"], _rec["np_pos"] = np.array(st[1], np.uint32), np.int64(st[2])
-                _rec["np_has_gauss"], _rec["np_gauss"] = np.int64(st[3]), np.float64(st[4])
-                pst = random.getstate()
-                _rec["py_version"], _rec["py_state"] = np.int64(pst[0]), np.array(pst[1], np.int64)
-                models = args[:-1]
-                _rec["best"] = np.float64(np.asarray(args[-1]).reshape(-1)[0])
-                _rec["X"] = models[-1].X                     # scalar model (the last model argument)
-                _rec["y0"] = models[-1].Y[:, 0]
-                if len(models) == 2:
-                    _rec["y1"] = models[0].Y[:, 0]           # KEEP: the Pareto-membership model
-            return _orig(self, population, *args)
-        setattr(cls, tname, hook)
-        evaluated = []
+def _ea_capture(parego_mod, keep_mod, sc, kind, seed, d, n_init):
+    """One BO iteration of the reference's ParEGO / KEEP solve(); → the record of its search."""
+    import random
+    cls = parego_mod.ParEGO if kind == "parego" else keep_mod.KEEP
+    tname = ("parego_binary_tournament_selection_without_replacment" if kind == "parego"
+             else "KEEP_binary_tournament_selection_without_replacment")
+    orig = getattr(cls, tname)
+    rec = {}
+
+    def hook(self, population, *args, _orig=orig, _rec=rec):
+        if not _rec:
+            st = np.random.get_state()
+            _rec["pop"] = np.array(population, np.float64)
+            _rec["np_keys"], _rec["np_pos"] = np.array(st[1], np.uint32), np.int64(st[2])
+            _rec["np_has_gauss"], _rec["np_gauss"] = np.int64(st[3]), np.float64(st[4])
+            pst = random.getstate()
+            _rec["py_version"], _rec["py_state"] = np.int64(pst[0]), np.array(pst[1], np.int64)
+            models = args[:-1]
+            _rec["best"] = np.float64(np.asarray(args[-1]).reshape(-1)[0])
+            _rec["X"] = models[-1].X                     # scalar model (the last model argument)
+            _rec["y0"] = models[-1].Y[:, 0]
+            if len(models) == 2:
+                _rec["y1"] = models[0].Y[:, 0]           # KEEP: the Pareto-membership model
+        return _orig(self, population, *args)
+    setattr(cls, tname, hook)
+    evaluated = []
+    try:
         inst = cls(_ZDT1Box(d))
         orig_obj = inst._objective_function
 
@@ -660,15 +653,68 @@ def make_ea(parego_mod, keep_mod, sc):
         np.random.seed(seed)
         random.seed(seed)
         inst.solve(sc.Tchebicheff(), budget=1, n_init_samples=n_init)
+    finally:
         setattr(cls, tname, orig)
-        k = f"c{c}"
-        out[f"{k}_kind"] = np.array(kind)
-        out[f"{k}_seed"], out[f"{k}_d"] = np.int64(seed), np.int64(d)
+    rec.update({"kind": np.array(kind), "seed": np.int64(seed), "d": np.int64(d), "next_x": evaluated[-1],
+                "lower": np.zeros(d), "upper": np.ones(d)})
+    return rec
+
+
+def _ea_copy_semantics(rec):
+    """The proposal a search keeping a *copy* of the best row would return (oracle/ea.py alias=False)."""
+    import random
+    from oracle import ea as oea
+    from optimobo_amd import ea as hea
+    np.random.set_state(("MT19937", rec["np_keys"], int(rec["np_pos"]), int(rec["np_has_gauss"]),
+                         float(rec["np_gauss"])))
+    random.setstate((int(rec["py_version"]), tuple(int(v) for v in rec["py_state"]), None))
+    d = int(rec["d"])
+    tape = hea.ea_tape(len(rec["pop"]), d)
+    scalar = ogp.ExactGP(rec["X"], rec["y0"], 1.0, 1.0)
+    fit = (oea.ei_fitness(scalar, float(rec["best"])) if str(rec["kind"]) == "parego" else
+           oea.pareto_ei_fitness(scalar, ogp.ExactGP(rec["X"], rec["y1"], 1.0, 1.0), float(rec["best"])))
+    x_copy, _ = oea.search(rec["pop"], fit, tape, rec["lower"], rec["upper"], alias=False)
+    return x_copy
+
+
+def make_ea(parego_mod, keep_mod, sc, alias_seeds=range(100, 400)):
+    """ParEGO / KEEP evolutionary acquisition search (parego.py:223-271, keep.py:240-292) run by the
+    reference's own solve() for one BO iteration.  GPy double: GPRegression = the oracle's GPy restatement
+    (oracle/gp.py) with GPy's default Matern52 ARD hyperparameters (ℓ = 1, σ_f² = 1; noise fixed to 0,
+    optimize a no-op).  A hook on the binary tournament records, at its first call (generation 0, after
+    which every random draw of the search follows), the temporary population, the numpy and `random`
+    generator states, the training set of the model(s) and the incumbent; the proposal is the x that
+    solve() evaluates after the search.
+
+    Cases 0-3 are fixed seeds.  The alias cases (``c*_alias`` = 1) are the first seeds in `alias_seeds`,
+    per algorithm, whose proposal differs from what a copy of the best-seen row would give: the reference
+    returns a view of that row (parego.py:251, keep.py:271), and the row was replaced afterwards (a child
+    at least as fit as the best row in the last generation)."""
+    _ea_prepare(parego_mod, keep_mod)
+    out = {}
+    recs = []
+    for kind, seed, d, n_init in [("parego", 1, 3, 12), ("parego", 2, 6, 20), ("keep", 3, 2, 12),
+                                  ("keep", 4, 5, 16)]:
+        recs.append(_ea_capture(parego_mod, keep_mod, sc, kind, seed, d, n_init))
+        recs[-1]["alias"] = np.int64(0)
+    for kind in ("parego", "keep"):
+        for seed in alias_seeds:
+            d, n_init = 2 + seed % 5, 10 + seed % 7
+            rec = _ea_capture(parego_mod, keep_mod, sc, kind, seed, d, n_init)
+            x_copy = _ea_copy_semantics(rec)
+            if not np.array_equal(x_copy, rec["next_x"]):
+                rec["alias"] = np.int64(1)
+                rec["next_x_if_copied"] = x_copy
+                recs.append(rec)
+                print(f"  alias case: {kind} seed={seed} d={d} n_init={n_init}", flush=True)
+                break
+        else:
+            raise RuntimeError(f"no aliasing {kind} run among seeds {alias_seeds}")
+    for c, rec in enumerate(recs):
         for key, v in rec.items():
-            out[f"{k}_{key}"] = v
-        out[f"{k}_next_x"] = evaluated[-1]
-        out[f"{k}_lower"], out[f"{k}_upper"] = np.zeros(d), np.ones(d)
-        print(f"  ea case {c}: {kind} d={d} n={len(rec['X'])} next_x={evaluated[-1]}")
+            out[f"c{c}_{key}"] = v
+        print(f"  ea case {c}: {rec['kind']} d={rec['d']} n={len(rec['X'])} next_x={rec['next_x']}")
+    out["n_cases"] = np.int64(len(recs))
     np.savez_compressed(os.path.join(HERE, "ea.npz"), **out)
 
 

@@ -40,14 +40,27 @@ def ea_golden(golden_dir):
     return np.load(os.path.join(golden_dir, "ea.npz"), allow_pickle=False)
 
 
-@pytest.mark.parametrize("c", range(4))
+N_CASES = 6      # tests/golden/ea.npz: 4 fixed seeds + one aliasing ParEGO and one aliasing KEEP run
+
+
+def test_golden_has_alias_cases(ea_golden):
+    assert int(ea_golden["n_cases"]) == N_CASES
+    kinds = [str(ea_golden[f"c{c}_kind"]) for c in range(N_CASES) if int(ea_golden[f"c{c}_alias"])]
+    assert sorted(kinds) == ["keep", "parego"]
+
+
+@pytest.mark.parametrize("c", range(N_CASES))
 def test_oracle_search_matches_reference(ea_golden, c):
+    """The reference returns a view of the best row (parego.py:248-251, keep.py:268-271): in the alias
+    cases the row was replaced after it was recorded, and a copy of it would be the wrong proposal."""
     cs = _case(ea_golden, c)
     d = int(cs["d"])
     _restore(cs)
     tape = ea.ea_tape(len(cs["pop"]), d)
     x, f = oea.search(cs["pop"], fitness_for(cs), tape, cs["lower"], cs["upper"])
     np.testing.assert_array_equal(x, cs["next_x"])
+    if int(cs["alias"]):
+        assert not np.array_equal(cs["next_x_if_copied"], cs["next_x"])
 
 
 def test_tape_shapes_and_codes():

@@ -1,5 +1,7 @@
 """GPU: the ParEGO / KEEP evolutionary acquisition search (omb_ea_search) against the
 reference's own solve() (tests/golden/ea.npz, make_golden.py make_ea) and the oracle's restatement.
+Cases 4 and 5 are runs where the reference's proposal is a view of a population row that was replaced
+after it was recorded (parego.py:248-251 / :270, keep.py:268-271 / :292).
 
 With both generators restored to the reference's state at the start of the search, the host tape
 (optimobo_amd.ea.ea_tape) plus the device search must return the reference's proposal exactly; the best
@@ -17,7 +19,7 @@ pytestmark = pytest.mark.gpu
 
 from oracle import ea as oea  # noqa: E402
 from oracle import gp as ogp  # noqa: E402
-from test_ea import _case, _restore, fitness_for  # noqa: E402
+from test_ea import N_CASES, _case, _restore, fitness_for  # noqa: E402
 
 
 @pytest.fixture(scope="module")
@@ -36,7 +38,7 @@ def _ctx_for(cs):
     return ctx
 
 
-@pytest.mark.parametrize("c", range(4))
+@pytest.mark.parametrize("c", range(N_CASES))
 def test_device_search_matches_reference(ea_golden, c):
     from optimobo_amd import ea
     cs = _case(ea_golden, c)

@@ -36,3 +36,52 @@ def test_lockstep_lbfgsb_equals_scipy(fun, x0, maxfun):
         r.supply(x, f, g)
     assert np.array_equal(ref.x, r.x)
     assert ref.nfev == r.nfev and ref.nit == r.nit and ref.fun == r.f
+
+
+@pytest.fixture
+def fresh_lockstep_check(monkeypatch):
+    from optimobo_amd import gp
+    monkeypatch.setattr(gp, "_LOCKSTEP_OK", None)
+    return gp
+
+
+def test_lockstep_disabled_without_routine(fresh_lockstep_check, monkeypatch):
+    """Another scipy layout (no private setulb): the one-time check fails and fits run one after another."""
+    gp = fresh_lockstep_check
+    monkeypatch.setattr(gp, "_lbfgsb_routine", lambda: None)
+    assert gp._lockstep_ok() is False
+
+
+def test_lockstep_disabled_when_routine_differs(fresh_lockstep_check, monkeypatch):
+    """A setulb whose iterates differ from scipy.optimize.minimize's (here: a perturbed gradient) fails the
+    equivalence check, as would one with another signature."""
+    gp = fresh_lockstep_check
+    real = gp._lbfgsb_routine()
+
+    def perturbed(m, x, low, up, nbd, f, g, *rest):
+        return real(m, x, low, up, nbd, f, g * (1 + 1e-3), *rest)
+    monkeypatch.setattr(gp, "_lbfgsb_routine", lambda: perturbed)
+    assert gp._lockstep_ok() is False
+    monkeypatch.setattr(gp, "_LOCKSTEP_OK", None)
+    monkeypatch.setattr(gp, "_lbfgsb_routine", lambda: (lambda *a: (_ for _ in ()).throw(TypeError("signature"))))
+    assert gp._lockstep_ok() is False
+
+
+def test_sequential_fallback_fits_like_single_fits(fresh_lockstep_check, monkeypatch):
+    """With the lockstep driver disabled, fit_concurrently gives each model exactly its single fit."""
+    gp = fresh_lockstep_check
+    monkeypatch.setattr(gp, "_LOCKSTEP_OK", False)
+    rng = np.random.default_rng(4)
+    X = rng.uniform(0, 1, (18, 2))
+    Y = np.column_stack([np.sin(5 * X[:, 0]) + X[:, 1], (X ** 2).sum(1)])
+
+    def models():
+        return [gp.GPRegression(X, Y[:, i:i + 1], gp.Matern52(2, ARD=True), device_fit=False) for i in range(2)]
+    ms, singles = models(), models()
+    for m in ms + singles:
+        m.Gaussian_noise.variance.fix(0)
+    res = gp.fit_concurrently(ms, max_f_eval=200)
+    for m, s, r in zip(ms, singles, res):
+        rs = s.optimize(max_f_eval=200)
+        assert np.array_equal(r.x, rs.x)
+        assert np.array_equal(m.kern.lengthscale.values, s.kern.lengthscale.values)

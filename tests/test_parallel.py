@@ -94,6 +94,45 @@ def test_drivers_agree_on_host_randomness_across_ranks():
     assert c0 == c1 and l0 == l1 and r0 == r1
 
 
+def _ea_rng_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import random
+        from optimobo_amd import ea
+        from optimobo_amd.algorithms import KEEP, ParEGO
+        np.random.seed(2000 + rank)                     # both generators start out of step
+        random.seed(3000 + rank)
+        out = []
+        for cls in (ParEGO, KEEP):
+            cls(_Prob(), seed=None)                     # BODriver.__init__ → agree_host_rng
+            X = np.linspace(0, 1, 36).reshape(12, 3)
+            pop = ea.initial_population(X, _Prob.xl, _Prob.xu)      # random.sample + numpy (parego.py:228-235)
+            tape = ea.ea_tape(len(pop), 3, iters=50)                # random.sample tournaments + numpy draws
+            out.append((pop.tolist(), tape.sel.tolist(), tape.mut.tolist(), tape.beta.tolist()))
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ea_drivers_agree_on_python_random_across_ranks():
+    """ParEGO / KEEP's evolutionary search draws from Python's `random` as well as numpy's
+    generator; with differently seeded ranks the temporary population and the search tape must agree."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ea_rng_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, o0), (_, o1) = sorted(got, key=lambda t: t[0])
+    assert o0 == o1
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_global_argmax_matches_single_process(world):
     rng = np.random.default_rng(world)

@@ -65,7 +65,10 @@ CONFIGS = {
     1: dict(problem="myproblem", n=20, d=2, budget=100, acq="solve_tch"),
     2: dict(problem="zdt1", n=128, d=6, log2=16, acq="ehvi2d"),
     3: dict(problem="zdt1", n=512, d=6, log2=20, acq="ehvi2d"),
-    4: dict(problem="dtlz2", n=256, d=6, log2=17, acq="ehvi3d"),
+    # config 4's training set covers [0.5, 1]^6 (an early BO iteration: the front is still far from the
+    # ideal point), so the reference's Monte-Carlo EHVI_3D is positive for ~17% of the candidates; over a
+    # training set spread through [0, 1]^6 it is 0 everywhere
+    4: dict(problem="dtlz2", n=256, d=6, log2=17, acq="ehvi3d", x_lo=0.5),
     5: dict(problem="zdt1", n=1024, d=30, log2=19, acq="ei_tch"),
     # not a BASELINE config: TuRBO's Thompson-sampling step (turbo.py:75-153) — one trust region,
     # n_cand = min(100·n_var, 5000) candidates, batch_size joint posterior draws, greedy arg-mins
@@ -74,9 +77,12 @@ CONFIGS = {
 METRIC = "EHVI candidate evals/sec at n_train=512, 2-obj; 1/2/4/8-GPU scaling"
 
 
-def setup_problem(n, d, seed=0, problem="zdt1"):
+def setup_problem(n, d, seed=0, problem="zdt1", x_lo=0.0):
+    """Training set of a BASELINE config: n points uniform in [x_lo, 1]^d (numpy default_rng(seed)), the
+    problem's objectives, ARD length scales ℓ_j ~ U[0.2, 2] (default_rng(seed + 1)), σ_f² = Var(Y_k)
+    (SURVEY §8d)."""
     rng = np.random.default_rng(seed)
-    X = rng.uniform(0.0, 1.0, (n, d))
+    X = rng.uniform(x_lo, 1.0, (n, d))
     Y = zdt1(X) if problem == "zdt1" else dtlz2(X)
     ls = np.random.default_rng(seed + 1).uniform(0.2, 2.0, d)
     variances = [float(np.var(Y[:, o])) for o in range(Y.shape[1])]
@@ -176,8 +182,7 @@ def run_solve(args, cfg, world_size, rank):
             "split_s": {"gp_fit": split["fit"], "device_maximiser": split["maximise"],
                         "other": el - split["fit"] - split["maximise"]},
             "final_hv": float(res.hypervolume_convergence[-1]), "n_evaluations": int(len(res.ysample)),
-            "roofline": None, "cpu_baseline": None,
-            "note": "the reference's own run needs GPy/pygmo/pymoo, absent here; no CPU baseline",
+            "roofline": None, "cpu_baseline": reference_solve_c1(),
         }))
 
 
@@ -302,6 +307,22 @@ def reference_cpu(config):
                     "what": r["what"], "measured_in": "build container (8 vCPU Xeon), tools/ref_cpu_baseline.py",
                     "source": "profiles/r02_ref_cpu_baseline.jsonl"}
     return None
+
+
+def reference_solve_c1():
+    """The reference's own MultiSurrogateOptimiser.solve on the README run, timed in the build container
+    (tools/ref_solve_baseline.py → profiles/r03_ref_solve_c1.json; GPy / pymoo replaced by doubles)."""
+    path = os.path.join(REPO, "profiles", "r03_ref_solve_c1.json")
+    try:
+        with open(path) as f:
+            r = json.loads(f.read().strip().splitlines()[-1])
+    except (OSError, ValueError, IndexError):
+        return None
+    return {"value": r["value"], "unit": r["unit"], "cores": r["cores"], "kind": "reference",
+            "sample": f"the whole run (budget 100, {r['seconds']:.0f} s, final HV {r['final_hv']:.2f}); "
+                      + r["doubles"],
+            "measured_in": "build container (8 vCPU Xeon), tools/ref_solve_baseline.py",
+            "source": "profiles/r03_ref_solve_c1.json"}
 
 
 def load_traffic(n, N, kernel="posterior"):
@@ -433,7 +454,7 @@ def main():
 
     n, d, acq_kind = cfg["n"], cfg["d"], cfg["acq"]
     N = 1 << (args.log2_cand if args.log2_cand is not None else cfg["log2"])
-    X, Y, ls, variances = setup_problem(n, d, problem=cfg["problem"])
+    X, Y, ls, variances = setup_problem(n, d, problem=cfg["problem"], x_lo=cfg.get("x_lo", 0.0))
     k_obj = Y.shape[1]
     pf = pareto.calc_pf(Y)
     r = Y.max(axis=0) + 0.1 * (Y.max(axis=0) - Y.min(axis=0))
@@ -646,11 +667,8 @@ def main():
             out["best"]["note"] = ("reference-mode EHVI passes sigma_B = var_0*s01 (util_functions.py:163-167); this "
                                    f"cache has s01 = {s01:.4g} < 0, so the acquisition is <= 0 everywhere and the "
                                    "arg-max is the lowest index among its maxima (DESIGN.md section 2, quirk 2)")
-        if acq_kind == "ehvi3d" and args.mode == "reference" and float(best[0]) <= 0.0:
-            out["best"]["note"] = ("reference EHVI_3D credits a Monte-Carlo sample only when the hypervolume of that "
-                                   "single point exceeds the whole front's (util_functions.py:202-211); with a dense "
-                                   "256-point front no sample does, so the acquisition is 0 and the arg-max is the "
-                                   "lowest index among its maxima; --mode textbook gives the exact EHVI")
+        if acq_kind == "ehvi3d":
+            out["config"]["train_box"] = f"[{cfg['x_lo']}, 1]^{d}"
         print(json.dumps(out))
     if world_size > 1:
         dist.barrier()

@@ -147,12 +147,16 @@ class AcquisitionEngine:
         """Local L-BFGS-B finish from (x0, v0) — what ``differential_evolution(polish=True)`` does to its
         best member (scipy's default; optimisers.py:87,118 use it).  The objective and its central-
         difference gradient come from ONE batched device evaluation of the (2d+1)-point stencil per
-        L-BFGS-B step (one-sided at the bounds).  Keeps x0 unless the polished point scores higher."""
+        L-BFGS-B step (one-sided at the bounds).  Keeps x0 unless the polished point scores higher.
+        The objective is scaled by 1/|v0|: L-BFGS-B's stopping test compares the decrease of f with
+        ftol·max(|f|, 1), so an unscaled acquisition of magnitude 1e-3 would stop at a relative accuracy
+        of ~1e-6 (the README run's expected decomposition is 1e-4 to 1e-2)."""
         from scipy.optimize import minimize
         lower = np.asarray(lower, np.float64)
         upper = np.asarray(upper, np.float64)
         d = lower.size
         h = 1e-6 * np.maximum(upper - lower, 1e-12)
+        scale = 1.0 / abs(v0) if np.isfinite(v0) and v0 != 0.0 else 1.0
 
         def fg(x):
             x = np.clip(x, lower, upper)
@@ -169,7 +173,7 @@ class AcquisitionEngine:
                 step = P[1 + 2 * j, j] - P[2 + 2 * j, j]
                 if np.isfinite(a) and np.isfinite(b) and step > 0:
                     g[j] = (a - b) / step
-            return -v[0], -g
+            return -v[0] * scale, -g * scale
 
         res = minimize(fg, np.asarray(x0, np.float64), jac=True, method="L-BFGS-B",
                        bounds=list(zip(lower, upper)), options={"maxiter": int(maxiter)})

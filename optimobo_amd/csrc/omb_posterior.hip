@@ -225,9 +225,14 @@ constexpr int kblock_rows(int DP) {
 // row tile) and wave w stores rows 2w, 2w+1 of the workgroup's 128 candidates, one 1-KB row segment
 // per store instruction (b128 per lane), instead of 4 × 128 B.
 constexpr int kTransPitch = 144;   // tb row pitch (doubles): the 4 row groups of a tile write land on disjoint banks
-template <int DP, int KIND, bool kNT = true, bool kSwap = false, bool kTrans = false>
+// RPI: row tiles per loop iteration (1 or 2, plain stores only).  With 2, the two tiles' cross-term MFMA
+// chains and Matern transforms are independent and interleave (a wave otherwise waits out each tile's
+// dependent 8-step chain at n_var > 8).  ABL (tools/ablate only): bit 1 drops the stores (the values are
+// folded into one guarded store per lane), bit 2 drops the cross term and the transform.
+template <int DP, int KIND, bool kNT = true, bool kSwap = false, bool kTrans = false, int RPI = 1, int ABL = 0>
 __global__ __launch_bounds__(512) void kernel_block_pipe_kernel(GPDev g, int d, const double* __restrict__ Xc,
                                                                 int64_t N, double* __restrict__ K, ExpCoef ec) {
+  static_assert(RPI == 1 || (RPI == 2 && !kSwap && !kTrans), "two row tiles per iteration: plain stores only");
   constexpr bool kAug = DP <= 8;
   constexpr int KSD = kAug ? (DP + 5) / 4 : (DP + 3) / 4;
   constexpr int KSDP = ((DP + 5) / 4 + 1) / 2;   // = packed_X_pairs(DP)
@@ -313,6 +318,76 @@ __global__ __launch_bounds__(512) void kernel_block_pipe_kernel(GPDev g, int d, 
   };
   __syncthreads();
   const int Tstart = T0 + (kSwap ? (wave >> 2) : 0);
+  if constexpr (RPI == 2) {
+    double sink = 0.0;
+    for (int T = Tstart; T < T1; T += 2) {
+      const int Tb = min(T + 1, T1 - 1);            // a lone last tile is computed twice, stored once
+      const d2* xa0 = reinterpret_cast<const d2*>(xfs + (T - T0) * (KSDP * 128) + 2 * lane);
+      const d2* xa1 = reinterpret_cast<const d2*>(xfs + (Tb - T0) * (KSDP * 128) + 2 * lane);
+      d2 a0[NA], a1[NA];
+#pragma unroll
+      for (int p = 0; p < NA; ++p) {
+        a0[p] = xa0[64 * p];
+        a1[p] = xa1[64 * p];
+      }
+      double v0[4], v1[4];
+      if constexpr ((ABL & 2) != 0) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v0[e] = a0[0].x + e;
+          v1[e] = a1[0].y + e;
+        }
+      } else {
+        d4 c0 = d4{0.0, 0.0, 0.0, 0.0}, c1 = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int q = 0; q < KSD; ++q) {
+          c0 = __builtin_amdgcn_mfma_f64_16x16x4f64((q & 1) ? a0[q >> 1].y : a0[q >> 1].x, bfr[0][q], c0, 0, 0, 0);
+          c1 = __builtin_amdgcn_mfma_f64_16x16x4f64((q & 1) ? a1[q >> 1].y : a1[q >> 1].x, bfr[0][q], c1, 0, 0, 0);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {
+          const int l0 = 16 * (T - T0) + 4 * e + (lane >> 4), m0 = 16 * (Tb - T0) + 4 * e + (lane >> 4);
+          const double r0a = kAug ? c0[e] : fma(-2.0, c0[e], xsqs[kAug ? 0 : l0] + csq[0]);
+          const double r0b = kAug ? c0[e + 1] : fma(-2.0, c0[e + 1], xsqs[kAug ? 0 : l0 + 4] + csq[0]);
+          const double r1a = kAug ? c1[e] : fma(-2.0, c1[e], xsqs[kAug ? 0 : m0] + csq[0]);
+          const double r1b = kAug ? c1[e + 1] : fma(-2.0, c1[e + 1], xsqs[kAug ? 0 : m0 + 4] + csq[0]);
+          if constexpr (kTab256) {
+            matern_r2_tab256_x2(r0a, r0b, pm, ec, etab, v0[e], v0[e + 1]);
+            matern_r2_tab256_x2(r1a, r1b, pm, ec, etab, v1[e], v1[e + 1]);
+          } else {
+            kernel_of_r2_tab_x2<KIND>(r0a, r0b, pm, ec, etab, v0[e], v0[e + 1]);
+            kernel_of_r2_tab_x2<KIND>(r1a, r1b, pm, ec, etab, v1[e], v1[e + 1]);
+          }
+        }
+      }
+      const bool second = Tb != T;
+      if constexpr ((ABL & 1) != 0) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sink += v0[e] + (second ? v1[e] : 0.0);
+      } else {
+        double* p0 = Kl + (int64_t)T * (4 * N4);
+        double* p1 = p0 + 4 * N4;
+        if (cols_full && Tb < full_tiles) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) st(p0 + e * N4, v0[e]);
+          if (second) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) st(p1 + e * N4, v1[e]);
+          }
+        } else if (col < N) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (16 * T + 4 * e + rsub < g.n) st(p0 + e * N4, v0[e]);
+            if (second && 16 * Tb + 4 * e + rsub < g.n) st(p1 + e * N4, v1[e]);
+          }
+        }
+      }
+    }
+    if constexpr ((ABL & 1) != 0)
+      if (sink == -1.2345e300 && col < N) K[col] = sink;       // never true: keeps the values live
+    return;
+  }
+  double sink1 = 0.0;
   for (int T = Tstart; T < T1; T += (kSwap ? 2 : 1)) {
     const d2* xa = reinterpret_cast<const d2*>(xfs + (T - T0) * (KSDP * 128) + 2 * lane);
     d2 a[NA];
@@ -321,6 +396,11 @@ __global__ __launch_bounds__(512) void kernel_block_pipe_kernel(GPDev g, int d, 
     double v[NCT][4];
 #pragma unroll
     for (int t = 0; t < NCT; ++t) {
+      if constexpr ((ABL & 2) != 0) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[t][e] = a[0].x + e;
+        continue;
+      }
       d4 cr = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int s = 0; s < KSD; ++s)
@@ -335,6 +415,11 @@ __global__ __launch_bounds__(512) void kernel_block_pipe_kernel(GPDev g, int d, 
         else
           kernel_of_r2_tab_x2<KIND>(r2a, r2b, pm, ec, etab, v[t][e], v[t][e + 1]);
       }
+    }
+    if constexpr ((ABL & 1) != 0) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sink1 += v[0][e];
+      continue;
     }
     double* p = Kl + (int64_t)T * (4 * N4);
     if constexpr (kSwap) {
@@ -377,6 +462,111 @@ __global__ __launch_bounds__(512) void kernel_block_pipe_kernel(GPDev g, int d, 
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           if (16 * T + 4 * e + rsub < g.n) st(p + e * N4, v[0][e]);
+      }
+    }
+  }
+  if constexpr ((ABL & 1) != 0)
+    if (sink1 == -1.2345e300 && col < N) K[col] = sink1;        // never true: keeps the values live
+}
+
+// K block, persistent over candidate blocks: the workgroup stages its kblock_rows(DP) training rows' fragments
+// once (as kernel_block_pipe_kernel does) and then sweeps CB blocks of 128 candidates, wave w owning the
+// 16-candidate tile w of each.  The next block's coordinates are loaded while the current block's row tiles
+// are computed and stored, so the staging and the candidate loads are paid once per CB blocks and their
+// latency is hidden (the compiler's wait for the prefetch is a vmcnt that leaves the block's stores in
+// flight).  RCP multiplies by 1/ℓ (one rounding more than GPy's division; ≤ 1 ulp in x/ℓ).
+template <int DP, int KIND, int CB, bool RCP = false>
+__global__ __launch_bounds__(512) void kernel_block_persist_kernel(GPDev g, int d, const double* __restrict__ Xc,
+                                                                   int64_t N, double* __restrict__ K, ExpCoef ec) {
+  constexpr bool kAug = DP <= 8;
+  constexpr int KSD = kAug ? (DP + 5) / 4 : (DP + 3) / 4;
+  constexpr int KSDP = ((DP + 5) / 4 + 1) / 2;   // = packed_X_pairs(DP)
+  constexpr int NA = (KSD + 1) / 2;
+  constexpr int TPW = kblock_rows(DP) / 16;
+  constexpr bool kTab256 = KIND == OMB_KERNEL_MATERN52;
+  __shared__ double etab[kTab256 ? 256 : 64];
+  __shared__ double xfs[TPW * KSDP * 128];
+  __shared__ double xsqs[kAug ? 1 : TPW * 16];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int T0 = blockIdx.y * TPW;
+  const int T1 = min((g.n + 15) / 16, T0 + TPW);
+  const int64_t base = (int64_t)blockIdx.x * (128 * CB) + 16 * wave;
+  double il[KSD];
+#pragma unroll
+  for (int s = 0; s < KSD; ++s) {
+    const int j = 4 * s + (lane >> 4);
+    il[s] = (j < d) ? (RCP ? 1.0 / g.ls[j] : g.ls[j]) : 1.0;
+  }
+  auto load_raw = [&](int64_t cb, double (&raw)[KSD]) {
+    const int64_t c = cb + (lane & 15);
+    const int64_t ci = c < N ? c : N - 1;
+#pragma unroll
+    for (int s = 0; s < KSD; ++s) {
+      const int j = 4 * s + (lane >> 4);
+      raw[s] = (j < d) ? Xc[ci * d + j] : 0.0;
+    }
+  };
+  double raw[KSD];
+  load_raw(base < N ? base : 0, raw);               // in flight during the staging
+  if (tid < (kTab256 ? 256 : 64)) etab[tid] = kTab256 ? kExp2Tab256[tid] : kExp2Tab64[tid];
+  for (int i = tid; i < (T1 - T0) * KSDP * 128; i += 512) xfs[i] = g.Xf[(int64_t)T0 * KSDP * 128 + i];
+  if constexpr (!kAug)
+    for (int i = tid; i < (T1 - T0) * 16; i += 512) xsqs[i] = g.xsq[16 * T0 + i];
+  const double pm[3] = {g.variance, kSqrt5 * g.variance, kFiveThirds * g.variance};
+  const int full_tiles = g.n / 16;
+  const int rsub = lane >> 4;
+  const int64_t N4 = 4 * N;
+  __syncthreads();
+  for (int jb = 0; jb < CB; ++jb) {
+    const int64_t cb = base + (int64_t)jb * 128;
+    if (cb >= N) break;                             // wave-uniform
+    double xs[KSD], csq = 0.0;
+#pragma unroll
+    for (int s = 0; s < KSD; ++s) {
+      xs[s] = RCP ? raw[s] * il[s] : raw[s] / il[s];
+      csq = fma(xs[s], xs[s], csq);
+    }
+    csq += __shfl_xor(csq, 16);
+    csq += __shfl_xor(csq, 32);
+    double bfr[KSD];
+#pragma unroll
+    for (int s = 0; s < KSD; ++s) {
+      const int j = 4 * s + (lane >> 4);
+      bfr[s] = kAug ? ((j < d) ? -2.0 * xs[s] : (j == d ? 1.0 : (j == d + 1 ? csq : 0.0))) : xs[s];
+    }
+    if (jb + 1 < CB && cb + 128 < N) load_raw(cb + 128, raw);   // next block, in flight during this one
+    const int64_t col = cb + (lane & 15);
+    const bool cols_full = (int64_t)(blockIdx.x) * (128 * CB) + (int64_t)(jb + 1) * 128 <= N;   // workgroup-uniform
+    double* Kl = K + (int64_t)rsub * N + col;
+    for (int T = T0; T < T1; ++T) {
+      const d2* xa = reinterpret_cast<const d2*>(xfs + (T - T0) * (KSDP * 128) + 2 * lane);
+      d2 a[NA];
+#pragma unroll
+      for (int p = 0; p < NA; ++p) a[p] = xa[64 * p];
+      d4 cr = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int q = 0; q < KSD; ++q)
+        cr = __builtin_amdgcn_mfma_f64_16x16x4f64((q & 1) ? a[q >> 1].y : a[q >> 1].x, bfr[q], cr, 0, 0, 0);
+      double v[4];
+#pragma unroll
+      for (int e = 0; e < 4; e += 2) {
+        const int l0 = 16 * (T - T0) + 4 * e + rsub;
+        const double r2a = kAug ? cr[e] : fma(-2.0, cr[e], xsqs[kAug ? 0 : l0] + csq);
+        const double r2b = kAug ? cr[e + 1] : fma(-2.0, cr[e + 1], xsqs[kAug ? 0 : l0 + 4] + csq);
+        if constexpr (kTab256)
+          matern_r2_tab256_x2(r2a, r2b, pm, ec, etab, v[e], v[e + 1]);
+        else
+          kernel_of_r2_tab_x2<KIND>(r2a, r2b, pm, ec, etab, v[e], v[e + 1]);
+      }
+      double* p = Kl + (int64_t)T * (4 * N4);
+      if (cols_full && T < full_tiles) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) __builtin_nontemporal_store(v[e], p + e * N4);
+      } else if (col < N) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (16 * T + 4 * e + rsub < g.n) __builtin_nontemporal_store(v[e], p + e * N4);
       }
     }
   }
@@ -1259,23 +1449,40 @@ template <int KIND>
 static hipError_t launch_kblock_kind(hipStream_t stream, const GPArgs& args, int obj, const double* Xc, int64_t N,
                                      double* K) {
   const GPDev& g = args.gp[obj];
-  // LDS-staged fragments, 128 candidates per workgroup (kernel_block_pipe_kernel) for every n_var.
-  // n_var > 8 first kept kernel_block_mfma_kernel (profiles/r02_v4_ablate_kblock_c5.txt: the staged
-  // kernel's per-workgroup candidate setup divided every coordinate); with each lane dividing only the
-  // coordinates of its B-fragment slots the staged kernel is faster there too (config 5, n = 1024,
-  // d = 30, N = 2^19: 1.70 → 1.44 ms, profiles/r02_v54_ablate_kblock_c5.txt)
-  auto pipe_grid = [&](int DP) {
-    return dim3((unsigned)((N + 127) / 128), (unsigned)((g.n + kblock_rows(DP) - 1) / kblock_rows(DP)));
+  // LDS-staged fragments (the store loop issues no loads, so the store queue never drains), persistent over
+  // CB blocks of 128 candidates (kernel_block_persist_kernel; tools/ablate/ablate_kblock3,
+  // profiles/r03_v7_ablate_kblock3_c*.txt):
+  //   n_var ≤ 8: CB = 1 (n = 512, d = 6, N = 2^20: 0.867 ms for kernel_block_pipe_kernel → 0.828 ms; more
+  //              blocks per workgroup cost occupancy there, 0.995 ms at CB = 4);
+  //   n_var > 8: CB = 8 with 1/ℓ multiplies (n = 1024, d = 30, N = 2^19: 1.459 → 1.268 ms at CB = 8, 1.229 ms
+  //              at CB = 4 with 1/ℓ; the staging and the per-candidate divisions are paid once per block).
+  //   small batches (TuRBO's K*, N ≤ 5000) keep CB = 1: the grid must still cover the CUs.
+  auto grid = [&](int DP, int CB) {
+    return dim3((unsigned)((N + 128 * CB - 1) / (128 * CB)), (unsigned)((g.n + kblock_rows(DP) - 1) / kblock_rows(DP)));
   };
-  const dim3 grid((unsigned)((N + 63) / 64), (unsigned)((g.n + kKBlockRows - 1) / kKBlockRows));
+  auto pick_cb = [&](int DP) {
+    for (int cb = 8; cb > 1; cb >>= 1) {
+      const dim3 gr = grid(DP, cb);
+      if ((int64_t)gr.x * gr.y >= 2048) return cb;
+    }
+    return 1;
+  };
   switch (args.DP) {
-#define OMB_KBP(DPV) \
-  case DPV: hipLaunchKernelGGL((kernel_block_pipe_kernel<DPV, KIND, true, kKBlockSwap>), pipe_grid(DPV), dim3(512), 0, stream, g, args.d, Xc, N, K, exp_coef()); break;
-#define OMB_KB(DPV) \
-  case DPV: hipLaunchKernelGGL((kernel_block_mfma_kernel<DPV, KIND>), grid, dim3(256), 0, stream, g, args.d, Xc, N, K, exp_coef()); break;
-    OMB_KBP(2) OMB_KBP(4) OMB_KBP(6) OMB_KBP(8) OMB_KBP(16) OMB_KBP(32) OMB_KBP(64)
-#undef OMB_KB
-#undef OMB_KBP
+#define OMB_KBS(DPV) \
+  case DPV: hipLaunchKernelGGL((kernel_block_persist_kernel<DPV, KIND, 1, false>), grid(DPV, 1), dim3(512), 0, stream, g, args.d, Xc, N, K, exp_coef()); break;
+#define OMB_KBW_CB(DPV, CBV) \
+  case CBV: hipLaunchKernelGGL((kernel_block_persist_kernel<DPV, KIND, CBV, true>), grid(DPV, CBV), dim3(512), 0, stream, g, args.d, Xc, N, K, exp_coef()); break;
+#define OMB_KBW(DPV) \
+  case DPV:                                                                  \
+    switch (pick_cb(DPV)) {                                                  \
+      OMB_KBW_CB(DPV, 8) OMB_KBW_CB(DPV, 4) OMB_KBW_CB(DPV, 2) OMB_KBW_CB(DPV, 1) \
+      default: return hipErrorInvalidValue;                                  \
+    }                                                                        \
+    break;
+    OMB_KBS(2) OMB_KBS(4) OMB_KBS(6) OMB_KBS(8) OMB_KBW(16) OMB_KBW(32) OMB_KBW(64)
+#undef OMB_KBS
+#undef OMB_KBW
+#undef OMB_KBW_CB
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -218,52 +218,134 @@ def make_ehvi3d_pos(rng, uf, seed=1):
                         cache_seed=np.int64(seed))
 
 
-def make_de_proposals(opt_mod, uf, sc):
-    """The reference's maximiser on fixed surrogates: ``MultiSurrogateOptimiser._get_proposed_EHVI``
-    (optimisers.py:91-119) and ``_get_proposed_scalarisation`` (:62-88), i.e. scipy
-    ``differential_evolution(obj, bounds)`` with its defaults (best1bin, popsize 15, tol 0.01,
-    polish=True: an L-BFGS-B finish), seeded through numpy's global state (scipy's DE draws from it
-    when no rng is given).  The fitted GPy models are the oracle's GPy restatement (oracle/gp.py),
-    duck-typed.  Stored: the surrogate data and the proposal x_DE with its acquisition value."""
+def make_ehvi3d_c4(uf, n_pick=512):
+    """The reference's own EHVI_3D (util_functions.py:170-214) on BASELINE config 4's workload as bench.py
+    builds it (DTLZ2, n = 256 training points in [0.5, 1]^6, d = 6, 2^17 unscrambled Sobol candidates, cache
+    seed 1): the posterior moments of `n_pick` sampled candidates from the oracle's GPy restatement, fed to
+    the reference through ConstModel.  About 17% of the values are positive, 19% raise (pygmo)."""
+    sys.path.insert(0, REPO)
+    import bench
+    cfg = bench.CONFIGS[4]
+    n, d, N = cfg["n"], cfg["d"], 1 << cfg["log2"]
+    X, Y, ls, variances = bench.setup_problem(n, d, problem=cfg["problem"], x_lo=cfg["x_lo"])
+    idx = np.sort(np.random.default_rng(44).choice(N, n_pick, replace=False))
+    Xc = qmc.Sobol(d=d, scramble=False).random_base2(m=cfg["log2"])[idx]
+    mu = np.empty((3, n_pick))
+    var = np.empty((3, n_pick))
+    for o in range(3):
+        m, v = ogp.ExactGP(X, Y[:, o], ls, variances[o]).predict(Xc)
+        mu[o], var[o] = m[:, 0], v[:, 0]
+    pf = opareto.calc_pf(Y)
+    r = Y.max(0) + 0.1 * (Y.max(0) - Y.min(0))
+    cache = cached_samples(3, 5, seed=1)
+    ref = np.full(n_pick, np.nan)
+    raises = np.zeros(n_pick, bool)
+    for i in range(n_pick):
+        try:
+            ref[i] = uf.EHVI_3D(np.zeros(3), [ConstModel(mu[j, i], var[j, i]) for j in range(3)], r, pf, cache)
+        except ValueError:
+            raises[i] = True
+    print(f"  ehvi3d_c4: P={len(pf)} positive {np.mean(ref > 0):.3f} raises {raises.mean():.3f}")
+    np.savez_compressed(os.path.join(HERE, "ehvi3d_c4.npz"), X=X, Y=Y, ls=ls, variances=np.asarray(variances),
+                        idx=idx, log2_cand=np.int64(cfg["log2"]), mu=mu, var=var, pf=pf, r=r, cache=cache,
+                        cache_seed=np.int64(1), hv_pf=opareto.hypervolume(pf, r), ehvi_reference=ref,
+                        raises=raises)
+
+
+def make_de_proposals(opt_mod, uf, sc, emo_mod=None):
+    """The reference's maximisers on fixed surrogates: scipy ``differential_evolution(obj, bounds)`` with its
+    defaults (best1bin, popsize 15, tol 0.01, polish=True: an L-BFGS-B finish), seeded through numpy's
+    global state (scipy's DE draws from it when no rng is given), called through the reference's own glue:
+      * "ehvi"   ``MultiSurrogateOptimiser._get_proposed_EHVI`` with ``EHVI`` (optimisers.py:91-119, :246);
+      * "tch"    ``_get_proposed_scalarisation`` with ``expected_decomposition`` (:62-88, :252);
+      * "hvpoi"  ``EMO.get_proposed`` with ``hypervolume_based_PoI`` over ``decompose_into_cells``
+                 (emo.py:231-241, :304-305);
+      * "ei"     ``MonoSurrogateOptimiser._get_proposed`` with ``_expected_improvement`` (optimisers.py:325-367)
+                 on a Tchebicheff-aggregated surrogate;
+      * "ehvi3d" ``_get_proposed_EHVI`` with ``EHVI_3D`` (optimisers.py:248; 3 objectives, DTLZ2 trained on
+                 [0.5, 1]^d so the Monte-Carlo value is positive over part of the box; r is set far enough
+                 out that no DE member makes pygmo raise — the reference would crash there).
+    The fitted GPy models are the oracle's GPy restatement (oracle/gp.py), duck-typed.  Stored: the
+    surrogate data and the proposal x_DE with its acquisition value."""
     class Prob:
-        def __init__(self, d, xl, xu):
-            self.n_var, self.n_obj = d, 2
+        def __init__(self, d, xl, xu, k=2):
+            self.n_var, self.n_obj = d, k
             self.xl, self.xu = np.asarray(xl, np.float64), np.asarray(xu, np.float64)
 
     out = {}
     cases = [("ehvi", 2, 20, 3), ("ehvi", 3, 40, 4), ("ehvi", 6, 64, 5), ("ehvi", 4, 30, 6),
-             ("tch", 2, 25, 7), ("tch", 5, 50, 8)]
+             ("tch", 2, 25, 7), ("tch", 5, 50, 8),
+             ("hvpoi", 2, 20, 9), ("hvpoi", 5, 60, 10), ("hvpoi", 8, 120, 11),
+             ("ei", 3, 30, 12), ("ei", 8, 120, 13),
+             ("ehvi3d", 3, 40, 14), ("ehvi3d", 6, 80, 15),
+             ("ehvi", 8, 120, 16)]
     for c, (kind, d, n, seed) in enumerate(cases):
         rng = np.random.default_rng(100 + seed)
         xl, xu = np.zeros(d), np.ones(d)
-        X = rng.uniform(0, 1, (n, d))
-        Y = zdt1(X) if d > 1 else X
+        if kind == "ehvi3d":
+            X = 0.5 + 0.5 * rng.uniform(0, 1, (n, d))
+            g = np.sum((X[:, 2:] - 0.5) ** 2, axis=1)
+            th = X[:, :2] * np.pi / 2
+            Y = np.column_stack([(1 + g) * np.cos(th[:, 0]) * np.cos(th[:, 1]),
+                                 (1 + g) * np.cos(th[:, 0]) * np.sin(th[:, 1]), (1 + g) * np.sin(th[:, 0])])
+        else:
+            X = rng.uniform(0, 1, (n, d))
+            Y = zdt1(X) if d > 1 else X
+        k = Y.shape[1]
         ls = rng.uniform(0.3, 1.5, d)
-        variances = np.array([float(np.var(Y[:, o])) for o in range(2)])
-        models = [ogp.ExactGP(X, Y[:, o], ls, variances[o]) for o in range(2)]
-        opt = opt_mod.MultiSurrogateOptimiser(Prob(d, xl, xu))
-        cache = cached_samples(2, 5 if kind == "ehvi" else 3, seed=1)
+        variances = np.array([float(np.var(Y[:, o])) for o in range(k)])
+        models = [ogp.ExactGP(X, Y[:, o], ls, variances[o]) for o in range(k)]
+        opt = opt_mod.MultiSurrogateOptimiser(Prob(d, xl, xu, k))
+        cache = cached_samples(k, 3 if kind == "tch" else 5, seed=1)
         pf = opareto.calc_pf(Y)
-        r = Y.max(0) + 0.1 * (Y.max(0) - Y.min(0))
+        r = Y.max(0) + (1.0 if kind == "ehvi3d" else 0.1) * (Y.max(0) - Y.min(0))
+        extra = {}
         np.random.seed(seed)
         if kind == "ehvi":
             x_de, fun = opt._get_proposed_EHVI(uf.EHVI, models, Y.min(0), r, pf, cache)
             val = float(np.asarray(uf.EHVI(x_de, models, r, pf, cache)).reshape(-1)[0])
-            extra = {}
-        else:
+        elif kind == "ehvi3d":
+            for grow in (1.0, 2.0, 4.0, 8.0):     # first r at which no DE member leaves the box
+                r = Y.max(0) + grow * (Y.max(0) - Y.min(0))
+                np.random.seed(seed)
+                try:
+                    x_de, fun = opt._get_proposed_EHVI(uf.EHVI_3D, models, Y.min(0), r, pf, cache)
+                    break
+                except ValueError:
+                    continue
+            val = float(uf.EHVI_3D(x_de, models, r, pf, cache))
+        elif kind == "tch":
             tch = sc.Tchebicheff(Y.min(0), Y.max(0))
             w = np.array([0.4, 0.6])
             agg_min = float(np.min([tch(y, w) for y in Y]))
             x_de, fun, _ = opt._get_proposed_scalarisation(uf.expected_decomposition, models, agg_min, tch, w, cache)
             val = float(uf.expected_decomposition(x_de, models, w, tch, agg_min, cache))
             extra = {"w": w, "agg_min": np.float64(agg_min), "ideal": Y.min(0), "max": Y.max(0)}
+        elif kind == "hvpoi":
+            emo = emo_mod.EMO(Prob(d, xl, xu, k), None, None)
+            emo.ideal_point, emo.max_point = Y.min(0), Y.max(0)      # emo.py:265-271 (bounds from ysample)
+            cells = emo.decompose_into_cells(uf.calc_pf(Y))           # emo.py:304
+            x_de, fun = emo.get_proposed(emo.hypervolume_based_PoI, Y, cells, models)
+            val = float(emo.hypervolume_based_PoI(x_de, models, Y, cells))
+            extra = {"cells": cells, "ideal": Y.min(0), "max": Y.max(0)}
+        else:   # "ei": mono surrogate over the Tchebicheff aggregate
+            mono = opt_mod.MonoSurrogateOptimiser(Prob(d, xl, xu, k))
+            tch = sc.Tchebicheff(Y.min(0), Y.max(0))
+            w = np.array([0.3, 0.7])
+            yagg = np.asarray([tch(y, w) for y in Y]).flatten()
+            agg_var = float(np.var(yagg))
+            model = ogp.ExactGP(X, yagg, ls, agg_var)
+            best = float(yagg[np.argmin(yagg)])
+            x_de, fun = mono._get_proposed(mono._expected_improvement, model, best)
+            val = float(mono._expected_improvement(x_de, model, best)[0])
+            extra = {"yagg": yagg, "agg_variance": np.float64(agg_var), "best": np.float64(best)}
         key = f"c{c}"
         out.update({f"{key}_kind": np.array(kind), f"{key}_X": X, f"{key}_Y": Y, f"{key}_ls": ls,
                     f"{key}_variances": variances, f"{key}_pf": pf, f"{key}_r": r, f"{key}_cache": cache,
                     f"{key}_xl": xl, f"{key}_xu": xu, f"{key}_x_de": np.asarray(x_de, np.float64),
                     f"{key}_fun_de": np.float64(fun), f"{key}_value_de": np.float64(val),
                     f"{key}_np_seed": np.int64(seed)})
-        out.update({f"{key}_{k}": v for k, v in extra.items()})
+        out.update({f"{key}_{k_}": v for k_, v in extra.items()})
         print(f"DE proposal {key} ({kind}, d={d}, n={n}): x={np.round(x_de, 4)} value={val:.6g}", flush=True)
     out["n_cases"] = np.int64(len(cases))
     np.savez_compressed(os.path.join(HERE, "de_proposals.npz"), **out)
@@ -758,9 +840,11 @@ def main():
     if not only or "cparego" in only:
         make_cparego(np.random.default_rng(20261018), cparego_mod, sc)
     if not only or "de" in only:
-        make_de_proposals(opt_mod, uf, sc)
+        make_de_proposals(opt_mod, uf, sc, emo_mod)
     if not only or "ea" in only:
         make_ea(parego_mod, keep_mod, sc)
+    if not only or "ehvi3d_c4" in only:
+        make_ehvi3d_c4(uf)
     if not only or "ehvi_pos" in only:
         make_ehvi2d_pos(np.random.default_rng(20261019), uf)
         make_ehvi3d_pos(np.random.default_rng(20261020), uf)

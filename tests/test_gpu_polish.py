@@ -1,7 +1,8 @@
 """GPU: the batched maximiser (device Sobol rounds + L-BFGS-B polish) against the reference's own
 maximiser, scipy ``differential_evolution`` with its defaults, on the same surrogates
 (tests/golden/de_proposals.npz, made by tests/golden/make_golden.py from the reference's
-``_get_proposed_EHVI`` / ``_get_proposed_scalarisation``, optimisers.py:62-119).
+``_get_proposed_EHVI`` / ``_get_proposed_scalarisation`` (optimisers.py:62-119, with EHVI and EHVI_3D),
+``EMO.get_proposed`` (emo.py:231-241) and ``MonoSurrogateOptimiser._get_proposed`` (optimisers.py:346-367)).
 
 The bar: the proposal of ``AcquisitionEngine.maximise`` scores at least the DE
 proposal's acquisition value, EHVI(x_DE) − 1e-6·|EHVI(x_DE)|, on every fixture.  The device value of
@@ -26,39 +27,47 @@ def _cases(golden_dir):
     return z, int(z["n_cases"])
 
 
-@pytest.mark.parametrize("c", range(6))
+from _de_fixture import N_CASES, oracle_value as _oracle_value  # noqa: E402
+
+
+@pytest.mark.parametrize("c", range(N_CASES))
 def test_maximise_reaches_de_proposal(golden_dir, c):
+    """Kinds: "ehvi" (_get_proposed_EHVI, 2 objectives), "tch" (_get_proposed_scalarisation), "hvpoi"
+    (EMO.get_proposed), "ei" (MonoSurrogateOptimiser._get_proposed), "ehvi3d" (_get_proposed_EHVI with
+    EHVI_3D); d up to 8, n up to 120."""
     from optimobo_amd import scalarisations as sc
     from optimobo_amd.acquisition import AcquisitionEngine
     from optimobo_amd.gp import GPState
     z, n = _cases(golden_dir)
-    assert c < n
+    assert n == N_CASES
     k = f"c{c}"
     kind = str(z[f"{k}_kind"])
     X, Y, ls, var = z[f"{k}_X"], z[f"{k}_Y"], z[f"{k}_ls"], z[f"{k}_variances"]
     xl, xu = z[f"{k}_xl"], z[f"{k}_xu"]
-    eng = AcquisitionEngine(0).load_models([GPState(X, Y[:, o], ls, float(var[o])) for o in range(2)])
-    if kind == "ehvi":
-        eng.plan_ehvi(z[f"{k}_r"], z[f"{k}_pf"], z[f"{k}_cache"], mode="reference")
+    if kind == "ei":
+        eng = AcquisitionEngine(0).load_models([GPState(X, z[f"{k}_yagg"], ls, float(z[f"{k}_agg_variance"]))])
+        eng.plan_ei(float(z[f"{k}_best"]), 0.0)                    # optimisers.py:325-344: σ = sqrt(σ²)
     else:
-        tch = sc.Tchebicheff(z[f"{k}_ideal"], z[f"{k}_max"])
-        eng.plan_expected_decomposition(z[f"{k}_w"], tch, float(z[f"{k}_agg_min"]), z[f"{k}_cache"])
+        eng = AcquisitionEngine(0).load_models([GPState(X, Y[:, o], ls, float(var[o])) for o in range(Y.shape[1])])
+        if kind == "ehvi":
+            eng.plan_ehvi(z[f"{k}_r"], z[f"{k}_pf"], z[f"{k}_cache"], mode="reference")
+        elif kind == "ehvi3d":
+            eng.plan_ehvi3d(z[f"{k}_r"], z[f"{k}_pf"], z[f"{k}_cache"])
+        elif kind == "hvpoi":
+            eng.plan_hvpoi(z[f"{k}_cells"])
+        else:
+            tch = sc.Tchebicheff(z[f"{k}_ideal"], z[f"{k}_max"])
+            eng.plan_expected_decomposition(z[f"{k}_w"], tch, float(z[f"{k}_agg_min"]), z[f"{k}_cache"])
     x, v = eng.maximise(None, xl, xu, n_candidates=1 << 16, seed=c)
     v_de = float(z[f"{k}_value_de"])
     assert v >= v_de - 1e-6 * abs(v_de), (kind, x, v, z[f"{k}_x_de"], v_de)
-    # the device value at the proposal is the reference arithmetic's value there (oracle restatement)
-    mus, vs = [], []
-    for o in range(2):
-        m, s2 = ogp.ExactGP(X, Y[:, o], ls, float(var[o])).predict(x[None, :])
-        mus.append(m[:, 0])
-        vs.append(s2[:, 0])
-    if kind == "ehvi":
-        ref = oacq.ehvi2d(np.array(mus), np.array(vs), z[f"{k}_pf"], z[f"{k}_r"], z[f"{k}_cache"])[0]
-    else:
-        ref = oacq.expected_decomposition(np.array(mus), np.array(vs), z[f"{k}_cache"],
-                                          osc.Tchebicheff(z[f"{k}_ideal"], z[f"{k}_max"]), z[f"{k}_w"],
-                                          float(z[f"{k}_agg_min"]))[0]
+    assert np.all(x >= xl) and np.all(x <= xu)
+    # the device value at the proposal is the reference arithmetic's value there (oracle restatement), and
+    # the oracle at the DE proposal reproduces the reference's own value there
+    ref = _oracle_value(z, k, kind, x)
     assert abs(ref - v) <= 1e-6 * abs(ref) + 1e-14
+    ref_de = _oracle_value(z, k, kind, np.asarray(z[f"{k}_x_de"]))
+    assert abs(ref_de - v_de) <= 1e-9 * abs(v_de) + 1e-14
     eng.ctx.close()
 
 

@@ -100,6 +100,23 @@ def test_ehvi3d_reference_positive(golden_dir):
     np.testing.assert_allclose(val[ok], z["ehvi_reference"][ok], rtol=1e-10, atol=1e-15)
 
 
+def test_ehvi3d_reference_config4_workload(golden_dir):
+    """The reference's EHVI_3D on BASELINE config 4's bench workload (make_golden.py make_ehvi3d_c4): the
+    oracle reproduces it, at least 5% of the values are positive, and bench.setup_problem still builds the
+    fixture's training set (the GPU test runs the whole 2^17 shard of that workload)."""
+    import bench
+    z = load(golden_dir, "ehvi3d_c4.npz")
+    val, raises = acq.ehvi3d_reference(z["mu"], z["var"], float(z["hv_pf"]), z["r"], z["cache"])
+    assert np.array_equal(raises, z["raises"])
+    ok = ~z["raises"]
+    assert (z["ehvi_reference"][ok] > 0).mean() * ok.mean() >= 0.05
+    np.testing.assert_allclose(val[ok], z["ehvi_reference"][ok], rtol=1e-10, atol=1e-15)
+    cfg = bench.CONFIGS[4]
+    X, Y, ls, variances = bench.setup_problem(cfg["n"], cfg["d"], problem=cfg["problem"], x_lo=cfg["x_lo"])
+    assert np.array_equal(X, z["X"]) and np.array_equal(Y, z["Y"]) and np.array_equal(ls, z["ls"])
+    assert np.array_equal(pareto.calc_pf(Y), z["pf"])
+
+
 def test_cells_and_hvpoi(golden_dir):
     z = load(golden_dir, "cells_hvpoi.npz")
     for t in range(4):
@@ -236,3 +253,19 @@ def test_full_cov_vs_sklearn():
     mu_s, cov_s = gpr.predict(Xc, return_cov=True)
     np.testing.assert_allclose(mu, mu_s, rtol=1e-6, atol=1e-8)
     np.testing.assert_allclose(cov, cov_s, rtol=1e-6, atol=1e-9 * var)
+
+
+def test_de_proposal_values_reproduced_by_oracle(golden_dir):
+    """The oracle's restatement gives the reference's own acquisition value at every DE proposal (EHVI,
+    EHVI_3D, expected decomposition, HV-PoI, mono-surrogate EI)."""
+    from _de_fixture import N_CASES, oracle_value
+    z = load(golden_dir, "de_proposals.npz")
+    assert int(z["n_cases"]) == N_CASES
+    kinds = set()
+    for c in range(N_CASES):
+        k = f"c{c}"
+        kind = str(z[f"{k}_kind"])
+        kinds.add(kind)
+        v = oracle_value(z, k, kind, np.asarray(z[f"{k}_x_de"]))
+        assert abs(v - float(z[f"{k}_value_de"])) <= 1e-9 * abs(float(z[f"{k}_value_de"])) + 1e-14, (c, kind)
+    assert kinds == {"ehvi", "tch", "hvpoi", "ei", "ehvi3d"}

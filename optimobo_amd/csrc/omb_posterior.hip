@@ -474,8 +474,9 @@ __global__ __launch_bounds__(512) void kernel_block_pipe_kernel(GPDev g, int d, 
 // 16-candidate tile w of each.  The next block's coordinates are loaded while the current block's row tiles
 // are computed and stored, so the staging and the candidate loads are paid once per CB blocks and their
 // latency is hidden (the compiler's wait for the prefetch is a vmcnt that leaves the block's stores in
-// flight).  RCP multiplies by 1/ℓ (one rounding more than GPy's division; ≤ 1 ulp in x/ℓ).
-template <int DP, int KIND, int CB, bool RCP = false>
+// flight).  RCP multiplies by 1/ℓ (one rounding more than GPy's division; ≤ 1 ulp in x/ℓ).  ROLL keeps the
+// block loop rolled (unrolled, its registers cost occupancy).
+template <int DP, int KIND, int CB, bool RCP = false, bool ROLL = false>
 __global__ __launch_bounds__(512) void kernel_block_persist_kernel(GPDev g, int d, const double* __restrict__ Xc,
                                                                    int64_t N, double* __restrict__ K, ExpCoef ec) {
   constexpr bool kAug = DP <= 8;
@@ -518,6 +519,7 @@ __global__ __launch_bounds__(512) void kernel_block_persist_kernel(GPDev g, int 
   const int rsub = lane >> 4;
   const int64_t N4 = 4 * N;
   __syncthreads();
+#pragma unroll(ROLL ? 1 : CB)
   for (int jb = 0; jb < CB; ++jb) {
     const int64_t cb = base + (int64_t)jb * 128;
     if (cb >= N) break;                             // wave-uniform
@@ -1454,8 +1456,9 @@ static hipError_t launch_kblock_kind(hipStream_t stream, const GPArgs& args, int
   // profiles/r03_v7_ablate_kblock3_c*.txt):
   //   n_var ≤ 8: CB = 1 (n = 512, d = 6, N = 2^20: 0.867 ms for kernel_block_pipe_kernel → 0.828 ms; more
   //              blocks per workgroup cost occupancy there, 0.995 ms at CB = 4);
-  //   n_var > 8: CB = 8 with 1/ℓ multiplies (n = 1024, d = 30, N = 2^19: 1.459 → 1.268 ms at CB = 8, 1.229 ms
-  //              at CB = 4 with 1/ℓ; the staging and the per-candidate divisions are paid once per block).
+  //   n_var > 8: CB = 8 with 1/ℓ multiplies and the block loop not unrolled (n = 1024, d = 30, N = 2^19:
+  //              1.463 → 1.230 ms, profiles/r03_v9_ablate_kblock3_c5.txt; the staging and the per-candidate
+  //              divisions are paid once per 8 blocks; outputs within 1.2e-14 of the division form).
   //   small batches (TuRBO's K*, N ≤ 5000) keep CB = 1: the grid must still cover the CUs.
   auto grid = [&](int DP, int CB) {
     return dim3((unsigned)((N + 128 * CB - 1) / (128 * CB)), (unsigned)((g.n + kblock_rows(DP) - 1) / kblock_rows(DP)));
@@ -1471,7 +1474,7 @@ static hipError_t launch_kblock_kind(hipStream_t stream, const GPArgs& args, int
 #define OMB_KBS(DPV) \
   case DPV: hipLaunchKernelGGL((kernel_block_persist_kernel<DPV, KIND, 1, false>), grid(DPV, 1), dim3(512), 0, stream, g, args.d, Xc, N, K, exp_coef()); break;
 #define OMB_KBW_CB(DPV, CBV) \
-  case CBV: hipLaunchKernelGGL((kernel_block_persist_kernel<DPV, KIND, CBV, true>), grid(DPV, CBV), dim3(512), 0, stream, g, args.d, Xc, N, K, exp_coef()); break;
+  case CBV: hipLaunchKernelGGL((kernel_block_persist_kernel<DPV, KIND, CBV, true, true>), grid(DPV, CBV), dim3(512), 0, stream, g, args.d, Xc, N, K, exp_coef()); break;
 #define OMB_KBW(DPV) \
   case DPV:                                                                  \
     switch (pick_cb(DPV)) {                                                  \

@@ -65,15 +65,19 @@ void bench(int n, int64_t N, int d) {
       {"2 row tiles, stores only", L(DP, 0, true, false, false, 2, 2), false},
   };
 #undef L
-#define P(CB, RCP) [](dim3 gr, GPDev gg, int dd, const double* xc, int64_t nn, double* k, ExpCoef e) { \
+#define P(CB, RCP, ROLL) [](dim3 gr, GPDev gg, int dd, const double* xc, int64_t nn, double* k, ExpCoef e) { \
     dim3 g2((unsigned)((nn + 128 * CB - 1) / (128 * CB)), gr.y);                                     \
-    hipLaunchKernelGGL((kernel_block_persist_kernel<DP, 0, CB, RCP>), g2, dim3(512), 0, 0, gg, dd, xc, nn, k, e); }
+    hipLaunchKernelGGL((kernel_block_persist_kernel<DP, 0, CB, RCP, ROLL>), g2, dim3(512), 0, 0, gg, dd, xc, nn, k, e); }
   const V ps[] = {
-      {"persistent CB=1", P(1, false), true},
-      {"persistent CB=2", P(2, false), true},
-      {"persistent CB=4", P(4, false), true},
-      {"persistent CB=8", P(8, false), true},
-      {"persistent CB=4, 1/l multiply", P(4, true), true},
+      {"persistent CB=1", P(1, false, false), true},
+      {"persistent CB=1, 1/l", P(1, true, false), true},
+      {"persistent CB=2, 1/l", P(2, true, false), true},
+      {"persistent CB=4, 1/l", P(4, true, false), true},
+      {"persistent CB=8, 1/l", P(8, true, false), true},
+      {"persistent CB=16, 1/l", P(16, true, false), true},
+      {"persistent CB=4, 1/l, rolled", P(4, true, true), true},
+      {"persistent CB=8, 1/l, rolled", P(8, true, true), true},
+      {"persistent CB=2, rolled", P(2, false, true), true},
   };
 #undef P
   std::vector<V> all(vs, vs + sizeof(vs) / sizeof(vs[0]));

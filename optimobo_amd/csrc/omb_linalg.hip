@@ -886,24 +886,36 @@ __global__ __launch_bounds__(256) void gp_reduce_kernel(const double* __restrict
 }
 
 // ----------------------------------------------------------------------------- GP fit, n ≤ 128: one workgroup
-// The whole log-marginal-likelihood + gradient evaluation in one launch for the training-set sizes
-// of a BO loop (n_init .. budget, the README run has n ≤ 120), where the blocked path above is ~15
-// dependent launches and two host synchronisations.  Ky (n×n, full, row pitch n+1) lives in LDS:
-//   * Ky⁻¹ by the sweep operator (Goodnight) on the lower triangle (each thread owns fixed packed
-//     entries): sweeping pivot k applies the Schur-complement update
-//     A_ij −= A_ik A_kj / d (i, j ≠ k), scales row and column k by 1/d and sets A_kk = −1/d; after all
-//     n pivots A = −Ky⁻¹.  The unswept block evolves exactly as right-looking LDLᵀ, so the pivots d_k
-//     are the Cholesky pivots L_kk² (log|Ky| = Σ log d_k, positive-definiteness test !(d_k > 0) as in
-//     chol_panel_kernel, GPy jitchol's jitter retries in-kernel).  Pivots go two per barrier; the
-//     columns of the next pair are double-buffered in LDS by the threads that update them.
+// The whole log-marginal-likelihood + gradient evaluation in one launch for the training-set sizes of a
+// BO loop (n_init .. n_init + budget; the README run has n = 20 … 119), where the blocked path above is
+// ~15 dependent launches and two host synchronisations.  Ky (full, symmetric, padded to 16·NB with an
+// identity block) lives in LDS:
+//   * Ky⁻¹ by the block sweep operator, 16 pivots per step: for the pivot block B (tile p) and the rest R,
+//         A_BB ← −A_BB⁻¹,  A_BR ← A_BB⁻¹ A_BR,  A_RB ← A_BRᵀ,  A_RR ← A_RR − A_RB A_BB⁻¹ A_BR,
+//     and after all NB steps A = −Ky⁻¹ (Goodnight's sweep, blocked).  With A_BB = L_B L_Bᵀ the update is
+//     taken in its Cholesky form, A_RR −= W_Rᵀ W_R with W = L_B⁻¹ A_BR (the error of W grows with
+//     cond(L_B) = cond(A_BB)^½; the form A_RB (A_BB⁻¹ A_BR) lost digits against scikit-learn on the
+//     ill-conditioned K of a BO loop).  Step p:
+//       (A) wave 0 factors the 16×16 diagonal tile in registers, one column per lane, the pivot column's
+//           entries as wave-uniform v_readlane values; the pivots L_kk² are those of right-looking
+//           Cholesky/LDLᵀ (log|Ky| = Σ log d_k, the positive-definiteness test !(d_k > 0) and GPy jitchol's
+//           jitter retries as before); then L_B⁻¹ (lane c solves L x = e_c);
+//       (B) wave J forms W_J = L_B⁻¹ A_BJ and V_J = L_B⁻ᵀ W_J = A_BB⁻¹ A_BJ on FP64 MFMA (wave p:
+//           V_p = L_B⁻ᵀ L_B⁻¹ = A_BB⁻¹) and stores W_J over A_BJ;
+//       (C) wave J updates its column's lower tiles A_IJ −= W_Iᵀ W_J (I ≥ J) on FP64 MFMA (4 k-steps, W_J
+//           in the B-fragment layout already), mirrored into A_JI;
+//       (D) wave J writes the panel tiles A_BJ = V_J, A_JB = V_Jᵀ; wave p the diagonal tile −A_BB⁻¹.
+//     Three barriers per 16 pivots (the 2-pivot scalar sweep this replaced needed n/2 barriers and n³/2
+//     scalar LDS updates: 0.18 ms at n = 96 against 0.24 ms for the multi-launch path at n = 128).  Every
+//     update keeps A exactly symmetric (products formed symmetrically, tiles mirrored).
 //   * α = Ky⁻¹y, then ½ Σ_ik W_ik ∂K_ik/∂θ with W = ααᵀ − Ky⁻¹ over the full matrix (the same sums as
 //     gp_grad_kernel), all reductions in a fixed order (deterministic).
 // out[0..DP] gradient, out[DP+1] = Σ log L_ii, out[DP+2] = yᵀα, out[DP+3] = jitter, out[DP+4] = info
 // (0, or the 1-based column of the failed pivot after the last retry).
 constexpr int kSmallFitN = 128;
-constexpr int kSmallFitLD = kSmallFitN + 1;
-constexpr int kSmallFitThreads = 1024;
-constexpr int kSmallFitMax = 96;    // above this the blocked multi-launch path is faster (see gp_lml_small_fits)
+constexpr int kSmallFitLD = 136;    // row pitch (doubles) of the LDS copy of Ky
+constexpr int kSmallFitThreads = 512;
+constexpr int kSmallFitMax = 128;
 constexpr int kSmallFitXs = 1024;   // LDS doubles for X/ℓ: n·DP ≤ 1024 (d ≤ 8 at n = 128)
 
 struct FitLs {
@@ -935,19 +947,30 @@ __device__ __forceinline__ void fit_pair(const double* __restrict__ a, const dou
   }
 }
 
-// Thread map: wave w owns rows i ≡ w (mod 16), lane l owns columns l and l + 64.
-template <int DP, int KIND>
+// Phase timestamps of the block sweep for tools/ablate/ablate_gpfit (empty here): OMB_FIT_TRACE(p, id).
+#ifndef OMB_FIT_TRACE
+#define OMB_FIT_TRACE(p, id)
+#endif
+
+// Thread map of the K build / gradient: wave w owns rows i ≡ w (mod NW), lane l owns columns l and l + 64.
+// ABL (tools/ablate/ablate_gpfit only): bit 1 skips the block sweep, bit 2 the gradient sums, bit 4 the
+// kernel evaluations of the K build.
+template <int DP, int KIND, int ABL = 0>
 __device__ __forceinline__ void gp_lml_small_body(const double* __restrict__ X, int d, int n, const FitLs& ls,
                                                   double variance, double base, const double* __restrict__ y,
                                                   double* __restrict__ out) {
   constexpr int NW = kSmallFitThreads / 64, LD = kSmallFitLD, RPW = kSmallFitN / NW;
   __shared__ double A[kSmallFitN * LD];
   __shared__ double xs[kSmallFitXs];
-  __shared__ double col[2][2][kSmallFitN];   // [buffer][pivot column k, k+1][row]
+  __shared__ double Ls[16 * 17];                   // L_B⁻¹ (inverse Cholesky factor of the pivot block)
+  __shared__ double Lf[16 * 17];                   // L_B
   __shared__ double piv[kSmallFitN], alpha[kSmallFitN];
   __shared__ double red[NW][DP + 3];
+  __shared__ int flag;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int NB = (n + 15) >> 4, np = 16 * NB;     // padded size: Ky ⊕ I
+  const int c16 = lane & 15, g4 = lane >> 4;      // MFMA fragment coordinates
   for (int e = tid; e < n * DP; e += kSmallFitThreads) {
     const int i = e / DP, j = e - i * DP;
     xs[e] = (j < d) ? X[i * d + j] / ls.v[j] : 0.0;
@@ -963,17 +986,6 @@ __device__ __forceinline__ void gp_lml_small_body(const double* __restrict__ X, 
       b1[q] = h1 ? xs[j1 * DP + q] : 0.0;
     }
   };
-  // the sweep updates the lower triangle only: thread t owns packed entries e = t + 1024·q
-  constexpr int kPairs = (kSmallFitN * (kSmallFitN + 1) / 2 + kSmallFitThreads - 1) / kSmallFitThreads;
-  int pij[kPairs];   // i << 8 | j, or −1
-#pragma unroll
-  for (int q = 0; q < kPairs; ++q) {
-    const int e = tid + kSmallFitThreads * q;
-    int i = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
-    while (i * (i + 1) / 2 > e) --i;
-    while ((i + 1) * (i + 2) / 2 <= e) ++i;
-    pij[q] = (i < n) ? (i << 8 | (e - i * (i + 1) / 2)) : -1;
-  }
   const double mean_diag = variance + base;
   int bad = 0;
   double jit = 0.0;
@@ -981,106 +993,181 @@ __device__ __forceinline__ void gp_lml_small_body(const double* __restrict__ X, 
     jit = (t < 0) ? 0.0 : mean_diag * 1e-6 * pow(10.0, (double)t);
     double b0[DP], b1[DP];
     load_cols(b0, b1);
-#pragma unroll 2
     for (int m = 0; m < RPW; ++m) {
       const int i = wave + NW * m;
-      if (i >= n) break;
+      if (i >= np) break;
+      if (i >= n) {                                 // padding rows: the identity block
+        if (j0 < np) A[i * LD + j0] = (i == j0) ? 1.0 : 0.0;
+        if (j1 < np) A[i * LD + j1] = (i == j1) ? 1.0 : 0.0;
+        continue;
+      }
       double K, dkr;
+      if constexpr ((ABL & 4) != 0) {
+        if (j0 < np) A[i * LD + j0] = (i == j0) ? 2.0 : 0.0;
+        if (j1 < np) A[i * LD + j1] = (i == j1) ? 2.0 : 0.0;
+        continue;
+      }
       if (h0) {
         fit_pair<DP, KIND>(xs + i * DP, b0, i == j0, variance, K, dkr);
         A[i * LD + j0] = (i == j0) ? K + (base + jit) : K;
+      } else if (j0 < np) {
+        A[i * LD + j0] = 0.0;
       }
       if (h1) {
         fit_pair<DP, KIND>(xs + i * DP, b1, i == j1, variance, K, dkr);
         A[i * LD + j1] = (i == j1) ? K + (base + jit) : K;
+      } else if (j1 < np) {
+        A[i * LD + j1] = 0.0;
       }
-    }
-    __syncthreads();
-    if (tid < n) {
-      col[0][0][tid] = A[tid * LD];                                    // column 0
-      if (n > 1) col[0][1][tid] = A[max(tid, 1) * LD + min(tid, 1)];   // column 1
     }
     __syncthreads();
     bad = 0;
-    // two pivots per barrier: sweeping k then k+1, written as the two sequential sweeps' arithmetic
-    // (t = c1/a, u = c2 − b·t = column k+1 after sweep k, d2 = c − b²/a) for their stability
-    int k = 0;
-    for (; k + 1 < n; k += 2) {
-      const double* C1 = col[(k >> 1) & 1][0];
-      const double* C2 = col[(k >> 1) & 1][1];
-      double* N1 = col[((k >> 1) + 1) & 1][0];
-      double* N2 = col[((k >> 1) + 1) & 1][1];
-      const double a = C1[k], b = C1[k + 1], c = C2[k + 1];
-      if (!(a > 0.0)) {   // uniform: every thread read the same pivots
-        bad = k + 1;
-        break;
-      }
-      double ia = __builtin_amdgcn_rcp(a);
-      ia = fma(ia, fma(-a, ia, 1.0), ia);
-      ia = fma(ia, fma(-a, ia, 1.0), ia);
-      const double ba = b * ia;
-      const double d2 = fma(-b, ba, c);
-      if (!(d2 > 0.0)) {
-        bad = k + 2;
-        break;
-      }
-      double id2 = __builtin_amdgcn_rcp(d2);
-      id2 = fma(id2, fma(-d2, id2, 1.0), id2);
-      id2 = fma(id2, fma(-d2, id2, 1.0), id2);
-      const double gk = ba * id2;
-      if (tid == 0) {
-        piv[k] = a;
-        piv[k + 1] = d2;
-      }
+    // fragment layout of a 16×16 tile in one wave: element (r, c) in lane ((r & 3) << 4) + c, register r >> 2
+    // (the FP64 MFMA accumulator layout: register e holds rows 4e + (lane >> 4))
+    for (int p = 0; p < ((ABL & 1) ? 0 : NB); ++p) {
+      const int p16 = 16 * p;
+      // (A) wave 0, lanes 0-15: lane c holds column c of the diagonal tile (the current Schur complement) in
+      //     16 registers; right-looking Cholesky with the column-k entries as wave-uniform values (v_readlane),
+      //     then L_B⁻¹ column by column (lane c solves L x = e_c), written to Ls.
+      if (wave == 0) {
+        const int c = lane & 15;
+        double col[16];
 #pragma unroll
-      for (int q = 0; q < kPairs; ++q) {
-        if (pij[q] < 0) continue;
-        const int i = pij[q] >> 8, j = pij[q] & 255;
-        const double ti = C1[i] * ia, tj = C1[j] * ia;
-        const double ui = fma(-b, ti, C2[i]), uj = fma(-b, tj, C2[j]);
-        const double vi = ui * id2;
-        const bool iK = (i == k) || (i == k + 1), jK = (j == k) || (j == k + 1);
-        double v = fma(-vi, uj, fma(-ti, C1[j], A[i * LD + j]));
-        if (!iK && j == k) v = fma(-ui, gk, ti);
-        if (!iK && j == k + 1) v = vi;
-        if (i == k && !jK) v = fma(-uj, gk, tj);
-        if (i == k + 1 && !jK) v = uj * id2;
-        if (i == k && j == k) v = fma(-ba, gk, -ia);
-        if (i == k + 1 && j == k) v = gk;
-        if (i == k + 1 && j == k + 1) v = -id2;
-        A[i * LD + j] = v;
-        if (j == k + 2) N1[i] = v;
-        if (i == k + 2) N1[j] = v;
-        if (j == k + 3) N2[i] = v;
-        if (i == k + 3) N2[j] = v;
-      }
-      __syncthreads();
-    }
-    if (!bad && k < n) {   // odd n: the last pivot alone (its column is in buffer slot 0)
-      const double* C = col[(k >> 1) & 1][0];
-      const double dk = C[k];
-      if (!(dk > 0.0)) {
-        bad = k + 1;
-      } else {
-        double ip = __builtin_amdgcn_rcp(dk);
-        ip = fma(ip, fma(-dk, ip, 1.0), ip);
-        ip = fma(ip, fma(-dk, ip, 1.0), ip);
-        if (tid == 0) piv[k] = dk;
+        for (int r = 0; r < 16; ++r) col[r] = A[(p16 + r) * LD + p16 + c];
+        double ild[16];
+        int fail = 0;
 #pragma unroll
-        for (int q = 0; q < kPairs; ++q) {
-          if (pij[q] < 0) continue;
-          const int i = pij[q] >> 8, j = pij[q] & 255;
-          const double ci = C[i] * ip, cj = C[j];
-          double v = fma(-ci, cj, A[i * LD + j]);
-          if (j == k) v = ci;
-          if (i == k) v = (j == k) ? -ip : cj * ip;
-          A[i * LD + j] = v;
+        for (int k = 0; k < 16; ++k) {
+          const double dkk = readlane_f64(col[k], k);
+          ild[k] = 0.0;
+          if (fail) continue;
+          if (!(dkk > 0.0)) {                       // uniform
+            fail = p16 + k + 1;
+            continue;
+          }
+          const double lkk = sqrt_nonneg(dkk);
+          double il = __builtin_amdgcn_rcp(lkk);
+          il = fma(il, fma(-lkk, il, 1.0), il);
+          il = fma(il, fma(-lkk, il, 1.0), il);
+          ild[k] = il;
+          const double lck = (c > k) ? col[k] * il : 0.0;                       // L[c][k] (lanes c > k)
+#pragma unroll
+          for (int r = k + 1; r < 16; ++r) {
+            const double lrk = readlane_f64(col[r], k) * il;      // L[r][k]
+            col[r] = fma(-lrk, lck, col[r]);                                     // D[r][c] (symmetric update)
+          }
+          if (c == k) {
+#pragma unroll
+            for (int r = k + 1; r < 16; ++r) col[r] *= il;
+            col[k] = lkk;
+          }
+          if (lane == 0) piv[p16 + k] = dkk;
+        }
+        if (lane == 0) flag = fail;
+        OMB_FIT_TRACE(p, 1);
+        if (!fail) {
+          // x = L_B⁻¹ e_c: x[m] = acc[m] / L[m][m], acc[r] −= L[r][m] x[m] (r > m); L[r][m] as an LDS
+          // broadcast (one wave: its LDS accesses complete in order)
+          if (lane < 16) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) Lf[r * 17 + c] = col[r];
+          }
+          double x[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) x[r] = (r == c) ? 1.0 : 0.0;
+#pragma unroll
+          for (int m = 0; m < 16; ++m) {
+            x[m] *= ild[m];
+#pragma unroll
+            for (int r = m + 1; r < 16; ++r) x[r] = fma(-Lf[r * 17 + m], x[m], x[r]);
+          }
+          if (lane < 16) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) Ls[r * 17 + c] = x[r];                  // L_B⁻¹[r][c]
+          }
         }
       }
+      OMB_FIT_TRACE(p, 2);
       __syncthreads();
+      OMB_FIT_TRACE(p, 3);
+      bad = flag;
+      if (bad) break;
+      // (B) wave J ≠ p: W_J = L_B⁻¹ A_BJ and V_J = L_B⁻ᵀ W_J = A_BB⁻¹ A_BJ on FP64 MFMA (W_J's accumulator is
+      //     the B fragment of the second product and of the trailing update); W_J replaces A_BJ in LDS.
+      //     Wave p: V_p = L_B⁻ᵀ L_B⁻¹ = A_BB⁻¹.
+      const int J = wave;
+      const bool active = J < NB;
+      double W[4], V[4];
+      if (active) {
+        d4 w = d4{0.0, 0.0, 0.0, 0.0};
+        if (J != p) {
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+            w = __builtin_amdgcn_mfma_f64_16x16x4f64(Ls[c16 * 17 + 4 * s + g4], A[(p16 + 4 * s + g4) * LD + 16 * J + c16],
+                                                    w, 0, 0, 0);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) w[e] = Ls[(4 * e + g4) * 17 + c16];
+        }
+        d4 v = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          v = __builtin_amdgcn_mfma_f64_16x16x4f64(Ls[(4 * s + g4) * 17 + c16], w[s], v, 0, 0, 0);   // (L⁻ᵀ)[c16][4s+g4]
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          W[e] = w[e];
+          V[e] = v[e];
+        }
+        if (J != p) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) A[(p16 + 4 * e + g4) * LD + 16 * J + c16] = W[e];
+        }
+      }
+      OMB_FIT_TRACE(p, 4);
+      __syncthreads();
+      OMB_FIT_TRACE(p, 5);
+      // (C) wave J ≠ p: its column's lower trailing tiles, A_IJ −= W_Iᵀ W_J (I ≥ J), mirrored into A_JI
+      if (active && J != p) {
+        for (int I = J; I < NB; ++I) {
+          if (I == p) continue;
+          d4 T;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) T[e] = A[(16 * I + 4 * e + g4) * LD + 16 * J + c16];
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            const double a = -A[(p16 + 4 * s + g4) * LD + 16 * I + c16];   // −W_I[4s + g4][c16]
+            T = __builtin_amdgcn_mfma_f64_16x16x4f64(a, W[s], T, 0, 0, 0);
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 4 * e + g4;
+            if (I != J || r >= c16) {               // diagonal tile: the lower half, mirrored
+              A[(16 * I + r) * LD + 16 * J + c16] = T[e];
+              A[(16 * J + c16) * LD + 16 * I + r] = T[e];
+            }
+          }
+        }
+      }
+      OMB_FIT_TRACE(p, 6);
+      __syncthreads();
+      OMB_FIT_TRACE(p, 7);
+      // (D) the panel A_BJ = V_J, A_JB = V_Jᵀ, and the diagonal tile −A_BB⁻¹ (lower half, mirrored)
+      if (active) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * e + g4;
+          if (J != p) {
+            A[(p16 + r) * LD + 16 * J + c16] = V[e];
+            A[(16 * J + c16) * LD + p16 + r] = V[e];
+          } else if (r >= c16) {
+            A[(p16 + r) * LD + p16 + c16] = -V[e];
+            A[(p16 + c16) * LD + p16 + r] = -V[e];
+          }
+        }
+      }
     }
-    if (!bad) break;
     __syncthreads();
+    if (!bad) break;
   }
   if (bad) {
     if (tid == 0) {
@@ -1095,8 +1182,8 @@ __device__ __forceinline__ void gp_lml_small_body(const double* __restrict__ X, 
   for (int m = 0; m < RPW; ++m) {
     const int i = wave + NW * m;
     if (i >= n) break;
-    double s = h0 ? A[max(i, j0) * LD + min(i, j0)] * y0 : 0.0;
-    if (h1) s = fma(A[max(i, j1) * LD + min(i, j1)], y1, s);
+    double s = h0 ? A[i * LD + j0] * y0 : 0.0;
+    if (h1) s = fma(A[i * LD + j1], y1, s);
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
     if (lane == 0) alpha[i] = -s;
@@ -1108,7 +1195,7 @@ __device__ __forceinline__ void gp_lml_small_body(const double* __restrict__ X, 
   const double al0 = h0 ? alpha[j0] : 0.0, al1 = h1 ? alpha[j1] : 0.0;
   double b0[DP], b1[DP];
   load_cols(b0, b1);
-  for (int m = 0; m < RPW; ++m) {
+  for (int m = 0; m < ((ABL & 2) ? 0 : RPW); ++m) {
     const int i = wave + NW * m;
     if (i >= n) break;
     const double* a = xs + i * DP;
@@ -1119,7 +1206,7 @@ __device__ __forceinline__ void gp_lml_small_body(const double* __restrict__ X, 
       const int k = h == 0 ? j0 : j1;
       double K, dkr;
       fit_pair<DP, KIND>(a, h == 0 ? b0 : b1, i == k, variance, K, dkr);
-      const double W = 0.5 * (ai * (h == 0 ? al0 : al1) + A[max(i, k) * LD + min(i, k)]);   // ½ (ααᵀ − Ky⁻¹)
+      const double W = 0.5 * (ai * (h == 0 ? al0 : al1) + A[i * LD + k]);   // ½ (ααᵀ − Ky⁻¹)
       acc[0] = fma(W, K, acc[0]);
       const double wd = W * (-dkr);
 #pragma unroll
@@ -1170,21 +1257,19 @@ struct FitBatch {
   double variance[kFitBatchMax];
 };
 
-template <int DP, int KIND>
+template <int DP, int KIND, int ABL = 0>
 __global__ __launch_bounds__(kSmallFitThreads) void gp_lml_small_batch_kernel(const double* __restrict__ X, int d,
                                                                               int n, FitBatch b, double base) {
   const int p = blockIdx.x;
   FitLs ls;
 #pragma unroll
   for (int j = 0; j < OMB_MAX_DIM; ++j) ls.v[j] = j < 8 ? b.ls[p][j] : 1.0;
-  gp_lml_small_body<DP, KIND>(X, d, n, ls, b.variance[p], base, b.y[p], b.out[p]);
+  gp_lml_small_body<DP, KIND, ABL>(X, d, n, ls, b.variance[p], base, b.y[p], b.out[p]);
 }
 
 // DP ≤ 8: the two candidate columns' scaled coordinates stay in registers (DP = 16 spills at 1024 threads).
-// n ≤ 96: the sweep is one CU's work, n/2 steps of n²/2 entries with a barrier each; measured per evaluation
-// (tools/bench_gpfit.py, profiles/r01_v20_gpfit.jsonl) 0.076 / 0.10 / 0.18 / 0.32 ms at n = 32 / 64 / 96 / 128
-// against 0.25 ms for the blocked multi-launch path at n = 128 (one pivot per barrier: 0.33 ms at n = 128,
-// so the barriers are not what limits it: the sweep touches every entry at every step, n³/2 updates).
+// n ≤ 128: Ky and its block sweep fit one CU's LDS (the scalar 2-pivot sweep this replaced took 0.18 ms at
+// n = 96 and lost to the multi-launch path above n = 96).
 bool gp_lml_small_fits(int n, int DP) { return n >= 1 && n <= kSmallFitMax && DP <= 8 && n * DP <= kSmallFitXs; }
 
 hipError_t launch_gp_lml_small(hipStream_t stream, int kind, int DP, const double* X, int d, int n,

@@ -272,12 +272,12 @@ class _LbfgsbRun:
 
 
 def _one_launch(n, d):
-    """omb_gp_lml_grad_batch's one-launch case (gp_lml_small_fits: n ≤ 96, padded n_var ≤ 8)."""
+    """omb_gp_lml_grad_batch's one-launch case (gp_lml_small_fits: n ≤ 128, padded n_var ≤ 8)."""
     dp = 2 if d <= 2 else (4 if d <= 4 else (6 if d <= 6 else (8 if d <= 8 else 16)))
-    return n <= 96 and dp <= 8 and n * dp <= 1024
+    return n <= 128 and dp <= 8 and n * dp <= 1024
 
 
-# Above n = 96 an evaluation is the blocked multi-launch path (≈ 0.26 ms at n = 119, mostly device time),
+# Above n = 128 an evaluation is the blocked multi-launch path (≈ 0.26 ms at n = 119, mostly device time),
 # which two host threads with their own context and stream do overlap (profiles/r02_v64_threads_probe.txt:
 # 1.6× at n = 96); the round's problems then go to pool threads, each through omb_gp_lml_grad.
 _FIT_POOL = None

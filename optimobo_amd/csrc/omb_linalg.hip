@@ -902,8 +902,8 @@ __global__ __launch_bounds__(256) void gp_reduce_kernel(const double* __restrict
 //           jitter retries as before); then L_B⁻¹ (lane c solves L x = e_c);
 //       (B) wave J forms W_J = L_B⁻¹ A_BJ and V_J = L_B⁻ᵀ W_J = A_BB⁻¹ A_BJ on FP64 MFMA (wave p:
 //           V_p = L_B⁻ᵀ L_B⁻¹ = A_BB⁻¹) and stores W_J over A_BJ;
-//       (C) wave J updates its column's lower tiles A_IJ −= W_Iᵀ W_J (I ≥ J) on FP64 MFMA (4 k-steps, W_J
-//           in the B-fragment layout already), mirrored into A_JI;
+//       (C) the lower trailing tiles A_IJ −= W_Iᵀ W_J (I ≥ J) on FP64 MFMA (4 k-steps), dealt over all
+//           waves, mirrored into A_JI;
 //       (D) wave J writes the panel tiles A_BJ = V_J, A_JB = V_Jᵀ; wave p the diagonal tile −A_BB⁻¹.
 //     Three barriers per 16 pivots (the 2-pivot scalar sweep this replaced needed n/2 barriers and n³/2
 //     scalar LDS updates: 0.18 ms at n = 96 against 0.24 ms for the multi-launch path at n = 128).  Every
@@ -945,6 +945,25 @@ __device__ __forceinline__ void fit_pair(const double* __restrict__ a, const dou
     K = variance * e;
     dkr = -variance * e;
   }
+}
+
+// Lane k of each 16-lane row, to every lane of that row (DPP row_newbcast, gfx90a+), for a double; k must
+// be a compile-time constant after unrolling (the switch folds away).
+__device__ __forceinline__ double row_bcast_f64(double v, int k) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  int rl = lo, rh = hi;
+  switch (k) {
+#define OMB_RB(K)                                                       \
+  case K:                                                               \
+    rl = __builtin_amdgcn_update_dpp(0, lo, 0x150 + K, 0xf, 0xf, false); \
+    rh = __builtin_amdgcn_update_dpp(0, hi, 0x150 + K, 0xf, 0xf, false); \
+    break;
+    OMB_RB(0) OMB_RB(1) OMB_RB(2) OMB_RB(3) OMB_RB(4) OMB_RB(5) OMB_RB(6) OMB_RB(7)
+    OMB_RB(8) OMB_RB(9) OMB_RB(10) OMB_RB(11) OMB_RB(12) OMB_RB(13) OMB_RB(14) OMB_RB(15)
+#undef OMB_RB
+    default: break;
+  }
+  return __hiloint2double(rh, rl);
 }
 
 // Phase timestamps of the block sweep for tools/ablate/ablate_gpfit (empty here): OMB_FIT_TRACE(p, id).
@@ -1026,52 +1045,67 @@ __device__ __forceinline__ void gp_lml_small_body(const double* __restrict__ X, 
     // (the FP64 MFMA accumulator layout: register e holds rows 4e + (lane >> 4))
     for (int p = 0; p < ((ABL & 1) ? 0 : NB); ++p) {
       const int p16 = 16 * p;
-      // (A) wave 0, lanes 0-15: lane c holds column c of the diagonal tile (the current Schur complement) in
-      //     16 registers; right-looking Cholesky with the column-k entries as wave-uniform values (v_readlane),
-      //     then L_B⁻¹ column by column (lane c solves L x = e_c), written to Ls.
+      // (A) wave 0: Cholesky of the diagonal tile (the current Schur complement) in the fragment layout:
+      //     the pivot by v_readlane, the pivot column's entries of a lane's 4 rows by DPP row_newbcast (lane k
+      //     of each 16-lane row), the pivot row's entry of its column by one shuffle issued ahead of the
+      //     pivot (off the dependent chain); then L_B⁻¹ with lane c solving L x = e_c (L from LDS).
       if (wave == 0) {
-        const int c = lane & 15;
-        double col[16];
+        double D[4];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) col[r] = A[(p16 + r) * LD + p16 + c];
+        for (int e = 0; e < 4; ++e) D[e] = A[(p16 + 4 * e + g4) * LD + p16 + c16];
         double ild[16];
         int fail = 0;
+        // look-ahead: the next pivot and the next pivot row's entry of this lane's column are formed from
+        // values read before the current update (x = D[k+1][k], the row k+1 shuffled ahead), with the same
+        // expressions as the element update, so the dependent chain per pivot is sqrt, rcp and one fma
+        double dk = readlane_f64(D[0], 0);                                       // D[0][0]
+        double rowk = __shfl(D[0], c16);                                         // D[0][c]
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
-          const double dkk = readlane_f64(col[k], k);
+          double x = 0.0, dn = 0.0, rown = 0.0;
+          if (k < 15) {
+            const int k1 = k + 1;
+            x = readlane_f64(D[k1 >> 2], ((k1 & 3) << 4) + k);                  // D[k+1][k]
+            dn = readlane_f64(D[k1 >> 2], ((k1 & 3) << 4) + k1);                // D[k+1][k+1]
+            rown = __shfl(D[k1 >> 2], ((k1 & 3) << 4) + c16);                   // D[k+1][c], before this update
+          }
           ild[k] = 0.0;
           if (fail) continue;
-          if (!(dkk > 0.0)) {                       // uniform
+          if (!(dk > 0.0)) {                        // uniform
             fail = p16 + k + 1;
             continue;
           }
-          const double lkk = sqrt_nonneg(dkk);
+          const double lkk = sqrt_nonneg(dk);
           double il = __builtin_amdgcn_rcp(lkk);
           il = fma(il, fma(-lkk, il, 1.0), il);
           il = fma(il, fma(-lkk, il, 1.0), il);
           ild[k] = il;
-          const double lck = (c > k) ? col[k] * il : 0.0;                       // L[c][k] (lanes c > k)
+          const double il2 = il * il;
 #pragma unroll
-          for (int r = k + 1; r < 16; ++r) {
-            const double lrk = readlane_f64(col[r], k) * il;      // L[r][k]
-            col[r] = fma(-lrk, lck, col[r]);                                     // D[r][c] (symmetric update)
+          for (int e = 0; e < 4; ++e) {
+            const int r = 4 * e + g4;
+            const double colk = row_bcast_f64(D[e], k);                          // D[r][k]
+            double v = D[e];
+            if (r > k && c16 > k) v = fma(-(colk * rowk), il2, v);               // symmetric in (r, c)
+            if (c16 == k) v = (r > k) ? colk * il : (r == k ? lkk : 0.0);
+            if (r == k && c16 > k) v = 0.0;
+            D[e] = v;
           }
-          if (c == k) {
-#pragma unroll
-            for (int r = k + 1; r < 16; ++r) col[r] *= il;
-            col[k] = lkk;
+          if (lane == 0) piv[p16 + k] = dk;
+          if (k < 15) {
+            const double dnext = fma(-(x * x), il2, dn);                          // = the updated D[k+1][k+1]
+            rowk = fma(-(x * rowk), il2, rown);                                   // = the updated D[k+1][c] (c > k+1)
+            dk = dnext;
           }
-          if (lane == 0) piv[p16 + k] = dkk;
         }
         if (lane == 0) flag = fail;
         OMB_FIT_TRACE(p, 1);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) Lf[(4 * e + g4) * 17 + c16] = D[e];
+        const int c = lane & 15;
         if (!fail) {
           // x = L_B⁻¹ e_c: x[m] = acc[m] / L[m][m], acc[r] −= L[r][m] x[m] (r > m); L[r][m] as an LDS
           // broadcast (one wave: its LDS accesses complete in order)
-          if (lane < 16) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) Lf[r * 17 + c] = col[r];
-          }
           double x[16];
 #pragma unroll
           for (int r = 0; r < 16; ++r) x[r] = (r == c) ? 1.0 : 0.0;
@@ -1126,24 +1160,32 @@ __device__ __forceinline__ void gp_lml_small_body(const double* __restrict__ X, 
       OMB_FIT_TRACE(p, 4);
       __syncthreads();
       OMB_FIT_TRACE(p, 5);
-      // (C) wave J ≠ p: its column's lower trailing tiles, A_IJ −= W_Iᵀ W_J (I ≥ J), mirrored into A_JI
-      if (active && J != p) {
-        for (int I = J; I < NB; ++I) {
-          if (I == p) continue;
+      // (C) the lower trailing tiles (I ≥ J, both ≠ p) dealt over all waves: A_IJ −= W_Iᵀ W_J on FP64 MFMA,
+      //     both operands from the W tiles in LDS, mirrored into A_JI
+      {
+        const int nt = (NB - 1) * NB / 2;           // lower tiles of the (NB−1)-block trailing matrix
+        for (int t2 = wave; t2 < nt; t2 += NW) {
+          // t2 → (i, j) over 0 ≤ j ≤ i < NB − 1, then skip the pivot block
+          int i = (int)((sqrt(8.0 * t2 + 1.0) - 1.0) * 0.5);
+          while (i * (i + 1) / 2 > t2) --i;
+          while ((i + 1) * (i + 2) / 2 <= t2) ++i;
+          const int j = t2 - i * (i + 1) / 2;
+          const int I = i + (i >= p), Jt = j + (j >= p);
           d4 T;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) T[e] = A[(16 * I + 4 * e + g4) * LD + 16 * J + c16];
+          for (int e = 0; e < 4; ++e) T[e] = A[(16 * I + 4 * e + g4) * LD + 16 * Jt + c16];
 #pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            const double a = -A[(p16 + 4 * s + g4) * LD + 16 * I + c16];   // −W_I[4s + g4][c16]
-            T = __builtin_amdgcn_mfma_f64_16x16x4f64(a, W[s], T, 0, 0, 0);
+          for (int q = 0; q < 4; ++q) {
+            const double a = -A[(p16 + 4 * q + g4) * LD + 16 * I + c16];    // −W_I[4q + g4][c16]
+            const double b = A[(p16 + 4 * q + g4) * LD + 16 * Jt + c16];    // W_J[4q + g4][c16]
+            T = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, T, 0, 0, 0);
           }
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int r = 4 * e + g4;
-            if (I != J || r >= c16) {               // diagonal tile: the lower half, mirrored
-              A[(16 * I + r) * LD + 16 * J + c16] = T[e];
-              A[(16 * J + c16) * LD + 16 * I + r] = T[e];
+            if (I != Jt || r >= c16) {              // diagonal tile: the lower half, mirrored
+              A[(16 * I + r) * LD + 16 * Jt + c16] = T[e];
+              A[(16 * Jt + c16) * LD + 16 * I + r] = T[e];
             }
           }
         }

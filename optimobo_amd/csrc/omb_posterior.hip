@@ -1226,7 +1226,8 @@ __global__ __launch_bounds__(512, 2) void posterior_tile_kernel(GPArgs args, con
 // meet only zeros), so the unrolled code has no wave-uniform control flow to merge around.
 // ABL (tools/ablate only): bit 1 stops after staging, bit 2 skips the multiply, bit 8 skips the
 // Matern transform (K* = r²), bit 16 drops the sqrt's residual correction, bit 32 scales by 2^m with
-// an integer exponent add instead of v_ldexp_f64.
+// an integer exponent add instead of v_ldexp_f64, bit 64 loads the next tile's coordinates during the current
+// tile (instead of at its start).
 template <int RMAX, int DP, int KIND, int NW = 8, bool XL = false, int ABL = 0>
 __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : NW / 4) void posterior_reg_kernel(
     GPArgs args, const double* __restrict__ Xc, int64_t N, double* __restrict__ mu_out, double* __restrict__ var_out) {
@@ -1286,7 +1287,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : NW / 4) void posterior_reg_k
   const d2* xf = XL ? reinterpret_cast<const d2*>(lds_X) + lane : reinterpret_cast<const d2*>(g.Xf) + lane;
   for (; t < ntiles; t += stride) {
     const int64_t c = 16 * t + (lane & 15);
-    if (t != first) load_raw(t, raw);
+    if constexpr ((ABL & 64) == 0)
+      if (t != first) load_raw(t, raw);
     // B fragment [−2·x*/ℓ, 1, ‖x*/ℓ‖²]: lane l needs dims 4s + (l>>4) only; ‖x*/ℓ‖² from the four
     // lane groups by two shuffles
     double xs[KSD], csq = 0.0;
@@ -1296,6 +1298,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : NW / 4) void posterior_reg_k
       xs[q] = (j < d) ? raw[q] / g.ls[j] : 0.0;
       csq = fma(xs[q], xs[q], csq);
     }
+    if constexpr ((ABL & 64) != 0)      // the next tile's coordinates in flight during this tile
+      if (t + stride < ntiles) load_raw(t + stride, raw);
     csq += __shfl_xor(csq, 16);
     csq += __shfl_xor(csq, 32);
     double bfr[KSD];

@@ -337,6 +337,8 @@ int main(int argc, char** argv) {
       {"reg 8 waves, Xf in LDS", run_reg<0, 8, true>},
 
       {"reg 16 waves 1 WG/CU Xf in LDS", run_reg<0, 16, true>},
+      {"reg16 prefetch next tile (64)", run_reg<64, 16, true>},
+      {"reg16 library again", run_reg<0, 16, true>},
       {"reg 12 waves gen only", run_reg<2, 12, true>},
       {"tile RMAX8 CT4 gen only (2)", run_tile<8, 4, 2>},
       {"tile RMAX8 CT4 const A (4)", run_tile<8, 4, 4>},

@@ -63,13 +63,17 @@ CONFIGS = {
     # BASELINE config 1: the README run end to end through the drop-in driver (host GP fit + device
     # maximiser) — reported as BO iterations/s with the time split, not a kernel benchmark
     1: dict(problem="myproblem", n=20, d=2, budget=100, acq="solve_tch"),
-    2: dict(problem="zdt1", n=128, d=6, log2=16, acq="ehvi2d"),
-    3: dict(problem="zdt1", n=512, d=6, log2=20, acq="ehvi2d"),
+    # configs 2, 3 and 5 train on x_1 in [0, 1], x_2..x_d in [0, 0.3] (tail_hi): a mid-run BO state whose
+    # evaluated points have drifted toward ZDT1's Pareto set (x_2..x_d = 0), so the acquisition's maximum is
+    # an interior candidate; over a training set spread through [0, 1]^d the unexplored corner x = 0 (Sobol
+    # index 0, ZDT1's extreme Pareto point) wins, which is also where the lowest-index tie rule lands
+    2: dict(problem="zdt1", n=128, d=6, log2=16, acq="ehvi2d", tail_hi=0.3),
+    3: dict(problem="zdt1", n=512, d=6, log2=20, acq="ehvi2d", tail_hi=0.3),
     # config 4's training set covers [0.5, 1]^6 (an early BO iteration: the front is still far from the
     # ideal point), so the reference's Monte-Carlo EHVI_3D is positive for ~17% of the candidates; over a
     # training set spread through [0, 1]^6 it is 0 everywhere
     4: dict(problem="dtlz2", n=256, d=6, log2=17, acq="ehvi3d", x_lo=0.5),
-    5: dict(problem="zdt1", n=1024, d=30, log2=19, acq="ei_tch"),
+    5: dict(problem="zdt1", n=1024, d=30, log2=19, acq="ei_tch", tail_hi=0.3),
     # not a BASELINE config: TuRBO's Thompson-sampling step (turbo.py:75-153) — one trust region,
     # n_cand = min(100·n_var, 5000) candidates, batch_size joint posterior draws, greedy arg-mins
     6: dict(problem="zdt1", n=512, d=30, n_cand=3000, draws=64, acq="thompson"),
@@ -77,12 +81,13 @@ CONFIGS = {
 METRIC = "EHVI candidate evals/sec at n_train=512, 2-obj; 1/2/4/8-GPU scaling"
 
 
-def setup_problem(n, d, seed=0, problem="zdt1", x_lo=0.0):
+def setup_problem(n, d, seed=0, problem="zdt1", x_lo=0.0, tail_hi=1.0):
     """Training set of a BASELINE config: n points uniform in [x_lo, 1]^d (numpy default_rng(seed)), the
-    problem's objectives, ARD length scales ℓ_j ~ U[0.2, 2] (default_rng(seed + 1)), σ_f² = Var(Y_k)
-    (SURVEY §8d)."""
+    coordinates x_2..x_d then scaled by tail_hi, the problem's objectives, ARD length scales ℓ_j ~ U[0.2, 2]
+    (default_rng(seed + 1)), σ_f² = Var(Y_k)."""
     rng = np.random.default_rng(seed)
     X = rng.uniform(x_lo, 1.0, (n, d))
+    X[:, 1:] *= tail_hi
     Y = zdt1(X) if problem == "zdt1" else dtlz2(X)
     ls = np.random.default_rng(seed + 1).uniform(0.2, 2.0, d)
     variances = [float(np.var(Y[:, o])) for o in range(Y.shape[1])]
@@ -131,7 +136,8 @@ def cpu_baseline(X, targets, ls, variances, Xc, acq_fn, label, seconds):
             break
     dt = time.perf_counter() - t0
     return {"value": done / dt, "unit": "candidates/s", "cores": threads, "host_cpu_count": ncpu, "kind": "port",
-            "sample": f"{done} of the {len(Xc)} candidates (chunks of {chunk}), oracle posterior (dtrtrs) + "
+            "sample": f"{done} candidate evaluations in chunks of {chunk}, cycling through the {len(Xc)}-candidate "
+                      f"batch; oracle posterior (dtrtrs) + "
                       f"{label} + arg-max, {dt:.1f} s; cores = numpy BLAS threads used (threadpoolctl)"}
 
 
@@ -454,7 +460,8 @@ def main():
 
     n, d, acq_kind = cfg["n"], cfg["d"], cfg["acq"]
     N = 1 << (args.log2_cand if args.log2_cand is not None else cfg["log2"])
-    X, Y, ls, variances = setup_problem(n, d, problem=cfg["problem"], x_lo=cfg.get("x_lo", 0.0))
+    X, Y, ls, variances = setup_problem(n, d, problem=cfg["problem"], x_lo=cfg.get("x_lo", 0.0),
+                                        tail_hi=cfg.get("tail_hi", 1.0))
     k_obj = Y.shape[1]
     pf = pareto.calc_pf(Y)
     r = Y.max(axis=0) + 0.1 * (Y.max(axis=0) - Y.min(axis=0))
@@ -669,6 +676,8 @@ def main():
                                    "arg-max is the lowest index among its maxima (DESIGN.md section 2, quirk 2)")
         if acq_kind == "ehvi3d":
             out["config"]["train_box"] = f"[{cfg['x_lo']}, 1]^{d}"
+        if "tail_hi" in cfg:
+            out["config"]["train_box"] = f"x_1 in [0, 1], x_2..x_{d} in [0, {cfg['tail_hi']}]"
         print(json.dumps(out))
     if world_size > 1:
         dist.barrier()

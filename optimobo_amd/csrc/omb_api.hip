@@ -974,8 +974,8 @@ static hipError_t cov_build(omb_ctx* ctx, const ObjState& s, const double* Xc, i
 
 // In-place lower Cholesky of A + jitter·I; synchronises and returns LAPACK's info in *info.
 static int run_cholesky(omb_ctx* ctx, double* A, int64_t N, int64_t lda, double jitter, int* info) {
-  // [info int | pad to 16 B | factor workspace (kCholWsDoubles)]
-  int rc = grow_dev(ctx, &ctx->ichol, &ctx->ichol_cap, 16 + sizeof(double) * kCholWsDoubles, "Cholesky workspace");
+  // [info int | pad to 16 B | factor workspace (chol_ws_doubles)]
+  int rc = grow_dev(ctx, &ctx->ichol, &ctx->ichol_cap, 16 + sizeof(double) * chol_ws_doubles(N), "Cholesky workspace");
   if (rc) return rc;
   int* dinfo = static_cast<int*>(ctx->ichol);
   double* ws = reinterpret_cast<double*>(static_cast<char*>(ctx->ichol) + 16);
@@ -985,6 +985,9 @@ static int run_cholesky(omb_ctx* ctx, double* A, int64_t N, int64_t lda, double 
   int h = 0;
   OMB_HIP(ctx, hipMemcpyAsync(&h, dinfo, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   OMB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (h == kCholSpinFault)
+    return fail(ctx, OMB_EHIP, "Cholesky: a workgroup's wait for the diagonal block exceeded %d polls; the factor is "
+                               "invalid", kCholSpinLimit);
   *info = h;
   return OMB_OK;
 }

@@ -319,6 +319,18 @@ constexpr int kLbP = 18;
 constexpr int kLbDoubles = 4 * kNB * kLbP;
 constexpr int kCholAux = 2 * kNB + kNB;
 
+// The W fragments are stored and (by the fused step's waiting workgroups) read as agent-scope relaxed
+// atomics: coherent across the XCDs' L2s without the L2 write-back / invalidate that an agent-scope
+// release / acquire fence costs (those fences cost more than the launch they were meant to save).
+__device__ __forceinline__ void wf_store(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), __builtin_bit_cast(unsigned long long, v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double wf_load(const double* p) {
+  return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT));
+}
+
 // Factor a 64×64 SPD block with the 4 waves of a 256-thread workgroup: thread (wave w, lane r) holds
 // a[q] = A[r][16w + q] (only 16w + q ≤ r is meaningful; rows past the block are identity rows).
 // Wave b factors sub-block b (columns 16b..16b+15).  Before its turn it applies every earlier
@@ -456,7 +468,7 @@ __device__ __forceinline__ void chol64_factor(double (&a)[16], int w, int r, int
     }
     // W_bb's fragments: rows jb = b, k-steps s = 4b + u: W[16b + c][16b + 4g + u]
 #pragma unroll
-    for (int u = 0; u < 4; ++u) Wf[(b * 16 + 4 * b + u) * 64 + r] = Lb[(b * 64 + 16 * b + c) * kLbP + 4 * g + u];
+    for (int u = 0; u < 4; ++u) wf_store(&Wf[(b * 16 + 4 * b + u) * 64 + r], Lb[(b * 64 + 16 * b + c) * kLbP + 4 * g + u]);
     OMB_CHOL_TRACE(10 + b, r == 0);
   });
 }
@@ -497,7 +509,7 @@ __device__ __forceinline__ void chol64_inverse(int w, int r, const double* Lb, d
       Wc[i] = -R;
       // W[16i + 4e + g][16w + c]: jb = i, s = 4w + (c & 3), lane 4e + g + 16 (c >> 2)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) Wf[(i * 16 + 4 * w + (c & 3)) * 64 + 4 * e + g + 16 * (c >> 2)] = Wc[i][e];
+      for (int e = 0; e < 4; ++e) wf_store(&Wf[(i * 16 + 4 * w + (c & 3)) * 64 + 4 * e + g + 16 * (c >> 2)], Wc[i][e]);
     }
   });
   OMB_CHOL_TRACE(16, w == 0 && r == 0);
@@ -592,14 +604,40 @@ __global__ __launch_bounds__(128) void chol_panel_kernel(double* __restrict__ A,
 // Trailing update of step `step` (A22 −= L21 L21ᵀ, lower 64×64 tiles, gemm_kernel's MFMA tiling with
 // K = 64) fused with the factorisation and inversion of the next diagonal block by the workgroup that
 // owns it.
+// One workgroup per lower tile of A22 (t tiles a side, t(t+1)/2 workgroups): workgroup 0 is the diagonal
+// tile (0, 0), workgroups 1 .. t−1 the tiles (m, 0) below it — the next step's panel rows — and the rest
+// the tiles (m, n), 1 ≤ n ≤ m, in row order.
+// FUSE (round 3): the workgroups of the tiles (m, 0) keep their updated tile in LDS, wait for the
+// diagonal workgroup to publish W_{k+1} = L_{k+1,k+1}⁻¹ (flags[step], set after the fragments are in the
+// workspace) and form the next step's panel rows L21 = A21 · Wᵀ themselves, so a step is one launch:
+// the panel's own launch (≈ 5 µs plus a launch gap per step at N = 3000) leaves the chain.  Workgroup 0
+// is dispatched first (in-order dispatch); the wait is bounded all the same (kCholSpinLimit polls, then
+// info = kCholSpinFault and the workgroup finishes), so a waiting workgroup can never hang the grid.
+__device__ __forceinline__ void chol_tile_of(int b, int t, int& mt, int& nt) {
+  if (b < t) {
+    mt = b;
+    nt = 0;
+    return;
+  }
+  const int q = b - t;                                       // tiles (m', n'), 0 ≤ n' ≤ m' ≤ t − 2
+  int mp = (int)((sqrt(8.0 * q + 1.0) - 1.0) * 0.5);
+  while ((mp + 1) * (mp + 2) / 2 <= q) ++mp;
+  while (mp * (mp + 1) / 2 > q) --mp;
+  mt = mp + 1;
+  nt = q - mp * (mp + 1) / 2 + 1;
+}
+
+template <bool FUSE>
 __global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A, int64_t N, int64_t lda, int step,
-                                                          double* __restrict__ ws, int* __restrict__ info) {
-  if (blockIdx.x > blockIdx.y) return;                      // tile strictly above the diagonal
+                                                          int t, double* __restrict__ ws, int* __restrict__ info,
+                                                          int* __restrict__ flags) {
   if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+  int mt, nt;
+  chol_tile_of((int)blockIdx.x, t, mt, nt);
   const int64_t c0 = (int64_t)step * kNB;
   const int64_t r0 = c0 + kNB;                              // first row / column of A22
   const int64_t M = N - r0;
-  const int64_t m0 = (int64_t)blockIdx.y * kGT, n0 = (int64_t)blockIdx.x * kGT;
+  const int64_t m0 = (int64_t)mt * kGT, n0 = (int64_t)nt * kGT;
   // one array: the GEMM's As and Bs, then (the diagonal workgroup) the 64 × 65 staging tile D, then
   // the factorisation's Lb
   static_assert(2 * 2 * kGK * kGP <= kLbDoubles && kNB * (kNB + 1) <= kLbDoubles, "LDS carve-up");
@@ -614,7 +652,7 @@ __global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A
   const int wm = wave >> 1, wn = wave & 1;
   const double* L21 = A + r0 * lda + c0;
   // the next diagonal block (A22's first tile) belongs to workgroup (0, 0)
-  if (!(blockIdx.x == 0 && blockIdx.y == 0)) {
+  if (!(mt == 0 && nt == 0)) {
     double ra[4], rb[4];
     auto fetch = [&](int k0) {
 #pragma unroll
@@ -663,6 +701,28 @@ __global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A
       buf ^= 1;
     }
     // C/D map of v_mfma_f64_16x16x4f64: col = lane & 15, row = (lane >> 4) + 4·i
+    if (!FUSE || nt != 0) {
+#pragma unroll
+      for (int rb2 = 0; rb2 < 2; ++rb2)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int lr = 32 * wm + 16 * rb2 + (lane >> 4) + 4 * i;
+            const int lc = 32 * wn + 16 * cb + (lane & 15);
+            const int64_t row = m0 + lr, col_g = n0 + lc;
+            if (row < M && col_g < M && col_g <= row) {
+              double* p = A + (r0 + row) * lda + r0 + col_g;
+              *p = *p - acc[rb2][cb][i];
+            }
+          }
+      return;
+    }
+    // FUSE, tile (m, 0): the updated tile (the next step's A21 rows) into LDS, D[lr·kPD + lc]; the
+    // GEMM loop ended on a barrier, so As/Bs are free
+    constexpr int kPD = kNB + 2;                              // 528-B rows: 16 lanes' b128 reads of 16 rows conflict-free
+    static_assert(kNB * kPD <= kLbDoubles, "LDS carve-up");
+    double* Dp = smem;
 #pragma unroll
     for (int rb2 = 0; rb2 < 2; ++rb2)
 #pragma unroll
@@ -671,12 +731,52 @@ __global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A
         for (int i = 0; i < 4; ++i) {
           const int lr = 32 * wm + 16 * rb2 + (lane >> 4) + 4 * i;
           const int lc = 32 * wn + 16 * cb + (lane & 15);
-          const int64_t row = m0 + lr, col_g = n0 + lc;
-          if (row < M && col_g < M && col_g <= row) {
-            double* p = A + (r0 + row) * lda + r0 + col_g;
-            *p = *p - acc[rb2][cb][i];
-          }
+          const int64_t row = m0 + lr;
+          Dp[lr * kPD + lc] = (row < M) ? A[(r0 + row) * lda + r0 + lc] - acc[rb2][cb][i] : 0.0;
         }
+    __syncthreads();
+    // W_{k+1}'s fragments: wait for the diagonal workgroup's flag (bounded); relaxed polls and coherent
+    // fragment loads (wf_load), no cache-wide invalidate
+    if (tid == 0) {
+      int polls = 0;
+      while (__hip_atomic_load(&flags[step], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+        if (++polls > kCholSpinLimit) {
+          atomicCAS(info, 0, kCholSpinFault);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    __syncthreads();
+    // the next step's panel rows, as chol_panel_kernel: wave w → rows 16w + (lane & 15) of the tile,
+    // all four output column blocks
+    {
+      const int c = lane & 15, g = lane >> 4;
+      double x[16];                                           // x[4sg + u] = D[16w + c][16sg + 4g + u]
+      const double* dr = Dp + (16 * wave + c) * kPD + 4 * g;
+#pragma unroll
+      for (int sg = 0; sg < 4; ++sg) {
+        const double2 v0 = reinterpret_cast<const double2*>(dr + 16 * sg)[0];
+        const double2 v1 = reinterpret_cast<const double2*>(dr + 16 * sg)[1];
+        x[4 * sg] = v0.x;
+        x[4 * sg + 1] = v0.y;
+        x[4 * sg + 2] = v1.x;
+        x[4 * sg + 3] = v1.y;
+      }
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) {
+        const double* wf = ws + jb * 16 * 64 + lane;
+        d4 pa = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2)
+          if (s2 < 4 * (jb + 1)) pa = __builtin_amdgcn_mfma_f64_16x16x4f64(x[s2], wf_load(wf + s2 * 64), pa, 0, 0, 0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int64_t orow = m0 + 16 * wave + 4 * e + g;
+          if (orow < M) A[(r0 + orow) * lda + r0 + 16 * jb + c] = pa[e];
+        }
+      }
+    }
     return;
   }
   // Diagonal workgroup: the tile's 64 L21 rows and its A22 values are loaded at once (one load latency
@@ -749,6 +849,13 @@ __global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A
   __syncthreads();
   if (tid == 0 && bad_lds[0]) atomicCAS(info, 0, (int)(r0 + bad_lds[0]));
   chol64_inverse(w, r, smem, ws);
+  if constexpr (FUSE) {
+    // publish W_{k+1} (also after a bad pivot: the waiting workgroups must finish; info marks the result):
+    // every thread's coherent fragment stores complete (vmcnt 0), then the flag
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(&flags[step], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // ----------------------------------------------------------------------------- triangular inverse
@@ -1569,26 +1676,55 @@ hipError_t launch_add_diag(hipStream_t stream, double* S, int64_t N, int64_t lds
   return hipGetLastError();
 }
 
-hipError_t launch_cholesky(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws) {
+int64_t chol_ws_doubles(int64_t N) {
+  const int64_t steps = (N + kNB - 1) / kNB;
+  return (int64_t)kCholWsDoubles + (steps + 1) / 2 + 2;     // W fragments | one int flag per step
+}
+
+static hipError_t chol_panel(hipStream_t stream, double* A, int64_t N, int64_t lda, int k, const double* ws,
+                             const int* info, bool vec) {
+  const int64_t rest = N - (int64_t)(k + 1) * kNB;          // rows below the diagonal block
+  const unsigned pblocks = (unsigned)((rest + 15) / 16);
+  if (vec)
+    hipLaunchKernelGGL((chol_panel_kernel<true>), dim3(pblocks), dim3(128), 0, stream, A, N, lda, k, ws, info);
+  else
+    hipLaunchKernelGGL((chol_panel_kernel<false>), dim3(pblocks), dim3(128), 0, stream, A, N, lda, k, ws, info);
+  return hipGetLastError();
+}
+
+hipError_t launch_cholesky_mode(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws, int mode) {
   if (N <= 0) return hipSuccess;
   const int steps = (int)((N + kNB - 1) / kNB);
   const bool vec = (lda % 2 == 0) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
+  const bool fuse = mode == kCholFused;
+  int* flags = reinterpret_cast<int*>(ws + kCholWsDoubles);
+  if (fuse && steps > 2) {
+    hipError_t e = hipMemsetAsync(flags, 0, sizeof(int) * steps, stream);
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), 0, stream, A, N, lda, ws, info);
   hipError_t e = hipGetLastError();
   for (int k = 0; k + 1 < steps && e == hipSuccess; ++k) {
-    const int64_t rest = N - (int64_t)(k + 1) * kNB;      // rows below the diagonal block
-    const unsigned pblocks = (unsigned)((rest + 15) / 16);
-    if (vec)
-      hipLaunchKernelGGL((chol_panel_kernel<true>), dim3(pblocks), dim3(128), 0, stream, A, N, lda, k, ws, info);
+    const int64_t rest = N - (int64_t)(k + 1) * kNB;
+    const int t = (int)((rest + kGT - 1) / kGT);
+    // fused: step k's panel came from step k−1's update launch (step 0's from its own launch)
+    if (!fuse || k == 0) {
+      e = chol_panel(stream, A, N, lda, k, ws, info, vec);
+      if (e != hipSuccess) break;
+    }
+    const unsigned wgs = (unsigned)(t * (t + 1) / 2);
+    if (fuse)
+      hipLaunchKernelGGL((chol_update_kernel<true>), dim3(wgs), dim3(256), 0, stream, A, N, lda, k, t, ws, info, flags);
     else
-      hipLaunchKernelGGL((chol_panel_kernel<false>), dim3(pblocks), dim3(128), 0, stream, A, N, lda, k, ws, info);
-    e = hipGetLastError();
-    if (e != hipSuccess) break;
-    const unsigned t = (unsigned)((rest + kGT - 1) / kGT);
-    hipLaunchKernelGGL(chol_update_kernel, dim3(t, t), dim3(256), 0, stream, A, N, lda, k, ws, info);
+      hipLaunchKernelGGL((chol_update_kernel<false>), dim3(wgs), dim3(256), 0, stream, A, N, lda, k, t, ws, info,
+                         flags);
     e = hipGetLastError();
   }
   return e;
+}
+
+hipError_t launch_cholesky(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws) {
+  return launch_cholesky_mode(stream, A, N, lda, info, ws, kCholFused);
 }
 
 // K slices of the sample product: enough (tile, slice) workgroups to fill the chip (≥ 1024), slices of

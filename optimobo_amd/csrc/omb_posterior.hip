@@ -1224,10 +1224,15 @@ __global__ __launch_bounds__(512, 2) void posterior_tile_kernel(GPArgs args, con
 // RMAX (2, 4 or 8 row tiles) is a compile-time bound with no branch on the actual R: rows past n are
 // zero in the staged L⁻¹ and α, and tiles T ≥ R reuse row tile R−1's fragments (finite values that
 // meet only zeros), so the unrolled code has no wave-uniform control flow to merge around.
+// Staging issues every load of the workgroup's share first (packed L⁻¹, Xf, α, the exp table: ≤ 8 per
+// thread) and writes LDS after one wait, so the prologue costs one memory round trip, not one per loop
+// trip and operand (the rolled loop waited vmcnt(0) after each of its 5 loads).  ℓ of the lane's B-fragment
+// dimensions sits in registers from the start, so the per-tile coordinate division no longer reloads it
+// (each reload's vmcnt(0) also drained the coordinate loads in flight).
 // ABL (tools/ablate only): bit 1 stops after staging, bit 2 skips the multiply, bit 8 skips the
 // Matern transform (K* = r²), bit 16 drops the sqrt's residual correction, bit 32 scales by 2^m with
 // an integer exponent add instead of v_ldexp_f64, bit 64 loads the next tile's coordinates during the current
-// tile (instead of at its start).
+// tile (instead of at its start), bit 128 stages with the round-2 rolled loops and reloads ℓ per tile.
 template <int RMAX, int DP, int KIND, int NW = 8, bool XL = false, int ABL = 0>
 __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : NW / 4) void posterior_reg_kernel(
     GPArgs args, const double* __restrict__ Xc, int64_t N, double* __restrict__ mu_out, double* __restrict__ var_out) {
@@ -1266,19 +1271,69 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : NW / 4) void posterior_reg_k
   };
   double raw[KSD];
   load_raw(t < ntiles ? t : 0, raw);
-  {
+  double lsr[KSD];                                  // ℓ of this lane's B-fragment dimensions
+#pragma unroll
+  for (int q = 0; q < KSD; ++q) {
+    const int j = 4 * q + (lane >> 4);
+    lsr[q] = (j < d) ? g.ls[j] : 1.0;
+  }
+  if constexpr ((ABL & 128) != 0) {
     const int nL2 = 64 * R * (R + 1);
     const d2* src = reinterpret_cast<const d2*>(g.Lp);
     d2* dst = reinterpret_cast<d2*>(lds_L);
     for (int i = tid; i < kL2; i += NT) dst[i] = i < nL2 ? src[i] : d2{0.0, 0.0};
     if constexpr (XL) {
-      const int nX2 = 64 * KSDP * R;                // row tiles past R repeat tile R−1 (see Tl below)
+      const int nX2 = 64 * KSDP * R;
       const d2* xs2 = reinterpret_cast<const d2*>(g.Xf);
       d2* xd2 = reinterpret_cast<d2*>(lds_X);
       for (int i = tid; i < kX2; i += NT) xd2[i] = xs2[i < nX2 ? i : i % (64 * KSDP) + nX2 - 64 * KSDP];
     }
     if (tid < 16 * RMAX) lds_alpha[tid] = tid < 16 * R ? g.alpha[tid] : 0.0;
     for (int i = tid; i < kTabN; i += NT) etab[i] = kTab256 ? kExp2Tab256[i] : kExp2Tab64[i];
+  } else {
+    // every load first, one wait, then the LDS writes
+    constexpr int kLper = (kL2 + NT - 1) / NT;
+    constexpr int kXper = XL ? (kX2 + NT - 1) / NT : 0;
+    constexpr int kTper = (kTabN + NT - 1) / NT;
+    const int nL2 = 64 * R * (R + 1);
+    const d2* src = reinterpret_cast<const d2*>(g.Lp);
+    d2 lv[kLper];
+#pragma unroll
+    for (int k = 0; k < kLper; ++k) {
+      const int i = tid + k * NT;
+      lv[k] = (i < nL2) ? src[i] : d2{0.0, 0.0};   // i ≥ nL2 covers i ≥ kL2 (nL2 ≤ kL2)
+    }
+    d2 xv[kXper > 0 ? kXper : 1];
+    if constexpr (XL) {
+      const int nX2 = 64 * KSDP * R;                // row tiles past R repeat tile R−1 (see Tl below)
+      const d2* xs2 = reinterpret_cast<const d2*>(g.Xf);
+#pragma unroll
+      for (int k = 0; k < kXper; ++k) {
+        const int i = tid + k * NT;
+        if (i < kX2) xv[k] = xs2[i < nX2 ? i : i % (64 * KSDP) + nX2 - 64 * KSDP];
+      }
+    }
+    const double av = (tid < 16 * R) ? g.alpha[tid] : 0.0;
+    double tv[kTper];
+#pragma unroll
+    for (int k = 0; k < kTper; ++k) {
+      const int i = tid + k * NT;
+      if (i < kTabN) tv[k] = kTab256 ? kExp2Tab256[i] : kExp2Tab64[i];
+    }
+    d2* dst = reinterpret_cast<d2*>(lds_L);
+#pragma unroll
+    for (int k = 0; k < kLper; ++k)
+      if (tid + k * NT < kL2) dst[tid + k * NT] = lv[k];
+    if constexpr (XL) {
+      d2* xd2 = reinterpret_cast<d2*>(lds_X);
+#pragma unroll
+      for (int k = 0; k < kXper; ++k)
+        if (tid + k * NT < kX2) xd2[tid + k * NT] = xv[k];
+    }
+    if (tid < 16 * RMAX) lds_alpha[tid] = av;
+#pragma unroll
+    for (int k = 0; k < kTper; ++k)
+      if (tid + k * NT < kTabN) etab[tid + k * NT] = tv[k];
   }
   __syncthreads();
   if constexpr ((ABL & 1) != 0) return;
@@ -1295,7 +1350,10 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : NW / 4) void posterior_reg_k
 #pragma unroll
     for (int q = 0; q < KSD; ++q) {
       const int j = 4 * q + (lane >> 4);
-      xs[q] = (j < d) ? raw[q] / g.ls[j] : 0.0;
+      if constexpr ((ABL & 128) != 0)
+        xs[q] = (j < d) ? raw[q] / g.ls[j] : 0.0;
+      else
+        xs[q] = (j < d) ? raw[q] / lsr[q] : 0.0;
       csq = fma(xs[q], xs[q], csq);
     }
     if constexpr ((ABL & 64) != 0)      // the next tile's coordinates in flight during this tile

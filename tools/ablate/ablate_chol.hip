@@ -31,7 +31,7 @@ static void trace_diag() {
   double *A, *ws;
   int* info;
   CK(hipMalloc(&A, N * N * 8));
-  CK(hipMalloc(&ws, kCholWsDoubles * 8));
+  CK(hipMalloc(&ws, chol_ws_doubles(N) * 8));
   CK(hipMalloc(&info, 64));
   const char* names[17] = {"start", "loaded", "b0 begin", "b0 factored", "b1 begin", "b1 factored", "b2 begin",
                            "b2 factored", "b3 begin", "b3 factored", "w0 L + W_00", "w1 L + W_11", "w2 L + W_22",
@@ -64,28 +64,36 @@ int main(int argc, char** argv) {
     int* info;
     CK(hipMalloc(&A0, N * N * 8));
     CK(hipMalloc(&A, N * N * 8));
-    CK(hipMalloc(&ws, kCholWsDoubles * 8));
+    CK(hipMalloc(&ws, chol_ws_doubles(N) * 8));
     CK(hipMalloc(&info, 64));
     CK(hipMemcpy(A0, h.data(), N * N * 8, hipMemcpyHostToDevice));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    float best = 1e30f, sum = 0.f;
+    // the two launch schedules interleaved: kCholTwoLaunch (panel + update per step, round 2) and
+    // kCholFused (the update launch forms the next panel; round 3)
+    float best = 1e30f, sum = 0.f, best2 = 1e30f, sum2 = 0.f;
     const int reps = 10;
     for (int r = 0; r < reps + 1; ++r) {
-      CK(hipMemcpy(A, A0, N * N * 8, hipMemcpyDeviceToDevice));
-      CK(hipMemset(info, 0, 4));
-      CK(hipEventRecord(e0));
-      CK(launch_cholesky(0, A, N, N, info, ws));
-      CK(hipEventRecord(e1));
-      CK(hipEventSynchronize(e1));
-      float ms;
-      CK(hipEventElapsedTime(&ms, e0, e1));
-      if (r > 0) {
-        best = ms < best ? ms : best;
-        sum += ms;
+      for (int mode = 0; mode < 2; ++mode) {
+        CK(hipMemcpy(A, A0, N * N * 8, hipMemcpyDeviceToDevice));
+        CK(hipMemset(info, 0, 4));
+        CK(hipEventRecord(e0));
+        CK(launch_cholesky_mode(0, A, N, N, info, ws, mode == 0 ? kCholTwoLaunch : kCholFused));
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (r > 0 && mode == 1) {
+          best = ms < best ? ms : best;
+          sum += ms;
+        } else if (r > 0) {
+          best2 = ms < best2 ? ms : best2;
+          sum2 += ms;
+        }
       }
     }
+    printf("N=%lld  two launches per step %.3f ms (best %.3f)\n", (long long)N, sum2 / reps, best2);
     // the same launch sequence captured once into a hipGraph and replayed (launch-gap ablation)
     float gbest = 1e30f, gsum = 0.f;
     {
@@ -129,7 +137,7 @@ int main(int argc, char** argv) {
       for (int64_t k = 0; k <= j; ++k) s += L[i * N + k] * L[j * N + k];
       worst = std::max(worst, std::abs(s - h[i * N + j]) / std::abs(h[i * N + i]));
     }
-    printf("N=%lld  Cholesky %.3f ms (best %.3f, %d steps = %.1f us/step)  info %d  max |LLt - A|/A_ii %.2e\n",
+    printf("N=%lld  Cholesky (fused) %.3f ms (best %.3f, %d steps = %.1f us/step)  info %d  max |LLt - A|/A_ii %.2e\n",
            (long long)N, sum / reps, best, (int)((N + 63) / 64), best * 1e3 / ((N + 63) / 64), hinfo, worst);
     CK(hipFree(A0)); CK(hipFree(A)); CK(hipFree(ws)); CK(hipFree(info));
   }

@@ -324,28 +324,17 @@ int main(int argc, char** argv) {
   };
   // n ≤ 256 (configs 2 and 4): the library launches RT = 2 (n ≤ 256) or 1 (n ≤ 128), CT = 4, barrier pipeline
   const Variant small128[] = {
-      {"tile RMAX8 CT4 (library n<=128)", run_tile<8, 4, 0>},
-      {"RT1 CT4 barrier (r01 library)", run<1, 4, 8, 32>},
-      {"reg: L^-1 in LDS, K* in registers", run_reg<0>},
-      {"reg gen only (2)", run_reg<2>},
-      {"reg staging only (1)", run_reg<1>},
-      {"reg no Matern, gen only (10)", run_reg<10>},
-      {"reg16 short sqrt (16)", run_reg<16, 16, true>},
-      {"reg16 int exponent (32)", run_reg<32, 16, true>},
-      {"reg16 short sqrt + int exp (48)", run_reg<48, 16, true>},
-      {"reg16 gen only", run_reg<2, 16, true>},
-      {"reg 8 waves, Xf in LDS", run_reg<0, 8, true>},
-
-      {"reg 16 waves 1 WG/CU Xf in LDS", run_reg<0, 16, true>},
+      {"reg16 library (warm-up slot)", run_reg<0, 16, true>},
+      {"reg16 r02 staging + ls reload (128)", run_reg<128, 16, true>},
+      {"reg16 library", run_reg<0, 16, true>},
       {"reg16 prefetch next tile (64)", run_reg<64, 16, true>},
+      {"reg16 r02 staging + prefetch (192)", run_reg<192, 16, true>},
+      {"reg16 staging only (1)", run_reg<1, 16, true>},
+      {"reg16 r02 staging only (129)", run_reg<129, 16, true>},
+      {"reg16 gen only (2)", run_reg<2, 16, true>},
+      {"reg16 short sqrt (16)", run_reg<16, 16, true>},
       {"reg16 library again", run_reg<0, 16, true>},
-      {"reg 12 waves gen only", run_reg<2, 12, true>},
-      {"tile RMAX8 CT4 gen only (2)", run_tile<8, 4, 2>},
-      {"tile RMAX8 CT4 const A (4)", run_tile<8, 4, 4>},
-      {"tile RMAX8 CT4 rcp candidates (8)", run_tile<8, 4, 8>},
-      {"tile RMAX8 CT4 rcp, gen only (10)", run_tile<8, 4, 10>},
-      {"tile RMAX16 CT2", run_tile<16, 2, 0>},
-      {"RT1 CT2 counter ring", run<1, 2, 8, 0>},
+      {"tile RMAX8 CT4", run_tile<8, 4, 0>},
   };
   const Variant small256[] = {
       {"tile RMAX16 CT2 (library n<=256)", run_tile<16, 2, 0>},

@@ -157,7 +157,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const double* __rest
 // GPy Stationary._unscaled_dist(X) on X/ℓ: r² = −2·(aᵢ·aⱼ) + (‖aᵢ‖² + ‖aⱼ‖²), diagonal forced
 // to 0, clipped at 0; then K_of_r.  Lower triangle only (j ≤ i).
 //   cand_scale_kernel  a = X/ℓ (GPy divides; once per element, not per pair) into rows of KP = ⌈DP/4⌉·4
-//                      doubles (zero padded) and ‖a‖² in coordinate order;
+//                      doubles (zero padded) and ‖a‖² (a shuffle tree over the row's lanes);
 //   cand_cov_kernel    one 64×64 lower tile per 256-thread workgroup (4 waves × 32×32, gemm_kernel's
 //                      tiling), the cross term aᵢ·aⱼ on v_mfma_f64_16x16x4f64 over KP/4 k-steps from LDS,
 //                      the kernel transform fused into the store.
@@ -167,18 +167,20 @@ template <int DP>
 __global__ __launch_bounds__(256) void cand_scale_kernel(const double* __restrict__ Xc, int d, int64_t N,
                                                          const double* __restrict__ ls, double* __restrict__ Xs,
                                                          double* __restrict__ xsq) {
+  // one thread per (candidate, coordinate), KP (a power of two ≤ 64) lanes per candidate; ‖a‖² by a
+  // shuffle tree over the candidate's lanes (round 2 ran one thread per candidate: 13.6 µs at N = 3000, d = 30)
   constexpr int KP = (DP + 3) / 4 * 4;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= N) return;
-  double s = 0.0;
+  static_assert((KP & (KP - 1)) == 0 && KP <= 64, "KP lanes of one wave per candidate");
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = t / KP;
+  const int k = (int)(t % KP);
+  double a = 0.0;
+  if (i < N && k < d) a = Xc[i * d + k] / ls[k];
+  if (i < N) Xs[i * KP + k] = a;
+  double s = a * a;
 #pragma unroll
-  for (int k = 0; k < KP; ++k) {
-    double a = 0.0;
-    if (k < d) a = Xc[i * d + k] / ls[k];
-    s = fma(a, a, s);
-    Xs[i * KP + k] = a;
-  }
-  xsq[i] = s;
+  for (int o = KP / 2; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (i < N && k == 0) xsq[i] = s;
 }
 
 template <int DP, int KIND>
@@ -260,6 +262,10 @@ constexpr int kNB = 64;
 // Phase timestamps of the diagonal-block factorisation for tools/ablate/ablate_chol (empty here).
 #ifndef OMB_CHOL_TRACE
 #define OMB_CHOL_TRACE(id, cond)
+#endif
+// per-column timestamps (wave w done with column j) for tools/ablate/ablate_chol (empty here)
+#ifndef OMB_CHOL_COL
+#define OMB_CHOL_COL(w, j, cond)
 #endif
 
 __device__ __forceinline__ double readlane_f64(double v, int l) {
@@ -365,6 +371,7 @@ __device__ __forceinline__ void chol64_factor(double (&a)[16], int w, int r, int
       const double lr = Lb[(b * 64 + r) * kLbP + jj];
 #pragma unroll
       for (int q = 0; q < 16; ++q) a[q] = fma(-lr, Lb[(b * 64 + 16 * w + q) * kLbP + jj], a[q]);
+      OMB_CHOL_COL(w, 16 * b + jj, r == 0);
     }
   }
   // ---- own sub-block
@@ -425,6 +432,7 @@ __device__ __forceinline__ void chol64_factor(double (&a)[16], int w, int r, int
         for (int q = jj + 3; q < 16; ++q) pv[q] = cb[16 * b + q];
         pl = lrj;
       }
+      OMB_CHOL_COL(w, j, r == 0);
       __builtin_amdgcn_sched_barrier(0);
     });
     OMB_CHOL_TRACE(3 + 2 * b, r == 0);
@@ -1643,7 +1651,7 @@ hipError_t launch_cand_cov(hipStream_t stream, const GPDev& g, int d, int DP, co
   const int KP = (DP + 3) / 4 * 4;
   double* Xs = ws;
   double* xsq = ws + N * KP;
-  const unsigned sb = (unsigned)((N + 255) / 256);
+  const unsigned sb = (unsigned)((N * KP + 255) / 256);
   const unsigned nt = (unsigned)((N + 63) / 64);
   dim3 grid(nt, nt);
 #define OMB_COV(DPV)                                                                                          \

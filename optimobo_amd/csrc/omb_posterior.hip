@@ -476,11 +476,14 @@ __global__ __launch_bounds__(512) void kernel_block_pipe_kernel(GPDev g, int d, 
 // latency is hidden (the compiler's wait for the prefetch is a vmcnt that leaves the block's stores in
 // flight).  RCP multiplies by 1/ℓ (one rounding more than GPy's division; ≤ 1 ulp in x/ℓ).  ROLL keeps the
 // block loop rolled (unrolled, its registers cost occupancy).
-template <int DP, int KIND, int CB, bool RCP = false, bool ROLL = false>
+// AW (n_var > 8 with d + 2 ≤ 4·⌈DP/4⌉, e.g. d = 30 in DP = 32): the packed rows already carry ‖x/ℓ‖² and 1 in
+// dimensions d and d + 1 (pack_X_kernel), inside the cross term's k-steps, so B = [−2·x*/ℓ, 1, ‖x*/ℓ‖²] gives
+// r² from the same 8 MFMA k-steps: the per-element fma, add and LDS read of ‖x/ℓ‖² go.
+template <int DP, int KIND, int CB, bool RCP = false, bool ROLL = false, bool AW = false>
 __global__ __launch_bounds__(512) void kernel_block_persist_kernel(GPDev g, int d, const double* __restrict__ Xc,
                                                                    int64_t N, double* __restrict__ K, ExpCoef ec) {
-  constexpr bool kAug = DP <= 8;
-  constexpr int KSD = kAug ? (DP + 5) / 4 : (DP + 3) / 4;
+  constexpr bool kAug = DP <= 8 || AW;              // r² straight from the MFMA
+  constexpr int KSD = DP <= 8 ? (DP + 5) / 4 : (DP + 3) / 4;
   constexpr int KSDP = ((DP + 5) / 4 + 1) / 2;   // = packed_X_pairs(DP)
   constexpr int NA = (KSD + 1) / 2;
   constexpr int TPW = kblock_rows(DP) / 16;
@@ -1535,8 +1538,13 @@ static hipError_t launch_kblock_kind(hipStream_t stream, const GPArgs& args, int
   switch (args.DP) {
 #define OMB_KBS(DPV) \
   case DPV: hipLaunchKernelGGL((kernel_block_persist_kernel<DPV, KIND, 1, false>), grid(DPV, 1), dim3(512), 0, stream, g, args.d, Xc, N, K, exp_coef()); break;
-#define OMB_KBW_CB(DPV, CBV) \
-  case CBV: hipLaunchKernelGGL((kernel_block_persist_kernel<DPV, KIND, CBV, true, true>), grid(DPV, CBV), dim3(512), 0, stream, g, args.d, Xc, N, K, exp_coef()); break;
+#define OMB_KBW_CB(DPV, CBV)                                                                                  \
+  case CBV:                                                                                                     \
+    if (args.d + 2 <= 4 * ((DPV + 3) / 4))                                                                      \
+      hipLaunchKernelGGL((kernel_block_persist_kernel<DPV, KIND, CBV, true, true, true>), grid(DPV, CBV), dim3(512), 0, stream, g, args.d, Xc, N, K, exp_coef()); \
+    else                                                                                                        \
+      hipLaunchKernelGGL((kernel_block_persist_kernel<DPV, KIND, CBV, true, true>), grid(DPV, CBV), dim3(512), 0, stream, g, args.d, Xc, N, K, exp_coef()); \
+    break;
 #define OMB_KBW(DPV) \
   case DPV:                                                                  \
     switch (pick_cb(DPV)) {                                                  \

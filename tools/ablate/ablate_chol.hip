@@ -17,6 +17,12 @@ __device__ unsigned long long g_trace[2][32];
     }                                                             \
   } while (0)
 
+__device__ unsigned long long g_col[4][64];
+#define OMB_CHOL_COL(w, j, cond)                                  \
+  do {                                                            \
+    if (cond) g_col[w][j] = __builtin_readcyclecounter();         \
+  } while (0)
+
 #include "../../optimobo_amd/csrc/omb_linalg.hip"
 
 using namespace omb;
@@ -47,6 +53,17 @@ static void trace_diag() {
     printf("chol_diag_kernel phases (cycles of s_memtime from start; us from the 100 MHz clock)\n");
     for (int i = 0; i < 17; ++i)
       printf("  %-12s %8lld cyc  %7.2f us\n", names[i], (long long)(t[0][i] - t[0][0]), (t[1][i] - t[1][0]) / 100.0);
+    unsigned long long c[4][64];
+    CK(hipMemcpyFromSymbol(c, HIP_SYMBOL(g_col), sizeof(c)));
+    printf("per column j: cycle (from start) at which wave w has applied (j < 16w) or factored (16w <= j < 16w+16) "
+           "column j\n");
+    for (int j = 0; j < 64; ++j) {
+      printf("  col %2d:", j);
+      for (int w = 0; w < 4; ++w) {
+        if (j < 16 * w + 16) printf(" w%d %7lld", w, (long long)(c[w][j] - t[0][0]));
+      }
+      printf("\n");
+    }
   }
   CK(hipFree(A)); CK(hipFree(ws)); CK(hipFree(info));
 }

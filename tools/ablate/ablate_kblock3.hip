@@ -58,28 +58,29 @@ void bench(int n, int64_t N, int d) {
     hipLaunchKernelGGL((kernel_block_pipe_kernel<__VA_ARGS__>), gr, dim3(512), 0, 0, gg, dd, xc, nn, k, e); }
   const V vs[] = {
       {"library: 1 row tile / iteration", L(DP, 0, true, false, false, 1, 0), true},
-      {"2 row tiles / iteration", L(DP, 0, true, false, false, 2, 0), true},
       {"1 row tile, no stores", L(DP, 0, true, false, false, 1, 1), false},
-      {"2 row tiles, no stores", L(DP, 0, true, false, false, 2, 1), false},
       {"1 row tile, stores only", L(DP, 0, true, false, false, 1, 2), false},
-      {"2 row tiles, stores only", L(DP, 0, true, false, false, 2, 2), false},
   };
 #undef L
 #define P(CB, RCP, ROLL) [](dim3 gr, GPDev gg, int dd, const double* xc, int64_t nn, double* k, ExpCoef e) { \
     dim3 g2((unsigned)((nn + 128 * CB - 1) / (128 * CB)), gr.y);                                     \
     hipLaunchKernelGGL((kernel_block_persist_kernel<DP, 0, CB, RCP, ROLL>), g2, dim3(512), 0, 0, gg, dd, xc, nn, k, e); }
+#define PA(CB, RCP, ROLL) [](dim3 gr, GPDev gg, int dd, const double* xc, int64_t nn, double* k, ExpCoef e) { \
+    dim3 g2((unsigned)((nn + 128 * CB - 1) / (128 * CB)), gr.y);                                     \
+    hipLaunchKernelGGL((kernel_block_persist_kernel<DP, 0, CB, RCP, ROLL, (DP > 8)>), g2, dim3(512), 0, 0, gg, dd, xc, nn, k, e); }
   const V ps[] = {
-      {"persistent CB=1", P(1, false, false), true},
-      {"persistent CB=1, 1/l", P(1, true, false), true},
-      {"persistent CB=2, 1/l", P(2, true, false), true},
-      {"persistent CB=4, 1/l", P(4, true, false), true},
-      {"persistent CB=8, 1/l", P(8, true, false), true},
-      {"persistent CB=16, 1/l", P(16, true, false), true},
-      {"persistent CB=4, 1/l, rolled", P(4, true, true), true},
+      {"(warm-up) persistent CB=8, 1/l, rolled", P(8, true, true), true},
+      {"persistent CB=8, 1/l, rolled, aug r2", PA(8, true, true), true},
       {"persistent CB=8, 1/l, rolled", P(8, true, true), true},
-      {"persistent CB=2, rolled", P(2, false, true), true},
+      {"persistent CB=8, 1/l, aug r2", PA(8, true, false), true},
+      {"persistent CB=8, 1/l", P(8, true, false), true},
+      {"persistent CB=16, 1/l, rolled, aug r2", PA(16, true, true), true},
+      {"persistent CB=4, 1/l, rolled, aug r2", PA(4, true, true), true},
+      {"persistent CB=8, 1/l, rolled, aug r2 (again)", PA(8, true, true), true},
+      {"persistent CB=8, 1/l, rolled (again)", P(8, true, true), true},
   };
 #undef P
+#undef PA
   std::vector<V> all(vs, vs + sizeof(vs) / sizeof(vs[0]));
   all.insert(all.end(), ps, ps + sizeof(ps) / sizeof(ps[0]));
   const int NV = (int)all.size();

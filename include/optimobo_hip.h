@@ -86,6 +86,8 @@ const char* omb_last_error(const omb_ctx* ctx);
  * lets the kernel finish.  The next call on the context that enters the library (and
  * omb_synchronize after its sync) then returns OMB_EHIP once, describing the fault: the moments
  * and acquisition values computed since the previous report are invalid.
+ * The same bound limits the fused Cholesky steps' wait for the diagonal block (omb_cholesky,
+ * omb_posterior_samples, the GP fit above n = 128): running out returns OMB_EHIP from that call.
  * omb_debug_set(ctx, OMB_DEBUG_SPIN_LIMIT, polls) changes the bound (tests force the path with 0). */
 enum { OMB_DEBUG_SPIN_LIMIT = 1 };
 int omb_debug_set(omb_ctx* ctx, int what, int64_t value);

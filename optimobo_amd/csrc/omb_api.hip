@@ -981,13 +981,13 @@ static int run_cholesky(omb_ctx* ctx, double* A, int64_t N, int64_t lda, double 
   double* ws = reinterpret_cast<double*>(static_cast<char*>(ctx->ichol) + 16);
   OMB_HIP(ctx, hipMemsetAsync(dinfo, 0, sizeof(int), ctx->stream));
   OMB_HIP(ctx, launch_add_diag(ctx->stream, A, N, lda, jitter));
-  OMB_HIP(ctx, launch_cholesky(ctx->stream, A, N, lda, dinfo, ws));
+  OMB_HIP(ctx, launch_cholesky(ctx->stream, A, N, lda, dinfo, ws, ctx->spin_limit));
   int h = 0;
   OMB_HIP(ctx, hipMemcpyAsync(&h, dinfo, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   OMB_HIP(ctx, hipStreamSynchronize(ctx->stream));
   if (h == kCholSpinFault)
     return fail(ctx, OMB_EHIP, "Cholesky: a workgroup's wait for the diagonal block exceeded %d polls; the factor is "
-                               "invalid", kCholSpinLimit);
+                               "invalid", ctx->spin_limit);
   *info = h;
   return OMB_OK;
 }

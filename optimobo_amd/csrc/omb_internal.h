@@ -122,14 +122,15 @@ hipError_t launch_add_diag(hipStream_t stream, double* S, int64_t N, int64_t lds
 // in-place lower Cholesky; info (device int, zeroed by the caller) = first bad column (1-based);
 // ws: chol_ws_doubles(N) device doubles of workspace (the inverse of the current diagonal block, as MFMA
 // fragments for the panel product, then one int flag per step).  info = kCholSpinFault: a workgroup's
-// wait for the diagonal block ran out (the factor is invalid; reported as OMB_EHIP).
+// wait for the diagonal block ran out after spin_limit polls (the factor is invalid; reported as OMB_EHIP).
 constexpr int kCholWsDoubles = 64 * 64;
 constexpr int kCholSpinFault = -2147483647;
-constexpr int kCholSpinLimit = 1 << 21;     // polls of the fused step's wait for W_{k+1}
 enum { kCholTwoLaunch = 0, kCholFused = 1 };
 int64_t chol_ws_doubles(int64_t N);
-hipError_t launch_cholesky(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws);
-hipError_t launch_cholesky_mode(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws, int mode);
+hipError_t launch_cholesky(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws,
+                           int spin_limit = kDefaultSpinLimit);
+hipError_t launch_cholesky_mode(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws, int mode,
+                                int spin_limit = kDefaultSpinLimit);
 // Y (B, N) = μ + Zt Lᵀ (L lower, N×N): row b of Y is the sample μ + L z_b.
 // ws: chol_samples_ws_doubles(N, B) device doubles (split-K partial products; 0 when unsplit).
 int64_t chol_samples_ws_doubles(int64_t N, int B);

@@ -619,7 +619,7 @@ __global__ __launch_bounds__(128) void chol_panel_kernel(double* __restrict__ A,
 // diagonal workgroup to publish W_{k+1} = L_{k+1,k+1}⁻¹ (flags[step], set after the fragments are in the
 // workspace) and form the next step's panel rows L21 = A21 · Wᵀ themselves, so a step is one launch:
 // the panel's own launch (≈ 5 µs plus a launch gap per step at N = 3000) leaves the chain.  Workgroup 0
-// is dispatched first (in-order dispatch); the wait is bounded all the same (kCholSpinLimit polls, then
+// is dispatched first (in-order dispatch); the wait is bounded all the same (spin_limit polls, then
 // info = kCholSpinFault and the workgroup finishes), so a waiting workgroup can never hang the grid.
 __device__ __forceinline__ void chol_tile_of(int b, int t, int& mt, int& nt) {
   if (b < t) {
@@ -638,7 +638,7 @@ __device__ __forceinline__ void chol_tile_of(int b, int t, int& mt, int& nt) {
 template <bool FUSE>
 __global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A, int64_t N, int64_t lda, int step,
                                                           int t, double* __restrict__ ws, int* __restrict__ info,
-                                                          int* __restrict__ flags) {
+                                                          int* __restrict__ flags, int spin_limit) {
   if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
   int mt, nt;
   chol_tile_of((int)blockIdx.x, t, mt, nt);
@@ -748,7 +748,7 @@ __global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A
     if (tid == 0) {
       int polls = 0;
       while (__hip_atomic_load(&flags[step], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-        if (++polls > kCholSpinLimit) {
+        if (++polls > spin_limit) {
           atomicCAS(info, 0, kCholSpinFault);
           break;
         }
@@ -1700,7 +1700,8 @@ static hipError_t chol_panel(hipStream_t stream, double* A, int64_t N, int64_t l
   return hipGetLastError();
 }
 
-hipError_t launch_cholesky_mode(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws, int mode) {
+hipError_t launch_cholesky_mode(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws, int mode,
+                                int spin_limit) {
   if (N <= 0) return hipSuccess;
   const int steps = (int)((N + kNB - 1) / kNB);
   const bool vec = (lda % 2 == 0) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
@@ -1722,17 +1723,18 @@ hipError_t launch_cholesky_mode(hipStream_t stream, double* A, int64_t N, int64_
     }
     const unsigned wgs = (unsigned)(t * (t + 1) / 2);
     if (fuse)
-      hipLaunchKernelGGL((chol_update_kernel<true>), dim3(wgs), dim3(256), 0, stream, A, N, lda, k, t, ws, info, flags);
+      hipLaunchKernelGGL((chol_update_kernel<true>), dim3(wgs), dim3(256), 0, stream, A, N, lda, k, t, ws, info, flags,
+                         spin_limit);
     else
       hipLaunchKernelGGL((chol_update_kernel<false>), dim3(wgs), dim3(256), 0, stream, A, N, lda, k, t, ws, info,
-                         flags);
+                         flags, spin_limit);
     e = hipGetLastError();
   }
   return e;
 }
 
-hipError_t launch_cholesky(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws) {
-  return launch_cholesky_mode(stream, A, N, lda, info, ws, kCholFused);
+hipError_t launch_cholesky(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws, int spin_limit) {
+  return launch_cholesky_mode(stream, A, N, lda, info, ws, kCholFused, spin_limit);
 }
 
 // K slices of the sample product: enough (tile, slice) workgroups to fill the chip (≥ 1024), slices of

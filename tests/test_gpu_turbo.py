@@ -91,6 +91,26 @@ def test_cholesky_info_matches_dpotrf(ctx, N, bad):
     assert info == info_ref == bad + 1
 
 
+def test_cholesky_step_wait_timeout_is_reported(ctx):
+    """The fused Cholesky step (the next panel formed in the update launch) waits for the diagonal
+    workgroup's flag with a bounded poll; omb_debug_set(SPIN_LIMIT, 0) makes the first unset poll run
+    out, and the call returns OMB_EHIP instead of an info or a wrong factor.  The default bound then
+    factors the same matrix correctly."""
+    from optimobo_amd import _lib
+    N = 700                                   # 11 steps: the tiles below the next diagonal block wait
+    A = spd(N, 31)
+    ctx.debug_set("spin_limit", 0)
+    try:
+        with pytest.raises(_lib.OMBError) as e:
+            ctx.cholesky(dev(A))
+        assert e.value.code == _lib.OMB_EHIP and "Cholesky" in str(e.value)
+    finally:
+        ctx.debug_set("spin_limit", 1 << 22)
+    At = dev(A)
+    assert ctx.cholesky(At) == 0
+    np.testing.assert_allclose(np.tril(At.cpu().numpy()), np.linalg.cholesky(A), rtol=1e-10, atol=1e-12)
+
+
 # ----------------------------------------------------------------------------- samples
 def test_posterior_samples_vs_oracle(ctx):
     X, y, ls, var, og = fit(ctx, 40, 3, seed=11)

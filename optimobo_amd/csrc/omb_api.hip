@@ -979,7 +979,6 @@ static int run_cholesky(omb_ctx* ctx, double* A, int64_t N, int64_t lda, double 
   if (rc) return rc;
   int* dinfo = static_cast<int*>(ctx->ichol);
   double* ws = reinterpret_cast<double*>(static_cast<char*>(ctx->ichol) + 16);
-  OMB_HIP(ctx, hipMemsetAsync(dinfo, 0, sizeof(int), ctx->stream));
   OMB_HIP(ctx, launch_add_diag(ctx->stream, A, N, lda, jitter));
   OMB_HIP(ctx, launch_cholesky(ctx->stream, A, N, lda, dinfo, ws, ctx->spin_limit));
   int h = 0;

@@ -119,7 +119,7 @@ hipError_t launch_cand_cov(hipStream_t stream, const GPDev& g, int d, int DP, co
                            int64_t lds, double* ws);
 hipError_t launch_mirror_lower(hipStream_t stream, double* S, int64_t N, int64_t lds);
 hipError_t launch_add_diag(hipStream_t stream, double* S, int64_t N, int64_t lds, double v);
-// in-place lower Cholesky; info (device int, zeroed by the caller) = first bad column (1-based);
+// in-place lower Cholesky; info (device int, zeroed by the first kernel) = first bad column (1-based);
 // ws: chol_ws_doubles(N) device doubles of workspace (the inverse of the current diagonal block, as MFMA
 // fragments for the panel product, then one int flag per step).  info = kCholSpinFault: a workgroup's
 // wait for the diagonal block ran out after spin_limit polls (the factor is invalid; reported as OMB_EHIP).

@@ -523,8 +523,13 @@ __device__ __forceinline__ void chol64_inverse(int w, int r, const double* Lb, d
   OMB_CHOL_TRACE(16, w == 0 && r == 0);
 }
 
+// Step 0's diagonal block; it also zeroes info and the fused steps' flags (the first kernel of the
+// factorisation, so no memset launches precede it).
 __global__ __launch_bounds__(256) void chol_diag_kernel(double* __restrict__ A, int64_t N, int64_t lda,
-                                                         double* __restrict__ ws, int* __restrict__ info) {
+                                                         double* __restrict__ ws, int* __restrict__ info,
+                                                         int* __restrict__ flags, int nflags) {
+  for (int i = threadIdx.x; i < nflags; i += blockDim.x) flags[i] = 0;
+  if (threadIdx.x == 0) *info = 0;
   __shared__ __attribute__((aligned(16))) double Lb[kLbDoubles];
   __shared__ double aux[kCholAux];
   __shared__ int prog[4];
@@ -1592,6 +1597,130 @@ __global__ __launch_bounds__(kSelThreads) void select_sort_kernel(const double* 
     heads[(int64_t)b * K + i] = (long long)ix[i] | (key[i] == kSelKeyInf ? kSelInfFlag : 0ll);
 }
 
+// The same heads for K ≤ 64 without the full sort (round 3): a radix select finds the K-th smallest key T
+// (8 passes of 8 bits over an LDS histogram), the entries below T and the lowest-index ties at T are gathered
+// (K of them), and one wave bitonic-sorts those K (key, index) pairs in registers.  The bitonic sort of the
+// whole row spent 78 barrier-separated LDS stages on 4,096 slots to keep 64 (config 6: 50 µs per step,
+// profiles/r03_v23_c6_kernel_per_step.txt).  Rows are read with E = ⌈N/1024⌉ consecutive entries per thread,
+// so a block scan over threads numbers the ties in index order.
+constexpr int kSelTopK = 64;
+__global__ __launch_bounds__(kSelThreads) void select_topk_kernel(const double* __restrict__ Y, int64_t N, int K,
+                                                                  long long* __restrict__ heads) {
+  constexpr int kE = kSelectSortN / kSelThreads;
+  __shared__ unsigned hist[256];
+  __shared__ unsigned long long s_prefix;
+  __shared__ unsigned s_rank, s_less;
+  __shared__ unsigned wsum[kSelThreads / 64];
+  __shared__ unsigned s_slot;
+  __shared__ unsigned long long sk[kSelTopK];
+  __shared__ unsigned short si[kSelTopK];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const double* y = Y + (int64_t)b * N;
+  const int E = (int)((N + kSelThreads - 1) / kSelThreads);
+  unsigned long long key[kE];
+#pragma unroll
+  for (int e = 0; e < kE; ++e) {
+    const int64_t i = (int64_t)tid * E + e;
+    key[e] = (e < E && i < N) ? sel_key(y[i]) : ~0ull;
+  }
+  if (tid == 0) {
+    s_prefix = 0ull;
+    s_rank = (unsigned)K;            // 1-based rank of T among the keys matching the prefix
+    s_less = 0u;
+  }
+  // ---- radix select of T = the K-th smallest key, most significant byte first
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    for (int i = tid; i < 256; i += kSelThreads) hist[i] = 0u;
+    __syncthreads();
+    const unsigned long long prefix = s_prefix;
+    const unsigned long long hmask = shift == 56 ? 0ull : (~0ull << (shift + 8));
+#pragma unroll
+    for (int e = 0; e < kE; ++e)
+      if (e < E && (int64_t)tid * E + e < N && (key[e] & hmask) == prefix)
+        atomicAdd(&hist[(key[e] >> shift) & 255u], 1u);
+    __syncthreads();
+    if (wave == 0) {
+      // inclusive scan of the 256 bins, 4 per lane; the first bin whose running count reaches the rank
+      unsigned c[4], run = 0u;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) c[q] = hist[4 * lane + q];
+      const unsigned tot = c[0] + c[1] + c[2] + c[3];
+      unsigned incl = tot;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const unsigned v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+      }
+      run = incl - tot;                                     // count before this lane's first bin
+      const unsigned rank = s_rank;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (run < rank && run + c[q] >= rank) {             // exactly one (lane, q) satisfies this
+          s_prefix = prefix | ((unsigned long long)(4 * lane + q) << shift);
+          s_rank = rank - run;
+          s_less += run;
+        }
+        run += c[q];
+      }
+    }
+    __syncthreads();
+  }
+  const unsigned long long T = s_prefix;
+  const unsigned need_ties = (unsigned)K - s_less;         // ties at T to take, lowest indices first
+  // ---- number the ties at T in index order (block scan of per-thread counts)
+  unsigned nt = 0u;
+#pragma unroll
+  for (int e = 0; e < kE; ++e) nt += (e < E && key[e] == T) ? 1u : 0u;
+  unsigned incl = nt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  if (tid == 0) s_slot = 0u;
+  __syncthreads();
+  unsigned before = incl - nt;
+  for (int w = 0; w < wave; ++w) before += wsum[w];
+  // ---- gather the K selected entries (slot order arbitrary)
+#pragma unroll
+  for (int e = 0; e < kE; ++e) {
+    const int64_t i = (int64_t)tid * E + e;
+    if (e >= E || i >= N) continue;
+    bool take = key[e] < T;
+    if (key[e] == T) {
+      take = before < need_ties;
+      ++before;
+    }
+    if (take) {
+      const unsigned slot = atomicAdd(&s_slot, 1u);
+      sk[slot] = key[e];
+      si[slot] = (unsigned short)i;
+    }
+  }
+  __syncthreads();
+  // ---- one wave sorts the K pairs by (key, index); slots past K hold +max sentinels
+  if (wave == 0) {
+    unsigned long long kk = lane < K ? sk[lane] : ~0ull;
+    unsigned ii = lane < K ? si[lane] : 0xFFFFu;
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        const unsigned long long ko = __shfl_xor(kk, j);
+        const unsigned io = __shfl_xor(ii, j);
+        const bool mine_gt = kk > ko || (kk == ko && ii > io);
+        const bool lower = (lane & j) == 0, up = (lane & k) == 0;
+        if ((lower == up) == mine_gt) {                     // keep the smaller at the lower slot when ascending
+          kk = ko;
+          ii = io;
+        }
+      }
+    }
+    if (lane < K) heads[(int64_t)b * K + lane] = (long long)ii | (kk == kSelKeyInf ? kSelInfFlag : 0ll);
+  }
+}
+
 constexpr int kSelHeadLds = 4096;   // staged head entries (64 per sample, samples 0..63)
 __global__ __launch_bounds__(256) void select_greedy_kernel(const long long* __restrict__ heads, int B, int64_t N,
                                                             int K, int64_t* __restrict__ idx_out) {
@@ -1707,11 +1836,7 @@ hipError_t launch_cholesky_mode(hipStream_t stream, double* A, int64_t N, int64_
   const bool vec = (lda % 2 == 0) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
   const bool fuse = mode == kCholFused;
   int* flags = reinterpret_cast<int*>(ws + kCholWsDoubles);
-  if (fuse && steps > 2) {
-    hipError_t e = hipMemsetAsync(flags, 0, sizeof(int) * steps, stream);
-    if (e != hipSuccess) return e;
-  }
-  hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), 0, stream, A, N, lda, ws, info);
+  hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), 0, stream, A, N, lda, ws, info, flags, fuse ? steps : 0);
   hipError_t e = hipGetLastError();
   for (int k = 0; k + 1 < steps && e == hipSuccess; ++k) {
     const int64_t rest = N - (int64_t)(k + 1) * kNB;
@@ -1885,7 +2010,10 @@ hipError_t launch_select(hipStream_t stream, const double* Y, int B, int64_t N, 
     while (N2 < N) N2 <<= 1;
     const int K = (int)(B < N ? B : N);
     long long* heads = static_cast<long long*>(ws);
-    hipLaunchKernelGGL(select_sort_kernel, dim3((unsigned)B), dim3(kSelThreads), 0, stream, Y, N, N2, K, heads);
+    if (K <= kSelTopK)
+      hipLaunchKernelGGL(select_topk_kernel, dim3((unsigned)B), dim3(kSelThreads), 0, stream, Y, N, K, heads);
+    else
+      hipLaunchKernelGGL(select_sort_kernel, dim3((unsigned)B), dim3(kSelThreads), 0, stream, Y, N, N2, K, heads);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(select_greedy_kernel, dim3(1), dim3(256), 0, stream, heads, B, N, K, idx);

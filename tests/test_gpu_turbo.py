@@ -181,6 +181,19 @@ def test_select_turbo_m_shapes(ctx):
         check_select(ctx, y)
 
 
+def test_select_topk_heads_ties_nans(ctx):
+    """K = min(B, N) ≤ 64 takes the radix-select head kernel: heavy ties (every 7th candidate equal),
+    NaNs (the first NaN wins, then the next ones in index order), +inf, and draws at config 6's shape."""
+    rng = np.random.default_rng(43)
+    for N, B in [(3000, 64), (3000, 17), (8192, 64), (65, 64)]:
+        y = rng.standard_normal((N, 1, B))
+        y[::7, 0, :] = y[0, 0, :]
+        y[100:140:3, 0, 5 % B] = np.nan
+        y[200:260, 0, 2 % B] = -np.inf
+        y[300:, 0, 3 % B] = np.inf
+        check_select(ctx, y)
+
+
 def test_select_all_equal_and_exhausted(ctx):
     check_select(ctx, np.zeros((4, 1, 9)))           # more samples than candidates: picks repeat index 0
     check_select(ctx, np.full((6, 1, 3), np.inf))

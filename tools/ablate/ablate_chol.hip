@@ -45,7 +45,8 @@ static void trace_diag() {
   for (int rep = 0; rep < 3; ++rep) {
     CK(hipMemcpy(A, h.data(), N * N * 8, hipMemcpyHostToDevice));
     CK(hipMemset(info, 0, 4));
-    hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), 0, 0, A, (int64_t)N, (int64_t)N, ws, info);
+    hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), 0, 0, A, (int64_t)N, (int64_t)N, ws, info,
+                       reinterpret_cast<int*>(ws + kCholWsDoubles), 0);
     CK(hipDeviceSynchronize());
     unsigned long long t[2][32];
     CK(hipMemcpyFromSymbol(t, HIP_SYMBOL(g_trace), sizeof(t)));

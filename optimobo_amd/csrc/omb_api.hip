@@ -966,8 +966,8 @@ static hipError_t cov_prepare(omb_ctx* ctx, const ObjState& s, const double* Xc,
 // lower triangle of Σ = K(X*, X*) − VᵀV (GPy PosteriorExact._raw_predict, full_cov=True); cws:
 // cand_cov_ws_doubles(N, DP) doubles.
 static hipError_t cov_build(omb_ctx* ctx, const ObjState& s, const double* Xc, int64_t N, const double* V, double* S,
-                            int64_t lds, double* cws) {
-  hipError_t e = launch_cand_cov(ctx->stream, s.dev, s.d, s.DP, Xc, N, S, lds, cws);
+                            int64_t lds, double* cws, double jitter = 0.0) {
+  hipError_t e = launch_cand_cov(ctx->stream, s.dev, s.d, s.DP, Xc, N, S, lds, cws, jitter);
   if (e == hipSuccess) e = launch_gemm_tn_lower(ctx->stream, N, s.n, -1.0, V, N, 1.0, S, lds);
   return e;
 }
@@ -1050,9 +1050,9 @@ int omb_posterior_samples(omb_ctx* ctx, int obj, const double* Xc_dev, int64_t N
   double jit = jitter_rel * s.variance;
   int info = -1, t = 0;
   for (; t < max_tries; ++t, jit *= 10.0) {
-    if ((e = cov_build(ctx, s, Xc_dev, N, V, S, N, cws)) != hipSuccess)
+    if ((e = cov_build(ctx, s, Xc_dev, N, V, S, N, cws, jit)) != hipSuccess)   // Σ + jit·I
       return hip_fail(ctx, e, "posterior_samples (cov)");
-    if ((rc = run_cholesky(ctx, S, N, N, jit, &info))) return rc;
+    if ((rc = run_cholesky(ctx, S, N, N, 0.0, &info))) return rc;
     if (info == 0) break;
   }
   if (info != 0)
@@ -1132,8 +1132,8 @@ static int gp_factor(omb_ctx* ctx, int kernel, int n, int d, const double* X, co
   f->jitter = 0.0;
   for (int t = -1; t < 5; ++t) {
     const double jit = (t < 0) ? 0.0 : mean_diag * 1e-6 * pow(10.0, (double)t);
-    OMB_HIP(ctx, launch_cand_cov(ctx->stream, g, d, DP, X, n, f->Ky, n, f->cws));
-    if ((rc = run_cholesky(ctx, f->Ky, n, n, base + jit, &info))) return rc;
+    OMB_HIP(ctx, launch_cand_cov(ctx->stream, g, d, DP, X, n, f->Ky, n, f->cws, base + jit));   // Ky = K + (base+jit)·I
+    if ((rc = run_cholesky(ctx, f->Ky, n, n, 0.0, &info))) return rc;
     if (info == 0) {
       f->jitter = jit;
       break;

@@ -112,11 +112,12 @@ hipError_t launch_gemm_nn(hipStream_t s, int64_t M, int64_t Nc, int64_t K, doubl
 // lower triangle of C (N, N) = β C + α AᵀA, A (K, N).
 hipError_t launch_gemm_tn_lower(hipStream_t s, int64_t N, int64_t K, double alpha, const double* A, int64_t lda,
                                 double beta, double* C, int64_t ldc);
-// lower triangle of K(X*, X*) of one GP's kernel (ℓ, σ_f² from g) at Xc (N, d); ws: cand_cov_ws_doubles
-// device doubles (X*/ℓ and its squared norms).
+// lower triangle of K(X*, X*) of one GP's kernel (ℓ, σ_f² from g) at Xc (N, d), diag_add added to the
+// diagonal as it is stored (the jitter, without an add_diag launch); ws: cand_cov_ws_doubles device doubles
+// (X*/ℓ and its squared norms).
 int64_t cand_cov_ws_doubles(int64_t N, int DP);
 hipError_t launch_cand_cov(hipStream_t stream, const GPDev& g, int d, int DP, const double* Xc, int64_t N, double* S,
-                           int64_t lds, double* ws);
+                           int64_t lds, double* ws, double diag_add = 0.0);
 hipError_t launch_mirror_lower(hipStream_t stream, double* S, int64_t N, int64_t lds);
 hipError_t launch_add_diag(hipStream_t stream, double* S, int64_t N, int64_t lds, double v);
 // in-place lower Cholesky; info (device int, zeroed by the first kernel) = first bad column (1-based);

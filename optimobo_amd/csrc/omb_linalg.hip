@@ -186,7 +186,7 @@ __global__ __launch_bounds__(256) void cand_scale_kernel(const double* __restric
 template <int DP, int KIND>
 __global__ __launch_bounds__(256) void cand_cov_kernel(const double* __restrict__ Xs, const double* __restrict__ xsq,
                                                        int64_t N, double variance, double* __restrict__ S,
-                                                       int64_t lds) {
+                                                       int64_t lds, double diag_add) {
   constexpr int KP = (DP + 3) / 4 * 4;
   if (blockIdx.x > blockIdx.y) return;
   const int64_t m0 = (int64_t)blockIdx.y * 64, n0 = (int64_t)blockIdx.x * 64;
@@ -228,7 +228,8 @@ __global__ __launch_bounds__(256) void cand_cov_kernel(const double* __restrict_
         const int64_t row = m0 + 32 * wm + 16 * rb + (lane >> 4) + 4 * e;
         if (row < N && col <= row) {
           const double r2 = (row == col) ? 0.0 : fma(-2.0, acc[rb][cb][e], xsq[row] + bsq);
-          S[row * lds + col] = kernel_of_r2<KIND>(r2, variance);
+          const double kv = kernel_of_r2<KIND>(r2, variance);
+          S[row * lds + col] = (row == col) ? kv + diag_add : kv;
         }
       }
   }
@@ -1775,7 +1776,7 @@ hipError_t launch_gemm_tn_lower(hipStream_t s, int64_t N, int64_t K, double alph
 int64_t cand_cov_ws_doubles(int64_t N, int DP) { return N * ((DP + 3) / 4 * 4) + N; }
 
 hipError_t launch_cand_cov(hipStream_t stream, const GPDev& g, int d, int DP, const double* Xc, int64_t N, double* S,
-                           int64_t lds, double* ws) {
+                           int64_t lds, double* ws, double diag_add) {
   if (N <= 0) return hipSuccess;
   const int KP = (DP + 3) / 4 * 4;
   double* Xs = ws;
@@ -1788,10 +1789,10 @@ hipError_t launch_cand_cov(hipStream_t stream, const GPDev& g, int d, int DP, co
     hipLaunchKernelGGL((cand_scale_kernel<DPV>), dim3(sb), dim3(256), 0, stream, Xc, d, N, g.ls, Xs, xsq);    \
     if (g.kind == OMB_KERNEL_RBF)                                                                             \
       hipLaunchKernelGGL((cand_cov_kernel<DPV, OMB_KERNEL_RBF>), grid, dim3(256), 0, stream, Xs, xsq, N,      \
-                         g.variance, S, lds);                                                                 \
+                         g.variance, S, lds, diag_add);                                                       \
     else                                                                                                      \
       hipLaunchKernelGGL((cand_cov_kernel<DPV, OMB_KERNEL_MATERN52>), grid, dim3(256), 0, stream, Xs, xsq, N, \
-                         g.variance, S, lds);                                                                 \
+                         g.variance, S, lds, diag_add);                                                       \
     break;
   switch (DP) {
     OMB_COV(2) OMB_COV(4) OMB_COV(6) OMB_COV(8) OMB_COV(16) OMB_COV(32) OMB_COV(64)
@@ -1829,6 +1830,11 @@ static hipError_t chol_panel(hipStream_t stream, double* A, int64_t N, int64_t l
   return hipGetLastError();
 }
 
+// Dynamic LDS added to every chol_update_kernel workgroup (tools/ablate/ablate_chol sets it): it caps the
+// workgroups per CU, which decides whether trailing-update workgroups share the diagonal workgroup's CU.
+static size_t g_chol_update_lds = 0;
+void set_chol_update_lds(size_t bytes) { g_chol_update_lds = bytes; }
+
 hipError_t launch_cholesky_mode(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws, int mode,
                                 int spin_limit) {
   if (N <= 0) return hipSuccess;
@@ -1848,11 +1854,11 @@ hipError_t launch_cholesky_mode(hipStream_t stream, double* A, int64_t N, int64_
     }
     const unsigned wgs = (unsigned)(t * (t + 1) / 2);
     if (fuse)
-      hipLaunchKernelGGL((chol_update_kernel<true>), dim3(wgs), dim3(256), 0, stream, A, N, lda, k, t, ws, info, flags,
-                         spin_limit);
+      hipLaunchKernelGGL((chol_update_kernel<true>), dim3(wgs), dim3(256), g_chol_update_lds, stream, A, N, lda, k, t, ws,
+                         info, flags, spin_limit);
     else
-      hipLaunchKernelGGL((chol_update_kernel<false>), dim3(wgs), dim3(256), 0, stream, A, N, lda, k, t, ws, info,
-                         flags, spin_limit);
+      hipLaunchKernelGGL((chol_update_kernel<false>), dim3(wgs), dim3(256), g_chol_update_lds, stream, A, N, lda, k, t,
+                         ws, info, flags, spin_limit);
     e = hipGetLastError();
   }
   return e;

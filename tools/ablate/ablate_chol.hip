@@ -71,6 +71,8 @@ static void trace_diag() {
 
 int main(int argc, char** argv) {
   trace_diag();
+  // extra dynamic LDS per update workgroup: 0 (3 workgroups per CU by VGPRs), 16 KB (2), 48 KB (1)
+  const size_t extra[3] = {0, 16 << 10, 48 << 10};
   std::vector<int64_t> sizes;
   for (int i = 1; i < argc; ++i) sizes.push_back(atoll(argv[i]));
   if (sizes.empty()) sizes = {512, 1024, 3000};
@@ -112,6 +114,24 @@ int main(int argc, char** argv) {
       }
     }
     printf("N=%lld  two launches per step %.3f ms (best %.3f)\n", (long long)N, sum2 / reps, best2);
+    {
+      float sx[3] = {0.f, 0.f, 0.f};
+      for (int r = 0; r < reps + 1; ++r)
+        for (int v = 0; v < 3; ++v) {
+          set_chol_update_lds(extra[v]);
+          CK(hipMemcpy(A, A0, N * N * 8, hipMemcpyDeviceToDevice));
+          CK(hipEventRecord(e0));
+          CK(launch_cholesky(0, A, N, N, info, ws));
+          CK(hipEventRecord(e1));
+          CK(hipEventSynchronize(e1));
+          float ms;
+          CK(hipEventElapsedTime(&ms, e0, e1));
+          if (r > 0) sx[v] += ms;
+        }
+      set_chol_update_lds(0);
+      printf("N=%lld  fused, extra LDS per update workgroup 0 / 16 KB / 48 KB: %.3f / %.3f / %.3f ms\n", (long long)N,
+             sx[0] / reps, sx[1] / reps, sx[2] / reps);
+    }
     // the same launch sequence captured once into a hipGraph and replayed (launch-gap ablation)
     float gbest = 1e30f, gsum = 0.f;
     {

@@ -1830,10 +1830,14 @@ static hipError_t chol_panel(hipStream_t stream, double* A, int64_t N, int64_t l
   return hipGetLastError();
 }
 
-// Dynamic LDS added to every chol_update_kernel workgroup (tools/ablate/ablate_chol sets it): it caps the
-// workgroups per CU, which decides whether trailing-update workgroups share the diagonal workgroup's CU.
+// Dynamic LDS added to every chol_update_kernel workgroup: it caps the workgroups per CU.  A knob of
+// tools/ablate/ablate_chol only (built with OMB_TOOLS_KNOBS); the library launches with none.
+#ifdef OMB_TOOLS_KNOBS
 static size_t g_chol_update_lds = 0;
 void set_chol_update_lds(size_t bytes) { g_chol_update_lds = bytes; }
+#else
+constexpr size_t g_chol_update_lds = 0;
+#endif
 
 hipError_t launch_cholesky_mode(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws, int mode,
                                 int spin_limit) {

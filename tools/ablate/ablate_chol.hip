@@ -23,6 +23,7 @@ __device__ unsigned long long g_col[4][64];
     if (cond) g_col[w][j] = __builtin_readcyclecounter();         \
   } while (0)
 
+#define OMB_TOOLS_KNOBS
 #include "../../optimobo_amd/csrc/omb_linalg.hip"
 
 using namespace omb;

@@ -365,14 +365,22 @@ __device__ __forceinline__ void chol64_factor(double (&a)[16], int w, int r, int
   // ---- earlier sub-blocks' columns, as they appear
 #pragma unroll 1
   for (int b = 0; b < w; ++b) {
+    // two published columns per step: row q's entries of columns jj, jj+1 are adjacent in Lb (one b128
+    // read), so a step is 17 b128 reads and 32 fmas (in column order: bitwise the one-column loop); one
+    // column per step took ≈ 530 cycles against the owner's ≈ 470 and fell ≈ 1,300 cycles behind per
+    // sub-block (profiles/r03_v27_chol_column_trace.txt)
 #pragma unroll 1   // rolled: unrolled, the column reads were merged and hoisted (512 VGPRs + spills)
-    for (int jj = 0; jj < 16; ++jj) {
-      while (__hip_atomic_load(&prog[b], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= jj)
+    for (int jj = 0; jj < 16; jj += 2) {
+      while (__hip_atomic_load(&prog[b], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= jj + 1)
         __builtin_amdgcn_s_sleep(1);
-      const double lr = Lb[(b * 64 + r) * kLbP + jj];
+      const double2 lr = *reinterpret_cast<const double2*>(Lb + (b * 64 + r) * kLbP + jj);
 #pragma unroll
-      for (int q = 0; q < 16; ++q) a[q] = fma(-lr, Lb[(b * 64 + 16 * w + q) * kLbP + jj], a[q]);
-      OMB_CHOL_COL(w, 16 * b + jj, r == 0);
+      for (int q = 0; q < 16; ++q) {
+        const double2 v = *reinterpret_cast<const double2*>(Lb + (b * 64 + 16 * w + q) * kLbP + jj);
+        a[q] = fma(-lr.x, v.x, a[q]);
+        a[q] = fma(-lr.y, v.y, a[q]);
+      }
+      OMB_CHOL_COL(w, 16 * b + jj + 1, r == 0);
     }
   }
   // ---- own sub-block

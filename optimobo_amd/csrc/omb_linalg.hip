@@ -321,7 +321,7 @@ __device__ __forceinline__ void static_for(F&& f) {
 //   Lb    4 sub-blocks × 64 rows × kLbP doubles: Lb[(b·64 + r)·kLbP + q] = L[r][16b + q]; the 144-B row
 //         pitch keeps 16 lanes reading 16 different rows conflict-free;
 //   aux   cbuf (2 × 64: the current column, double buffered) | dinv (64: 1/L_jj);
-//   prog  4 ints: columns of sub-block b published to Lb so far.
+//   prog  8 ints: columns of sub-block b published to Lb so far (0..3); W_bb in Lb (4..7).
 constexpr int kLbP = 18;
 constexpr int kLbDoubles = 4 * kNB * kLbP;
 constexpr int kCholAux = 2 * kNB + kNB;
@@ -336,6 +336,55 @@ __device__ __forceinline__ void wf_store(double* p, double v) {
 __device__ __forceinline__ double wf_load(const double* p) {
   return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
                                                       __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// The off-diagonal blocks of W = L⁻¹ into Wf, the MFMA B fragments of chol_panel_kernel:
+//   Wf[(jb·16 + s)·64 + l] = W[16jb + (l & 15)][m(s, l >> 4)],   m(s, g) = 16(s >> 2) + 4g + (s & 3)
+// (k-step s of the panel's output column block jb; only s < 4(jb + 1) is read — the rest of that row
+// block of W is zero — so the panel skips W's upper triangle in whole k-steps).
+// Wave j forms its column block, W_ij = −W_ii Σ_{k=j}^{i−1} L_ik W_kj for i = j+1..3, on MFMA: a product's
+// accumulator layout (lane l: rows 4e + (l >> 4), column l & 15) is the next product's B operand
+// layout, so the W_kj (k > j) stay in registers and only L and the W_ii are read from LDS.
+// Round 3: each wave runs this right after its own sub-block's tail, while the later waves still factor.
+// The sums Σ L_ik W_kj need only L (complete for row block i once sub-blocks < i are factored) and the
+// wave's own earlier blocks; only the final product waits for W_ii (wdone[i], set by wave i after its
+// tail).  After the last sub-block only the three products with W_33 remain (the whole inverse used to
+// follow a barrier after the factor: ≈ 4.8k cycles on the step's chain, profiles/r03_v37_chol_trace_paired_consumer.txt).
+__device__ __forceinline__ void chol64_inverse(int w, int r, const double* Lb, int* wdone, double* __restrict__ Wf) {
+  const int c = r & 15, g = r >> 4;
+  d4 Wc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) Wc[i] = d4{0.0, 0.0, 0.0, 0.0};
+  static_for<1, 4>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+    if (i > w) {
+      d4 T = d4{0.0, 0.0, 0.0, 0.0};
+      static_for<0, i>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        if (k >= w) {
+          static_for<0, 4>([&](auto sc) {
+            constexpr int s = decltype(sc)::value;
+            const double av = Lb[(k * 64 + 16 * i + c) * kLbP + 4 * s + g];   // L[16i + c][16k + 4s + g]
+            // B operand W_kj[4s + g][c]: W_ww from LDS, the others from registers
+            const double bv = (k == w) ? Lb[(k * 64 + 16 * k + 4 * s + g) * kLbP + c] : Wc[k][s];
+            T = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, T, 0, 0, 0);
+          });
+        }
+      });
+      // W_ii in Lb (published by wave i after its tail)
+      while (__hip_atomic_load(&wdone[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+        __builtin_amdgcn_s_sleep(1);
+      d4 R = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        R = __builtin_amdgcn_mfma_f64_16x16x4f64(Lb[(i * 64 + 16 * i + c) * kLbP + 4 * s + g], T[s], R, 0, 0, 0);
+      Wc[i] = -R;
+      // W[16i + 4e + g][16w + c]: jb = i, s = 4w + (c & 3), lane 4e + g + 16 (c >> 2)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) wf_store(&Wf[(i * 16 + 4 * w + (c & 3)) * 64 + 4 * e + g + 16 * (c >> 2)], Wc[i][e]);
+    }
+  });
+  OMB_CHOL_TRACE(16, w == 0 && r == 0);
 }
 
 // Factor a 64×64 SPD block with the 4 waves of a 256-thread workgroup: thread (wave w, lane r) holds
@@ -486,54 +535,13 @@ __device__ __forceinline__ void chol64_factor(double (&a)[16], int w, int r, int
     // W_bb's fragments: rows jb = b, k-steps s = 4b + u: W[16b + c][16b + 4g + u]
 #pragma unroll
     for (int u = 0; u < 4; ++u) wf_store(&Wf[(b * 16 + 4 * b + u) * 64 + r], Lb[(b * 64 + 16 * b + c) * kLbP + 4 * g + u]);
+    // W_bb is in Lb: release it to the waves forming W's earlier column blocks (wdone = prog + 4)
+    if (r == 0) __hip_atomic_store(&prog[4 + b], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     OMB_CHOL_TRACE(10 + b, r == 0);
   });
+  chol64_inverse(w, r, Lb, prog + 4, Wf);
 }
 
-// After chol64_factor and a barrier: the off-diagonal blocks of W = L⁻¹ into Wf, the MFMA B fragments
-// of chol_panel_kernel:
-//   Wf[(jb·16 + s)·64 + l] = W[16jb + (l & 15)][m(s, l >> 4)],   m(s, g) = 16(s >> 2) + 4g + (s & 3)
-// (k-step s of the panel's output column block jb; only s < 4(jb + 1) is read — the rest of that row
-// block of W is zero — so the panel skips W's upper triangle in whole k-steps).
-// Wave j forms its column block, W_ij = −W_ii Σ_{k=j}^{i−1} L_ik W_kj for i = j+1..3, on MFMA: a product's
-// accumulator layout (lane l: rows 4e + (l >> 4), column l & 15) is the next product's B operand
-// layout, so the W_kj (k > j) stay in registers and only L and the W_ii are read from LDS.
-__device__ __forceinline__ void chol64_inverse(int w, int r, const double* Lb, double* __restrict__ Wf) {
-  const int c = r & 15, g = r >> 4;
-  d4 Wc[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) Wc[i] = d4{0.0, 0.0, 0.0, 0.0};
-  static_for<1, 4>([&](auto ic) {
-    constexpr int i = decltype(ic)::value;
-    if (i > w) {
-      d4 T = d4{0.0, 0.0, 0.0, 0.0};
-      static_for<0, i>([&](auto kc) {
-        constexpr int k = decltype(kc)::value;
-        if (k >= w) {
-          static_for<0, 4>([&](auto sc) {
-            constexpr int s = decltype(sc)::value;
-            const double av = Lb[(k * 64 + 16 * i + c) * kLbP + 4 * s + g];   // L[16i + c][16k + 4s + g]
-            // B operand W_kj[4s + g][c]: W_ww from LDS, the others from registers
-            const double bv = (k == w) ? Lb[(k * 64 + 16 * k + 4 * s + g) * kLbP + c] : Wc[k][s];
-            T = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, T, 0, 0, 0);
-          });
-        }
-      });
-      d4 R = d4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-        R = __builtin_amdgcn_mfma_f64_16x16x4f64(Lb[(i * 64 + 16 * i + c) * kLbP + 4 * s + g], T[s], R, 0, 0, 0);
-      Wc[i] = -R;
-      // W[16i + 4e + g][16w + c]: jb = i, s = 4w + (c & 3), lane 4e + g + 16 (c >> 2)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) wf_store(&Wf[(i * 16 + 4 * w + (c & 3)) * 64 + 4 * e + g + 16 * (c >> 2)], Wc[i][e]);
-    }
-  });
-  OMB_CHOL_TRACE(16, w == 0 && r == 0);
-}
-
-// Step 0's diagonal block; it also zeroes info and the fused steps' flags (the first kernel of the
-// factorisation, so no memset launches precede it).
 __global__ __launch_bounds__(256) void chol_diag_kernel(double* __restrict__ A, int64_t N, int64_t lda,
                                                          double* __restrict__ ws, int* __restrict__ info,
                                                          int* __restrict__ flags, int nflags) {
@@ -541,13 +549,13 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(double* __restrict__ A, 
   if (threadIdx.x == 0) *info = 0;
   __shared__ __attribute__((aligned(16))) double Lb[kLbDoubles];
   __shared__ double aux[kCholAux];
-  __shared__ int prog[4];
+  __shared__ int prog[8];   // column progress per sub-block | W_bb published
   __shared__ int bad_lds[1];
   const int nb = (int)(N < kNB ? N : kNB);
   const int r = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   OMB_CHOL_TRACE(0, threadIdx.x == 0);
   if (threadIdx.x == 0) bad_lds[0] = 0;
-  if (threadIdx.x < 4) prog[threadIdx.x] = 0;
+  if (threadIdx.x < 8) prog[threadIdx.x] = 0;
   double a[16];
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
@@ -558,11 +566,10 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(double* __restrict__ A, 
   }
   __syncthreads();
   OMB_CHOL_TRACE(1, threadIdx.x == 0);
-  chol64_factor(a, w, r, nb, Lb, aux, prog, bad_lds, A, lda, 0, ws);
+  chol64_factor(a, w, r, nb, Lb, aux, prog, bad_lds, A, lda, 0, ws);   // with W = L⁻¹ (chol64_inverse)
   __syncthreads();
   OMB_CHOL_TRACE(15, threadIdx.x == 0);
   if (threadIdx.x == 0 && bad_lds[0]) atomicCAS(info, 0, bad_lds[0]);
-  chol64_inverse(w, r, Lb, ws);
 }
 
 // Panel of step `step`: rows c0+64 .. N−1, L21 = A21 · Wᵀ (W = L_kk⁻¹ from the fragments of chol64_factor /
@@ -665,7 +672,7 @@ __global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A
   static_assert(2 * 2 * kGK * kGP <= kLbDoubles && kNB * (kNB + 1) <= kLbDoubles, "LDS carve-up");
   __shared__ __attribute__((aligned(16))) double smem[kLbDoubles];
   __shared__ double aux[kCholAux];
-  __shared__ int prog[4];
+  __shared__ int prog[8];   // column progress per sub-block | W_bb published
   auto& As = *reinterpret_cast<double (*)[2][kGK][kGP]>(smem);                      // As[buf][k][m] = L21(m0 + m, k0 + k)
   auto& Bs = *reinterpret_cast<double (*)[2][kGK][kGP]>(smem + 2 * kGK * kGP);      // Bs[buf][k][n] = L21(n0 + n, k0 + k)
   __shared__ int bad_lds[1];
@@ -865,12 +872,11 @@ __global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A
     a[q] = (r < nb && c <= r) ? D[r * 65 + c] : (c == r ? 1.0 : 0.0);
   }
   if (tid == 0) bad_lds[0] = 0;
-  if (tid < 4) prog[tid] = 0;
+  if (tid < 8) prog[tid] = 0;
   __syncthreads();                                           // D consumed: smem becomes Lb
-  chol64_factor(a, w, r, nb, smem, aux, prog, bad_lds, A, lda, r0, ws);
+  chol64_factor(a, w, r, nb, smem, aux, prog, bad_lds, A, lda, r0, ws);   // with W = L⁻¹ (chol64_inverse)
   __syncthreads();
   if (tid == 0 && bad_lds[0]) atomicCAS(info, 0, (int)(r0 + bad_lds[0]));
-  chol64_inverse(w, r, smem, ws);
   if constexpr (FUSE) {
     // publish W_{k+1} (also after a bad pivot: the waiting workgroups must finish; info marks the result):
     // every thread's coherent fragment stores complete (vmcnt 0), then the flag

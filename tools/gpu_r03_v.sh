@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 pass V: Cholesky consumers apply two published columns per step; traces, parity, config-6 bench.
+# Round-3 pass V: Cholesky diagonal factor changes; traces, parity, config-6 bench.
 set -e
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp

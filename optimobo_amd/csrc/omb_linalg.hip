@@ -302,7 +302,8 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 // ----------------------------------------------------------------------------- Cholesky, fused steps
-// The blocked factorisation as two kernels per 64-column step k (launch_cholesky):
+// The blocked factorisation per 64-column step k (launch_cholesky; round 3 folds the panel into the update
+// launch, see chol_update_kernel<FUSE>):
 //   chol_panel_kernel   the panel below the diagonal block, L21 = A21 · W_kkᵀ with W_kk = L_kk⁻¹, on
 //                       MFMA (16 rows per 2-wave workgroup; W_kk's B fragments read from the workspace);
 //   chol_update_kernel  the trailing update A22 −= L21 L21ᵀ (lower triangle, 64×64 MFMA tiles) whose

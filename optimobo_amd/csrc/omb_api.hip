@@ -307,7 +307,7 @@ hipError_t posterior_any(omb_ctx* ctx, const GPArgs& args, const double* const* 
     for (int64_t c0 = 0; c0 < N; c0 += Nc) {
       const int64_t nc = (N - c0) < Nc ? (N - c0) : Nc;
       hipError_t e = launch_kernel_block(ctx->stream, args, o, Xc + c0 * args.d, nc, Kst);
-      if (e == hipSuccess) e = launch_gemm_nn(ctx->stream, n, nc, n, 1.0, Ld[o], n, Kst, nc, 0.0, V, nc);
+      if (e == hipSuccess) e = launch_gemm_ltri_nn(ctx->stream, n, nc, 1.0, Ld[o], n, Kst, nc, 0.0, V, nc);
       if (e == hipSuccess)
         e = launch_post_colreduce(ctx->stream, Kst, V, n, nc, args.gp[o].alpha, args.gp[o].variance,
                                   mu + (int64_t)o * N + c0, var + (int64_t)o * N + c0);
@@ -958,7 +958,7 @@ static hipError_t cov_prepare(omb_ctx* ctx, const ObjState& s, const double* Xc,
   args.d = s.d;
   args.DP = s.DP;
   hipError_t e = launch_kernel_block(ctx->stream, args, 0, Xc, N, Kst);
-  if (e == hipSuccess) e = launch_gemm_nn(ctx->stream, s.n, N, s.n, 1.0, s.Ld, s.n, Kst, N, 0.0, V, N);
+  if (e == hipSuccess) e = launch_gemm_ltri_nn(ctx->stream, s.n, N, 1.0, s.Ld, s.n, Kst, N, 0.0, V, N);
   if (e == hipSuccess) e = launch_post_colreduce(ctx->stream, Kst, V, s.n, N, s.dev.alpha, s.dev.variance, mu, var);
   return e;
 }

@@ -106,6 +106,10 @@ hipError_t launch_sobol(hipStream_t stream, const void* state_dev, int d, int bi
 // Dense fp64 linear algebra for Thompson sampling (omb_linalg.hip).  Row-major throughout.
 constexpr int64_t kSelectMaxN = 1 << 18;    // candidates per selection (LDS exclusion bitmap)
 constexpr int64_t kMaxCovN = 32768;         // candidates of one full posterior covariance
+// C (M, Nc) = β·C + α·L·B with L (M, M) lower-triangular: its upper triangle is never read, and slabs past
+// each row tile are skipped (half the work of launch_gemm_nn)
+hipError_t launch_gemm_ltri_nn(hipStream_t s, int64_t M, int64_t Nc, double alpha, const double* L, int64_t ldl,
+                               const double* B, int64_t ldb, double beta, double* C, int64_t ldc);
 // C (M, Nc) = β C + α A B, A (M, K), B (K, Nc).
 hipError_t launch_gemm_nn(hipStream_t s, int64_t M, int64_t Nc, int64_t K, double alpha, const double* A, int64_t lda,
                           const double* B, int64_t ldb, double beta, double* C, int64_t ldc);

@@ -31,14 +31,18 @@ constexpr int kGT = 64;         // C tile edge
 constexpr int kGK = 16;         // k slab
 constexpr int kGP = kGT + 2;    // LDS row pitch in doubles (rows 528 B apart: conflict-free stores)
 
-template <bool TA, bool TB, bool BTRI, bool LOWER>
+// ATRI (round 3): op(A) is lower-triangular (op(A)(m, k) = 0 for k > m, e.g. the dense L⁻¹ of V = L⁻¹K*):
+// slabs past the tile's last row are skipped and the entries above the diagonal read as zero, so the
+// upper triangle is never read (as the packed posterior path never reads it) and half the work goes.
+template <bool TA, bool TB, bool BTRI, bool LOWER, bool ATRI = false>
 __global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t Nc, int64_t K, double alpha,
                                                    const double* __restrict__ A, int64_t lda,
                                                    const double* __restrict__ B, int64_t ldb, double beta,
                                                    double* __restrict__ C, int64_t ldc,
                                                    const double* __restrict__ col_bias, int64_t kchunk,
                                                    int64_t zstride) {
-  const int64_t m0 = (int64_t)blockIdx.y * kGT, n0 = (int64_t)blockIdx.x * kGT;
+  // ATRI: the last row tiles carry the most slabs, so they are dispatched first
+  const int64_t m0 = (int64_t)(ATRI ? gridDim.y - 1 - blockIdx.y : blockIdx.y) * kGT, n0 = (int64_t)blockIdx.x * kGT;
   if (LOWER && n0 > m0) return;   // tile strictly above the diagonal
   __shared__ double As[2][kGK][kGP];   // As[k][m] = op(A)(m0 + m, k0 + k)
   __shared__ double Bs[2][kGK][kGP];   // Bs[k][n] = op(B)(k0 + k, n0 + n)
@@ -47,6 +51,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t Nc, int64_
   const int wm = wave >> 1, wn = wave & 1;
   // with BTRI, slabs past the tile's last column are all zero in op(B)
   int64_t kend = BTRI ? (K < n0 + kGT ? K : n0 + kGT) : K;
+  if (ATRI && kend > m0 + kGT) kend = m0 + kGT;
   // split K (gridDim.z > 1): slice z covers [z·kchunk, (z+1)·kchunk) into its own partial C + z·zstride
   const int64_t kbeg = (int64_t)blockIdx.z * kchunk;
   if (gridDim.z > 1) {
@@ -63,7 +68,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t Nc, int64_
       const int idx = tid + 256 * e;
       const int am = TA ? (idx & 63) : (idx >> 4), ak = TA ? (idx >> 6) : (idx & 15);
       const int64_t gm = m0 + am, gka = k0 + ak;
-      ra[e] = (gm < M && gka < K) ? (TA ? A[gka * lda + gm] : A[gm * lda + gka]) : 0.0;
+      ra[e] = (gm < M && gka < K && !(ATRI && gka > gm)) ? (TA ? A[gka * lda + gm] : A[gm * lda + gka]) : 0.0;
       const int bn = TB ? (idx >> 4) : (idx & 63), bk = TB ? (idx & 15) : (idx >> 6);
       const int64_t gn = n0 + bn, gkb = k0 + bk;
       const bool ok = gn < Nc && gkb < K && !(BTRI && gkb > gn);
@@ -130,14 +135,14 @@ __global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t Nc, int64_
       }
 }
 
-template <bool TA, bool TB, bool BTRI, bool LOWER>
+template <bool TA, bool TB, bool BTRI, bool LOWER, bool ATRI = false>
 static hipError_t gemm(hipStream_t stream, int64_t M, int64_t Nc, int64_t K, double alpha, const double* A,
                        int64_t lda, const double* B, int64_t ldb, double beta, double* C, int64_t ldc,
                        const double* col_bias) {
   if (M <= 0 || Nc <= 0) return hipSuccess;
   dim3 grid((unsigned)((Nc + kGT - 1) / kGT), (unsigned)((M + kGT - 1) / kGT));
-  hipLaunchKernelGGL((gemm_kernel<TA, TB, BTRI, LOWER>), grid, dim3(256), 0, stream, M, Nc, K, alpha, A, lda, B, ldb,
-                     beta, C, ldc, col_bias, (int64_t)0, (int64_t)0);
+  hipLaunchKernelGGL((gemm_kernel<TA, TB, BTRI, LOWER, ATRI>), grid, dim3(256), 0, stream, M, Nc, K, alpha, A, lda, B,
+                     ldb, beta, C, ldc, col_bias, (int64_t)0, (int64_t)0);
   return hipGetLastError();
 }
 
@@ -1778,6 +1783,11 @@ __global__ __launch_bounds__(256) void select_greedy_kernel(const long long* __r
 }
 
 // ----------------------------------------------------------------------------- launchers
+hipError_t launch_gemm_ltri_nn(hipStream_t s, int64_t M, int64_t Nc, double alpha, const double* L, int64_t ldl,
+                               const double* B, int64_t ldb, double beta, double* C, int64_t ldc) {
+  return gemm<false, false, false, false, true>(s, M, Nc, M, alpha, L, ldl, B, ldb, beta, C, ldc, nullptr);
+}
+
 hipError_t launch_gemm_nn(hipStream_t s, int64_t M, int64_t Nc, int64_t K, double alpha, const double* A, int64_t lda,
                           const double* B, int64_t ldb, double beta, double* C, int64_t ldc) {
   return gemm<false, false, false, false>(s, M, Nc, K, alpha, A, lda, B, ldb, beta, C, ldc, nullptr);

@@ -165,6 +165,28 @@ def test_dense_posterior_path_vs_oracle(ctx, n, d, N):
     np.testing.assert_allclose(v[0].cpu().numpy(), vo[:, 0], rtol=1e-6, atol=1e-9 * var)
 
 
+def test_dense_paths_read_lower_triangle_of_linv_only(ctx):
+    """V = L⁻¹K* (launch_gemm_ltri_nn, dense posterior and full covariance) reads only the lower
+    triangle of L⁻¹, as the fused kernel's packed L⁻¹ does: junk above the diagonal changes nothing."""
+    from optimobo_amd.gp import GPState
+    rng = np.random.default_rng(41)
+    n, d, N = 1100, 3, 777
+    X = rng.uniform(0, 1, (n, d))
+    y = np.sin(3 * X).sum(1)
+    st = GPState(X, y, np.full(d, 0.7), float(np.var(y)))
+    Xc = dev(rng.uniform(0, 1, (N, d)))
+    ctx.set_gp_state(0, st)
+    mu, var = ctx.posterior(Xc, n_obj=1)
+    mc, cov = ctx.posterior_cov(0, Xc[:300])
+    assert np.all(np.triu(st.Linv, 1) == 0)
+    st.Linv = st.Linv + np.triu(rng.uniform(-1e3, 1e3, (n, n)), 1)
+    ctx.set_gp_state(0, st)
+    mu2, var2 = ctx.posterior(Xc, n_obj=1)
+    mc2, cov2 = ctx.posterior_cov(0, Xc[:300])
+    assert torch.equal(mu, mu2) and torch.equal(var, var2)
+    assert torch.equal(mc, mc2) and torch.equal(cov, cov2)
+
+
 def test_dense_path_in_fused_chain(ctx):
     """The fused chain (plan → eval_argmax) runs the dense path too; same values as per-kernel calls."""
     from optimobo_amd import pareto

@@ -1,0 +1,246 @@
+// Dense fp64 GEMM on gfx950 for the Thompson-sampling chain (omb_api.hip posterior_samples, §4b of
+// DESIGN.md) and the GP fit:
+//   V = L⁻¹K* (dense posterior, full covariance), Σ −= VᵀV (lower triangle), Y = μ + Z·Lᵀ (joint draws),
+//   the blocked triangular inverse (launch_trinv) and the GP fit's α.
+//
+//   gemm_kernel        C = β·C + α·op(A)·op(B) (+ column bias) on v_mfma_f64_16x16x4f64: one 64×64 C
+//                      tile per 256-thread workgroup (4 waves × 32×32), k-slabs of 16 double-buffered
+//                      in LDS behind a register prefetch.  Variants: store the lower triangle only
+//                      (SYRK-shaped Σ update), "op(B)(k, j) = 0 for k > j" (a lower-triangular factor
+//                      read transposed: the samples μ + L z) and "op(A)(m, k) = 0 for k > m" (L⁻¹).
+//
+// Built on its own with -mllvm -amdgpu-mfma-vgpr-form (Makefile): in the default AGPR form the compiler
+// carries the accumulators across the slab loop in VGPRs and copies all 32 registers to AGPRs and back
+// every slab (64 VALU instructions per 16 MFMAs; FP64 MFMA does not overlap VALU on gfx950).  The
+// Cholesky kernels in omb_linalg.hip keep the default form: their diagonal-block chain runs slower in
+// the VGPR form (N = 3000 factorisation 1.37 → 1.40 ms, profiles/r03_z2_chol_{agpr,vgpr}.txt).
+#include "omb_internal.h"
+
+namespace omb {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+// ATRI (round 3): op(A) is lower-triangular (op(A)(m, k) = 0 for k > m, e.g. the dense L⁻¹ of V = L⁻¹K*):
+// slabs past the tile's last row are skipped and the entries above the diagonal read as zero, so the
+// upper triangle is never read (as the packed posterior path never reads it) and half the work goes.
+template <bool TA, bool TB, bool BTRI, bool LOWER, bool ATRI = false>
+__global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t Nc, int64_t K, double alpha,
+                                                   const double* __restrict__ A, int64_t lda,
+                                                   const double* __restrict__ B, int64_t ldb, double beta,
+                                                   double* __restrict__ C, int64_t ldc,
+                                                   const double* __restrict__ col_bias, int64_t kchunk,
+                                                   int64_t zstride) {
+  // ATRI: the last row tiles carry the most slabs, so they are dispatched first
+  const int64_t m0 = (int64_t)(ATRI ? gridDim.y - 1 - blockIdx.y : blockIdx.y) * kGT, n0 = (int64_t)blockIdx.x * kGT;
+  if (LOWER && n0 > m0) return;   // tile strictly above the diagonal
+  __shared__ double As[2][kGK][kGP];   // As[k][m] = op(A)(m0 + m, k0 + k)
+  __shared__ double Bs[2][kGK][kGP];   // Bs[k][n] = op(B)(k0 + k, n0 + n)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  // with BTRI, slabs past the tile's last column are all zero in op(B)
+  int64_t kend = BTRI ? (K < n0 + kGT ? K : n0 + kGT) : K;
+  if (ATRI && kend > m0 + kGT) kend = m0 + kGT;
+  // split K (gridDim.z > 1): slice z covers [z·kchunk, (z+1)·kchunk) into its own partial C + z·zstride
+  const int64_t kbeg = (int64_t)blockIdx.z * kchunk;
+  if (gridDim.z > 1) {
+    kend = kend < kbeg + kchunk ? kend : kbeg + kchunk;
+    C += (int64_t)blockIdx.z * zstride;
+  }
+
+  // 1024 elements of each operand per slab, 4 per thread; consecutive threads walk the
+  // contiguous dimension of the stored matrix (coalesced), LDS stores land conflict-free.
+  // Rows of op(A) past M and columns of op(B) past Nc only feed C entries that are never stored,
+  // so their addresses are clamped into the matrix rather than masked; each element keeps a
+  // running pointer (one 64-bit add per slab), and only the last slab, when it reaches past K,
+  // checks k.
+  const double* pa[4];
+  const double* pb[4];
+  int ak_[4], bk_[4];
+  int64_t gm_[4], gn_[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int idx = tid + 256 * e;
+    const int am = TA ? (idx & 63) : (idx >> 4), ak = TA ? (idx >> 6) : (idx & 15);
+    const int bn = TB ? (idx >> 4) : (idx & 63), bk = TB ? (idx & 15) : (idx >> 6);
+    gm_[e] = m0 + am;
+    gn_[e] = n0 + bn;
+    ak_[e] = ak;
+    bk_[e] = bk;
+    const int64_t cm = gm_[e] < M ? gm_[e] : M - 1, cn = gn_[e] < Nc ? gn_[e] : Nc - 1;
+    pa[e] = TA ? A + (kbeg + ak) * lda + cm : A + cm * lda + kbeg + ak;
+    pb[e] = TB ? B + cn * ldb + kbeg + bk : B + (kbeg + bk) * ldb + cn;
+  }
+  const int64_t sa = TA ? kGK * lda : kGK, sb = TB ? kGK : kGK * ldb;   // one slab along k
+  double ra[4], rb[4];
+  auto fetch = [&](int64_t k0, bool edge) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t gka = k0 + ak_[e], gkb = k0 + bk_[e];
+      double va, vb;
+      if (edge) {
+        va = gka < kend ? *pa[e] : 0.0;
+        vb = gkb < kend ? *pb[e] : 0.0;
+      } else {
+        va = *pa[e];
+        vb = *pb[e];
+      }
+      ra[e] = (ATRI && gka > gm_[e]) ? 0.0 : va;
+      rb[e] = (BTRI && gkb > gn_[e]) ? 0.0 : vb;
+      pa[e] += sa;
+      pb[e] += sb;
+    }
+  };
+  auto stash = [&](int buf) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int idx = tid + 256 * e;
+      As[buf][TA ? (idx >> 6) : (idx & 15)][TA ? (idx & 63) : (idx >> 4)] = ra[e];
+      Bs[buf][TB ? (idx & 15) : (idx >> 6)][TB ? (idx >> 4) : (idx & 63)] = rb[e];
+    }
+  };
+
+  d4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+  auto multiply = [&](int buf) {
+#pragma unroll
+    for (int ks = 0; ks < kGK / 4; ++ks) {
+      const int kk = 4 * ks + (lane >> 4);
+      const double a0 = As[buf][kk][32 * wm + (lane & 15)];
+      const double a1 = As[buf][kk][32 * wm + 16 + (lane & 15)];
+      const double b0 = Bs[buf][kk][32 * wn + (lane & 15)];
+      const double b1 = Bs[buf][kk][32 * wn + 16 + (lane & 15)];
+      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+    }
+  };
+
+  if (kend > kbeg) {
+    fetch(kbeg, kbeg + kGK > kend);
+    stash(0);
+    __syncthreads();
+    // every slab followed by a full one: its loads are in flight while this one multiplies
+    int buf = 0;
+    int64_t k0 = kbeg;
+    for (; k0 + 2 * kGK <= kend; k0 += kGK) {
+      fetch(k0 + kGK, false);
+      multiply(buf);
+      // the other buffer was last read in the previous slab, which every wave has finished
+      stash(buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+    }
+    if (k0 + kGK < kend) {   // a last, partial slab (kend = K, K not a multiple of 16)
+      fetch(k0 + kGK, true);
+      multiply(buf);
+      stash(buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+    }
+    multiply(buf);
+  }
+
+  // C/D map of v_mfma_f64_16x16x4f64: col = lane & 15, row = (lane >> 4) + 4·i
+#pragma unroll
+  for (int rb2 = 0; rb2 < 2; ++rb2)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t row = m0 + 32 * wm + 16 * rb2 + (lane >> 4) + 4 * i;
+        const int64_t col = n0 + 32 * wn + 16 * cb + (lane & 15);
+        if (row < M && col < Nc && (!LOWER || col <= row)) {
+          double v = alpha * acc[rb2][cb][i];
+          if (beta != 0.0) v = fma(beta, C[row * ldc + col], v);
+          if (col_bias) v += col_bias[col];
+          C[row * ldc + col] = v;
+        }
+      }
+}
+
+template <bool TA, bool TB, bool BTRI, bool LOWER, bool ATRI = false>
+static hipError_t gemm(hipStream_t stream, int64_t M, int64_t Nc, int64_t K, double alpha, const double* A,
+                       int64_t lda, const double* B, int64_t ldb, double beta, double* C, int64_t ldc,
+                       const double* col_bias) {
+  if (M <= 0 || Nc <= 0) return hipSuccess;
+  dim3 grid((unsigned)((Nc + kGT - 1) / kGT), (unsigned)((M + kGT - 1) / kGT));
+  hipLaunchKernelGGL((gemm_kernel<TA, TB, BTRI, LOWER, ATRI>), grid, dim3(256), 0, stream, M, Nc, K, alpha, A, lda, B,
+                     ldb, beta, C, ldc, col_bias, (int64_t)0, (int64_t)0);
+  return hipGetLastError();
+}
+
+// C (M, Nc) = bias + Σ_z P[z] in slice order (deterministic), P[z] (M, Nc) dense at P + z·zstride.
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const double* __restrict__ P, int S, int64_t zstride,
+                                                            int64_t M, int64_t Nc, const double* __restrict__ bias,
+                                                            double* __restrict__ C, int64_t ldc) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * Nc) return;
+  const int64_t r = i / Nc, c = i - r * Nc;
+  double v = 0.0;
+  for (int z = 0; z < S; ++z) v += P[z * zstride + i];
+  C[r * ldc + c] = v + (bias ? bias[c] : 0.0);
+}
+
+
+// ----------------------------------------------------------------------------- launchers
+hipError_t launch_gemm_ltri_nn(hipStream_t s, int64_t M, int64_t Nc, double alpha, const double* L, int64_t ldl,
+                               const double* B, int64_t ldb, double beta, double* C, int64_t ldc) {
+  return gemm<false, false, false, false, true>(s, M, Nc, M, alpha, L, ldl, B, ldb, beta, C, ldc, nullptr);
+}
+
+hipError_t launch_gemm_nn(hipStream_t s, int64_t M, int64_t Nc, int64_t K, double alpha, const double* A, int64_t lda,
+                          const double* B, int64_t ldb, double beta, double* C, int64_t ldc) {
+  return gemm<false, false, false, false>(s, M, Nc, K, alpha, A, lda, B, ldb, beta, C, ldc, nullptr);
+}
+
+hipError_t launch_gemm_tn_lower(hipStream_t s, int64_t N, int64_t K, double alpha, const double* A, int64_t lda,
+                                double beta, double* C, int64_t ldc) {
+  return gemm<true, false, false, true>(s, N, N, K, alpha, A, lda, A, lda, beta, C, ldc, nullptr);
+}
+
+// K slices of the sample product: enough (tile, slice) workgroups to fill the chip (≥ 1024), slices of
+// ≥ 256 columns.  At B = 64 draws of N = 3000 candidates the unsplit product has 47 workgroups
+// (208 µs, profiles/r02_v21_c6_kernel_stats.csv).
+static int samples_split(int64_t N, int B) {
+  const int64_t tiles = ((B + kGT - 1) / kGT) * ((N + kGT - 1) / kGT);
+  int64_t S = (1024 + tiles - 1) / tiles;
+  const int64_t smax = (N + 255) / 256;
+  if (S > smax) S = smax;
+  if (S > 16) S = 16;
+  return S < 1 ? 1 : (int)S;
+}
+
+int64_t chol_samples_ws_doubles(int64_t N, int B) {
+  const int S = samples_split(N, B);
+  return S > 1 ? (int64_t)S * B * N : 0;
+}
+
+hipError_t launch_chol_samples(hipStream_t stream, const double* L, int64_t N, int64_t ldl, const double* mu,
+                               const double* Zt, int B, double* Y, double* ws) {
+  // Y (B, N) = Zt · Lᵀ + μ  with  op(B)(k, j) = L[j][k] for k ≤ j (the factor's upper part is ignored)
+  const int S = samples_split(N, B);
+  if (S == 1) return gemm<false, true, true, false>(stream, B, N, N, 1.0, Zt, N, L, ldl, 0.0, Y, N, mu);
+  const int64_t kchunk = ((N + S - 1) / S + kGK - 1) / kGK * kGK;
+  const int64_t zstride = (int64_t)B * N;
+  dim3 grid((unsigned)((N + kGT - 1) / kGT), (unsigned)((B + kGT - 1) / kGT), (unsigned)S);
+  hipLaunchKernelGGL((gemm_kernel<false, true, true, false>), grid, dim3(256), 0, stream, (int64_t)B, N, N, 1.0, Zt,
+                     N, L, ldl, 0.0, ws, N, (const double*)nullptr, kchunk, zstride);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int64_t tot = (int64_t)B * N;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, ws, S, zstride,
+                     (int64_t)B, N, mu, Y, N);
+  return hipGetLastError();
+}
+
+hipError_t launch_gemm_tn(hipStream_t s, int64_t M, int64_t Nc, int64_t K, double alpha, const double* A, int64_t lda,
+                          const double* B, int64_t ldb, double beta, double* C, int64_t ldc) {
+  return gemm<true, false, false, false>(s, M, Nc, K, alpha, A, lda, B, ldb, beta, C, ldc, nullptr);
+}
+
+}  // namespace omb

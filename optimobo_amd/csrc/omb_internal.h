@@ -106,6 +106,10 @@ hipError_t launch_sobol(hipStream_t stream, const void* state_dev, int d, int bi
 // Dense fp64 linear algebra for Thompson sampling (omb_linalg.hip).  Row-major throughout.
 constexpr int64_t kSelectMaxN = 1 << 18;    // candidates per selection (LDS exclusion bitmap)
 constexpr int64_t kMaxCovN = 32768;         // candidates of one full posterior covariance
+// GEMM tile geometry (omb_gemm.hip; the Cholesky trailing update and K(X*, X*) reuse it)
+constexpr int kGT = 64;         // C tile edge
+constexpr int kGK = 16;         // k slab
+constexpr int kGP = kGT + 2;    // LDS row pitch in doubles (rows 528 B apart: conflict-free stores)
 // C (M, Nc) = β·C + α·L·B with L (M, M) lower-triangular: its upper triangle is never read, and slabs past
 // each row tile are skipped (half the work of launch_gemm_nn)
 hipError_t launch_gemm_ltri_nn(hipStream_t s, int64_t M, int64_t Nc, double alpha, const double* L, int64_t ldl,

@@ -7,11 +7,7 @@
 // and then takes the arg-min of every sample, greedily excluding earlier picks
 // (TuRBO_1.select_candidates turbo.py:142-153, TuRBO_M._select_candidates turbo.py:365-383).
 //
-//   gemm_kernel        C = β·C + α·op(A)·op(B) (+ column bias) on v_mfma_f64_16x16x4f64: one 64×64 C
-//                      tile per 256-thread workgroup (4 waves × 32×32), k-slabs of 16 double-buffered
-//                      in LDS behind a register prefetch.  Variants: store the lower triangle only
-//                      (SYRK-shaped Σ update, Cholesky trailing update) and "op(B)(k, j) = 0 for k > j"
-//                      (a lower-triangular factor read transposed: the samples μ + L z).
+//   gemm_kernel        (omb_gemm.hip) V = L⁻¹K*, Σ −= VᵀV, the draws μ + L z and the triangular inverse.
 //   cand_cov_kernel    lower triangle of K(X*, X*) (GPy _unscaled_dist: diagonal forced to 0).
 //   chol_*_kernel      blocked right-looking Cholesky in 64-column steps (see "Cholesky, fused steps").
 //   select_kernel      the greedy per-sample arg-min (np.argmin order) with an LDS exclusion bitmap.
@@ -26,137 +22,8 @@ namespace omb {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-// ----------------------------------------------------------------------------- GEMM
-constexpr int kGT = 64;         // C tile edge
-constexpr int kGK = 16;         // k slab
-constexpr int kGP = kGT + 2;    // LDS row pitch in doubles (rows 528 B apart: conflict-free stores)
+// GEMM (gemm_kernel and its launchers): omb_gemm.hip
 
-// ATRI (round 3): op(A) is lower-triangular (op(A)(m, k) = 0 for k > m, e.g. the dense L⁻¹ of V = L⁻¹K*):
-// slabs past the tile's last row are skipped and the entries above the diagonal read as zero, so the
-// upper triangle is never read (as the packed posterior path never reads it) and half the work goes.
-template <bool TA, bool TB, bool BTRI, bool LOWER, bool ATRI = false>
-__global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t Nc, int64_t K, double alpha,
-                                                   const double* __restrict__ A, int64_t lda,
-                                                   const double* __restrict__ B, int64_t ldb, double beta,
-                                                   double* __restrict__ C, int64_t ldc,
-                                                   const double* __restrict__ col_bias, int64_t kchunk,
-                                                   int64_t zstride) {
-  // ATRI: the last row tiles carry the most slabs, so they are dispatched first
-  const int64_t m0 = (int64_t)(ATRI ? gridDim.y - 1 - blockIdx.y : blockIdx.y) * kGT, n0 = (int64_t)blockIdx.x * kGT;
-  if (LOWER && n0 > m0) return;   // tile strictly above the diagonal
-  __shared__ double As[2][kGK][kGP];   // As[k][m] = op(A)(m0 + m, k0 + k)
-  __shared__ double Bs[2][kGK][kGP];   // Bs[k][n] = op(B)(k0 + k, n0 + n)
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  // with BTRI, slabs past the tile's last column are all zero in op(B)
-  int64_t kend = BTRI ? (K < n0 + kGT ? K : n0 + kGT) : K;
-  if (ATRI && kend > m0 + kGT) kend = m0 + kGT;
-  // split K (gridDim.z > 1): slice z covers [z·kchunk, (z+1)·kchunk) into its own partial C + z·zstride
-  const int64_t kbeg = (int64_t)blockIdx.z * kchunk;
-  if (gridDim.z > 1) {
-    kend = kend < kbeg + kchunk ? kend : kbeg + kchunk;
-    C += (int64_t)blockIdx.z * zstride;
-  }
-
-  // 1024 elements of each operand per slab, 4 per thread; consecutive threads walk the
-  // contiguous dimension of the stored matrix (coalesced), LDS stores land conflict-free.
-  double ra[4], rb[4];
-  auto fetch = [&](int64_t k0) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int idx = tid + 256 * e;
-      const int am = TA ? (idx & 63) : (idx >> 4), ak = TA ? (idx >> 6) : (idx & 15);
-      const int64_t gm = m0 + am, gka = k0 + ak;
-      ra[e] = (gm < M && gka < K && !(ATRI && gka > gm)) ? (TA ? A[gka * lda + gm] : A[gm * lda + gka]) : 0.0;
-      const int bn = TB ? (idx >> 4) : (idx & 63), bk = TB ? (idx & 15) : (idx >> 6);
-      const int64_t gn = n0 + bn, gkb = k0 + bk;
-      const bool ok = gn < Nc && gkb < K && !(BTRI && gkb > gn);
-      rb[e] = ok ? (TB ? B[gn * ldb + gkb] : B[gkb * ldb + gn]) : 0.0;
-    }
-  };
-  auto stash = [&](int buf) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int idx = tid + 256 * e;
-      As[buf][TA ? (idx >> 6) : (idx & 15)][TA ? (idx & 63) : (idx >> 4)] = ra[e];
-      Bs[buf][TB ? (idx & 15) : (idx >> 6)][TB ? (idx >> 4) : (idx & 63)] = rb[e];
-    }
-  };
-
-  d4 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
-
-  if (kend > kbeg) {
-    fetch(kbeg);
-    stash(0);
-  }
-  __syncthreads();
-  int buf = 0;
-  for (int64_t k0 = kbeg; k0 < kend; k0 += kGK) {
-    const bool more = k0 + kGK < kend;
-    if (more) fetch(k0 + kGK);      // in flight while this slab multiplies
-#pragma unroll
-    for (int ks = 0; ks < kGK / 4; ++ks) {
-      const int kk = 4 * ks + (lane >> 4);
-      const double a0 = As[buf][kk][32 * wm + (lane & 15)];
-      const double a1 = As[buf][kk][32 * wm + 16 + (lane & 15)];
-      const double b0 = Bs[buf][kk][32 * wn + (lane & 15)];
-      const double b1 = Bs[buf][kk][32 * wn + 16 + (lane & 15)];
-      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
-    }
-    // the other buffer was last read in the previous slab, which every wave has finished
-    if (more) stash(buf ^ 1);
-    __syncthreads();
-    buf ^= 1;
-  }
-
-  // C/D map of v_mfma_f64_16x16x4f64: col = lane & 15, row = (lane >> 4) + 4·i
-#pragma unroll
-  for (int rb2 = 0; rb2 < 2; ++rb2)
-#pragma unroll
-    for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int64_t row = m0 + 32 * wm + 16 * rb2 + (lane >> 4) + 4 * i;
-        const int64_t col = n0 + 32 * wn + 16 * cb + (lane & 15);
-        if (row < M && col < Nc && (!LOWER || col <= row)) {
-          double v = alpha * acc[rb2][cb][i];
-          if (beta != 0.0) v = fma(beta, C[row * ldc + col], v);
-          if (col_bias) v += col_bias[col];
-          C[row * ldc + col] = v;
-        }
-      }
-}
-
-template <bool TA, bool TB, bool BTRI, bool LOWER, bool ATRI = false>
-static hipError_t gemm(hipStream_t stream, int64_t M, int64_t Nc, int64_t K, double alpha, const double* A,
-                       int64_t lda, const double* B, int64_t ldb, double beta, double* C, int64_t ldc,
-                       const double* col_bias) {
-  if (M <= 0 || Nc <= 0) return hipSuccess;
-  dim3 grid((unsigned)((Nc + kGT - 1) / kGT), (unsigned)((M + kGT - 1) / kGT));
-  hipLaunchKernelGGL((gemm_kernel<TA, TB, BTRI, LOWER, ATRI>), grid, dim3(256), 0, stream, M, Nc, K, alpha, A, lda, B,
-                     ldb, beta, C, ldc, col_bias, (int64_t)0, (int64_t)0);
-  return hipGetLastError();
-}
-
-// C (M, Nc) = bias + Σ_z P[z] in slice order (deterministic), P[z] (M, Nc) dense at P + z·zstride.
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(const double* __restrict__ P, int S, int64_t zstride,
-                                                            int64_t M, int64_t Nc, const double* __restrict__ bias,
-                                                            double* __restrict__ C, int64_t ldc) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= M * Nc) return;
-  const int64_t r = i / Nc, c = i - r * Nc;
-  double v = 0.0;
-  for (int z = 0; z < S; ++z) v += P[z * zstride + i];
-  C[r * ldc + c] = v + (bias ? bias[c] : 0.0);
-}
 
 // ----------------------------------------------------------------------------- K(X*, X*)
 // GPy Stationary._unscaled_dist(X) on X/ℓ: r² = −2·(aᵢ·aⱼ) + (‖aᵢ‖² + ‖aⱼ‖²), diagonal forced
@@ -1783,21 +1650,6 @@ __global__ __launch_bounds__(256) void select_greedy_kernel(const long long* __r
 }
 
 // ----------------------------------------------------------------------------- launchers
-hipError_t launch_gemm_ltri_nn(hipStream_t s, int64_t M, int64_t Nc, double alpha, const double* L, int64_t ldl,
-                               const double* B, int64_t ldb, double beta, double* C, int64_t ldc) {
-  return gemm<false, false, false, false, true>(s, M, Nc, M, alpha, L, ldl, B, ldb, beta, C, ldc, nullptr);
-}
-
-hipError_t launch_gemm_nn(hipStream_t s, int64_t M, int64_t Nc, int64_t K, double alpha, const double* A, int64_t lda,
-                          const double* B, int64_t ldb, double beta, double* C, int64_t ldc) {
-  return gemm<false, false, false, false>(s, M, Nc, K, alpha, A, lda, B, ldb, beta, C, ldc, nullptr);
-}
-
-hipError_t launch_gemm_tn_lower(hipStream_t s, int64_t N, int64_t K, double alpha, const double* A, int64_t lda,
-                                double beta, double* C, int64_t ldc) {
-  return gemm<true, false, false, true>(s, N, N, K, alpha, A, lda, A, lda, beta, C, ldc, nullptr);
-}
-
 int64_t cand_cov_ws_doubles(int64_t N, int DP) { return N * ((DP + 3) / 4 * 4) + N; }
 
 hipError_t launch_cand_cov(hipStream_t stream, const GPDev& g, int d, int DP, const double* Xc, int64_t N, double* S,
@@ -1897,46 +1749,6 @@ hipError_t launch_cholesky(hipStream_t stream, double* A, int64_t N, int64_t lda
   return launch_cholesky_mode(stream, A, N, lda, info, ws, kCholFused, spin_limit);
 }
 
-// K slices of the sample product: enough (tile, slice) workgroups to fill the chip (≥ 1024), slices of
-// ≥ 256 columns.  At B = 64 draws of N = 3000 candidates the unsplit product has 47 workgroups
-// (208 µs, profiles/r02_v21_c6_kernel_stats.csv).
-static int samples_split(int64_t N, int B) {
-  const int64_t tiles = ((B + kGT - 1) / kGT) * ((N + kGT - 1) / kGT);
-  int64_t S = (1024 + tiles - 1) / tiles;
-  const int64_t smax = (N + 255) / 256;
-  if (S > smax) S = smax;
-  if (S > 16) S = 16;
-  return S < 1 ? 1 : (int)S;
-}
-
-int64_t chol_samples_ws_doubles(int64_t N, int B) {
-  const int S = samples_split(N, B);
-  return S > 1 ? (int64_t)S * B * N : 0;
-}
-
-hipError_t launch_chol_samples(hipStream_t stream, const double* L, int64_t N, int64_t ldl, const double* mu,
-                               const double* Zt, int B, double* Y, double* ws) {
-  // Y (B, N) = Zt · Lᵀ + μ  with  op(B)(k, j) = L[j][k] for k ≤ j (the factor's upper part is ignored)
-  const int S = samples_split(N, B);
-  if (S == 1) return gemm<false, true, true, false>(stream, B, N, N, 1.0, Zt, N, L, ldl, 0.0, Y, N, mu);
-  const int64_t kchunk = ((N + S - 1) / S + kGK - 1) / kGK * kGK;
-  const int64_t zstride = (int64_t)B * N;
-  dim3 grid((unsigned)((N + kGT - 1) / kGT), (unsigned)((B + kGT - 1) / kGT), (unsigned)S);
-  hipLaunchKernelGGL((gemm_kernel<false, true, true, false>), grid, dim3(256), 0, stream, (int64_t)B, N, N, 1.0, Zt,
-                     N, L, ldl, 0.0, ws, N, (const double*)nullptr, kchunk, zstride);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  const int64_t tot = (int64_t)B * N;
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, ws, S, zstride,
-                     (int64_t)B, N, mu, Y, N);
-  return hipGetLastError();
-}
-
-hipError_t launch_gemm_tn(hipStream_t s, int64_t M, int64_t Nc, int64_t K, double alpha, const double* A, int64_t lda,
-                          const double* B, int64_t ldb, double beta, double* C, int64_t ldc) {
-  return gemm<true, false, false, false>(s, M, Nc, K, alpha, A, lda, B, ldb, beta, C, ldc, nullptr);
-}
-
 hipError_t launch_trinv(hipStream_t stream, const double* L, int64_t n, int64_t lda, double* X, int64_t ldx,
                         double* T) {
   const int64_t nbk = (n + kNB - 1) / kNB;
@@ -1945,10 +1757,9 @@ hipError_t launch_trinv(hipStream_t stream, const double* L, int64_t n, int64_t 
   for (int64_t i = 1; i < nbk && e == hipSuccess; ++i) {
     const int64_t r0 = i * kNB, rows = (n - r0) < kNB ? (n - r0) : kNB;
     // T (rows, r0) = L[r0:, :r0] · X[:r0, :r0];  X[r0:, :r0] = −X_ii · T
-    e = gemm<false, false, false, false>(stream, rows, r0, r0, 1.0, L + r0 * lda, lda, X, ldx, 0.0, T, r0, nullptr);
+    e = launch_gemm_nn(stream, rows, r0, r0, 1.0, L + r0 * lda, lda, X, ldx, 0.0, T, r0);
     if (e == hipSuccess)
-      e = gemm<false, false, false, false>(stream, rows, r0, rows, -1.0, X + r0 * ldx + r0, ldx, T, r0, 0.0,
-                                           X + r0 * ldx, ldx, nullptr);
+      e = launch_gemm_nn(stream, rows, r0, rows, -1.0, X + r0 * ldx + r0, ldx, T, r0, 0.0, X + r0 * ldx, ldx);
   }
   return e;
 }

@@ -25,6 +25,7 @@ __device__ unsigned long long g_col[4][64];
 
 #define OMB_TOOLS_KNOBS
 #include "../../optimobo_amd/csrc/omb_linalg.hip"
+#include "../../optimobo_amd/csrc/omb_gemm.hip"
 
 using namespace omb;
 

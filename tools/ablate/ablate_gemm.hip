@@ -12,7 +12,7 @@
 
 #include <rocblas/rocblas.h>
 
-#include "../../optimobo_amd/csrc/omb_linalg.hip"
+#include "../../optimobo_amd/csrc/omb_gemm.hip"
 
 using namespace omb;
 

@@ -409,6 +409,9 @@ def main():
     ap.add_argument("--no-kblock", action="store_true")
     ap.add_argument("--chain", default="fused", choices=["fused", "separate", "sobol"])
     ap.add_argument("--stage-timing", action="store_true", help="events around every stage (adds ~5 us/stage)")
+    ap.add_argument("--one-launch", type=int, default=None, choices=[0, 1, 2],
+                    help="omb_debug_set(FUSED_CHAIN): 0 separate launches, 1/2 the one-launch EHVI-2D chain "
+                         "(16 / 8 waves; default: the library's)")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks and the process group only, print what torch.distributed saw")
     ap.add_argument("--cache-seed", type=int, default=1,
@@ -468,6 +471,8 @@ def main():
     cache = pareto.cached_samples(k_obj, 5, seed=args.cache_seed)
 
     ctx = AcqContext(local_rank)
+    if args.one_launch is not None:
+        ctx.debug_set("fused_chain", args.one_launch)
     if acq_kind == "ei_tch":
         # ParEGO-style mono surrogate: Tchebicheff-aggregate the objectives (parego.py:212-219)
         tch = sc.Tchebicheff(Y.min(axis=0), Y.max(axis=0))

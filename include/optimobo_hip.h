@@ -88,8 +88,13 @@ const char* omb_last_error(const omb_ctx* ctx);
  * and acquisition values computed since the previous report are invalid.
  * The same bound limits the fused Cholesky steps' wait for the diagonal block (omb_cholesky,
  * omb_posterior_samples, the GP fit above n = 128): running out returns OMB_EHIP from that call.
- * omb_debug_set(ctx, OMB_DEBUG_SPIN_LIMIT, polls) changes the bound (tests force the path with 0). */
-enum { OMB_DEBUG_SPIN_LIMIT = 1 };
+ * omb_debug_set(ctx, OMB_DEBUG_SPIN_LIMIT, polls) changes the bound (tests force the path with 0).
+ * omb_debug_set(ctx, OMB_DEBUG_COV_TABLE, 1) builds K(X, X) / K(X*, X*) (GP-fit state, posterior covariance) with
+ * the posterior kernels' table-driven Matern transform instead of the polynomial exp (a parity check of that
+ * transform near r = 0; default 0).
+ * omb_debug_set(ctx, OMB_DEBUG_FUSED_CHAIN, 0) makes omb_eval_argmax[_sobol] run posterior, acquisition and
+ * arg-max as separate launches even where the one-launch chain applies (tests compare the two; default 1). */
+enum { OMB_DEBUG_SPIN_LIMIT = 1, OMB_DEBUG_COV_TABLE = 2, OMB_DEBUG_FUSED_CHAIN = 3 };
 int omb_debug_set(omb_ctx* ctx, int what, int64_t value);
 
 /* Fitted-GP state of objective `obj` — replaces the fitted GPy model

@@ -19,6 +19,8 @@ EHVI_REFERENCE, EHVI_TEXTBOOK, EHVI_SIGMA = 0, 1, 2
 EI_PLAIN, EI_PARETO, EI_CONSTRAINED = 0, 1, 2
 EA_EI, EA_PARETO_EI = 0, 1
 DEBUG_SPIN_LIMIT = 1
+DEBUG_COV_TABLE = 2
+DEBUG_FUSED_CHAIN = 3
 MAX_OBJ, MAX_DIM, MAX_TRAIN, MAX_TRAIN_DENSE = 8, 64, 1024, 16384
 
 _p = ctypes.c_void_p

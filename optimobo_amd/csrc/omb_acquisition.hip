@@ -20,9 +20,8 @@ static unsigned acq_grid(int64_t N) {
 }
 
 // ------------------------------------------------------------------------------ EHVI 2-D
-// util_functions.py:81-128 (EHVI_2D_aux) with the stripe array S = [(r0,−∞), PF↑f2, (−∞,r1)]
-// of :93-109.  φ/Φ of t_i = (y1[i]−μ0)/σA are reused by stripe i+1 (the reference evaluates
-// ψ(y1[i−1], y1[i−1]) from the same t), so each stripe costs 2 Φ + 2 φ instead of 7 calls.
+// One thread per candidate; the per-candidate arithmetic is ehvi2d_point (omb_math.h), shared with the fused
+// posterior epilogue (omb_posterior.hip, posterior_reg_ehvi_kernel).
 __global__ __launch_bounds__(kAcqThreads) void ehvi2d_kernel(const double* __restrict__ mu,
                                                              const double* __restrict__ var, int64_t ld, int64_t N,
                                                              const double* __restrict__ pf, int P, double r0,
@@ -37,50 +36,9 @@ __global__ __launch_bounds__(kAcqThreads) void ehvi2d_kernel(const double* __res
   }
   if (threadIdx.x == 0) y1[0] = r0;
   __syncthreads();
-  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < N; c += (int64_t)gridDim.x * blockDim.x) {
-    const double m0 = mu[c], m1 = mu[ld + c], v0 = var[c];
-    double sA, sB;
-    if (mode == OMB_EHVI_REFERENCE) {
-      // change() scales the cached samples by sqrt(σ²0) (util_functions.py:233-235): a negative
-      // variance makes every sample NaN, and np.cov of them NaN.
-      if (!(v0 >= 0.0)) {
-        out[c] = __builtin_nan("");
-        continue;
-      }
-      sA = v0 * s00;   // c00 = σ²0·Cov(cache)00   (util_functions.py:163-167, 114-115)
-      sB = v0 * s01;   // c01 = σ²0·Cov(cache)01   (a covariance used as a std: quirk 2)
-    } else if (mode == OMB_EHVI_TEXTBOOK) {
-      sA = sqrt(v0);
-      sB = sqrt(var[ld + c]);
-    } else {   // OMB_EHVI_SIGMA: EHVI_2D_aux called with σ directly
-      sA = v0;
-      sB = var[ld + c];
-    }
-    double tp = (y1[0] - m0) / sA;
-    double cdf_p = ndtr(tp), pdf_p = npdf(tp);
-    double sum1 = 0.0, sum2 = 0.0;
-    for (int i = 1; i <= P; ++i) {
-      const double y1p = y1[i - 1], y1i = y1[i], y2i = y2[i - 1];
-      const double t = (y1i - m0) / sA;
-      const double cdf_t = ndtr(t), pdf_t = npdf(t);
-      const double u = (y2i - m1) / sB;
-      const double p2 = sB * npdf(u) + (y2i - m1) * ndtr(u);          // ψ(y2i, y2i, μ1, σB)
-      sum1 = sum1 + (y1p - y1i) * cdf_t * p2;
-      const double psi_pp = sA * pdf_p + (y1p - m0) * cdf_p;          // ψ(y1[i−1], y1[i−1], μ0, σA)
-      const double psi_pi = sA * pdf_t + (y1p - m0) * cdf_t;          // ψ(y1[i−1], y1[i],   μ0, σA)
-      sum2 = sum2 + (psi_pp - psi_pi) * p2;
-      cdf_p = cdf_t;
-      pdf_p = pdf_t;
-    }
-    double res = sum1 + sum2;
-    if (mode == OMB_EHVI_TEXTBOOK) {
-      // the stripe i = P+1 that range(1, n+1) leaves out (quirk 3): ψ(y1P,y1P,μ0,σA)·ψ(r1,r1,μ1,σB)
-      const double psiA = sA * pdf_p + (y1[P] - m0) * cdf_p;
-      const double u = (r1 - m1) / sB;
-      res += psiA * (sB * npdf(u) + (r1 - m1) * ndtr(u));
-    }
-    out[c] = res;
-  }
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < N; c += (int64_t)gridDim.x * blockDim.x)
+    out[c] = ehvi2d_point(mu[c], mu[ld + c], var[c], mode == OMB_EHVI_REFERENCE ? 0.0 : var[ld + c], y1, y2, P, r1,
+                          s00, s01, mode);
 }
 
 hipError_t launch_ehvi2d(hipStream_t stream, const double* mu, const double* var, int64_t ld, int64_t N,

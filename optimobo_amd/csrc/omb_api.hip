@@ -86,6 +86,8 @@ struct omb_ctx {
   double* fit_host = nullptr;
   double* fit_dev = nullptr;
   int spin_limit = kDefaultSpinLimit;
+  bool cov_table = false;   // OMB_DEBUG_COV_TABLE
+  int fused_chain = 1;      // OMB_DEBUG_FUSED_CHAIN (0 off; 1, 2 the kernel variant)
 };
 
 namespace {
@@ -378,6 +380,16 @@ int run_chain(omb_ctx* ctx, const double* Xc, bool sobol, int64_t start, int64_t
   if (e == hipSuccess && sobol && N > 0) e = launch_sobol(ctx->stream, ctx->sob, ctx->sob_d, ctx->sob_bits, start, N, Xs);
   if (sobol) Xc = Xs;
   if (e == hipSuccess) e = mark(1);
+  if (e == hipSuccess && result_dev && !vals_out && N > 0 && ctx->fused_chain && pl.kind == PLAN_EHVI2D &&
+      16 * max_R <= OMB_MAX_TRAIN && fused_ehvi2d_fits(k, max_R, args.DP, pl.P)) {
+    // posterior → EHVI-2D → arg-max in one launch (launch_fused_ehvi2d); bitwise the unfused chain's result
+    FusedEhvi2d fe{pl.geo, pl.P, pl.mode, pl.r[0], pl.r[1], pl.s00, pl.s01, offset, ctx->partials,
+                   reinterpret_cast<unsigned*>(ctx->partials + 2 * kArgmaxMaxBlocks), result_dev};
+    e = launch_fused_ehvi2d(ctx->stream, args, max_R, Xc, N, fe, ctx->fused_chain);
+    for (int i = 2; i <= 4 && e == hipSuccess; ++i) e = mark(i);
+    if (e != hipSuccess) return hip_fail(ctx, e, "fused chain");
+    return OMB_OK;
+  }
   const double* Ld[OMB_MAX_OBJ];
   gather_Ld(ctx, k, Ld);
   if (e == hipSuccess && N > 0) e = posterior_any(ctx, args, Ld, k, max_R, Xc, N, mu, var);
@@ -429,7 +441,8 @@ int omb_create(int device, omb_ctx** out) {
   ctx->device = device;
   if (hipSetDevice(device) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking) != hipSuccess ||
-      hipMalloc(&ctx->partials, sizeof(double) * 2 * kArgmaxMaxBlocks) != hipSuccess ||
+      hipMalloc(&ctx->partials, sizeof(double) * (2 * kArgmaxMaxBlocks + 2)) != hipSuccess ||
+      hipMemset(ctx->partials, 0, sizeof(double) * (2 * kArgmaxMaxBlocks + 2)) != hipSuccess ||
       hipMalloc(&ctx->result_dev, sizeof(double) * 2) != hipSuccess ||
       hipHostMalloc(&ctx->result_host, sizeof(double) * 2, hipHostMallocDefault) != hipSuccess ||
       hipMalloc(&ctx->sob, sobol_state_bytes(OMB_MAX_DIM, 32)) != hipSuccess ||
@@ -498,6 +511,15 @@ int omb_debug_set(omb_ctx* ctx, int what, int64_t value) {
   if (what == OMB_DEBUG_SPIN_LIMIT) {
     if (value < 0 || value > 0x7fffffff) return fail(ctx, OMB_EINVAL, "spin limit %lld outside [0, 2^31)", (long long)value);
     ctx->spin_limit = (int)value;
+    return OMB_OK;
+  }
+  if (what == OMB_DEBUG_FUSED_CHAIN) {
+    if (value < 0 || value > 2) return fail(ctx, OMB_EINVAL, "fused-chain setting %lld outside [0, 2]", (long long)value);
+    ctx->fused_chain = (int)value;
+    return OMB_OK;
+  }
+  if (what == OMB_DEBUG_COV_TABLE) {
+    ctx->cov_table = value != 0;
     return OMB_OK;
   }
   return fail(ctx, OMB_EINVAL, "unknown debug setting %d", what);
@@ -967,7 +989,7 @@ static hipError_t cov_prepare(omb_ctx* ctx, const ObjState& s, const double* Xc,
 // cand_cov_ws_doubles(N, DP) doubles.
 static hipError_t cov_build(omb_ctx* ctx, const ObjState& s, const double* Xc, int64_t N, const double* V, double* S,
                             int64_t lds, double* cws, double jitter = 0.0) {
-  hipError_t e = launch_cand_cov(ctx->stream, s.dev, s.d, s.DP, Xc, N, S, lds, cws, jitter);
+  hipError_t e = launch_cand_cov(ctx->stream, s.dev, s.d, s.DP, Xc, N, S, lds, cws, jitter, ctx->cov_table);
   if (e == hipSuccess) e = launch_gemm_tn_lower(ctx->stream, N, s.n, -1.0, V, N, 1.0, S, lds);
   return e;
 }
@@ -1132,7 +1154,7 @@ static int gp_factor(omb_ctx* ctx, int kernel, int n, int d, const double* X, co
   f->jitter = 0.0;
   for (int t = -1; t < 5; ++t) {
     const double jit = (t < 0) ? 0.0 : mean_diag * 1e-6 * pow(10.0, (double)t);
-    OMB_HIP(ctx, launch_cand_cov(ctx->stream, g, d, DP, X, n, f->Ky, n, f->cws, base + jit));   // Ky = K + (base+jit)·I
+    OMB_HIP(ctx, launch_cand_cov(ctx->stream, g, d, DP, X, n, f->Ky, n, f->cws, base + jit, ctx->cov_table));   // Ky = K + (base+jit)·I
     if ((rc = run_cholesky(ctx, f->Ky, n, n, 0.0, &info))) return rc;
     if (info == 0) {
       f->jitter = jit;

@@ -57,6 +57,22 @@ hipError_t launch_kernel_block(hipStream_t stream, const GPArgs& args, int obj, 
 hipError_t launch_posterior(hipStream_t stream, const GPArgs& args, int n_obj, int max_R, const double* Xc,
                             int64_t N, double* mu, double* var);
 
+// The fused 2-objective EHVI chain (posterior → EHVI-2D → arg-max in one launch; omb_posterior.hip).
+constexpr int kFusedMaxP = 128;    // stripes staged in LDS (the LDS left beside two packed L⁻¹ at n = 128)
+struct FusedEhvi2d {
+  const double* pf;       // (P, 2) stripes, sorted (the plan's geometry)
+  int P, mode;
+  double r0, r1, s00, s01;
+  int64_t offset;         // global index of candidate 0
+  double* partials;       // 2 doubles per workgroup (≤ kArgmaxMaxBlocks)
+  unsigned* ticket;       // 0 between launches (the last workgroup resets it)
+  double* result;         // {value, global index}
+};
+bool fused_ehvi2d_fits(int n_obj, int max_R, int DP, int P);
+// variant 1: 16 waves per workgroup (4 per SIMD), 2: 8 waves
+hipError_t launch_fused_ehvi2d(hipStream_t stream, const GPArgs& args, int max_R, const double* Xc, int64_t N,
+                               const FusedEhvi2d& fe, int variant = 1);
+
 hipError_t launch_ehvi2d(hipStream_t stream, const double* mu, const double* var, int64_t ld, int64_t N,
                          const double* pf, int P, double r0, double r1, double s00, double s01, int mode,
                          double* out);
@@ -125,7 +141,7 @@ hipError_t launch_gemm_tn_lower(hipStream_t s, int64_t N, int64_t K, double alph
 // (X*/ℓ and its squared norms).
 int64_t cand_cov_ws_doubles(int64_t N, int DP);
 hipError_t launch_cand_cov(hipStream_t stream, const GPDev& g, int d, int DP, const double* Xc, int64_t N, double* S,
-                           int64_t lds, double* ws, double diag_add = 0.0);
+                           int64_t lds, double* ws, double diag_add = 0.0, bool table = false);
 hipError_t launch_mirror_lower(hipStream_t stream, double* S, int64_t N, int64_t lds);
 hipError_t launch_add_diag(hipStream_t stream, double* S, int64_t N, int64_t lds, double v);
 // in-place lower Cholesky; info (device int, zeroed by the first kernel) = first bad column (1-based);
@@ -134,7 +150,9 @@ hipError_t launch_add_diag(hipStream_t stream, double* S, int64_t N, int64_t lds
 // wait for the diagonal block ran out after spin_limit polls (the factor is invalid; reported as OMB_EHIP).
 constexpr int kCholWsDoubles = 64 * 64;
 constexpr int kCholSpinFault = -2147483647;
-enum { kCholTwoLaunch = 0, kCholFused = 1 };
+// kCholBlocked (round 4): the diagonal blocks by tiles of 16 (chol64_blocked); kCholBlockedAcqRel: the same with
+// the fused step's flag as an agent-scope release / acquire (tools/ablate/ablate_chol)
+enum { kCholTwoLaunch = 0, kCholFused = 1, kCholBlocked = 2, kCholBlockedAcqRel = 3 };
 int64_t chol_ws_doubles(int64_t N);
 hipError_t launch_cholesky(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws,
                            int spin_limit = kDefaultSpinLimit);

@@ -55,17 +55,21 @@ __global__ __launch_bounds__(256) void cand_scale_kernel(const double* __restric
   if (i < N && k == 0) xsq[i] = s;
 }
 
-template <int DP, int KIND>
+// TAB (Matern 5/2 only; omb_debug_set(OMB_DEBUG_COV_TABLE)): the posterior kernels' table-driven transform
+// matern_r2_tab256_x2 in place of kernel_of_r2 (DESIGN §4b "Covariance on the table transform").
+template <int DP, int KIND, bool TAB>
 __global__ __launch_bounds__(256) void cand_cov_kernel(const double* __restrict__ Xs, const double* __restrict__ xsq,
                                                        int64_t N, double variance, double* __restrict__ S,
-                                                       int64_t lds, double diag_add) {
+                                                       int64_t lds, double diag_add, ExpCoef ec) {
   constexpr int KP = (DP + 3) / 4 * 4;
   if (blockIdx.x > blockIdx.y) return;
   const int64_t m0 = (int64_t)blockIdx.y * 64, n0 = (int64_t)blockIdx.x * 64;
   __shared__ double As[KP][65], Bs[KP][65];   // As[k][m] = a_{m0+m}[k]
+  __shared__ double etab[TAB ? 256 : 1];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
+  if constexpr (TAB) etab[tid] = kExp2Tab256[tid];                          // 256 threads
   for (int idx = tid; idx < 64 * KP; idx += 256) {
     const int m = idx / KP, k = idx % KP;
     As[k][m] = (m0 + m < N) ? Xs[(m0 + m) * KP + k] : 0.0;
@@ -94,16 +98,28 @@ __global__ __launch_bounds__(256) void cand_cov_kernel(const double* __restrict_
     const int64_t col = n0 + 32 * wn + 16 * cb + (lane & 15);
     const double bsq = col < N ? xsq[col] : 0.0;
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb)
+    for (int rb = 0; rb < 2; ++rb) {
+      double r2[4], kv[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int64_t row = m0 + 32 * wm + 16 * rb + (lane >> 4) + 4 * e;
-        if (row < N && col <= row) {
-          const double r2 = (row == col) ? 0.0 : fma(-2.0, acc[rb][cb][e], xsq[row] + bsq);
-          const double kv = kernel_of_r2<KIND>(r2, variance);
-          S[row * lds + col] = (row == col) ? kv + diag_add : kv;
-        }
+        const double asq = row < N ? xsq[row] : 0.0;
+        r2[e] = (row == col) ? 0.0 : fma(-2.0, acc[rb][cb][e], asq + bsq);
       }
+      if constexpr (TAB && KIND == OMB_KERNEL_MATERN52) {
+        const double pm[3] = {variance, kSqrt5 * variance, kFiveThirds * variance};
+        matern_r2_tab256_x2(r2[0], r2[1], pm, ec, etab, kv[0], kv[1]);
+        matern_r2_tab256_x2(r2[2], r2[3], pm, ec, etab, kv[2], kv[3]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) kv[e] = kernel_of_r2<KIND>(r2[e], variance);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t row = m0 + 32 * wm + 16 * rb + (lane >> 4) + 4 * e;
+        if (row < N && col <= row) S[row * lds + col] = (row == col) ? kv[e] + diag_add : kv[e];
+      }
+    }
   }
 }
 
@@ -415,6 +431,312 @@ __device__ __forceinline__ void chol64_factor(double (&a)[16], int w, int r, int
   chol64_inverse(w, r, Lb, prog + 4, Wf);
 }
 
+// ----------------------------------------------------------------------------- Cholesky, blocked diagonal block
+// Round 4.  The 64×64 diagonal block is factored as 4 × 4 tiles of 16 (right-looking inside the block), with
+// row ownership: wave w owns tile row w — the tiles (w, j), j ≤ w, of D in LDS (pitch kDP) — and runs
+//   for b < w:  P_b  L_wb = D_wb · W_bbᵀ (W_bb = L_bb⁻¹), 4 MFMAs, formed transposed (L_wbᵀ = W_bb D_wbᵀ) so the
+//                    accumulator is L_wb in the operand layout of the next products (lane (g, c): L_wb[c][4e + g]);
+//              U_b  D_wj −= L_wb L_jbᵀ for b < j ≤ w, 4 MFMAs each (L_jb of wave j after its flag; for j = w both
+//                   operands are the P_b accumulator);
+//   F_w        the tile (w, w): its Cholesky factor and inverse W_ww in registers (chol16_factor);
+// then, as chol64_inverse, W's column block w: W_iw = −W_ii Σ_{k=w}^{i−1} L_ik W_kw (i > w) on MFMA.
+// The block's serial chain is F_0 → P_0 U_0 (wave 1) → F_1 → … → F_3 → the three products with W_33: four
+// 16-column factors and three 8-MFMA hand-offs.  Round 3 ran one wave per 16-column strip of all 64 rows
+// (≈ 470 cycles per column on the owner, ≈ 40k cycles for the block, profiles/r03_v38_chol_trace_pipelined_inverse.txt).
+// The waves synchronise through LDS flags (wready: W_bb in Wl; lready: L_ib in D); no barrier inside.
+// OUTER (the diagonal workgroup of chol_update_kernel): D = A22_00 − L21_0 L21_0ᵀ, wave w forming its own tiles
+// (16 MFMAs each, K = 64, the k index permuted so a lane reads 4 contiguous doubles per 16-column group), so wave
+// 0 starts F_0 after one tile instead of after the whole 64×64 product.
+// per-wave phase timestamps of chol64_blocked, and step-level timestamps of chol_update_kernel (workgroup 0,
+// workgroup (1, 0)), for tools/ablate/ablate_chol (empty here)
+#ifndef OMB_CHOL_BTRACE
+#define OMB_CHOL_BTRACE(w, id, cond)
+#endif
+#ifndef OMB_CHOL_STRACE
+#define OMB_CHOL_STRACE(step, id, cond)
+#endif
+constexpr int kDP = 66;                    // D row pitch in doubles
+constexpr int kWlP = 16 * 18;              // one W_bb in Wl, column-major: Wl[b·kWlP + c·18 + m] = W_bb[m][c]
+constexpr int kBlkFlags = 4 + 16 + 2;      // wready[4] | lready[4i + b] | bad | wait fault
+
+// bounded (2^20 polls ≈ 30 ms): a wait that runs out marks fl[kBlkFlags − 1] (→ info = kCholSpinFault) and
+// goes on, so a wrong flag protocol ends the kernel instead of hanging it
+__device__ __forceinline__ void lds_wait_flag(int* f, int* fault) {
+  int polls = 0;
+  while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) {
+    if (++polls > (1 << 20)) {
+      *fault = 1;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+// lane 0 posts; the release orders the whole wave's earlier LDS stores before the flag
+__device__ __forceinline__ void lds_post_flag(int* f, int lane) {
+  if (lane == 0) __hip_atomic_store(f, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// orders one wave's LDS accesses across lanes for the compiler (LDS executes a wave's accesses in order)
+__device__ __forceinline__ void wave_lds_order() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+
+// a += L·na and x += L·nx with L = lane K's l (DPP row_newbcast folded into two v_fmac_f64_dpp: one instruction per
+// update instead of a v_mov_b64_dpp broadcast and two v_fma_f64).  The leading s_nop gives the 2 wait states a DPP
+// read needs after the VALU write of l: the compiler's hazard recognizer does not look inside inline asm.
+template <int K>
+__device__ __forceinline__ void fmac2_bcast(double& a, double& x, double l, double na, double nx) {
+  asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %2, %3 row_newbcast:%5 row_mask:0xf bank_mask:0xf\n\t"
+               "v_fmac_f64_dpp %1, %2, %4 row_newbcast:%5 row_mask:0xf bank_mask:0xf"
+               : "+v"(a), "+v"(x)
+               : "v"(l), "v"(na), "v"(nx), "n"(K));
+}
+
+// Cholesky of a 16×16 SPD tile held row-per-lane (lane → row r = lane & 15; the four 16-lane rows of the wave
+// hold the same copy), with W = L⁻¹ by column-oriented forward substitution of L x = e_r sharing the broadcasts:
+//   a[q] = D[r][q] (q ≤ r; entries above the diagonal start at 0 and are never broadcast) → L[r][q];
+//   x = e_r → x[m] = W[m][r].
+// Column j: inv_j = 1/√d_j (v_rsq + 2 Newton steps), L[r][j] = a[j]·inv_j; for k > j a[k] −= L[r][j]·L[k][j] and
+// x[k] −= x[j]·L[k][j], L[k][j] being lane k's value (fmac2_bcast: two v_fmac_f64_dpp row_newbcast per k).
+// The pivot chain runs ahead on wave-uniform values: d_{j+1} = a_{j+1}[j+1] − (a_{j+1}[j]·inv_j)² with both entries
+// read (v_readlane) before inv_j is known — bitwise the value the update leaves in lane j+1 (the same fma).
+// Returns 0 or the 1-based first column with a non-positive pivot (continued with 1.0: no NaNs; flagged).
+__device__ __forceinline__ int chol16_factor(double (&a)[16], double (&x)[16]) {
+  int bad = 0;
+  double dj = readlane_f64(a[0], 0);
+  static_for<0, 16>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    double a1 = 0.0, ap = 0.0;
+    if constexpr (j < 15) {
+      a1 = readlane_f64(a[j], j + 1);
+      ap = readlane_f64(a[j + 1], j + 1);
+    }
+    if (!(dj > 0.0)) {
+      if (bad == 0) bad = j + 1;
+      dj = 1.0;
+    }
+    const double y0 = __builtin_amdgcn_rsq(dj);
+    const double hd = 0.5 * dj;
+    const double y1 = fma(y0, fma(-hd * y0, y0, 0.5), y0);
+    const double inv = fma(y1, fma(-hd * y1, y1, 0.5), y1);
+    if constexpr (j < 15) {
+      const double s1 = a1 * inv;
+      dj = fma(-s1, s1, ap);
+    }
+    const double l = a[j] * inv;
+    a[j] = l;
+    const double xj = x[j] * inv;
+    x[j] = xj;
+    const double nl = -l, nx = -xj;
+    static_for<j + 1, 16>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      fmac2_bcast<k>(a[k], x[k], l, nl, nx);
+    });
+  });
+  // the callers store a and x under a lane condition; without this the updates were sunk into that branch,
+  // keeping every broadcast alive (256 VGPRs + 58 AGPRs)
+#pragma unroll
+  for (int q = 0; q < 16; ++q) asm volatile("" : "+v"(a[q]), "+v"(x[q]));
+  return bad;
+}
+
+// 16 doubles of row `p` (k permuted: v[4q + u] = p[16q + u], p already offset by 4g), or zeros
+__device__ __forceinline__ void load_row16(const double* __restrict__ p, bool ok, double (&v)[16]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[4 * q + u] = ok ? p[16 * q + u] : 0.0;
+}
+
+// The diagonal block at rows / columns r0 .. r0+63 of A (nb ≤ 64 real rows; the rest identity), factored in place
+// (lower triangle of rows < nb), with W = L⁻¹'s MFMA fragments to Wf (the layout of chol64_inverse).  OUTER: A22_00
+// minus the product of the panel rows A[r0 + ·][c0 .. c0+63].  Ds, Wl, fl: LDS (fl zeroed by the caller and a
+// barrier passed).  The caller reads fl[20] (block-relative 1-based first bad column, 0 = none) after a barrier.
+template <bool OUTER>
+__device__ __forceinline__ void chol64_blocked(double* __restrict__ A, int64_t lda, int64_t r0, int nb, int64_t c0,
+                                               double* __restrict__ Wf, double* Ds, double* Wl, int* fl) {
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  OMB_CHOL_BTRACE(w, 0, lane == 0);
+  // ---- D tiles (w, j), j ≤ w (accumulator layout: lane (g, c) → rows 4e + g, column c); tile j + 1's loads are
+  // issued before tile j's product (one load latency per wave instead of one per tile)
+  {
+    auto load_a22 = [&](int j, double (&av)[4]) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = 16 * w + 4 * e + g, col = 16 * j + c;
+        av[e] = (row < nb && col <= row) ? A[(r0 + row) * lda + r0 + col] : (row == col ? 1.0 : 0.0);
+      }
+    };
+    double xa[16], xb[16], av[4];
+    if constexpr (OUTER) {
+      load_row16(A + (r0 + 16 * w + c) * lda + c0 + 4 * g, 16 * w + c < nb, xa);
+      if (w > 0) {
+        load_row16(A + (r0 + c) * lda + c0 + 4 * g, c < nb, xb);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) xb[q] = xa[q];
+      }
+    }
+    load_a22(0, av);
+    for (int j = 0; j <= w; ++j) {
+      double nxb[16], nav[4];
+      if (j < w) {
+        if constexpr (OUTER) {
+          if (j + 1 < w) {
+            load_row16(A + (r0 + 16 * (j + 1) + c) * lda + c0 + 4 * g, 16 * (j + 1) + c < nb, nxb);
+          } else {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) nxb[q] = xa[q];                  // tile (w, w): both operands the own rows
+          }
+        }
+        load_a22(j + 1, nav);
+      }
+      d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+      if constexpr (OUTER) {
+#pragma unroll
+        for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[s], xb[s], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Ds[(16 * w + 4 * e + g) * kDP + 16 * j + c] = av[e] - acc[e];
+      if (j < w) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) av[e] = nav[e];
+        if constexpr (OUTER) {
+#pragma unroll
+          for (int q = 0; q < 16; ++q) xb[q] = nxb[q];
+        }
+      }
+    }
+  }
+  OMB_CHOL_BTRACE(w, 1, lane == 0);
+  // ---- P_b, U_b for b < w
+  for (int b = 0; b < w; ++b) {
+    double dop[4];                                                    // D_wb[c][4s + g], read before the wait
+#pragma unroll
+    for (int s = 0; s < 4; ++s) dop[s] = Ds[(16 * w + c) * kDP + 16 * b + 4 * s + g];
+    lds_wait_flag(&fl[b], &fl[21]);
+    OMB_CHOL_BTRACE(w, 2 + 2 * b, lane == 0);
+    const double* Wb = Wl + b * kWlP;
+    d4 lt = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      lt = __builtin_amdgcn_mfma_f64_16x16x4f64(Wb[(4 * s + g) * 18 + c], dop[s], lt, 0, 0, 0);   // W_bb[c][4s + g]
+#pragma unroll
+    for (int e = 0; e < 4; ++e) Ds[(16 * w + c) * kDP + 16 * b + 4 * e + g] = lt[e];     // L_wb[c][4e + g]
+    lds_post_flag(&fl[4 + 4 * w + b], lane);
+    // U_b: the own diagonal tile first (on the chain when b = w − 1), then the tiles (w, j), b < j < w
+    for (int j = w; j > b; --j) {
+      d4 u = d4{0.0, 0.0, 0.0, 0.0};
+      if (j == w) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) u = __builtin_amdgcn_mfma_f64_16x16x4f64(lt[s], lt[s], u, 0, 0, 0);
+      } else {
+        lds_wait_flag(&fl[4 + 4 * j + b], &fl[21]);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          u = __builtin_amdgcn_mfma_f64_16x16x4f64(lt[s], Ds[(16 * j + c) * kDP + 16 * b + 4 * s + g], u, 0, 0, 0);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        double* p = Ds + (16 * w + 4 * e + g) * kDP + 16 * j + c;
+        *p = *p - u[e];
+      }
+    }
+    // the panel tile's L into A (after the flag: off the chain)
+    if (16 * w + c < nb) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) A[(r0 + 16 * w + c) * lda + r0 + 16 * b + 4 * e + g] = lt[e];
+    }
+    OMB_CHOL_BTRACE(w, 3 + 2 * b, lane == 0);
+  }
+  // ---- F_w
+  wave_lds_order();
+  {
+    // row c of the tile (entries above the diagonal are finite leftovers: never broadcast, never stored to A)
+    double a[16], x[16];
+    const double2* dr = reinterpret_cast<const double2*>(Ds + (16 * w + c) * kDP + 16 * w);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const double2 v = dr[q];
+      a[2 * q] = v.x;
+      a[2 * q + 1] = v.y;
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) x[q] = (q == c) ? 1.0 : 0.0;
+    OMB_CHOL_BTRACE(w, 8, lane == 0);
+    const int bad = chol16_factor(a, x);
+    OMB_CHOL_BTRACE(w, 9, lane == 0);
+    if (g == 0) {
+      double2* drw = reinterpret_cast<double2*>(Ds + (16 * w + c) * kDP + 16 * w);
+      double2* wc = reinterpret_cast<double2*>(Wl + w * kWlP + c * 18);                // W_ww[·][c]
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        drw[q] = double2{a[2 * q], a[2 * q + 1]};
+        wc[q] = double2{x[2 * q], x[2 * q + 1]};
+      }
+      if (c == 0 && bad != 0 && fl[20] == 0) fl[20] = 16 * w + bad;
+    }
+    lds_post_flag(&fl[w], lane);
+    OMB_CHOL_BTRACE(w, 10, lane == 0);
+    if (g == 0 && 16 * w + c < nb) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        if (q <= c) A[(r0 + 16 * w + c) * lda + r0 + 16 * w + q] = a[q];
+    }
+  }
+  // W_ww's fragments: block (w, w), k-step 4w + u: W[16w + c][16w + 4g + u]
+  wave_lds_order();
+#pragma unroll
+  for (int u = 0; u < 4; ++u) wf_store(&Wf[(w * 16 + 4 * w + u) * 64 + 16 * g + c], Wl[w * kWlP + (4 * g + u) * 18 + c]);
+  // ---- W's column block w: W_iw = −W_ii Σ_{k=w}^{i−1} L_ik W_kw, i = w+1 .. 3 (Wc[k] = W_kw, accumulator layout,
+  // is the B operand of the next product: lane (g, c) holds W_kw[4s + g][c] in register s)
+  d4 Wc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) Wc[i] = d4{0.0, 0.0, 0.0, 0.0};
+  static_for<1, 4>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+    if (i > w) {
+      d4 T = d4{0.0, 0.0, 0.0, 0.0};
+      static_for<0, i>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        if (k >= w) {
+          lds_wait_flag(&fl[4 + 4 * i + k], &fl[21]);                                             // L_ik final
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            const double av = Ds[(16 * i + c) * kDP + 16 * k + 4 * s + g];              // L_ik[c][4s + g]
+            const double bv = (k == w) ? Wl[w * kWlP + c * 18 + 4 * s + g] : Wc[k][s];   // W_kw[4s + g][c]
+            T = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, T, 0, 0, 0);
+          }
+        }
+      });
+      lds_wait_flag(&fl[i], &fl[21]);                                                             // W_ii in Wl
+      d4 R = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        R = __builtin_amdgcn_mfma_f64_16x16x4f64(Wl[i * kWlP + (4 * s + g) * 18 + c], T[s], R, 0, 0, 0);   // W_ii[c][4s + g]
+      Wc[i] = -R;
+      // W[16i + 4e + g][16w + c]: row block i, k-step 4w + (c & 3), lane 4e + g + 16 (c >> 2)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) wf_store(&Wf[(i * 16 + 4 * w + (c & 3)) * 64 + 4 * e + g + 16 * (c >> 2)], Wc[i][e]);
+      OMB_CHOL_BTRACE(w, 10 + i, lane == 0);
+    }
+  });
+}
+
+// Step 0's diagonal block (chol_diag_kernel's blocked form); zeroes info and the fused steps' flags.
+__global__ __launch_bounds__(256) void chol_diag_blk_kernel(double* __restrict__ A, int64_t N, int64_t lda,
+                                                            double* __restrict__ ws, int* __restrict__ info,
+                                                            int* __restrict__ flags, int nflags) {
+  for (int i = threadIdx.x; i < nflags; i += blockDim.x) flags[i] = 0;
+  if (threadIdx.x == 0) *info = 0;
+  __shared__ __attribute__((aligned(16))) double Ds[kNB * kDP];
+  __shared__ __attribute__((aligned(16))) double Wl[4 * kWlP];
+  __shared__ int fl[kBlkFlags];
+  if (threadIdx.x < kBlkFlags) fl[threadIdx.x] = 0;
+  __syncthreads();
+  chol64_blocked<false>(A, lda, 0, (int)(N < kNB ? N : kNB), 0, ws, Ds, Wl, fl);
+  __syncthreads();
+  if (threadIdx.x == 0 && (fl[20] || fl[21])) atomicCAS(info, 0, fl[21] ? kCholSpinFault : fl[20]);
+}
+
 __global__ __launch_bounds__(256) void chol_diag_kernel(double* __restrict__ A, int64_t N, int64_t lda,
                                                          double* __restrict__ ws, int* __restrict__ info,
                                                          int* __restrict__ flags, int nflags) {
@@ -515,6 +837,40 @@ __global__ __launch_bounds__(128) void chol_panel_kernel(double* __restrict__ A,
 // the panel's own launch (≈ 5 µs plus a launch gap per step at N = 3000) leaves the chain.  Workgroup 0
 // is dispatched first (in-order dispatch); the wait is bounded all the same (spin_limit polls, then
 // info = kCholSpinFault and the workgroup finishes), so a waiting workgroup can never hang the grid.
+// The fused step's hand-off of W_{k+1} (chol_update_kernel<FUSE>): the diagonal workgroup stores the fragments
+// with agent-scope relaxed atomics (wf_store: sc1, coherent across the XCDs' L2s), waits for all of them (vmcnt 0)
+// and sets the flag; a waiting workgroup polls the flag (relaxed), passes a barrier and reads the fragments with
+// wf_load.  The compiler fences (signal fences) keep the fragment accesses on their side of the flag; the
+// hardware order is the vmcnt wait (a store counts as done once it is acknowledged at the coherent level).
+// acq_rel = 1 (tools/ablate/ablate_chol): the flag store a release and one acquire fence after the poll, at
+// agent scope — the HIP memory model's own guarantee; its cost is measured in DESIGN §4b.
+__device__ __forceinline__ void chol_publish_w(int* flag, int tid, int acq_rel) {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (tid == 0) {
+    if (acq_rel)
+      __hip_atomic_store(flag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+__device__ __forceinline__ void chol_wait_w(const int* flag, int tid, int spin_limit, int* info, int acq_rel) {
+  if (tid == 0) {
+    int polls = 0;
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+      if (++polls > spin_limit) {
+        atomicCAS(info, 0, kCholSpinFault);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (acq_rel) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
 __device__ __forceinline__ void chol_tile_of(int b, int t, int& mt, int& nt) {
   if (b < t) {
     mt = b;
@@ -529,10 +885,11 @@ __device__ __forceinline__ void chol_tile_of(int b, int t, int& mt, int& nt) {
   nt = q - mp * (mp + 1) / 2 + 1;
 }
 
-template <bool FUSE>
-__global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A, int64_t N, int64_t lda, int step,
+template <bool FUSE, bool BLK>
+__global__ __launch_bounds__(256, 3) void chol_update_kernel(double* __restrict__ A, int64_t N, int64_t lda, int step,
                                                           int t, double* __restrict__ ws, int* __restrict__ info,
-                                                          int* __restrict__ flags, int spin_limit) {
+                                                          int* __restrict__ flags, int spin_limit, int acq_rel) {
+  OMB_CHOL_STRACE(step, blockIdx.x == 0 ? 0 : 3, threadIdx.x == 0 && blockIdx.x <= 1);
   if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
   int mt, nt;
   chol_tile_of((int)blockIdx.x, t, mt, nt);
@@ -553,6 +910,23 @@ __global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const double* L21 = A + r0 * lda + c0;
+  if constexpr (BLK) {
+    // round 4: the next diagonal block factored by tiles of 16 (chol64_blocked), its product with the panel
+    // formed by the waves that own the tiles
+    if (mt == 0 && nt == 0) {
+      __shared__ __attribute__((aligned(16))) double Wl[4 * kWlP];
+      __shared__ int fl[kBlkFlags];
+      if (tid < kBlkFlags) fl[tid] = 0;
+      __syncthreads();
+      chol64_blocked<true>(A, lda, r0, (int)(M < kNB ? M : kNB), c0, ws, smem, Wl, fl);
+      __syncthreads();
+      if (tid == 0 && (fl[20] || fl[21])) atomicCAS(info, 0, fl[21] ? kCholSpinFault : (int)(r0 + fl[20]));
+      OMB_CHOL_STRACE(step, 1, tid == 0);
+      if constexpr (FUSE) chol_publish_w(flags + step, tid, acq_rel);
+      OMB_CHOL_STRACE(step, 2, tid == 0);
+      return;
+    }
+  }
   // the next diagonal block (A22's first tile) belongs to workgroup (0, 0)
   if (!(mt == 0 && nt == 0)) {
     double ra[4], rb[4];
@@ -639,17 +1013,9 @@ __global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A
     __syncthreads();
     // W_{k+1}'s fragments: wait for the diagonal workgroup's flag (bounded); relaxed polls and coherent
     // fragment loads (wf_load), no cache-wide invalidate
-    if (tid == 0) {
-      int polls = 0;
-      while (__hip_atomic_load(&flags[step], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-        if (++polls > spin_limit) {
-          atomicCAS(info, 0, kCholSpinFault);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-      }
-    }
-    __syncthreads();
+    OMB_CHOL_STRACE(step, 4, tid == 0 && mt == 1);
+    chol_wait_w(flags + step, tid, spin_limit, info, acq_rel);
+    OMB_CHOL_STRACE(step, 5, tid == 0 && mt == 1);
     // the next step's panel rows, as chol_panel_kernel: wave w → rows 16w + (lane & 15) of the tile,
     // all four output column blocks
     {
@@ -679,6 +1045,7 @@ __global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A
         }
       }
     }
+    OMB_CHOL_STRACE(step, 6, tid == 0 && mt == 1);
     return;
   }
   // Diagonal workgroup: the tile's 64 L21 rows and its A22 values are loaded at once (one load latency
@@ -750,13 +1117,7 @@ __global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A
   chol64_factor(a, w, r, nb, smem, aux, prog, bad_lds, A, lda, r0, ws);   // with W = L⁻¹ (chol64_inverse)
   __syncthreads();
   if (tid == 0 && bad_lds[0]) atomicCAS(info, 0, (int)(r0 + bad_lds[0]));
-  if constexpr (FUSE) {
-    // publish W_{k+1} (also after a bad pivot: the waiting workgroups must finish; info marks the result):
-    // every thread's coherent fragment stores complete (vmcnt 0), then the flag
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    if (tid == 0) __hip_atomic_store(&flags[step], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  if constexpr (FUSE) chol_publish_w(flags + step, tid, acq_rel);
 }
 
 // ----------------------------------------------------------------------------- triangular inverse
@@ -1653,8 +2014,9 @@ __global__ __launch_bounds__(256) void select_greedy_kernel(const long long* __r
 int64_t cand_cov_ws_doubles(int64_t N, int DP) { return N * ((DP + 3) / 4 * 4) + N; }
 
 hipError_t launch_cand_cov(hipStream_t stream, const GPDev& g, int d, int DP, const double* Xc, int64_t N, double* S,
-                           int64_t lds, double* ws, double diag_add) {
+                           int64_t lds, double* ws, double diag_add, bool table) {
   if (N <= 0) return hipSuccess;
+  const ExpCoef ec = exp_coef();
   const int KP = (DP + 3) / 4 * 4;
   double* Xs = ws;
   double* xsq = ws + N * KP;
@@ -1665,11 +2027,14 @@ hipError_t launch_cand_cov(hipStream_t stream, const GPDev& g, int d, int DP, co
   case DPV:                                                                                                   \
     hipLaunchKernelGGL((cand_scale_kernel<DPV>), dim3(sb), dim3(256), 0, stream, Xc, d, N, g.ls, Xs, xsq);    \
     if (g.kind == OMB_KERNEL_RBF)                                                                             \
-      hipLaunchKernelGGL((cand_cov_kernel<DPV, OMB_KERNEL_RBF>), grid, dim3(256), 0, stream, Xs, xsq, N,      \
-                         g.variance, S, lds, diag_add);                                                       \
+      hipLaunchKernelGGL((cand_cov_kernel<DPV, OMB_KERNEL_RBF, false>), grid, dim3(256), 0, stream, Xs, xsq, N, \
+                         g.variance, S, lds, diag_add, ec);                                                   \
+    else if (table)                                                                                           \
+      hipLaunchKernelGGL((cand_cov_kernel<DPV, OMB_KERNEL_MATERN52, true>), grid, dim3(256), 0, stream, Xs, xsq,  \
+                         N, g.variance, S, lds, diag_add, ec);                                                \
     else                                                                                                      \
-      hipLaunchKernelGGL((cand_cov_kernel<DPV, OMB_KERNEL_MATERN52>), grid, dim3(256), 0, stream, Xs, xsq, N, \
-                         g.variance, S, lds, diag_add);                                                       \
+      hipLaunchKernelGGL((cand_cov_kernel<DPV, OMB_KERNEL_MATERN52, false>), grid, dim3(256), 0, stream, Xs, xsq, \
+                         N, g.variance, S, lds, diag_add, ec);                                                \
     break;
   switch (DP) {
     OMB_COV(2) OMB_COV(4) OMB_COV(6) OMB_COV(8) OMB_COV(16) OMB_COV(32) OMB_COV(64)
@@ -1716,12 +2081,37 @@ void set_chol_update_lds(size_t bytes) { g_chol_update_lds = bytes; }
 constexpr size_t g_chol_update_lds = 0;
 #endif
 
+// Round 4: the diagonal blocks by tiles of 16 (chol64_blocked), one launch per step with the next panel inside.
+static hipError_t launch_cholesky_blocked(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws,
+                                          int spin_limit, int acq_rel) {
+  const int steps = (int)((N + kNB - 1) / kNB);
+  const bool vec = (lda % 2 == 0) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
+  int* flags = reinterpret_cast<int*>(ws + kCholWsDoubles);
+  hipLaunchKernelGGL(chol_diag_blk_kernel, dim3(1), dim3(256), 0, stream, A, N, lda, ws, info, flags, steps);
+  hipError_t e = hipGetLastError();
+  for (int k = 0; k + 1 < steps && e == hipSuccess; ++k) {
+    const int64_t rest = N - (int64_t)(k + 1) * kNB;
+    const int t = (int)((rest + kGT - 1) / kGT);
+    if (k == 0) {
+      e = chol_panel(stream, A, N, lda, k, ws, info, vec);
+      if (e != hipSuccess) break;
+    }
+    hipLaunchKernelGGL((chol_update_kernel<true, true>), dim3((unsigned)(t * (t + 1) / 2)), dim3(256), g_chol_update_lds,
+                       stream, A, N, lda, k, t, ws, info, flags, spin_limit, acq_rel);
+    e = hipGetLastError();
+  }
+  return e;
+}
+
 hipError_t launch_cholesky_mode(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws, int mode,
                                 int spin_limit) {
   if (N <= 0) return hipSuccess;
   const int steps = (int)((N + kNB - 1) / kNB);
   const bool vec = (lda % 2 == 0) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
   const bool fuse = mode == kCholFused;
+  const bool blk = mode == kCholBlocked || mode == kCholBlockedAcqRel;
+  const int acq_rel = mode == kCholBlockedAcqRel ? 1 : 0;
+  if (blk) return launch_cholesky_blocked(stream, A, N, lda, info, ws, spin_limit, acq_rel);
   int* flags = reinterpret_cast<int*>(ws + kCholWsDoubles);
   hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), 0, stream, A, N, lda, ws, info, flags, fuse ? steps : 0);
   hipError_t e = hipGetLastError();
@@ -1735,18 +2125,18 @@ hipError_t launch_cholesky_mode(hipStream_t stream, double* A, int64_t N, int64_
     }
     const unsigned wgs = (unsigned)(t * (t + 1) / 2);
     if (fuse)
-      hipLaunchKernelGGL((chol_update_kernel<true>), dim3(wgs), dim3(256), g_chol_update_lds, stream, A, N, lda, k, t, ws,
-                         info, flags, spin_limit);
+      hipLaunchKernelGGL((chol_update_kernel<true, false>), dim3(wgs), dim3(256), g_chol_update_lds, stream, A, N, lda, k,
+                         t, ws, info, flags, spin_limit, 0);
     else
-      hipLaunchKernelGGL((chol_update_kernel<false>), dim3(wgs), dim3(256), g_chol_update_lds, stream, A, N, lda, k, t,
-                         ws, info, flags, spin_limit);
+      hipLaunchKernelGGL((chol_update_kernel<false, false>), dim3(wgs), dim3(256), g_chol_update_lds, stream, A, N, lda,
+                         k, t, ws, info, flags, spin_limit, 0);
     e = hipGetLastError();
   }
   return e;
 }
 
 hipError_t launch_cholesky(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws, int spin_limit) {
-  return launch_cholesky_mode(stream, A, N, lda, info, ws, kCholFused, spin_limit);
+  return launch_cholesky_mode(stream, A, N, lda, info, ws, kCholBlocked, spin_limit);
 }
 
 hipError_t launch_trinv(hipStream_t stream, const double* L, int64_t n, int64_t lda, double* X, int64_t ldx,

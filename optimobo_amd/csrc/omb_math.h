@@ -3,6 +3,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include "../../include/optimobo_hip.h"
+
 namespace omb {
 
 constexpr double kSqrt5 = 2.23606797749979;            // np.sqrt(5.)
@@ -399,6 +401,71 @@ __device__ __forceinline__ void matern_r2_tab256_x2(double r2a, double r2b, cons
     outa = pa_ * ea;
     outb = pb_ * eb;
   }
+}
+
+// EHVI-2D of one candidate: util_functions.py:81-128 (EHVI_2D_aux) with the stripe array S = [(r0,−∞), PF↑f2,
+// (−∞,r1)] of :93-109; y1[0] = r0, y1[i] / y2[i−1] = stripe i's f1 / f2 (i = 1..P).  φ/Φ of t_i = (y1[i]−μ0)/σA
+// are reused by stripe i+1 (the reference evaluates ψ(y1[i−1], y1[i−1]) from the same t), so each stripe costs
+// 2 Φ + 2 φ instead of 7 calls.  One function for ehvi2d_kernel and the fused posterior epilogue, so both give
+// bitwise the same values (and the same arg-max).
+__device__ __forceinline__ double ehvi2d_point(double m0, double m1, double v0, double v1, const double* y1,
+                                               const double* y2, int P, double r1, double s00, double s01, int mode) {
+  double sA, sB;
+  if (mode == OMB_EHVI_REFERENCE) {
+    // change() scales the cached samples by sqrt(σ²0) (util_functions.py:233-235): a negative variance makes
+    // every sample NaN, and np.cov of them NaN.
+    if (!(v0 >= 0.0)) return __builtin_nan("");
+    sA = v0 * s00;   // c00 = σ²0·Cov(cache)00   (util_functions.py:163-167, 114-115)
+    sB = v0 * s01;   // c01 = σ²0·Cov(cache)01   (a covariance used as a std: quirk 2)
+  } else if (mode == OMB_EHVI_TEXTBOOK) {
+    sA = sqrt(v0);
+    sB = sqrt(v1);
+  } else {   // OMB_EHVI_SIGMA: EHVI_2D_aux called with σ directly
+    sA = v0;
+    sB = v1;
+  }
+  double tp = (y1[0] - m0) / sA;
+  double cdf_p = ndtr(tp), pdf_p = npdf(tp);
+  double sum1 = 0.0, sum2 = 0.0;
+  for (int i = 1; i <= P; ++i) {
+    const double y1p = y1[i - 1], y1i = y1[i], y2i = y2[i - 1];
+    const double t = (y1i - m0) / sA;
+    const double cdf_t = ndtr(t), pdf_t = npdf(t);
+    const double u = (y2i - m1) / sB;
+    const double p2 = sB * npdf(u) + (y2i - m1) * ndtr(u);          // ψ(y2i, y2i, μ1, σB)
+    sum1 = sum1 + (y1p - y1i) * cdf_t * p2;
+    const double psi_pp = sA * pdf_p + (y1p - m0) * cdf_p;          // ψ(y1[i−1], y1[i−1], μ0, σA)
+    const double psi_pi = sA * pdf_t + (y1p - m0) * cdf_t;          // ψ(y1[i−1], y1[i],   μ0, σA)
+    sum2 = sum2 + (psi_pp - psi_pi) * p2;
+    cdf_p = cdf_t;
+    pdf_p = pdf_t;
+  }
+  double res = sum1 + sum2;
+  if (mode == OMB_EHVI_TEXTBOOK) {
+    // the stripe i = P+1 that range(1, n+1) leaves out (quirk 3): ψ(y1P,y1P,μ0,σA)·ψ(r1,r1,μ1,σB)
+    const double psiA = sA * pdf_p + (y1[P] - m0) * cdf_p;
+    const double u = (r1 - m1) / sB;
+    res += psiA * (sB * npdf(u) + (r1 - m1) * ndtr(u));
+  }
+  return res;
+}
+
+// Agent-scope relaxed f64 store / load (coherent across the XCDs' L2s): the fused chains' per-workgroup pairs.
+__device__ __forceinline__ void wf_store_f64(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), __builtin_bit_cast(unsigned long long, v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double wf_load_f64(const double* p) {
+  return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// Arg-max pair of the fused chains: higher value wins, the lower index on ties; index < 0 = none (NaN and −∞
+// never enter).  The same rule as omb_argmax.hip's `better`.
+__device__ __forceinline__ bool argmax_better(double av, long long ai, double bv, long long bi) {
+  if (ai < 0) return false;
+  if (bi < 0) return true;
+  return (av > bv) || (av == bv && ai < bi);
 }
 
 // GPy Matern52.K_of_r: variance*(1+sqrt(5)*r+5/3*r**2)*exp(-sqrt(5)*r)  (r ≥ 0)

@@ -1236,6 +1236,91 @@ __global__ __launch_bounds__(512, 2) void posterior_tile_kernel(GPArgs args, con
 // Matern transform (K* = r²), bit 16 drops the sqrt's residual correction, bit 32 scales by 2^m with
 // an integer exponent add instead of v_ldexp_f64, bit 64 loads the next tile's coordinates during the current
 // tile (instead of at its start), bit 128 stages with the round-2 rolled loops and reloads ℓ per tile.
+// One 16-candidate tile of one objective in posterior_reg_ehvi_kernel (wave-level; posterior_reg_kernel below keeps
+// the same steps inline — through this function its RMAX = 8 instances spilled 2-10 VGPRs at the 128-VGPR bound): the
+// B fragment of the r²-MFMA from the raw coordinates, K* row tile by row tile (augmented r² on MFMA, the Matern
+// transform), μ = αᵀK* and ΣV² with V = L⁻¹K* accumulated in registers (row tile T retired after step T); μ and
+// ΣV² reduced over the wave's four row groups (every lane ends with its candidate's values).
+template <int RMAX, int DP, int KIND, bool XL, int ABL, int KSD>
+__device__ __forceinline__ void reg_tile_moments(const double* __restrict__ gls, int d, int R, const double (&raw)[KSD],
+                                                 const double (&lsr)[KSD], const d2* xf, const double* lds_L,
+                                                 const double* lds_alpha, const double* etab, const ExpCoef& ec,
+                                                 const double (&pm)[3], int lane, double& mu_out, double& s_out) {
+  constexpr int KSDP = (KSD + 1) / 2;
+  constexpr bool kTab256 = KIND == OMB_KERNEL_MATERN52;
+  // B fragment [−2·x*/ℓ, 1, ‖x*/ℓ‖²]: lane l needs dims 4s + (l>>4) only; ‖x*/ℓ‖² from the four
+  // lane groups by two shuffles
+  double xs[KSD], csq = 0.0;
+#pragma unroll
+  for (int q = 0; q < KSD; ++q) {
+    const int j = 4 * q + (lane >> 4);
+    if constexpr ((ABL & 128) != 0)
+      xs[q] = (j < d) ? raw[q] / gls[j] : 0.0;
+    else
+      xs[q] = (j < d) ? raw[q] / lsr[q] : 0.0;
+    csq = fma(xs[q], xs[q], csq);
+  }
+  csq += __shfl_xor(csq, 16);
+  csq += __shfl_xor(csq, 32);
+  double bfr[KSD];
+#pragma unroll
+  for (int s = 0; s < KSD; ++s) {
+    const int j = 4 * s + (lane >> 4);
+    bfr[s] = (j < d) ? -2.0 * xs[s] : (j == d ? 1.0 : (j == d + 1 ? csq : 0.0));
+  }
+
+  d4 acc[RMAX];
+  double mu_part = 0.0, s = 0.0;
+#pragma unroll
+  for (int T = 0; T < RMAX; ++T) {
+    const int Tl = XL ? T : min(T, R - 1);        // T ≥ R: finite stand-in rows (zero L⁻¹ / α)
+    d2 a[KSDP];
+#pragma unroll
+    for (int p = 0; p < KSDP; ++p) a[p] = xf[64 * (KSDP * Tl + p)];
+    d4 cr = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < KSD; ++q)
+      cr = __builtin_amdgcn_mfma_f64_16x16x4f64((q & 1) ? a[q >> 1].y : a[q >> 1].x, bfr[q], cr, 0, 0, 0);
+    double kv[4];
+#pragma unroll
+    for (int e = 0; e < 4; e += 2) {
+      if constexpr ((ABL & 8) != 0) {
+        kv[e] = cr[e];
+        kv[e + 1] = cr[e + 1];
+      } else if constexpr (kTab256) {
+        matern_r2_tab256_x2<(ABL & 16) != 0, (ABL & 32) != 0>(cr[e], cr[e + 1], pm, ec, etab, kv[e], kv[e + 1]);
+      } else {
+        kernel_of_r2_tab_x2<KIND>(cr[e], cr[e + 1], pm, ec, etab, kv[e], kv[e + 1]);
+      }
+      mu_part = fma(lds_alpha[16 * T + 4 * e + (lane >> 4)], kv[e], mu_part);
+      mu_part = fma(lds_alpha[16 * T + 4 * e + 4 + (lane >> 4)], kv[e + 1], mu_part);
+    }
+    if constexpr (!(ABL & 2)) {
+#pragma unroll
+      for (int r = T; r < RMAX; ++r) {
+        const d2* A = reinterpret_cast<const d2*>(lds_L + 128 * r * (r + 1) + 256 * T) + lane;
+        const d2 a0 = A[0], a1 = A[64];
+        d4 v = (T == 0) ? d4{0.0, 0.0, 0.0, 0.0} : acc[r];
+        v = __builtin_amdgcn_mfma_f64_16x16x4f64(a0.x, kv[0], v, 0, 0, 0);
+        v = __builtin_amdgcn_mfma_f64_16x16x4f64(a0.y, kv[1], v, 0, 0, 0);
+        v = __builtin_amdgcn_mfma_f64_16x16x4f64(a1.x, kv[2], v, 0, 0, 0);
+        acc[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1.y, kv[3], v, 0, 0, 0);
+      }
+    } else {
+      acc[T] = d4{kv[0], kv[1], kv[2], kv[3]};
+    }
+    // row tile T has all its k-steps (T' ≤ T): retire its accumulator, so at most RMAX − T are live
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s = fma(acc[T][i], acc[T][i], s);
+  }
+  s += __shfl_xor(s, 16);
+  s += __shfl_xor(s, 32);
+  mu_part += __shfl_xor(mu_part, 16);
+  mu_part += __shfl_xor(mu_part, 32);
+  mu_out = mu_part;
+  s_out = s;
+}
+
 template <int RMAX, int DP, int KIND, int NW = 8, bool XL = false, int ABL = 0>
 __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : NW / 4) void posterior_reg_kernel(
     GPArgs args, const double* __restrict__ Xc, int64_t N, double* __restrict__ mu_out, double* __restrict__ var_out) {
@@ -1443,6 +1528,237 @@ static dim3 reg_grid(int64_t N, int n_obj, int NW = 8, int per_cu = 2) {
   const int64_t wgs = (waves_needed + NW - 1) / NW;
   const int64_t resident = std::max<int64_t>(1, (per_cu * (int64_t)device_cu_count()) / std::max(1, n_obj));
   return dim3((unsigned)std::max<int64_t>(1, std::min(wgs, resident)), (unsigned)n_obj);
+}
+
+// ----------------------------------------------------------------------------- fused 2-objective EHVI chain
+// omb_eval_argmax with an EHVI-2D plan at n ≤ 128, n_var ≤ 8 (BASELINE config 2): posterior
+// of both objectives, EHVI (ehvi2d_point, util_functions.py:136-167) and the arg-max in one persistent launch —
+// μ and σ² never leave the registers, and the acquisition values never reach HBM.
+//   * one 1024-thread workgroup per CU stages BOTH objectives' packed L⁻¹ and α (2 × 72 KiB at n = 128), the exp
+//     table and the EHVI stripes in LDS; the training-row fragments (Xf) are read from L2;
+//   * each wave loops over 16-candidate tiles: reg_tile_moments for objective 0, then 1 (bitwise the moments
+//     posterior_reg_kernel writes), then lanes 0..15 evaluate their candidate's EHVI and keep a running
+//     (value, index) best — higher value, lower index on ties, NaN and −∞ never win (omb_argmax.hip's rule);
+//   * the wave's best → LDS → the workgroup's pair → partials; the last workgroup to finish (an agent-scope
+//     ticket) reduces the pairs and writes {value, index + offset}, then resets the ticket for the next launch.
+// The result equals posterior → ehvi2d_kernel → argmax_pass1/2 bit for bit (tests/test_gpu_fused.py).
+// ehvi2d_point as a call: inlined into the tile loop, its ndtr coefficients were hoisted into VGPRs for the whole loop
+__device__ __noinline__ double ehvi2d_point_call(double m0, double m1, double v0, double v1, const double* y1,
+                                                 const double* y2, int P, double r1, double s00, double s01, int mode) {
+  return ehvi2d_point(m0, m1, v0, v1, y1, y2, P, r1, s00, s01, mode);
+}
+
+template <int RMAX, int DP, int KIND, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void posterior_reg_ehvi_kernel(GPArgs args, const double* __restrict__ Xc,
+                                                                        int64_t N, FusedEhvi2d fe) {
+  constexpr int NT = 64 * NW;
+  static_assert(DP <= 8, "augmented r² needs n_var ≤ 8");
+  constexpr int KSD = (DP + 5) / 4;
+  constexpr bool kTab256 = KIND == OMB_KERNEL_MATERN52;
+  constexpr int kTabN = kTab256 ? 256 : 64;
+  constexpr int kL2 = 64 * RMAX * (RMAX + 1);       // d2 elements of one packed L⁻¹
+  __shared__ double lds_L[2][2 * kL2];
+  __shared__ double lds_alpha[2][16 * RMAX];
+  __shared__ double etab[kTabN];
+  __shared__ double geo[2 * kFusedMaxP + 1];         // y1[0..P] | y2[0..P−1]
+  __shared__ double red_v[NW];
+  __shared__ long long red_i[NW];
+  __shared__ int is_last;
+  // per wave and candidate lane: objective 0's moments while objective 1's tile runs, and the running best
+  // (in LDS, not registers: the tile loop is at the 128-VGPR bound of 16 waves per CU)
+  __shared__ double st_mu[NW][16], st_var[NW][16], st_bv[NW][16];
+  __shared__ long long st_bi[NW][16];
+
+  const int d = args.d;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t ntiles = (N + 15) / 16;
+  const int64_t stride = (int64_t)gridDim.x * NW;
+  const int P = fe.P;
+  // ---- staging: both objectives' L⁻¹ and α, the exp table, the stripes
+#pragma unroll
+  for (int o = 0; o < 2; ++o) {
+    const GPDev& g = args.gp[o];
+    const int nL2 = 64 * g.R * (g.R + 1);
+    const d2* src = reinterpret_cast<const d2*>(g.Lp);
+    d2* dst = reinterpret_cast<d2*>(lds_L[o]);
+    for (int i = tid; i < kL2; i += NT) dst[i] = i < nL2 ? src[i] : d2{0.0, 0.0};
+    if (tid < 16 * RMAX) lds_alpha[o][tid] = tid < 16 * g.R ? g.alpha[tid] : 0.0;
+  }
+  for (int i = tid; i < kTabN; i += NT) etab[i] = kTab256 ? kExp2Tab256[i] : kExp2Tab64[i];
+  double* y1 = geo;
+  double* y2 = geo + P + 1;
+  for (int i = tid; i < P; i += NT) {
+    y1[i + 1] = fe.pf[2 * i];
+    y2[i] = fe.pf[2 * i + 1];
+  }
+  if (tid == 0) y1[0] = fe.r0;
+  __syncthreads();
+
+  if (lane < 16) {
+    st_bv[wave][lane] = -__builtin_inf();
+    st_bi[wave][lane] = -1;
+  }
+  for (int64_t t = (int64_t)blockIdx.x * NW + wave; t < ntiles; t += stride) {
+    const int64_t c = 16 * t + (lane & 15);
+    // the objectives one after the other (a rolled loop: unrolled, the compiler interleaved the two tiles' registers
+    // and spilled ≈ 200 VGPRs); the coordinates are reloaded for the second (L1/L2 hits)
+    double mu1 = 0.0, var1 = 0.0;
+#pragma unroll 1
+    for (int o = 0; o < 2; ++o) {
+      double raw[KSD];
+      {
+        const int64_t cc = c < N ? c : N - 1;
+#pragma unroll
+        for (int q = 0; q < KSD; ++q) {
+          const int j = 4 * q + (lane >> 4);
+          raw[q] = (j < d) ? Xc[cc * d + j] : 0.0;
+        }
+      }
+      const GPDev* g = o == 0 ? &args.gp[0] : &args.gp[1];
+      double lsr[KSD];
+#pragma unroll
+      for (int q = 0; q < KSD; ++q) {
+        const int j = 4 * q + (lane >> 4);
+        lsr[q] = (j < d) ? g->ls[j] : 1.0;
+      }
+      const double pm[3] = {g->variance, kSqrt5 * g->variance, kFiveThirds * g->variance};
+      double m, s;
+      // an opaque per-tile offset keeps LICM from hoisting the (tile-invariant) Xf fragments out of the tile loop
+      int xoff = lane;
+      asm volatile("" : "+v"(xoff));
+      reg_tile_moments<RMAX, DP, KIND, false, 0>(g->ls, d, g->R, raw, lsr, reinterpret_cast<const d2*>(g->Xf) + xoff,
+                                                 lds_L[o], lds_alpha[o], etab, args.ec, pm, lane, m, s);
+      if (o == 0) {
+        if (lane < 16) {
+          st_mu[wave][lane] = m;
+          st_var[wave][lane] = g->variance - s;
+        }
+      } else {
+        mu1 = m;
+        var1 = g->variance - s;
+      }
+    }
+    if (lane < 16 && c < N) {
+      const double v = ehvi2d_point_call(st_mu[wave][lane], mu1, st_var[wave][lane],
+                                         fe.mode == OMB_EHVI_REFERENCE ? 0.0 : var1, y1, y2, P, fe.r1, fe.s00, fe.s01,
+                                         fe.mode);
+      if (v == v && v > -__builtin_inf() && argmax_better(v, c, st_bv[wave][lane], st_bi[wave][lane])) {
+        st_bv[wave][lane] = v;
+        st_bi[wave][lane] = c;
+      }
+    }
+  }
+  // ---- the wave's best (lanes 0..15), the workgroup's, the grid's
+  double best_v = lane < 16 ? st_bv[wave][lane] : -__builtin_inf();
+  long long best_i = lane < 16 ? st_bi[wave][lane] : -1;
+#pragma unroll
+  for (int off = 8; off > 0; off >>= 1) {
+    const double ov = __shfl_xor(best_v, off);
+    const long long oi = __shfl_xor(best_i, off);
+    if (argmax_better(ov, oi, best_v, best_i)) {
+      best_v = ov;
+      best_i = oi;
+    }
+  }
+  if (lane == 0) {
+    red_v[wave] = best_v;
+    red_i[wave] = best_i;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < NW; ++w)
+      if (argmax_better(red_v[w], red_i[w], best_v, best_i)) {
+        best_v = red_v[w];
+        best_i = red_i[w];
+      }
+    wf_store_f64(&fe.partials[2 * blockIdx.x], best_v);
+    wf_store_f64(&fe.partials[2 * blockIdx.x + 1], __builtin_bit_cast(double, best_i));
+    const unsigned prev = __hip_atomic_fetch_add(fe.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    is_last = prev == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!is_last) return;
+  // the last workgroup: all pairs, in workgroup order (the rule is order-free; the scan is fixed anyway)
+  double v = -__builtin_inf();
+  long long i = -1;
+  for (int b = tid; b < (int)gridDim.x; b += NT) {
+    const double bv = wf_load_f64(&fe.partials[2 * b]);
+    const long long bi = __builtin_bit_cast(long long, wf_load_f64(&fe.partials[2 * b + 1]));
+    if (argmax_better(bv, bi, v, i)) {
+      v = bv;
+      i = bi;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const double ov = __shfl_xor(v, off);
+    const long long oi = __shfl_xor(i, off);
+    if (argmax_better(ov, oi, v, i)) {
+      v = ov;
+      i = oi;
+    }
+  }
+  __syncthreads();
+  if (lane == 0) {
+    red_v[wave] = v;
+    red_i[wave] = i;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < NW; ++w)
+      if (argmax_better(red_v[w], red_i[w], v, i)) {
+        v = red_v[w];
+        i = red_i[w];
+      }
+    fe.result[0] = i < 0 ? -__builtin_inf() : v;
+    fe.result[1] = i < 0 ? -1.0 : (double)(i + fe.offset);
+    __hip_atomic_store(fe.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+bool fused_ehvi2d_fits(int n_obj, int max_R, int DP, int P) {
+  return n_obj == 2 && max_R <= 8 && DP <= 8 && P >= 1 && P <= kFusedMaxP;
+}
+
+template <int DP, int KIND, int NW>
+static hipError_t launch_fused_ehvi2d_nw(hipStream_t stream, const GPArgs& args, int max_R, const double* Xc,
+                                         int64_t N, const FusedEhvi2d& fe) {
+  const dim3 grid = reg_grid(N, 1, NW, 1);
+  const dim3 block(64 * NW);
+  if (max_R <= 2)
+    hipLaunchKernelGGL((posterior_reg_ehvi_kernel<2, DP, KIND, NW>), grid, block, 0, stream, args, Xc, N, fe);
+  else if (max_R <= 4)
+    hipLaunchKernelGGL((posterior_reg_ehvi_kernel<4, DP, KIND, NW>), grid, block, 0, stream, args, Xc, N, fe);
+  else
+    hipLaunchKernelGGL((posterior_reg_ehvi_kernel<8, DP, KIND, NW>), grid, block, 0, stream, args, Xc, N, fe);
+  return hipGetLastError();
+}
+
+template <int DP, int KIND>
+static hipError_t launch_fused_ehvi2d_dp(hipStream_t stream, const GPArgs& args, int max_R, const double* Xc,
+                                         int64_t N, const FusedEhvi2d& fe, int variant) {
+  if constexpr (DP <= 8) {
+    return variant == 2 ? launch_fused_ehvi2d_nw<DP, KIND, 8>(stream, args, max_R, Xc, N, fe)
+                        : launch_fused_ehvi2d_nw<DP, KIND, 16>(stream, args, max_R, Xc, N, fe);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_fused_ehvi2d(hipStream_t stream, const GPArgs& args_in, int max_R, const double* Xc, int64_t N,
+                               const FusedEhvi2d& fe, int variant) {
+  GPArgs args = args_in;
+  args.ec = exp_coef();
+  const bool rbf = args.gp[0].kind == OMB_KERNEL_RBF;
+  switch (args.DP) {
+#define OMB_FE(DPV)                                                                                       \
+  case DPV:                                                                                               \
+    return rbf ? launch_fused_ehvi2d_dp<DPV, OMB_KERNEL_RBF>(stream, args, max_R, Xc, N, fe, variant)    \
+               : launch_fused_ehvi2d_dp<DPV, OMB_KERNEL_MATERN52>(stream, args, max_R, Xc, N, fe, variant);
+    OMB_FE(2) OMB_FE(4) OMB_FE(6) OMB_FE(8)
+#undef OMB_FE
+    default: return hipErrorInvalidValue;
+  }
 }
 
 // ----------------------------------------------------------------------------- dispatch

@@ -68,8 +68,11 @@ class AcqContext:
         self._check(self.lib.omb_synchronize(self._h), "omb_synchronize")
 
     def debug_set(self, what, value):
-        """omb_debug_set: e.g. ("spin_limit", polls) bounds the posterior's LDS-counter waits."""
-        code = {"spin_limit": _lib.DEBUG_SPIN_LIMIT}[what]
+        """omb_debug_set: ("spin_limit", polls) bounds the posterior's LDS-counter waits; ("cov_table", 0/1)
+        builds K(X, X) / K(X*, X*) with the posterior's table-driven Matern transform; ("fused_chain", 0/1) turns
+        the one-launch posterior → EHVI → arg-max chain off / on."""
+        code = {"spin_limit": _lib.DEBUG_SPIN_LIMIT, "cov_table": _lib.DEBUG_COV_TABLE,
+                "fused_chain": _lib.DEBUG_FUSED_CHAIN}[what]
         self._check(self.lib.omb_debug_set(self._h, code, int(value)), "omb_debug_set")
 
     # ------------------------------------------------------------------ GP state

@@ -73,10 +73,17 @@ def agree_host_rng(seed=None):
     return box[0]
 
 
-def global_argmax(local_pair, group=None):
-    """All-gather each rank's {value, global index} pair and reduce it identically everywhere."""
-    w, _ = world()
-    if w == 1:
+def global_argmax(local_pair, group=None, force=False):
+    """All-gather each rank's {value, global index} pair and reduce it identically everywhere.
+
+    At world size 1 the pair is returned as is, unless ``force``: then the all-gather and the
+    reduction run anyway (a one-rank RCCL communicator exercises the same library load,
+    communicator init and device all-gather that a multi-GPU run uses).
+    """
+    if not (dist.is_available() and dist.is_initialized()):
+        return local_pair
+    w = dist.get_world_size(group)
+    if w == 1 and not force:
         return local_pair
     pair = local_pair.contiguous()
     if dist.get_backend(group) == "gloo" and pair.is_cuda:

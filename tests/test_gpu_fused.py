@@ -229,6 +229,7 @@ def test_stage_timing(ctx, gp3):
     Y = gp3[0]
     _plans(ctx, Y)[0][2]()
     ctx.set_sobol(4, np.zeros(4), np.ones(4), seed=0)
+    ctx.debug_set("fused_chain", 0)          # stage split of the separate launches (the one-launch chain has none)
     ctx.timing(2)
     for _ in range(3):
         ctx.eval_argmax_sobol(0, 1 << 14)
@@ -239,7 +240,85 @@ def test_stage_timing(ctx, gp3):
         ctx.eval_argmax_sobol(0, 1 << 14)
     ms, n = ctx.timing_read()
     ctx.timing(0)
+    ctx.debug_set("fused_chain", 1)
     assert n == 2 and ms["posterior"] > 0 and ms["acquisition"] == 0 and ms["sobol"] == 0
+
+
+# ----------------------------------------------------------------------------- one-launch EHVI-2D chain
+def _ehvi2d_problem(n, d, seed):
+    from optimobo_amd import pareto
+    from optimobo_amd.gp import GPState
+    rng = np.random.default_rng(seed)
+    X = rng.uniform(0, 1, (n, d))
+    f1 = X[:, 0]
+    g = 1 + 9.0 / max(d - 1, 1) * X[:, 1:].sum(1)
+    Y = np.column_stack([f1, g * (1 - np.sqrt(f1 / g))])
+    ls = rng.uniform(0.3, 1.5, d)
+    states = [GPState(X, Y[:, o], ls, float(np.var(Y[:, o]))) for o in range(2)]
+    pf = pareto.calc_pf(Y)
+    r = Y.max(0) + 0.1 * (Y.max(0) - Y.min(0))
+    return states, pareto.stripes_2d(pf), r
+
+
+@pytest.mark.parametrize("n,d,N,mode,cseed", [
+    (20, 2, 1000, "reference", 1), (64, 6, (1 << 16) + 37, "reference", 1), (100, 6, 50000, "textbook", 1),
+    (128, 6, 1 << 16, "reference", 1), (128, 8, 4099, "sigma", 1), (97, 4, 30000, "reference", 0),
+    (33, 3, 17, "textbook", 1)])
+def test_one_launch_ehvi2d_chain_equals_separate_launches(n, d, N, mode, cseed):
+    """posterior_reg_ehvi_kernel (both wave-count variants) returns bit for bit the pair of posterior →
+    ehvi2d_kernel → argmax_pass1/2 (cache seed 0: s01 < 0, EHVI ≤ 0, ties at 0 decided by the lowest index)."""
+    from optimobo_amd import pareto
+    from optimobo_amd.device import AcqContext
+    ctx = AcqContext(0)
+    try:
+        states, stripes, r = _ehvi2d_problem(n, d, 100 + n + d)
+        for o, st in enumerate(states):
+            ctx.set_gp_state(o, st)
+        s00, s01 = pareto.cache_stats(pareto.cached_samples(2, 5, seed=cseed))
+        ctx.plan_ehvi2d(stripes, r, s00, s01, mode=mode)
+        Xc = dev(np.random.default_rng(n + N).uniform(0, 1, (N, d)))
+        pairs = {}
+        for variant in (0, 1, 2):
+            ctx.debug_set("fused_chain", variant)
+            pairs[variant] = ctx.eval_argmax(Xc, offset=123).cpu().numpy()
+        ctx.debug_set("fused_chain", 0)
+        vals = ctx.eval(Xc).cpu().numpy()
+        ctx.debug_set("fused_chain", 1)
+        v, i = oacq.argmax(vals, offset=123)
+        for variant in (0, 1, 2):
+            assert (pairs[variant][0], int(pairs[variant][1])) == (v, i), (variant, pairs[variant], v, i)
+        if cseed == 0:
+            assert v == 0.0 and i == 123 + int(np.flatnonzero(vals == 0.0)[0])
+        # the Sobol entry point takes the same one-launch path
+        ctx.set_sobol(d, np.zeros(d), np.ones(d), seed=3)
+        p1 = ctx.eval_argmax_sobol(11, N).cpu().numpy()
+        ctx.debug_set("fused_chain", 0)
+        p0 = ctx.eval_argmax_sobol(11, N).cpu().numpy()
+        ctx.debug_set("fused_chain", 1)
+        assert np.array_equal(p0, p1)
+    finally:
+        ctx.close()
+
+
+def test_one_launch_ehvi2d_chain_falls_back_beyond_its_stripes():
+    """More stripes than the LDS holds (P > 128) or n > 128: the separate launches, same rule."""
+    from optimobo_amd import pareto
+    from optimobo_amd.device import AcqContext
+    ctx = AcqContext(0)
+    try:
+        states, _, r = _ehvi2d_problem(64, 4, 5)
+        for o, st in enumerate(states):
+            ctx.set_gp_state(o, st)
+        f1 = np.linspace(0.0, 1.0, 200)
+        pf = np.column_stack([f1, 1.0 - np.sqrt(f1)])
+        s00, s01 = pareto.cache_stats(pareto.cached_samples(2, 5, seed=1))
+        ctx.plan_ehvi2d(pareto.stripes_2d(pf), r, s00, s01, mode="textbook")
+        Xc = dev(np.random.default_rng(1).uniform(0, 1, (5000, 4)))
+        pair = ctx.eval_argmax(Xc).cpu().numpy()
+        v, i = oacq.argmax(ctx.eval(Xc).cpu().numpy())
+        assert (pair[0], int(pair[1])) == (v, i)
+    finally:
+        ctx.close()
 
 
 def test_engine_maximise_plan_equals_callable(gp3):

@@ -1,7 +1,10 @@
 // Timing of the blocked Cholesky (launch_cholesky: chol_diag / chol_panel / chol_update kernels) on an
 // SPD matrix (tools only; not part of the library).  Correctness is tests/test_gpu_turbo.py.
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/ablate/ablate_chol tools/ablate/ablate_chol.hip
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/ablate/ablate_chol tools/ablate/ablate_chol.hip \
+//          -lrocsolver -lrocblas
 // Run on the GPU box: ./tools/ablate/ablate_chol [N ...]
+// Round 4: the blocked diagonal factor (kCholBlocked) against round 3's (kCholFused), interleaved, with its
+// per-wave phase trace; rocsolver_dpotrf on the same matrices as a stated reference rate (not a dependency).
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -22,6 +25,25 @@ __device__ unsigned long long g_col[4][64];
   do {                                                            \
     if (cond) g_col[w][j] = __builtin_readcyclecounter();         \
   } while (0)
+
+__device__ unsigned long long g_btrace[4][16];
+__device__ int64_t g_btrace_r0 = 0;        // chol64_blocked calls traced: the block at this r0
+#define OMB_CHOL_BTRACE(w, id, cond)                                                                   \
+  do {                                                                                                 \
+    if ((cond) && r0 == g_btrace_r0) g_btrace[w][id] = __builtin_readcyclecounter();                  \
+  } while (0)
+// step-level stamps (100 MHz constant clock) of steps g_strace_step and g_strace_step + 1:
+// 0 WG0 start, 1 WG0 factor done, 2 W published, 3 WG1 start, 4 WG(1,0) waits, 5 flag seen, 6 panel done
+__device__ int g_strace_step = -1;
+__device__ unsigned long long g_strace[2][8];
+#define OMB_CHOL_STRACE(step, id, cond)                                                                \
+  do {                                                                                                 \
+    if ((cond) && (step == g_strace_step || step == g_strace_step + 1))                               \
+      g_strace[step - g_strace_step][id] = __builtin_amdgcn_s_memrealtime();                            \
+  } while (0)
+
+#include <rocblas/rocblas.h>
+#include <rocsolver/rocsolver.h>
 
 #define OMB_TOOLS_KNOBS
 #include "../../optimobo_amd/csrc/omb_linalg.hip"
@@ -71,8 +93,153 @@ static void trace_diag() {
   CK(hipFree(A)); CK(hipFree(ws)); CK(hipFree(info));
 }
 
+static void* g_strace_ptr() {
+  void* p = nullptr;
+  CK(hipGetSymbolAddress(&p, HIP_SYMBOL(g_strace)));
+  return p;
+}
+
+// per-wave phases of the blocked diagonal factor (chol_diag_blk_kernel, alone on the GPU)
+static void trace_diag_blocked() {
+  const int N = 64;
+  std::vector<double> h(N * N);
+  for (int i = 0; i < N; ++i)
+    for (int j = 0; j < N; ++j) h[i * N + j] = (i == j) ? N : 1.0 / (1.0 + std::abs((double)(i - j)));
+  double *A, *ws;
+  int* info;
+  CK(hipMalloc(&A, N * N * 8));
+  CK(hipMalloc(&ws, chol_ws_doubles(N) * 8));
+  CK(hipMalloc(&info, 64));
+  unsigned long long t0[4][16];
+  for (int rep = 0; rep < 3; ++rep) {
+    CK(hipMemcpy(A, h.data(), N * N * 8, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(chol_diag_blk_kernel, dim3(1), dim3(256), 0, 0, A, (int64_t)N, (int64_t)N, ws, info,
+                       reinterpret_cast<int*>(ws + kCholWsDoubles), 0);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpyFromSymbol(t0, HIP_SYMBOL(g_btrace), sizeof(t0)));
+  }
+  unsigned long long base = t0[0][0];
+  for (int w = 0; w < 4; ++w) base = std::min(base, t0[w][0]);
+  const char* names[14] = {"start", "D tiles", "P0 wait", "P0/U0", "P1 wait", "P1/U1", "P2 wait", "P2/U2",
+                           "F begin", "F end", "W_ww post", "W_1w", "W_2w", "W_3w"};
+  printf("chol_diag_blk_kernel per-wave phases (cycles from the first wave's start)\n");
+  for (int w = 0; w < 4; ++w) {
+    printf("  wave %d:", w);
+    for (int id = 0; id < 14; ++id) {
+      const bool used = (id < 2) || (id >= 2 && id < 8 && (id - 2) / 2 < w) || (id >= 8 && id <= 10) ||
+                        (id >= 11 && id - 10 > w);
+      if (used) printf(" %s %lld |", names[id], (long long)(t0[w][id] - base));
+    }
+    printf("\n");
+  }
+  std::vector<double> L(N * N);
+  CK(hipMemcpy(L.data(), A, N * N * 8, hipMemcpyDeviceToHost));
+  double worst = 0.0;
+  for (int i = 0; i < N; ++i)
+    for (int j = 0; j <= i; ++j) {
+      double s = 0.0;
+      for (int k = 0; k <= j; ++k) s += L[i * N + k] * L[j * N + k];
+      worst = std::max(worst, std::abs(s - h[i * N + j]) / std::abs(h[i * N + i]));
+    }
+  printf("  blocked 64x64: max |LLt - A|/A_ii %.2e\n", worst);
+  CK(hipFree(A)); CK(hipFree(ws)); CK(hipFree(info));
+}
+
+static void time_rocsolver(const std::vector<int64_t>& sizes) {
+  rocblas_handle handle;
+  if (rocblas_create_handle(&handle) != rocblas_status_success) {
+    printf("rocblas_create_handle failed\n");
+    return;
+  }
+  for (int64_t N : sizes) {
+    std::vector<double> h(N * N);
+    for (int64_t i = 0; i < N; ++i)
+      for (int64_t j = 0; j < N; ++j) h[i * N + j] = (i == j) ? N : 1.0 / (1.0 + std::abs((double)(i - j)));
+    double *A0, *A;
+    int* info;
+    CK(hipMalloc(&A0, N * N * 8));
+    CK(hipMalloc(&A, N * N * 8));
+    CK(hipMalloc(&info, 64));
+    CK(hipMemcpy(A0, h.data(), N * N * 8, hipMemcpyHostToDevice));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    float sum = 0.f, best = 1e30f;
+    const int reps = 10;
+    for (int r = 0; r < reps + 2; ++r) {
+      CK(hipMemcpy(A, A0, N * N * 8, hipMemcpyDeviceToDevice));
+      CK(hipDeviceSynchronize());
+      CK(hipEventRecord(e0));
+      // row-major lower = column-major upper
+      rocblas_status st = rocsolver_dpotrf(handle, rocblas_fill_upper, (rocblas_int)N, A, (rocblas_int)N, info);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      if (st != rocblas_status_success) printf("rocsolver_dpotrf status %d\n", (int)st);
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      if (r >= 2) {
+        sum += ms;
+        best = std::min(best, ms);
+      }
+    }
+    int hinfo = -1;
+    CK(hipMemcpy(&hinfo, info, 4, hipMemcpyDeviceToHost));
+    printf("N=%lld  rocsolver_dpotrf %.3f ms (best %.3f)  info %d\n", (long long)N, sum / reps, best, hinfo);
+    CK(hipFree(A0)); CK(hipFree(A)); CK(hipFree(info));
+  }
+  rocblas_destroy_handle(handle);
+}
+
+// one blocked factorisation at N with the step-level stamps and the diagonal phases of step `st`
+static void trace_steps(int64_t N, int st) {
+  std::vector<double> h(N * N);
+  for (int64_t i = 0; i < N; ++i)
+    for (int64_t j = 0; j < N; ++j) h[i * N + j] = (i == j) ? N : 1.0 / (1.0 + std::abs((double)(i - j)));
+  double *A, *ws;
+  int* info;
+  CK(hipMalloc(&A, N * N * 8));
+  CK(hipMalloc(&ws, chol_ws_doubles(N) * 8));
+  CK(hipMalloc(&info, 64));
+  const int64_t r0 = (int64_t)(st + 1) * 64;
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(g_strace_step), &st, sizeof(int)));
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(g_btrace_r0), &r0, sizeof(int64_t)));
+  unsigned long long t[2][8], b[4][16];
+  for (int rep = 0; rep < 3; ++rep) {
+    CK(hipMemcpy(A, h.data(), N * N * 8, hipMemcpyHostToDevice));
+    CK(hipMemset(g_strace_ptr(), 0, sizeof(t)));
+    CK(launch_cholesky_mode(0, A, N, N, info, ws, kCholBlocked));
+    CK(hipDeviceSynchronize());
+  }
+  CK(hipMemcpyFromSymbol(t, HIP_SYMBOL(g_strace), sizeof(t)));
+  CK(hipMemcpyFromSymbol(b, HIP_SYMBOL(g_btrace), sizeof(b)));
+  const char* nm[7] = {"WG0 start", "WG0 factored", "W published", "WG1 start", "WG(1,0) waits", "flag seen",
+                       "panel done"};
+  printf("N=%lld step %d (blocked): stamps in us from WG0's start (100 MHz clock)\n", (long long)N, st);
+  for (int k = 0; k < 2; ++k) {
+    printf("  step %d:", st + k);
+    for (int id = 0; id < 7; ++id)
+      if (t[k][id]) printf(" %s %.2f |", nm[id], ((long long)t[k][id] - (long long)t[0][0]) / 100.0);
+    printf("\n");
+  }
+  unsigned long long base = b[0][0];
+  for (int w = 0; w < 4; ++w) base = std::min(base, b[w][0]);
+  printf("  its diagonal block (cycles from the first wave's start):\n");
+  for (int w = 0; w < 4; ++w) {
+    printf("    wave %d: tiles %lld | F %lld-%lld | post %lld\n", w, (long long)(b[w][1] - base),
+           (long long)(b[w][8] - base), (long long)(b[w][9] - base), (long long)(b[w][10] - base));
+  }
+  CK(hipFree(A)); CK(hipFree(ws)); CK(hipFree(info));
+  const int64_t none = -1;
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(g_btrace_r0), &none, sizeof(int64_t)));
+  const int nostep = -1;
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(g_strace_step), &nostep, sizeof(int)));
+}
+
 int main(int argc, char** argv) {
   trace_diag();
+  trace_diag_blocked();
+  trace_steps(3000, 20);
+  trace_steps(3000, 2);
   // extra dynamic LDS per update workgroup: 0 (3 workgroups per CU by VGPRs), 16 KB (2), 48 KB (1)
   const size_t extra[3] = {0, 16 << 10, 48 << 10};
   std::vector<int64_t> sizes;
@@ -92,29 +259,42 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    // the two launch schedules interleaved: kCholTwoLaunch (panel + update per step, round 2) and
-    // kCholFused (the update launch forms the next panel; round 3)
-    float best = 1e30f, sum = 0.f, best2 = 1e30f, sum2 = 0.f;
+    // the launch schedules interleaved: kCholTwoLaunch (round 2), kCholFused (round 3), kCholBlocked (round 4),
+    // kCholBlockedAcqRel (round 4 with the agent-scope release / acquire flag)
+    const int modes[4] = {kCholTwoLaunch, kCholFused, kCholBlocked, kCholBlockedAcqRel};
+    float msum[4] = {0, 0, 0, 0}, mbest[4] = {1e30f, 1e30f, 1e30f, 1e30f};
     const int reps = 10;
+    std::vector<double> Lref(N * N), Lm(N * N);
+    double mdiff[4] = {0, 0, 0, 0};
+    int minfo[4] = {0, 0, 0, 0};
     for (int r = 0; r < reps + 1; ++r) {
-      for (int mode = 0; mode < 2; ++mode) {
+      for (int m = 0; m < 4; ++m) {
         CK(hipMemcpy(A, A0, N * N * 8, hipMemcpyDeviceToDevice));
         CK(hipMemset(info, 0, 4));
         CK(hipEventRecord(e0));
-        CK(launch_cholesky_mode(0, A, N, N, info, ws, mode == 0 ? kCholTwoLaunch : kCholFused));
+        CK(launch_cholesky_mode(0, A, N, N, info, ws, modes[m]));
         CK(hipEventRecord(e1));
         CK(hipEventSynchronize(e1));
         float ms;
         CK(hipEventElapsedTime(&ms, e0, e1));
-        if (r > 0 && mode == 1) {
-          best = ms < best ? ms : best;
-          sum += ms;
-        } else if (r > 0) {
-          best2 = ms < best2 ? ms : best2;
-          sum2 += ms;
+        if (r > 0) {
+          msum[m] += ms;
+          mbest[m] = std::min(mbest[m], ms);
+        } else {
+          CK(hipMemcpy(m == 0 ? Lref.data() : Lm.data(), A, N * N * 8, hipMemcpyDeviceToHost));
+          CK(hipMemcpy(&minfo[m], info, 4, hipMemcpyDeviceToHost));
+          if (m > 0)
+            for (int64_t i = 0; i < N; ++i)
+              for (int64_t j = 0; j <= i; ++j)
+                mdiff[m] = std::max(mdiff[m], std::abs(Lm[i * N + j] - Lref[i * N + j]) / std::sqrt(h[i * N + i]));
         }
       }
     }
+    printf("N=%lld  two-launch %.3f (best %.3f) | fused %.3f (%.3f) | blocked %.3f (%.3f) | blocked acq/rel %.3f (%.3f) ms;"
+           " info %d %d %d %d; max |L - L_twolaunch|/sqrt(A_ii) %.1e %.1e %.1e\n",
+           (long long)N, msum[0] / reps, mbest[0], msum[1] / reps, mbest[1], msum[2] / reps, mbest[2], msum[3] / reps,
+           mbest[3], minfo[0], minfo[1], minfo[2], minfo[3], mdiff[1], mdiff[2], mdiff[3]);
+    float best = mbest[1], sum = msum[1], best2 = mbest[0], sum2 = msum[0];
     printf("N=%lld  two launches per step %.3f ms (best %.3f)\n", (long long)N, sum2 / reps, best2);
     {
       float sx[3] = {0.f, 0.f, 0.f};
@@ -177,9 +357,11 @@ int main(int argc, char** argv) {
       for (int64_t k = 0; k <= j; ++k) s += L[i * N + k] * L[j * N + k];
       worst = std::max(worst, std::abs(s - h[i * N + j]) / std::abs(h[i * N + i]));
     }
+    // the library's default schedule after the loops above: the residual of launch_cholesky's factor
     printf("N=%lld  Cholesky (fused) %.3f ms (best %.3f, %d steps = %.1f us/step)  info %d  max |LLt - A|/A_ii %.2e\n",
            (long long)N, sum / reps, best, (int)((N + 63) / 64), best * 1e3 / ((N + 63) / 64), hinfo, worst);
     CK(hipFree(A0)); CK(hipFree(A)); CK(hipFree(ws)); CK(hipFree(info));
   }
+  time_rocsolver(sizes);
   return 0;
 }

@@ -123,8 +123,8 @@ def cpu_baseline(X, targets, ls, variances, Xc, acq_fn, label, seconds):
     chunk = 4096
     done = 0
     t0 = time.perf_counter()
-    while True:
-        xc = Xc[done % len(Xc): done % len(Xc) + chunk]
+    while done < len(Xc):                 # a prefix of the batch: never past its end
+        xc = Xc[done: done + chunk]
         mus, vs = [], []
         for g in gps:
             m, v = g.predict(xc)
@@ -135,10 +135,15 @@ def cpu_baseline(X, targets, ls, variances, Xc, acq_fn, label, seconds):
         if time.perf_counter() - t0 >= seconds:
             break
     dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "candidates/s", "cores": threads, "host_cpu_count": ncpu, "kind": "port",
-            "sample": f"{done} candidate evaluations in chunks of {chunk}, cycling through the {len(Xc)}-candidate "
-                      f"batch; oracle posterior (dtrtrs) + "
-                      f"{label} + arg-max, {dt:.1f} s; cores = numpy BLAS threads used (threadpoolctl)"}
+    # the box gives one GPU's job a share of the host's CPUs (OMP_NUM_THREADS; 16 on this pool), and numpy's
+    # BLAS runs with that many threads: `cores`.  per_core and the host-wide figure (the rate scaled linearly to
+    # all of os.cpu_count(), an upper bound: BLAS-2 dtrtrs does not scale linearly) are reported beside it.
+    rate = done / dt
+    return {"value": rate, "unit": "candidates/s", "cores": threads, "host_cpu_count": ncpu, "kind": "port",
+            "per_core": rate / max(threads, 1), "host_linear_upper_bound": rate / max(threads, 1) * ncpu,
+            "sample": f"the first {done} of the {len(Xc)} candidates of this GPU's batch in chunks of {chunk}; "
+                      f"oracle posterior (dtrtrs) + {label} + arg-max, {dt:.1f} s; cores = numpy BLAS threads "
+                      f"used (threadpoolctl; the job's CPU share)"}
 
 
 def run_solve(args, cfg, world_size, rank):
@@ -318,17 +323,22 @@ def reference_cpu(config):
 def reference_solve_c1():
     """The reference's own MultiSurrogateOptimiser.solve on the README run, timed in the build container
     (tools/ref_solve_baseline.py → profiles/r03_ref_solve_c1.json; GPy / pymoo replaced by doubles)."""
-    path = os.path.join(REPO, "profiles", "r03_ref_solve_c1.json")
-    try:
-        with open(path) as f:
-            r = json.loads(f.read().strip().splitlines()[-1])
-    except (OSError, ValueError, IndexError):
+    for name in ("r04_ref_solve_c1.json", "r03_ref_solve_c1.json"):
+        path = os.path.join(REPO, "profiles", name)
+        try:
+            with open(path) as f:
+                r = json.loads(f.read().strip().splitlines()[-1])
+            break
+        except (OSError, ValueError, IndexError):
+            r = None
+    if r is None:
         return None
     return {"value": r["value"], "unit": r["unit"], "cores": r["cores"], "kind": "reference",
             "sample": f"the whole run (budget 100, {r['seconds']:.0f} s, final HV {r['final_hv']:.2f}); "
                       + r["doubles"],
-            "measured_in": "build container (8 vCPU Xeon), tools/ref_solve_baseline.py",
-            "source": "profiles/r03_ref_solve_c1.json"}
+            "measured_in": r.get("measured_in", "build container (8 vCPU Xeon)") + ", tools/ref_solve_baseline.py; "
+                           "GPy and pymoo are absent there and replaced by the doubles named in `sample`",
+            "source": f"profiles/{name}"}
 
 
 def load_traffic(n, N, kernel="posterior"):
@@ -587,10 +597,18 @@ def main():
         torch.cuda.synchronize()
         kb_ms = e0.elapsed_time(e1) / reps
         kb_bytes = 8.0 * (n + d) * N + 8.0 * n * (d + 1)      # 8(n+d) per candidate + model state
-        kblock = {"bound": "hbm", "achieved": kb_bytes / (kb_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        # the same launch against the FP64 pipe: distance n(2d+2) + ~10n Matern flop per candidate (SURVEY §8d's
+        # posterior count without the triangular product); at n_var > 8 the cross-term MFMAs + transform, not the
+        # stores, bound it
+        kb_flops = float(n) * (2 * d + 2 + 10) * N
+        kb_fp64 = kb_flops / (kb_ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS
+        kblock = {"bound": "hbm" if d <= 8 else "mfma",   # n_var > 8: the FP64 pipe (cross-term MFMAs + Matern VALU)
+                  "achieved": kb_bytes / (kb_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                   "frac": kb_bytes / (kb_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": load_traffic(n, N, "kblock"),
+                  "fp64_frac": kb_fp64, "fp64_tflops": kb_flops / (kb_ms * 1e-3) / 1e12,
                   "ms": kb_ms,
-                  "note": f"omb_kernel_block writes K ({n}, {N}) fp64 to HBM"}
+                  "note": f"omb_kernel_block writes K ({n}, {N}) fp64 to HBM; frac = HBM fraction, fp64_frac = "
+                          f"{n * (2 * d + 12)} flop per candidate / time / {FP64_MFMA_PEAK_TFLOPS} TFLOP/s"}
         del K
 
     # per-iteration model-state install, outside `value`: what a BO iteration does before its

@@ -181,8 +181,43 @@ class AcquisitionEngine:
         v1 = float(self.score(acq_fn, x1[None, :])[0])
         return (x1, v1) if v1 > v0 else (np.asarray(x0, np.float64), float(v0))
 
+    def _starts(self, acq_fn, lower, upper, n_candidates, seed, k, pool=64, sep=0.1):
+        """Round 0 of a multi-start search: the ``n_candidates`` Sobol points scored on the device, every rank's
+        ``pool`` best (value, global index) pairs gathered, then up to ``k`` starts picked greedily in
+        (value desc, index asc) order — the arg-max rule, so start 0 is round 0's arg-max — each at least ``sep``
+        (in units of the box) from the starts already taken.  Returns [(x, v)], best first."""
+        d = lower.size
+        W, rank = world()
+        start, count = shard_range(n_candidates, W, rank)
+        self.ctx.set_sobol(d, lower, upper, seed=seed)
+        vals = self.ctx.eval(self.ctx.sobol(start, count)) if acq_fn is None else acq_fn(self.ctx.sobol(start, count))
+        v = torch.nan_to_num(vals, nan=-float("inf"))
+        top = torch.topk(v, min(pool, count))
+        pairs = torch.stack([top.values, top.indices.to(torch.float64) + start], 1)
+        if W > 1:
+            pad = torch.full((pool, 2), -float("inf"), dtype=torch.float64, device=pairs.device)
+            pad[:pairs.shape[0]] = pairs
+            pad[pairs.shape[0]:, 1] = -1.0
+            if torch.distributed.get_backend() == "gloo":
+                pad = pad.cpu()
+            gathered = [torch.empty_like(pad) for _ in range(W)]
+            torch.distributed.all_gather(gathered, pad)
+            pairs = torch.cat(gathered)
+        P = pairs.cpu().numpy()
+        P = P[(P[:, 1] >= 0) & np.isfinite(P[:, 0])]
+        P = P[np.lexsort((P[:, 1], -P[:, 0]))]
+        span = np.maximum(upper - lower, 1e-300)
+        out = []
+        for val, idx in P:
+            x = self.ctx.sobol(int(idx), 1).cpu().numpy()[0]
+            if all(np.max(np.abs(x - y) / span) >= sep for y, _ in out):
+                out.append((x, float(val)))
+            if len(out) == k:
+                break
+        return out
+
     def maximise(self, acq_fn, lower, upper, n_candidates=1 << 16, seed=0, refine_rounds=2, shrink=0.1,
-                 polish=True):
+                 polish=True, starts=None):
         """Arg-max of the acquisition over [lower, upper]^d.
 
         ``acq_fn`` is None for the current plan (fused chain, one C call per batch) or a callable
@@ -192,45 +227,59 @@ class AcquisitionEngine:
         ``shrink`` times smaller on the incumbent and keeps it if it improves.  ``polish`` then
         finishes with L-BFGS-B from the incumbent, as scipy's differential_evolution does by
         default (``polish``); with several ranks rank 0 polishes and broadcasts the point.
+        ``starts`` (default: 1 for n_var ≤ 2, 4 above): independent incumbents refined and polished from
+        round 0's best well-separated points (_starts) — round 0's arg-max alone stopped 1.2% short of
+        scipy's DE on a 6-D expected decomposition (tests/test_gpu_config1.py); the first start is the
+        single-start search's, so the result is never worse.
         Returns (x_best (d,), value).
         """
         lower = np.asarray(lower, np.float64)
         upper = np.asarray(upper, np.float64)
         d = lower.size
         W, rank = world()
-        best_x, best_v = None, -np.inf
-        lo, hi = lower, upper
-        for rnd in range(refine_rounds + 1):
+        k = (1 if d <= 2 else 4) if starts is None else int(starts)
+        if k > 1:
+            cands = self._starts(acq_fn, lower, upper, n_candidates, seed, k)
+        else:
             start, count = shard_range(n_candidates, W, rank)
-            self.ctx.set_sobol(d, lo, hi, seed=seed + rnd)
+            self.ctx.set_sobol(d, lower, upper, seed=seed)
             if acq_fn is None:
                 pair = self.ctx.eval_argmax_sobol(start, count)
             else:
-                vals = acq_fn(self.ctx.sobol(start, count))
-                pair = self.ctx.argmax_dev(vals, offset=start)
+                pair = self.ctx.argmax_dev(acq_fn(self.ctx.sobol(start, count)), offset=start)
             g = global_argmax(pair).cpu().numpy()
-            if g[1] >= 0 and g[0] > best_v:
-                best_x = self.ctx.sobol(int(g[1]), 1).cpu().numpy()[0]   # the winner, regenerated
-                best_v = float(g[0])
-            if best_x is None:
-                break
-            half = shrink ** (rnd + 1) * (upper - lower) / 2
-            lo = np.maximum(lower, best_x - half)
-            hi = np.minimum(upper, best_x + half)
-        if best_x is None:   # every candidate was NaN/−inf: fall back to the first Sobol point
+            cands = [(self.ctx.sobol(int(g[1]), 1).cpu().numpy()[0], float(g[0]))] if g[1] >= 0 else []
+        if not cands:   # every candidate was NaN/−inf: fall back to the first Sobol point
             self.ctx.set_sobol(d, lower, upper, seed=seed)
-            best_x = self.ctx.sobol(0, 1).cpu().numpy()[0]
-            return best_x, best_v
-        if polish:
-            if W == 1:
-                best_x, best_v = self.polish(acq_fn, best_x, best_v, lower, upper)
-            else:
-                box = [None]
-                if rank == 0:
-                    box[0] = self.polish(acq_fn, best_x, best_v, lower, upper)
-                torch.distributed.broadcast_object_list(box, src=0)
-                best_x, best_v = np.asarray(box[0][0], np.float64), float(box[0][1])
-        return best_x, best_v
+            return self.ctx.sobol(0, 1).cpu().numpy()[0], -np.inf
+        results = []
+        for best_x, best_v in cands:
+            for rnd in range(1, refine_rounds + 1):
+                half = shrink ** rnd * (upper - lower) / 2
+                lo = np.maximum(lower, best_x - half)
+                hi = np.minimum(upper, best_x + half)
+                start, count = shard_range(n_candidates, W, rank)
+                self.ctx.set_sobol(d, lo, hi, seed=seed + rnd)
+                if acq_fn is None:
+                    pair = self.ctx.eval_argmax_sobol(start, count)
+                else:
+                    pair = self.ctx.argmax_dev(acq_fn(self.ctx.sobol(start, count)), offset=start)
+                g = global_argmax(pair).cpu().numpy()
+                if g[1] >= 0 and g[0] > best_v:
+                    best_x = self.ctx.sobol(int(g[1]), 1).cpu().numpy()[0]   # the winner, regenerated
+                    best_v = float(g[0])
+            if polish:
+                if W == 1:
+                    best_x, best_v = self.polish(acq_fn, best_x, best_v, lower, upper)
+                else:
+                    box = [None]
+                    if rank == 0:
+                        box[0] = self.polish(acq_fn, best_x, best_v, lower, upper)
+                    torch.distributed.broadcast_object_list(box, src=0)
+                    best_x, best_v = np.asarray(box[0][0], np.float64), float(box[0][1])
+            results.append((best_x, best_v))
+        # the best start; ties to the earliest (the single-start search's when it ties)
+        return max(results, key=lambda r: r[1])
 
 
 _ENGINES = {}

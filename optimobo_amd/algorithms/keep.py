@@ -41,6 +41,8 @@ class KEEP(BODriver):
             pop = ea.initial_population(Xsample, lower, upper)           # keep.py:246-252
             tape = ea.ea_tape(len(pop), Xsample.shape[1])               # keep.py:256-290
             return eng.ctx.ea_search(pop, tape, current_best, lower, upper, mode=1)
+        if self.acq_search == "ea" and Xsample is not None:
+            ea.warn_batch_fallback("KEEP", len(Xsample))
         eng.plan_pareto_ei(current_best)
         return self._maximise([scalar_model, pareto_model], None)
 

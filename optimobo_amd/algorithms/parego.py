@@ -33,6 +33,8 @@ class ParEGO(BODriver):
             pop = ea.initial_population(Xsample, lower, upper)           # parego.py:229-235
             tape = ea.ea_tape(len(pop), Xsample.shape[1])               # the search's draws, parego.py:238-269
             return eng.ctx.ea_search(pop, tape, current_best, lower, upper, mode=0)
+        if self.acq_search == "ea" and Xsample is not None:
+            ea.warn_batch_fallback("ParEGO", len(Xsample))
         eng.plan_ei(current_best, 1e-6)
         return self._maximise([model], None)
 

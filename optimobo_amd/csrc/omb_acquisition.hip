@@ -20,8 +20,9 @@ static unsigned acq_grid(int64_t N) {
 }
 
 // ------------------------------------------------------------------------------ EHVI 2-D
-// One thread per candidate; the per-candidate arithmetic is ehvi2d_point (omb_math.h), shared with the fused
-// posterior epilogue (omb_posterior.hip, posterior_reg_ehvi_kernel).
+// Four lanes per candidate (ehvi2d_point4, omb_math.h — shared with the one-launch chains, so both give bitwise the
+// same values and the same arg-max): wave w of a workgroup takes 16 candidates, lane group g = lane >> 4 a quarter of
+// their stripes.
 __global__ __launch_bounds__(kAcqThreads) void ehvi2d_kernel(const double* __restrict__ mu,
                                                              const double* __restrict__ var, int64_t ld, int64_t N,
                                                              const double* __restrict__ pf, int P, double r0,
@@ -36,17 +37,23 @@ __global__ __launch_bounds__(kAcqThreads) void ehvi2d_kernel(const double* __res
   }
   if (threadIdx.x == 0) y1[0] = r0;
   __syncthreads();
-  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < N; c += (int64_t)gridDim.x * blockDim.x)
-    out[c] = ehvi2d_point(mu[c], mu[ld + c], var[c], mode == OMB_EHVI_REFERENCE ? 0.0 : var[ld + c], y1, y2, P, r1,
-                          s00, s01, mode);
+  const int lane = threadIdx.x & 63, g = lane >> 4;
+  const int64_t per_block = kAcqThreads / 4;
+  for (int64_t base = (int64_t)blockIdx.x * per_block; base < N; base += (int64_t)gridDim.x * per_block) {
+    const int64_t c = base + 16 * (threadIdx.x >> 6) + (lane & 15);
+    const int64_t cc = c < N ? c : N - 1;                // every lane of the wave takes part in the shuffles
+    const double v = ehvi2d_point4(mu[cc], mu[ld + cc], var[cc], mode == OMB_EHVI_REFERENCE ? 0.0 : var[ld + cc], y1,
+                                   y2, P, r1, s00, s01, mode, g);
+    if (g == 0 && c < N) out[c] = v;
+  }
 }
 
 hipError_t launch_ehvi2d(hipStream_t stream, const double* mu, const double* var, int64_t ld, int64_t N,
                          const double* pf, int P, double r0, double r1, double s00, double s01, int mode,
                          double* out) {
   size_t shm = sizeof(double) * (2 * P + 1);
-  hipLaunchKernelGGL(ehvi2d_kernel, dim3(acq_grid(N)), dim3(kAcqThreads), shm, stream, mu, var, ld, N, pf, P, r0, r1,
-                     s00, s01, mode, out);
+  hipLaunchKernelGGL(ehvi2d_kernel, dim3(acq_grid(4 * N)), dim3(kAcqThreads), shm, stream, mu, var, ld, N, pf, P, r0,
+                     r1, s00, s01, mode, out);
   return hipGetLastError();
 }
 

@@ -346,8 +346,15 @@ int run_chain(omb_ctx* ctx, const double* Xc, bool sobol, int64_t start, int64_t
   if ((N + 31) / 32 > 0x7fffffffLL) return fail(ctx, OMB_EUNSUP, "N=%lld too large", (long long)N);
   const int k = pl.k;
   const size_t nd = (size_t)N;
+  // the one-launch EHVI-2D chain (launch_fused_ehvi2d) where it applies; its per-workgroup pairs go to the chain
+  // workspace past the Sobol points when ctx->partials is too small
+  const bool one_launch = result_dev && !vals_out && N > 0 && ctx->fused_chain && pl.kind == PLAN_EHVI2D &&
+                          16 * max_R <= OMB_MAX_TRAIN && fused_ehvi2d_fits(k, max_R, args.DP, pl.P);
+  const int64_t fblocks = one_launch ? fused_ehvi2d_blocks(max_R, args.DP, N) : 0;
   const size_t doubles = 2 * (size_t)k * nd + nd + (nd + 1) / 2 + (sobol ? nd * args.d : 0);
-  if ((rc = grow_dev(ctx, &ctx->work, &ctx->work_cap, (doubles ? doubles : 1) * sizeof(double), "chain workspace")))
+  const size_t extra = fblocks > kArgmaxMaxBlocks ? 2 * (size_t)fblocks : 0;
+  if ((rc = grow_dev(ctx, &ctx->work, &ctx->work_cap, (doubles + extra ? doubles + extra : 1) * sizeof(double),
+                     "chain workspace")))
     return rc;
   double* mu = static_cast<double*>(ctx->work);
   double* var = mu + (size_t)k * nd;
@@ -380,10 +387,11 @@ int run_chain(omb_ctx* ctx, const double* Xc, bool sobol, int64_t start, int64_t
   if (e == hipSuccess && sobol && N > 0) e = launch_sobol(ctx->stream, ctx->sob, ctx->sob_d, ctx->sob_bits, start, N, Xs);
   if (sobol) Xc = Xs;
   if (e == hipSuccess) e = mark(1);
-  if (e == hipSuccess && result_dev && !vals_out && N > 0 && ctx->fused_chain && pl.kind == PLAN_EHVI2D &&
-      16 * max_R <= OMB_MAX_TRAIN && fused_ehvi2d_fits(k, max_R, args.DP, pl.P)) {
-    // posterior → EHVI-2D → arg-max in one launch (launch_fused_ehvi2d); bitwise the unfused chain's result
-    FusedEhvi2d fe{pl.geo, pl.P, pl.mode, pl.r[0], pl.r[1], pl.s00, pl.s01, offset, ctx->partials,
+  if (e == hipSuccess && one_launch) {
+    // posterior → EHVI-2D → arg-max in one launch; bitwise the separate launches' result.  The ticket lives after
+    // ctx->partials.
+    double* pairs = extra ? mu + doubles : ctx->partials;
+    FusedEhvi2d fe{pl.geo, pl.P, pl.mode, pl.r[0], pl.r[1], pl.s00, pl.s01, offset, pairs,
                    reinterpret_cast<unsigned*>(ctx->partials + 2 * kArgmaxMaxBlocks), result_dev};
     e = launch_fused_ehvi2d(ctx->stream, args, max_R, Xc, N, fe, ctx->fused_chain);
     for (int i = 2; i <= 4 && e == hipSuccess; ++i) e = mark(i);

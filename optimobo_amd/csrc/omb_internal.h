@@ -64,11 +64,13 @@ struct FusedEhvi2d {
   int P, mode;
   double r0, r1, s00, s01;
   int64_t offset;         // global index of candidate 0
-  double* partials;       // 2 doubles per workgroup (≤ kArgmaxMaxBlocks)
+  double* partials;       // 2 doubles per workgroup (fused_ehvi2d_blocks)
   unsigned* ticket;       // 0 between launches (the last workgroup resets it)
   double* result;         // {value, global index}
 };
 bool fused_ehvi2d_fits(int n_obj, int max_R, int DP, int P);
+// workgroups of the one-launch chain: FusedEhvi2d.partials must hold 2 doubles per workgroup
+int64_t fused_ehvi2d_blocks(int max_R, int DP, int64_t N);
 // variant 1: 16 waves per workgroup (4 per SIMD), 2: 8 waves
 hipError_t launch_fused_ehvi2d(hipStream_t stream, const GPArgs& args, int max_R, const double* Xc, int64_t N,
                                const FusedEhvi2d& fe, int variant = 1);
@@ -151,8 +153,9 @@ hipError_t launch_add_diag(hipStream_t stream, double* S, int64_t N, int64_t lds
 constexpr int kCholWsDoubles = 64 * 64;
 constexpr int kCholSpinFault = -2147483647;
 // kCholBlocked (round 4): the diagonal blocks by tiles of 16 (chol64_blocked); kCholBlockedAcqRel: the same with
-// the fused step's flag as an agent-scope release / acquire (tools/ablate/ablate_chol)
-enum { kCholTwoLaunch = 0, kCholFused = 1, kCholBlocked = 2, kCholBlockedAcqRel = 3 };
+// the fused step's flag as an agent-scope release / acquire, kCholBlockedMov: with the compiler's DPP moves in
+// place of the inline-asm v_fmac_f64_dpp (tools/ablate/ablate_chol)
+enum { kCholTwoLaunch = 0, kCholFused = 1, kCholBlocked = 2, kCholBlockedAcqRel = 3, kCholBlockedMov = 4 };
 int64_t chol_ws_doubles(int64_t N);
 hipError_t launch_cholesky(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws,
                            int spin_limit = kDefaultSpinLimit);

@@ -13,7 +13,11 @@ constexpr double kSqrt2Pi = 2.5066282746310002;         // np.sqrt(2*np.pi)   (s
 constexpr double kSqrt1_2 = 0.70710678118654752440;     // NPY_SQRT1_2
 
 // scipy.special.ndtr (cephes ndtr.c) — scipy.stats.norm.cdf.
+// The acquisition arithmetic below runs unfused (fp contract off): the same function inlined into two kernels
+// must give bitwise the same value (the one-launch chains against the separate launches), and the contraction
+// choices of -ffp-contract=fast depend on the surrounding code (a 1-ulp EHVI difference, gpurun_out/r04_d).
 __device__ __forceinline__ double ndtr(double a) {
+#pragma clang fp contract(off)
   double x = a * kSqrt1_2;
   double z = fabs(x);
   if (z < kSqrt1_2) return 0.5 + 0.5 * erf(x);
@@ -22,7 +26,10 @@ __device__ __forceinline__ double ndtr(double a) {
 }
 
 // scipy.stats.norm.pdf: exp(-x**2/2.0) / sqrt(2π).
-__device__ __forceinline__ double npdf(double t) { return exp(-(t * t) / 2.0) / kSqrt2Pi; }
+__device__ __forceinline__ double npdf(double t) {
+#pragma clang fp contract(off)
+  return exp(-(t * t) / 2.0) / kSqrt2Pi;
+}
 
 // util_functions.py:130-133  ψ(a,b,m,s) = s·φ((b−m)/s) + (a−m)·Φ((b−m)/s), given t=(b−m)/s.
 __device__ __forceinline__ double psi_t(double a, double m, double s, double t, double pdf_t, double cdf_t) {
@@ -403,18 +410,25 @@ __device__ __forceinline__ void matern_r2_tab256_x2(double r2a, double r2b, cons
   }
 }
 
-// EHVI-2D of one candidate: util_functions.py:81-128 (EHVI_2D_aux) with the stripe array S = [(r0,−∞), PF↑f2,
-// (−∞,r1)] of :93-109; y1[0] = r0, y1[i] / y2[i−1] = stripe i's f1 / f2 (i = 1..P).  φ/Φ of t_i = (y1[i]−μ0)/σA
-// are reused by stripe i+1 (the reference evaluates ψ(y1[i−1], y1[i−1]) from the same t), so each stripe costs
-// 2 Φ + 2 φ instead of 7 calls.  One function for ehvi2d_kernel and the fused posterior epilogue, so both give
-// bitwise the same values (and the same arg-max).
-__device__ __forceinline__ double ehvi2d_point(double m0, double m1, double v0, double v1, const double* y1,
-                                               const double* y2, int P, double r1, double s00, double s01, int mode) {
+// EHVI-2D of one candidate over four lanes: util_functions.py:81-128 (EHVI_2D_aux) with the stripe array
+// S = [(r0,−∞), PF↑f2, (−∞,r1)] of :93-109; y1[0] = r0, y1[i] / y2[i−1] = stripe i's f1 / f2 (i = 1..P).
+// Lane g (0..3; the candidate's four lanes are l, l^16, l^32, l^48 of one wave) sums the stripes of the g-th
+// contiguous quarter of 1..P; within a quarter φ/Φ of t_i = (y1[i]−μ0)/σA are reused by stripe i+1 (the
+// reference evaluates ψ(y1[i−1], y1[i−1]) from the same t), so a stripe costs 2 Φ + 2 φ instead of 7 calls, and a
+// quarter one Φ + φ more for its first t.  The quarters' partial sums meet by two xor-shuffles: every lane of the
+// candidate returns the same value, identical in every kernel that calls this (ehvi2d_kernel and the one-launch
+// chains), which is what makes their arg-max bitwise the same.  One lane per candidate (the round-3 kernel) summed
+// all P stripes serially: 4× the latency for the same issue count.
+__device__ __forceinline__ double ehvi2d_point4(double m0, double m1, double v0, double v1, const double* y1,
+                                                const double* y2, int P, double r1, double s00, double s01, int mode,
+                                                int g) {
+#pragma clang fp contract(off)
   double sA, sB;
+  bool nan = false;
   if (mode == OMB_EHVI_REFERENCE) {
     // change() scales the cached samples by sqrt(σ²0) (util_functions.py:233-235): a negative variance makes
     // every sample NaN, and np.cov of them NaN.
-    if (!(v0 >= 0.0)) return __builtin_nan("");
+    nan = !(v0 >= 0.0);
     sA = v0 * s00;   // c00 = σ²0·Cov(cache)00   (util_functions.py:163-167, 114-115)
     sB = v0 * s01;   // c01 = σ²0·Cov(cache)01   (a covariance used as a std: quirk 2)
   } else if (mode == OMB_EHVI_TEXTBOOK) {
@@ -424,26 +438,36 @@ __device__ __forceinline__ double ehvi2d_point(double m0, double m1, double v0, 
     sA = v0;
     sB = v1;
   }
-  double tp = (y1[0] - m0) / sA;
-  double cdf_p = ndtr(tp), pdf_p = npdf(tp);
+  const int chunk = (P + 3) >> 2;
+  const int i0 = 1 + g * chunk, i1 = min(P, (g + 1) * chunk);
   double sum1 = 0.0, sum2 = 0.0;
-  for (int i = 1; i <= P; ++i) {
-    const double y1p = y1[i - 1], y1i = y1[i], y2i = y2[i - 1];
-    const double t = (y1i - m0) / sA;
-    const double cdf_t = ndtr(t), pdf_t = npdf(t);
-    const double u = (y2i - m1) / sB;
-    const double p2 = sB * npdf(u) + (y2i - m1) * ndtr(u);          // ψ(y2i, y2i, μ1, σB)
-    sum1 = sum1 + (y1p - y1i) * cdf_t * p2;
-    const double psi_pp = sA * pdf_p + (y1p - m0) * cdf_p;          // ψ(y1[i−1], y1[i−1], μ0, σA)
-    const double psi_pi = sA * pdf_t + (y1p - m0) * cdf_t;          // ψ(y1[i−1], y1[i],   μ0, σA)
-    sum2 = sum2 + (psi_pp - psi_pi) * p2;
-    cdf_p = cdf_t;
-    pdf_p = pdf_t;
+  if (!nan && i0 <= i1) {
+    const double tp = (y1[i0 - 1] - m0) / sA;
+    double cdf_p = ndtr(tp), pdf_p = npdf(tp);
+    for (int i = i0; i <= i1; ++i) {
+      const double y1p = y1[i - 1], y1i = y1[i], y2i = y2[i - 1];
+      const double t = (y1i - m0) / sA;
+      const double cdf_t = ndtr(t), pdf_t = npdf(t);
+      const double u = (y2i - m1) / sB;
+      const double p2 = sB * npdf(u) + (y2i - m1) * ndtr(u);          // ψ(y2i, y2i, μ1, σB)
+      sum1 = sum1 + (y1p - y1i) * cdf_t * p2;
+      const double psi_pp = sA * pdf_p + (y1p - m0) * cdf_p;          // ψ(y1[i−1], y1[i−1], μ0, σA)
+      const double psi_pi = sA * pdf_t + (y1p - m0) * cdf_t;          // ψ(y1[i−1], y1[i],   μ0, σA)
+      sum2 = sum2 + (psi_pp - psi_pi) * p2;
+      cdf_p = cdf_t;
+      pdf_p = pdf_t;
+    }
   }
+  sum1 += __shfl_xor(sum1, 16);
+  sum1 += __shfl_xor(sum1, 32);
+  sum2 += __shfl_xor(sum2, 16);
+  sum2 += __shfl_xor(sum2, 32);
+  if (nan) return __builtin_nan("");
   double res = sum1 + sum2;
   if (mode == OMB_EHVI_TEXTBOOK) {
     // the stripe i = P+1 that range(1, n+1) leaves out (quirk 3): ψ(y1P,y1P,μ0,σA)·ψ(r1,r1,μ1,σB)
-    const double psiA = sA * pdf_p + (y1[P] - m0) * cdf_p;
+    const double tP = (y1[P] - m0) / sA;
+    const double psiA = sA * npdf(tP) + (y1[P] - m0) * ndtr(tP);
     const double u = (r1 - m1) / sB;
     res += psiA * (sB * npdf(u) + (r1 - m1) * ndtr(u));
   }

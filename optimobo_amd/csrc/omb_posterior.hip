@@ -479,9 +479,22 @@ __global__ __launch_bounds__(512) void kernel_block_pipe_kernel(GPDev g, int d, 
 // AW (n_var > 8 with d + 2 ≤ 4·⌈DP/4⌉, e.g. d = 30 in DP = 32): the packed rows already carry ‖x/ℓ‖² and 1 in
 // dimensions d and d + 1 (pack_X_kernel), inside the cross term's k-steps, so B = [−2·x*/ℓ, 1, ‖x*/ℓ‖²] gives
 // r² from the same 8 MFMA k-steps: the per-element fma, add and LDS read of ‖x/ℓ‖² go.
+// XCD-aware workgroup order (round 4, nx > 0; the grid is then 1-D with ⌈nx/8⌉·8·ny workgroups): consecutive
+// workgroups go to the 8 XCDs in turn, so workgroup b is mapped to candidate block x = 8·((b/8)/ny) + b mod 8 and
+// row block y = (b/8) mod ny — the ny row blocks of one candidate slab run back to back on ONE XCD and re-read
+// the slab from its L2 instead of from HBM (8 row blocks per slab at n = 1024, d = 30: 5.31 GB per launch
+// against 4.42 GB of algorithmic bytes, profiles/r03_v19_pmc_c5).  nx = 0: the plain 2-D grid (tools/ablate).
 template <int DP, int KIND, int CB, bool RCP = false, bool ROLL = false, bool AW = false>
 __global__ __launch_bounds__(512) void kernel_block_persist_kernel(GPDev g, int d, const double* __restrict__ Xc,
-                                                                   int64_t N, double* __restrict__ K, ExpCoef ec) {
+                                                                   int64_t N, double* __restrict__ K, ExpCoef ec,
+                                                                   int nx = 0, int ny = 0) {
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (nx > 0) {
+    const int slot = blockIdx.x >> 3;
+    bx = 8 * (slot / ny) + (blockIdx.x & 7);
+    by = slot % ny;
+    if (bx >= nx) return;
+  }
   constexpr bool kAug = DP <= 8 || AW;              // r² straight from the MFMA
   constexpr int KSD = DP <= 8 ? (DP + 5) / 4 : (DP + 3) / 4;
   constexpr int KSDP = ((DP + 5) / 4 + 1) / 2;   // = packed_X_pairs(DP)
@@ -493,9 +506,9 @@ __global__ __launch_bounds__(512) void kernel_block_persist_kernel(GPDev g, int 
   __shared__ double xsqs[kAug ? 1 : TPW * 16];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int T0 = blockIdx.y * TPW;
+  const int T0 = by * TPW;
   const int T1 = min((g.n + 15) / 16, T0 + TPW);
-  const int64_t base = (int64_t)blockIdx.x * (128 * CB) + 16 * wave;
+  const int64_t base = (int64_t)bx * (128 * CB) + 16 * wave;
   double il[KSD];
 #pragma unroll
   for (int s = 0; s < KSD; ++s) {
@@ -542,7 +555,7 @@ __global__ __launch_bounds__(512) void kernel_block_persist_kernel(GPDev g, int 
     }
     if (jb + 1 < CB && cb + 128 < N) load_raw(cb + 128, raw);   // next block, in flight during this one
     const int64_t col = cb + (lane & 15);
-    const bool cols_full = (int64_t)(blockIdx.x) * (128 * CB) + (int64_t)(jb + 1) * 128 <= N;   // workgroup-uniform
+    const bool cols_full = (int64_t)bx * (128 * CB) + (int64_t)(jb + 1) * 128 <= N;   // workgroup-uniform
     double* Kl = K + (int64_t)rsub * N + col;
     for (int T = T0; T < T1; ++T) {
       const d2* xa = reinterpret_cast<const d2*>(xfs + (T - T0) * (KSDP * 128) + 2 * lane);
@@ -577,6 +590,109 @@ __global__ __launch_bounds__(512) void kernel_block_persist_kernel(GPDev g, int 
   }
 }
 
+// Epilogue of the fused EHVI-2D chains (posterior_kernel<…, EPI = 1>): the BN candidates' EHVI from their moments in
+// LDS (mom: μ0 | σ²0 | μ1 | σ²1), the block's arg-max (higher value, lower index; NaN and −∞ never win), its pair to
+// fe.partials[blockIdx.x] (agent-scope stores) and an agent-scope ticket; the last workgroup reduces every pair
+// and writes fe.result = {value, index + offset}, then resets the ticket.  geo: 2·kFusedMaxP + 1 doubles of LDS,
+// scratch: ≥ 2·(NT/64) doubles of LDS.
+template <int BN, int NT>
+__device__ __forceinline__ void fused_ehvi2d_epilogue(const FusedEhvi2d& fe, const double* mom, double* geo,
+                                                      int64_t N, int64_t c0, double* scratch) {
+  static_assert(BN % 16 == 0 && BN / 16 <= NT / 64, "16 candidates per wave");
+  constexpr int NW = NT / 64;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = tid >> 6;
+  const int P = fe.P;
+  double* y1 = geo;
+  double* y2 = geo + P + 1;
+  for (int i = tid; i < P; i += NT) {
+    y1[i + 1] = fe.pf[2 * i];
+    y2[i] = fe.pf[2 * i + 1];
+  }
+  if (tid == 0) y1[0] = fe.r0;
+  __syncthreads();
+  __shared__ int is_last;
+  long long* sbi = reinterpret_cast<long long*>(scratch + NW);
+  if (wave < BN / 16) {
+    // wave w: candidates 16w + (lane & 15), four lanes each (ehvi2d_point4)
+    double bv = -__builtin_inf();
+    long long bi = -1;
+    const int cl = 16 * wave + (lane & 15);
+    const int64_t c = c0 + cl;
+    const double v = ehvi2d_point4(mom[cl], mom[2 * BN + cl], mom[BN + cl],
+                                   fe.mode == OMB_EHVI_REFERENCE ? 0.0 : mom[3 * BN + cl], y1, y2, P, fe.r1, fe.s00,
+                                   fe.s01, fe.mode, lane >> 4);
+    if (lane < 16 && c < N && v == v && v > -__builtin_inf()) {
+      bv = v;
+      bi = c;
+    }
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) {
+      const double ov = __shfl_xor(bv, off);
+      const long long oi = __shfl_xor(bi, off);
+      if (argmax_better(ov, oi, bv, bi)) {
+        bv = ov;
+        bi = oi;
+      }
+    }
+    if (lane == 0) {
+      scratch[wave] = bv;
+      sbi[wave] = bi;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double bv = scratch[0];
+    long long bi = sbi[0];
+    for (int w = 1; w < BN / 16; ++w)
+      if (argmax_better(scratch[w], sbi[w], bv, bi)) {
+        bv = scratch[w];
+        bi = sbi[w];
+      }
+    wf_store_f64(&fe.partials[2 * blockIdx.x], bv);
+    wf_store_f64(&fe.partials[2 * blockIdx.x + 1], __builtin_bit_cast(double, bi));
+    const unsigned prev = __hip_atomic_fetch_add(fe.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    is_last = prev == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!is_last) return;
+  double v = -__builtin_inf();
+  long long i = -1;
+  for (int b = tid; b < (int)gridDim.x; b += NT) {
+    const double bv = wf_load_f64(&fe.partials[2 * b]);
+    const long long bi = __builtin_bit_cast(long long, wf_load_f64(&fe.partials[2 * b + 1]));
+    if (argmax_better(bv, bi, v, i)) {
+      v = bv;
+      i = bi;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const double ov = __shfl_xor(v, off);
+    const long long oi = __shfl_xor(i, off);
+    if (argmax_better(ov, oi, v, i)) {
+      v = ov;
+      i = oi;
+    }
+  }
+  __syncthreads();                                       // the block pairs in scratch are read
+  if (lane == 0) {
+    scratch[wave] = v;
+    sbi[wave] = i;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < NW; ++w)
+      if (argmax_better(scratch[w], sbi[w], v, i)) {
+        v = scratch[w];
+        i = sbi[w];
+      }
+    fe.result[0] = i < 0 ? -__builtin_inf() : v;
+    fe.result[1] = i < 0 ? -1.0 : (double)(i + fe.offset);
+    __hip_atomic_store(fe.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // Per-workgroup phase timestamps of the posterior kernels for tools/ablate/ablate_posterior (empty here).
 #ifndef OMB_POST_TRACE
 #define OMB_POST_TRACE(id)
@@ -592,10 +708,15 @@ __global__ __launch_bounds__(512) void kernel_block_persist_kernel(GPDev g, int 
 // chain at ‖x‖² + ‖x*‖² with −2x* pre-scaled (one fma fewer per element), bit 65536 forces a spin
 // bound of 0 on the counter-ring waits (the fault-word path).
 // NW = waves per workgroup (8 or 16): waves w, w+4, w+8, w+12 share a SIMD.
-template <int RT, int CT, int DP, int KIND, int NW = 8, int ABL = 0>
+// EPI = 1 (round 4, omb_eval_argmax with an EHVI-2D plan, n > 128): one workgroup computes BOTH objectives of its
+// BN candidates — the whole pipeline below runs once per objective, the moments go to LDS instead of HBM — and
+// then the epilogue evaluates the candidates' EHVI (ehvi2d_point4, util_functions.py:136-167), reduces the
+// block's arg-max and hands it to the last workgroup (fe.ticket), which writes {value, index + offset}: the
+// posterior → ehvi2d_kernel → argmax_pass1/2 chain in one launch, bit for bit.
+template <int RT, int CT, int DP, int KIND, int NW = 8, int ABL = 0, int EPI = 0>
 __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args, const double* __restrict__ Xc,
                                                                      int64_t N, double* __restrict__ mu_out,
-                                                                     double* __restrict__ var_out) {
+                                                                     double* __restrict__ var_out, FusedEhvi2d fe) {
   constexpr int NT = 64 * NW;                 // threads per workgroup
   constexpr int G = NW / 4;                   // waves sharing one SIMD
   constexpr int BN = 16 * CT;                 // candidates per workgroup
@@ -617,14 +738,17 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
   constexpr bool kTab256 = !(ABL & 16384) && KIND == OMB_KERNEL_MATERN52;
   constexpr int kTabN = kTab256 ? 256 : 64;
   __shared__ double kbuf[NBUF * CHUNK + kCtrDoubles + (kCandLds ? DP * BN : 0) + kTabN];
+  __shared__ double fe_mom[EPI ? 4 * BN : 1];            // EPI: μ0 | σ²0 | μ1 | σ²1 of the block's candidates
+  __shared__ double fe_geo[EPI ? 2 * kFusedMaxP + 1 : 1];
 
   OMB_POST_TRACE(0);
-  const int obj = blockIdx.y;
-  const GPDev g = args.gp[obj];
   const int d = args.d;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t c0 = (int64_t)blockIdx.x * BN;
+#pragma unroll 1
+  for (int obj = EPI ? 0 : (int)blockIdx.y; obj < (EPI ? 2 : (int)blockIdx.y + 1); ++obj) {
+  const GPDev g = args.gp[obj];
 
   // ---- this thread's generation candidate (fixed across chunks since BN | NT)
   const int cg = tid % BN;
@@ -991,11 +1115,17 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
       for (int t = tid; t < NT; t += BN) m += redmu[t];
     }
     const int64_t c = c0 + tid;
-    if (c < N) {
+    if constexpr (EPI != 0) {
+      fe_mom[2 * obj * BN + tid] = m;
+      fe_mom[(2 * obj + 1) * BN + tid] = g.variance - s;
+    } else if (c < N) {
       mu_out[(int64_t)obj * N + c] = m;
       var_out[(int64_t)obj * N + c] = g.variance - s;
     }
   }
+  if constexpr (EPI != 0) __syncthreads();             // the K* ring and the reduction scratch are reused
+  }   // objectives
+  if constexpr (EPI != 0) fused_ehvi2d_epilogue<BN, 64 * NW>(fe, fe_mom, fe_geo, N, c0, kbuf);
   OMB_POST_TRACE(4);
 }
 
@@ -1532,7 +1662,7 @@ static dim3 reg_grid(int64_t N, int n_obj, int NW = 8, int per_cu = 2) {
 
 // ----------------------------------------------------------------------------- fused 2-objective EHVI chain
 // omb_eval_argmax with an EHVI-2D plan at n ≤ 128, n_var ≤ 8 (BASELINE config 2): posterior
-// of both objectives, EHVI (ehvi2d_point, util_functions.py:136-167) and the arg-max in one persistent launch —
+// of both objectives, EHVI (ehvi2d_point4, util_functions.py:136-167) and the arg-max in one persistent launch —
 // μ and σ² never leave the registers, and the acquisition values never reach HBM.
 //   * one 1024-thread workgroup per CU stages BOTH objectives' packed L⁻¹ and α (2 × 72 KiB at n = 128), the exp
 //     table and the EHVI stripes in LDS; the training-row fragments (Xf) are read from L2;
@@ -1542,10 +1672,12 @@ static dim3 reg_grid(int64_t N, int n_obj, int NW = 8, int per_cu = 2) {
 //   * the wave's best → LDS → the workgroup's pair → partials; the last workgroup to finish (an agent-scope
 //     ticket) reduces the pairs and writes {value, index + offset}, then resets the ticket for the next launch.
 // The result equals posterior → ehvi2d_kernel → argmax_pass1/2 bit for bit (tests/test_gpu_fused.py).
-// ehvi2d_point as a call: inlined into the tile loop, its ndtr coefficients were hoisted into VGPRs for the whole loop
-__device__ __noinline__ double ehvi2d_point_call(double m0, double m1, double v0, double v1, const double* y1,
-                                                 const double* y2, int P, double r1, double s00, double s01, int mode) {
-  return ehvi2d_point(m0, m1, v0, v1, y1, y2, P, r1, s00, s01, mode);
+// ehvi2d_point4 as a call: inlined into the tile loop, its ndtr coefficients were hoisted into VGPRs for the whole
+// loop (≈ 90 spilled VGPRs at the 128-VGPR bound)
+__device__ __noinline__ double ehvi2d_point4_call(double m0, double m1, double v0, double v1, const double* y1,
+                                                  const double* y2, int P, double r1, double s00, double s01, int mode,
+                                                  int g) {
+  return ehvi2d_point4(m0, m1, v0, v1, y1, y2, P, r1, s00, s01, mode, g);
 }
 
 template <int RMAX, int DP, int KIND, int NW>
@@ -1639,10 +1771,11 @@ __global__ __launch_bounds__(64 * NW, 1) void posterior_reg_ehvi_kernel(GPArgs a
         var1 = g->variance - s;
       }
     }
+    // every lane: its quarter of the candidate's stripes (ehvi2d_point4; the shuffles need the whole wave)
+    const double v = ehvi2d_point4_call(st_mu[wave][lane & 15], mu1, st_var[wave][lane & 15],
+                                        fe.mode == OMB_EHVI_REFERENCE ? 0.0 : var1, y1, y2, P, fe.r1, fe.s00, fe.s01,
+                                        fe.mode, lane >> 4);
     if (lane < 16 && c < N) {
-      const double v = ehvi2d_point_call(st_mu[wave][lane], mu1, st_var[wave][lane],
-                                         fe.mode == OMB_EHVI_REFERENCE ? 0.0 : var1, y1, y2, P, fe.r1, fe.s00, fe.s01,
-                                         fe.mode);
       if (v == v && v > -__builtin_inf() && argmax_better(v, c, st_bv[wave][lane], st_bi[wave][lane])) {
         st_bv[wave][lane] = v;
         st_bi[wave][lane] = c;
@@ -1717,8 +1850,20 @@ __global__ __launch_bounds__(64 * NW, 1) void posterior_reg_ehvi_kernel(GPArgs a
   }
 }
 
+// The one-launch EHVI-2D chain applies with two objectives, ≤ kFusedMaxP stripes and n_var ≤ 8, through
+// posterior_reg_ehvi_kernel (n ≤ 128) or posterior_kernel<…, EPI = 1> (128 < n ≤ 512).  Wider inputs and
+// n > 512 keep the separate launches: there the EPI = 1 ring kernels spilled 6-93 VGPRs.
+static bool fused_reg_path(int max_R, int DP) { return max_R <= 8 && DP <= 8; }
+static int ring_rt(int max_R) { return ((max_R + 3) / 4 + 1) / 2; }   // RTneed of launch_posterior_dp
 bool fused_ehvi2d_fits(int n_obj, int max_R, int DP, int P) {
-  return n_obj == 2 && max_R <= 8 && DP <= 8 && P >= 1 && P <= kFusedMaxP;
+  if (n_obj != 2 || P < 1 || P > kFusedMaxP || DP > 8) return false;
+  return fused_reg_path(max_R, DP) || ring_rt(max_R) <= 4;
+}
+int64_t fused_ehvi2d_blocks(int max_R, int DP, int64_t N) {
+  if (fused_reg_path(max_R, DP)) return device_cu_count();                  // ≥ the persistent grid
+  const int rt = ring_rt(max_R);
+  const int64_t BN = rt <= 2 ? 32 : (rt <= 4 ? 64 : 32);
+  return (N + BN - 1) / BN;
 }
 
 template <int DP, int KIND, int NW>
@@ -1739,8 +1884,21 @@ template <int DP, int KIND>
 static hipError_t launch_fused_ehvi2d_dp(hipStream_t stream, const GPArgs& args, int max_R, const double* Xc,
                                          int64_t N, const FusedEhvi2d& fe, int variant) {
   if constexpr (DP <= 8) {
-    return variant == 2 ? launch_fused_ehvi2d_nw<DP, KIND, 8>(stream, args, max_R, Xc, N, fe)
-                        : launch_fused_ehvi2d_nw<DP, KIND, 16>(stream, args, max_R, Xc, N, fe);
+    if (fused_reg_path(max_R, DP))
+      return variant == 2 ? launch_fused_ehvi2d_nw<DP, KIND, 8>(stream, args, max_R, Xc, N, fe)
+                          : launch_fused_ehvi2d_nw<DP, KIND, 16>(stream, args, max_R, Xc, N, fe);
+    // the ring kernels of launch_posterior_dp, both objectives per workgroup (EPI = 1)
+    const int rt = ring_rt(max_R);
+    const unsigned blocks = (unsigned)fused_ehvi2d_blocks(max_R, DP, N);
+    if (rt <= 2)
+      hipLaunchKernelGGL((posterior_kernel<2, 2, DP, KIND, 8, 0, 1>), dim3(blocks), dim3(kBlockThreads), 0, stream,
+                         args, Xc, N, nullptr, nullptr, fe);
+    else if (rt <= 4)
+      hipLaunchKernelGGL((posterior_kernel<4, 4, DP, KIND, 8, 0, 1>), dim3(blocks), dim3(kBlockThreads), 0, stream,
+                         args, Xc, N, nullptr, nullptr, fe);
+    else
+      return hipErrorInvalidValue;
+    return hipGetLastError();
   }
   return hipErrorInvalidValue;
 }
@@ -1792,13 +1950,16 @@ static hipError_t launch_posterior_dp(hipStream_t stream, const GPArgs& args, in
     // tools/ablate at n = 256, 3 objectives, 2^17 candidates: 0.709 ms (CT 4, barrier) → 0.641 ms;
     // the whole-tile kernel (RMAX 16, CT 2) takes 0.688 ms there (profiles/r02_v2_ablate_c4.txt)
     dim3 grid((unsigned)((N + 31) / 32), n_obj);
-    hipLaunchKernelGGL((posterior_kernel<2, 2, DP, KIND, 8, 0>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var);
+    hipLaunchKernelGGL((posterior_kernel<2, 2, DP, KIND, 8, 0>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var,
+                       FusedEhvi2d{});
   } else if (RTneed <= 4) {
     dim3 grid((unsigned)((N + 63) / 64), n_obj);
-    hipLaunchKernelGGL((posterior_kernel<4, 4, DP, KIND>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var);
+    hipLaunchKernelGGL((posterior_kernel<4, 4, DP, KIND>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var,
+                       FusedEhvi2d{});
   } else if (RTneed <= 8) {
     dim3 grid((unsigned)((N + 31) / 32), n_obj);
-    hipLaunchKernelGGL((posterior_kernel<8, 2, DP, KIND>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var);
+    hipLaunchKernelGGL((posterior_kernel<8, 2, DP, KIND>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var,
+                       FusedEhvi2d{});
   } else {
     return hipErrorInvalidValue;
   }
@@ -1844,6 +2005,17 @@ static hipError_t launch_kblock_kind(hipStream_t stream, const GPArgs& args, int
   auto grid = [&](int DP, int CB) {
     return dim3((unsigned)((N + 128 * CB - 1) / (128 * CB)), (unsigned)((g.n + kblock_rows(DP) - 1) / kblock_rows(DP)));
   };
+  // the launch itself: 1-D, XCD-aware order when there are several row blocks (see the kernel)
+  auto grid1 = [&](int DP, int CB) {
+    const dim3 gr = grid(DP, CB);
+    return gr.y > 1 ? dim3((unsigned)((gr.x + 7) / 8 * 8 * gr.y)) : gr;
+  };
+  auto nxy = [&](int DP, int CB, int& nx, int& ny) {
+    const dim3 gr = grid(DP, CB);
+    nx = gr.y > 1 ? (int)gr.x : 0;
+    ny = (int)gr.y;
+  };
+  int nx = 0, ny = 0;
   auto pick_cb = [&](int DP) {
     for (int cb = 8; cb > 1; cb >>= 1) {
       const dim3 gr = grid(DP, cb);
@@ -1853,13 +2025,17 @@ static hipError_t launch_kblock_kind(hipStream_t stream, const GPArgs& args, int
   };
   switch (args.DP) {
 #define OMB_KBS(DPV) \
-  case DPV: hipLaunchKernelGGL((kernel_block_persist_kernel<DPV, KIND, 1, false>), grid(DPV, 1), dim3(512), 0, stream, g, args.d, Xc, N, K, exp_coef()); break;
+  case DPV:                                                                                                     \
+    nxy(DPV, 1, nx, ny);                                                                                        \
+    hipLaunchKernelGGL((kernel_block_persist_kernel<DPV, KIND, 1, false>), grid1(DPV, 1), dim3(512), 0, stream, g, args.d, Xc, N, K, exp_coef(), nx, ny); \
+    break;
 #define OMB_KBW_CB(DPV, CBV)                                                                                  \
   case CBV:                                                                                                     \
+    nxy(DPV, CBV, nx, ny);                                                                                      \
     if (args.d + 2 <= 4 * ((DPV + 3) / 4))                                                                      \
-      hipLaunchKernelGGL((kernel_block_persist_kernel<DPV, KIND, CBV, true, true, true>), grid(DPV, CBV), dim3(512), 0, stream, g, args.d, Xc, N, K, exp_coef()); \
+      hipLaunchKernelGGL((kernel_block_persist_kernel<DPV, KIND, CBV, true, true, true>), grid1(DPV, CBV), dim3(512), 0, stream, g, args.d, Xc, N, K, exp_coef(), nx, ny); \
     else                                                                                                        \
-      hipLaunchKernelGGL((kernel_block_persist_kernel<DPV, KIND, CBV, true, true>), grid(DPV, CBV), dim3(512), 0, stream, g, args.d, Xc, N, K, exp_coef()); \
+      hipLaunchKernelGGL((kernel_block_persist_kernel<DPV, KIND, CBV, true, true>), grid1(DPV, CBV), dim3(512), 0, stream, g, args.d, Xc, N, K, exp_coef(), nx, ny); \
     break;
 #define OMB_KBW(DPV) \
   case DPV:                                                                  \

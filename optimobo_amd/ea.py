@@ -19,6 +19,7 @@ in one device workgroup (`omb_ea_search`), which evaluates only the child's fitn
 With the generators in the reference's state, the device search returns the reference's proposal.
 """
 import random
+import warnings
 
 import numpy as np
 
@@ -33,6 +34,20 @@ def device_search_fits(n_train):
     """True when omb_ea_search takes a surrogate of `n_train` points; the drivers use the batched
     device arg-max of the same fitness above that (omb_ea_search returns OMB_EUNSUP there)."""
     return int(n_train) <= EA_MAX_TRAIN
+
+
+_FALLBACK_WARNED = [False]
+
+
+def warn_batch_fallback(driver, n_train):
+    """Once per process: above EA_MAX_TRAIN the drivers maximise with the batched Sobol arg-max instead of the
+    reference's evolutionary search (parego.py:223-271, keep.py:240-292), which makes none of its
+    ``random.sample`` / numpy draws, so the host random streams depart from the reference's from then on."""
+    if not _FALLBACK_WARNED[0]:
+        _FALLBACK_WARNED[0] = True
+        warnings.warn(f"{driver}: {n_train} training points exceed the device evolutionary search's {EA_MAX_TRAIN}; "
+                      "using the batched arg-max of the same fitness instead, so the host random streams no "
+                      "longer follow the reference's", RuntimeWarning, stacklevel=3)
 
 
 class EATape:

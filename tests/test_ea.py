@@ -81,3 +81,16 @@ def test_initial_population_follows_reference_draws():
     X = rs.uniform(0, 1, (15, 3))
     pop = ea.initial_population(X, np.zeros(3), np.ones(3), nprand=np.random.RandomState(8), pyrand=random.Random(8))
     assert pop.shape == (20, 3) and np.all((pop >= 0) & (pop <= 1))
+
+
+def test_batch_fallback_warns_once():
+    """Above EA_MAX_TRAIN the drivers leave the reference's search: one RuntimeWarning per process."""
+    import warnings
+    from optimobo_amd import ea
+    ea._FALLBACK_WARNED[0] = False
+    with warnings.catch_warnings(record=True) as rec:
+        warnings.simplefilter("always")
+        ea.warn_batch_fallback("ParEGO", ea.EA_MAX_TRAIN + 1)
+        ea.warn_batch_fallback("KEEP", ea.EA_MAX_TRAIN + 5)
+    assert len(rec) == 1 and issubclass(rec[0].category, RuntimeWarning)
+    assert "random streams" in str(rec[0].message)

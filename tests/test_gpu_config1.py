@@ -68,11 +68,19 @@ def test_readme_run_full_size():
             conds = [np.linalg.cond(ogp.matern52_K(m.X, m.X, m.kern.ls_vector(), float(m.kern.variance))
                                     + 1e-8 * np.eye(len(m.X))) for m in models]
             gps = [ogp.ExactGP(m.X, m.Y[:, 0], m.kern.ls_vector(), float(m.kern.variance)) for m in models]
-            mus, vs = zip(*[g.predict(np.asarray(x)[None, :]) for g in gps])
-            v_o = oacq.expected_decomposition(np.array([u[:, 0] for u in mus]), np.array([w[:, 0] for w in vs]),
-                                              np.array(cache), tch, np.asarray(ref_dir, np.float64), float(min_val))[0]
+            def oracle_acq(P):
+                P = np.atleast_2d(np.asarray(P, np.float64))
+                mus, vs = zip(*[g.predict(P) for g in gps])
+                return oacq.expected_decomposition(np.array([u[:, 0] for u in mus]), np.array([w[:, 0] for w in vs]),
+                                                   np.array(cache), tch, np.asarray(ref_dir, np.float64),
+                                                   float(min_val))
+            v_o = oracle_acq(x)[0]
+            # the reference's maximiser on the oracle's acquisition (independent of the device: VERDICT r03 next 7)
+            de_o = differential_evolution(lambda P: -oracle_acq(P.T), [(-2, 2), (-2, 2)], vectorized=True,
+                                          rng=np.random.default_rng(1000 + it[0]))
             checked[it[0]] = dict(x=np.array(x), v=-float(negv), v_de=dev_acq(de.x), x_de=de.x, cond=max(conds),
-                                  v_oracle=v_o, v_dev_at_x=dev_acq(x))
+                                  v_oracle=v_o, v_dev_at_x=dev_acq(x), v_de_oracle=-float(de_o.fun),
+                                  x_de_oracle=de_o.x, v_oracle_at_dev_x=v_o)
         it[0] += 1
         return x, negv, rd
     opt._get_proposed_scalarisation = recording
@@ -92,6 +100,12 @@ def test_readme_run_full_size():
                        for k, r in checked.items()}, fh, indent=1)
     for k, r in checked.items():
         assert r is not None
+        # the gaps, both ways: the device proposal on the device's surface against DE there, and the oracle's value
+        # at the device proposal against DE on the oracle's surface (recorded; asserted only where cond ≤ 1e10)
+        print(f"it {k}: cond {r['cond']:.1e}  device {r['v']:.6e} vs DE(device) {r['v_de']:.6e}  |  oracle at device x "
+              f"{r['v_oracle']:.6e} vs DE(oracle) {r['v_de_oracle']:.6e}")
+        if r["cond"] <= 1e10:
+            assert r["v_oracle"] >= r["v_de_oracle"] - 1e-6 * abs(r["v_de_oracle"]), (k, r)
         assert abs(r["v"] - r["v_dev_at_x"]) <= 1e-12 * abs(r["v"]) + 1e-300   # the returned value is the value at x
         # on a singular surrogate the acquisition is itself determined only to ~1e-5 relative (DE's many
         # single-point calls find its rounding ripples); on a conditioned one the bar is test_gpu_polish's
@@ -99,3 +113,60 @@ def test_readme_run_full_size():
         assert r["v"] >= r["v_de"] - tol * abs(r["v_de"]), (k, r)
         if r["cond"] <= 1e10:
             assert abs(r["v_oracle"] - r["v"]) <= 1e-6 * abs(r["v_oracle"]) + 1e-14, (k, r)
+
+
+def test_readme_shaped_run_on_a_conditioned_surrogate():
+    """The README call shape — MultiSurrogateOptimiser.solve(..., sample_exponent=3, Tchebicheff) — on a problem whose
+    noise-free GPy-style fits stay conditioned (two-objective DTLZ2, n_var 6: cond(K + 1e-8 I) ≤ 1e10 through n = 50,
+    tools probe in DESIGN §2), so that value parity with the oracle holds at every iteration: the device's
+    expected decomposition at its own proposal against the oracle's (GPy restated) on the same fitted
+    hyperparameters, and the device proposal at least as good on the oracle's surface as scipy DE on that surface
+    at 3 iterations."""
+    from scipy.optimize import differential_evolution
+    import optimobo_amd.algorithms.optimisers as opti
+    import optimobo_amd.scalarisations as sc
+    from optimobo_amd.problem import ElementwiseProblem
+
+    class DTLZ2(ElementwiseProblem):
+        def __init__(self):
+            super().__init__(n_var=6, n_obj=2, xl=np.zeros(6), xu=np.ones(6))
+
+        def _evaluate(self, x, out, *a, **k):
+            g = float(((x[1:] - 0.5) ** 2).sum())
+            out["F"] = [(1 + g) * np.cos(x[0] * np.pi / 2), (1 + g) * np.sin(x[0] * np.pi / 2)]
+
+    np.random.seed(3)
+    opt = opti.MultiSurrogateOptimiser(DTLZ2(), [0, 0], [2.5, 2.5], seed=5)
+    orig = opt._get_proposed_scalarisation
+    rows, it = [], [0]
+    tch = osc.Tchebicheff(np.array([0.0, 0.0]), np.array([2.5, 2.5]))
+
+    def recording(function, models, min_val, scalar_func, ref_dir, cache):
+        x, negv, rd = orig(function, models, min_val, scalar_func, ref_dir, cache)
+        gps = [ogp.ExactGP(m.X, m.Y[:, 0], m.kern.ls_vector(), float(m.kern.variance)) for m in models]
+        cond = max(np.linalg.cond(ogp.matern52_K(m.X, m.X, m.kern.ls_vector(), float(m.kern.variance))
+                                  + 1e-8 * np.eye(len(m.X))) for m in models)
+
+        def oracle_acq(P):
+            P = np.atleast_2d(np.asarray(P, np.float64))
+            mus, vs = zip(*[g.predict(P) for g in gps])
+            return oacq.expected_decomposition(np.array([u[:, 0] for u in mus]), np.array([w[:, 0] for w in vs]),
+                                               np.array(cache), tch, np.asarray(ref_dir, np.float64), float(min_val))
+        row = dict(it=it[0], cond=cond, v=-float(negv), v_oracle=float(oracle_acq(x)[0]))
+        if it[0] in (0, 12, 29):
+            de = differential_evolution(lambda P: -oracle_acq(P.T), [(0, 1)] * 6, vectorized=True,
+                                        rng=np.random.default_rng(it[0]))
+            row["v_de_oracle"] = -float(de.fun)
+        rows.append(row)
+        it[0] += 1
+        return x, negv, rd
+    opt._get_proposed_scalarisation = recording
+    res = opt.solve(budget=30, n_init_samples=20, sample_exponent=3,
+                    acquisition_func=sc.Tchebicheff([0, 0], [2.5, 2.5]))
+    assert len(res.ysample) == 50 and len(rows) == 30
+    for r in rows:
+        print(r)
+        assert r["cond"] <= 1e10, r
+        assert abs(r["v"] - r["v_oracle"]) <= 1e-6 * abs(r["v_oracle"]) + 1e-12, r
+        if "v_de_oracle" in r:
+            assert r["v_oracle"] >= r["v_de_oracle"] - 1e-6 * abs(r["v_de_oracle"]) - 1e-12, r

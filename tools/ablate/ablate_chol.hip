@@ -261,14 +261,14 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&e1));
     // the launch schedules interleaved: kCholTwoLaunch (round 2), kCholFused (round 3), kCholBlocked (round 4),
     // kCholBlockedAcqRel (round 4 with the agent-scope release / acquire flag)
-    const int modes[4] = {kCholTwoLaunch, kCholFused, kCholBlocked, kCholBlockedAcqRel};
-    float msum[4] = {0, 0, 0, 0}, mbest[4] = {1e30f, 1e30f, 1e30f, 1e30f};
+    const int modes[5] = {kCholTwoLaunch, kCholFused, kCholBlocked, kCholBlockedAcqRel, kCholBlockedMov};
+    float msum[5] = {0, 0, 0, 0, 0}, mbest[5] = {1e30f, 1e30f, 1e30f, 1e30f, 1e30f};
     const int reps = 10;
     std::vector<double> Lref(N * N), Lm(N * N);
-    double mdiff[4] = {0, 0, 0, 0};
-    int minfo[4] = {0, 0, 0, 0};
+    double mdiff[5] = {0, 0, 0, 0, 0};
+    int minfo[5] = {0, 0, 0, 0, 0};
     for (int r = 0; r < reps + 1; ++r) {
-      for (int m = 0; m < 4; ++m) {
+      for (int m = 0; m < 5; ++m) {
         CK(hipMemcpy(A, A0, N * N * 8, hipMemcpyDeviceToDevice));
         CK(hipMemset(info, 0, 4));
         CK(hipEventRecord(e0));
@@ -290,10 +290,11 @@ int main(int argc, char** argv) {
         }
       }
     }
-    printf("N=%lld  two-launch %.3f (best %.3f) | fused %.3f (%.3f) | blocked %.3f (%.3f) | blocked acq/rel %.3f (%.3f) ms;"
-           " info %d %d %d %d; max |L - L_twolaunch|/sqrt(A_ii) %.1e %.1e %.1e\n",
+    printf("N=%lld  two-launch %.3f (best %.3f) | fused %.3f (%.3f) | blocked %.3f (%.3f) | blocked acq/rel %.3f (%.3f) | "
+           "blocked dpp-mov %.3f (%.3f) ms; info %d %d %d %d %d; max |L - L_twolaunch|/sqrt(A_ii) %.1e %.1e %.1e %.1e\n",
            (long long)N, msum[0] / reps, mbest[0], msum[1] / reps, mbest[1], msum[2] / reps, mbest[2], msum[3] / reps,
-           mbest[3], minfo[0], minfo[1], minfo[2], minfo[3], mdiff[1], mdiff[2], mdiff[3]);
+           mbest[3], msum[4] / reps, mbest[4], minfo[0], minfo[1], minfo[2], minfo[3], minfo[4], mdiff[1], mdiff[2],
+           mdiff[3], mdiff[4]);
     float best = mbest[1], sum = msum[1], best2 = mbest[0], sum2 = msum[0];
     printf("N=%lld  two launches per step %.3f ms (best %.3f)\n", (long long)N, sum2 / reps, best2);
     {

@@ -1,0 +1,18 @@
+# Round 4, call f: 16x16 factor microbench; Cholesky variants (asm non-volatile / mov DPP); one-launch EHVI-2D chains
+# with four lanes per candidate (tests, configs 2 and 3); config-1 tests (multi-start maximiser); config 6.
+set -e
+O=gpurun_out/${1:-r04_f}
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 60 ./tools/microbench/mb_chol16 > $O/mb_chol16.txt 2>&1
+timeout -k 10 240 ./tools/ablate/ablate_chol 512 3000 5000 > $O/ablate_chol.txt 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_gpu_fused.py tests/test_gpu_parity.py -x -q --timeout 240 --timeout-method thread > $O/fused_tests.txt 2>&1
+for v in 0 1 2; do
+  timeout -k 10 200 python -u bench.py --config 2 --steps 200 --warmup 20 --no-cpu-baseline --one-launch $v > $O/bench_c2_ol$v.json 2>&1
+done
+for v in 0 1; do
+  timeout -k 10 200 python -u bench.py --config 3 --steps 20 --warmup 5 --no-cpu-baseline --one-launch $v > $O/bench_c3_ol$v.json 2>&1
+done
+timeout -k 10 600 python -u -m pytest tests/test_gpu_config1.py tests/test_gpu_cov_table.py tests/test_gpu_polish.py -x -q -s --timeout 300 --timeout-method thread > $O/tests.txt 2>&1
+timeout -k 10 300 python -u bench.py --config 6 --steps 20 --warmup 3 --no-cpu-baseline > $O/bench_c6.json 2>&1
+echo done

@@ -15,7 +15,7 @@ hypervolume trace.  Third-party packages absent here are test doubles (tests/gol
   * the problem is a duck-typed MyProblem (the reference's Problem base class needs pymoo).
 GPy/paramz add per-call overhead the doubles do not have, so the rate is an UPPER bound on the reference's.
 
-Usage: python tools/ref_solve_baseline.py [budget] [seed] > profiles/r03_ref_solve_c1.json
+Usage: python tools/ref_solve_baseline.py [budget] [seed] > profiles/r04_ref_solve_c1.json
 """
 import json
 import os
@@ -90,14 +90,19 @@ def main():
     opti.get_reference_directions = lambda name, n_dim, n_partitions=None: mg._das_dennis(n_dim, n_partitions)
     np.random.seed(seed)
     opt = opti.MultiSurrogateOptimiser(MyProblem(), [0, 0], [700, 12])
-    t0 = time.perf_counter()
-    res = opt.solve(budget=budget, n_init_samples=20, sample_exponent=3,
-                    acquisition_func=sc.Tchebicheff([0, 0], [700, 12]))
-    el = time.perf_counter() - t0
+    # one BLAS thread, enforced and read back ("cores" was hard-coded)
+    from threadpoolctl import threadpool_info, threadpool_limits
+    with threadpool_limits(limits=1):
+        threads = max([p.get("num_threads", 1) for p in threadpool_info()] or [1])
+        t0 = time.perf_counter()
+        res = opt.solve(budget=budget, n_init_samples=20, sample_exponent=3,
+                        acquisition_func=sc.Tchebicheff([0, 0], [700, 12]))
+        el = time.perf_counter() - t0
     print(json.dumps({
         "what": "reference MultiSurrogateOptimiser.solve (README run, BASELINE config 1): budget "
                 f"{budget}, n_init 20, sample_exponent 3, Tchebicheff; scipy DE one candidate per call",
-        "value": budget / el, "unit": "iterations/s", "seconds": el, "cores": 1, "kind": "reference",
+        "value": budget / el, "unit": "iterations/s", "seconds": el, "cores": int(threads), "kind": "reference",
+        "measured_in": f"build container ({os.cpu_count()} vCPU), not the GPU box's host",
         "split_s": {"gp_fit": split["fit"], "de_and_rest": el - split["fit"]},
         "predict_calls": split["predict_calls"], "final_hv": float(res.hypervolume_convergence[-1]),
         "n_evaluations": int(len(res.ysample)), "np_seed": seed,

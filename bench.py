@@ -419,9 +419,9 @@ def main():
     ap.add_argument("--no-kblock", action="store_true")
     ap.add_argument("--chain", default="fused", choices=["fused", "separate", "sobol"])
     ap.add_argument("--stage-timing", action="store_true", help="events around every stage (adds ~5 us/stage)")
-    ap.add_argument("--one-launch", type=int, default=None, choices=[0, 1, 2],
-                    help="omb_debug_set(FUSED_CHAIN): 0 separate launches, 1/2 the one-launch EHVI-2D chain "
-                         "(16 / 8 waves; default: the library's)")
+    ap.add_argument("--one-launch", type=int, default=None, choices=[0, 1],
+                    help="omb_debug_set(FUSED_CHAIN): 0 EHVI-2D and the arg-max as separate launches, 1 as one "
+                         "(default: the library's, 0 — the one launch measured slower)")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks and the process group only, print what torch.distributed saw")
     ap.add_argument("--cache-seed", type=int, default=1,

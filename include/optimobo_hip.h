@@ -92,8 +92,9 @@ const char* omb_last_error(const omb_ctx* ctx);
  * omb_debug_set(ctx, OMB_DEBUG_COV_TABLE, 1) builds K(X, X) / K(X*, X*) (GP-fit state, posterior covariance) with
  * the posterior kernels' table-driven Matern transform instead of the polynomial exp (a parity check of that
  * transform near r = 0; default 0).
- * omb_debug_set(ctx, OMB_DEBUG_FUSED_CHAIN, 0) makes omb_eval_argmax[_sobol] run posterior, acquisition and
- * arg-max as separate launches even where the one-launch chain applies (tests compare the two; default 1). */
+ * omb_debug_set(ctx, OMB_DEBUG_FUSED_CHAIN, 1) makes omb_eval_argmax[_sobol] with an EHVI-2D plan run the
+ * acquisition and the arg-max in one launch instead of two (bit-identical pair; default 0: the one launch measured
+ * 1.9 % / 0.6 % slower on configs 2 / 3, gpurun_out/r04_j). */
 enum { OMB_DEBUG_SPIN_LIMIT = 1, OMB_DEBUG_COV_TABLE = 2, OMB_DEBUG_FUSED_CHAIN = 3 };
 int omb_debug_set(omb_ctx* ctx, int what, int64_t value);
 

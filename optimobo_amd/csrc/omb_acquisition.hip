@@ -57,6 +57,86 @@ hipError_t launch_ehvi2d(hipStream_t stream, const double* mu, const double* var
   return hipGetLastError();
 }
 
+// EHVI-2D with the arg-max (omb_eval_argmax[_sobol] with an EHVI-2D plan): the values of ehvi2d_kernel, bit for bit,
+// are reduced in the same launch — per wave by shuffles, per workgroup in LDS, per grid by the last workgroup to
+// take the ticket — by the rule of argmax_pass1/2 (higher value, lower index; NaN and −∞ never win).  Two launches
+// (the arg-max's) and the values' round trip through HBM leave the chain.
+__global__ __launch_bounds__(kAcqThreads) void ehvi2d_argmax_kernel(const double* __restrict__ mu,
+                                                                    const double* __restrict__ var, int64_t ld,
+                                                                    int64_t N, const double* __restrict__ pf, int P,
+                                                                    double r0, double r1, double s00, double s01,
+                                                                    int mode, ArgmaxOut am) {
+  extern __shared__ double sm[];
+  double* y1 = sm;
+  double* y2 = sm + P + 1;
+  __shared__ double red_v[kAcqThreads / 64];
+  __shared__ long long red_i[kAcqThreads / 64];
+  __shared__ int is_last;
+  for (int i = threadIdx.x; i < P; i += blockDim.x) {
+    y1[i + 1] = pf[2 * i];
+    y2[i] = pf[2 * i + 1];
+  }
+  if (threadIdx.x == 0) y1[0] = r0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, g = lane >> 4, wave = threadIdx.x >> 6;
+  const int64_t per_block = kAcqThreads / 4;
+  double bv = -__builtin_inf();
+  long long bi = -1;
+  for (int64_t base = (int64_t)blockIdx.x * per_block; base < N; base += (int64_t)gridDim.x * per_block) {
+    const int64_t c = base + 16 * wave + (lane & 15);
+    const int64_t cc = c < N ? c : N - 1;
+    const double v = ehvi2d_point4(mu[cc], mu[ld + cc], var[cc], mode == OMB_EHVI_REFERENCE ? 0.0 : var[ld + cc], y1,
+                                   y2, P, r1, s00, s01, mode, g);
+    if (g == 0 && c < N && v == v && v > -__builtin_inf() && argmax_better(v, c, bv, bi)) {
+      bv = v;
+      bi = c;
+    }
+  }
+  argmax_wave_block(bv, bi, red_v, red_i);          // thread 0: the workgroup's pair
+  if (threadIdx.x == 0) {
+    // the pair as agent-scope (sc1) stores, complete (vmcnt 0) before the ticket: the ordering the Cholesky's W
+    // hand-off uses (chol_publish_w).  An acquire-release ticket made every workgroup write back its XCD's L2
+    // (config 2: 31 µs for the one launch against 20 + 9 µs for the separate EHVI and arg-max launches).
+    wf_store_f64(&am.partials[2 * blockIdx.x], bv);
+    wf_store_f64(&am.partials[2 * blockIdx.x + 1], __builtin_bit_cast(double, bi));
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt(0);
+    const unsigned prev = __hip_atomic_fetch_add(am.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    is_last = prev == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!is_last) return;
+  double v = -__builtin_inf();
+  long long i = -1;
+  for (int b = threadIdx.x; b < (int)gridDim.x; b += blockDim.x) {
+    const double pv = wf_load_f64(&am.partials[2 * b]);
+    const long long pi = __builtin_bit_cast(long long, wf_load_f64(&am.partials[2 * b + 1]));
+    if (argmax_better(pv, pi, v, i)) {
+      v = pv;
+      i = pi;
+    }
+  }
+  __syncthreads();                                   // red_v / red_i reused
+  argmax_wave_block(v, i, red_v, red_i);
+  if (threadIdx.x == 0) {
+    am.result[0] = i < 0 ? -__builtin_inf() : v;
+    am.result[1] = i < 0 ? -1.0 : (double)(i + am.offset);
+    __hip_atomic_store(am.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+int64_t ehvi2d_argmax_blocks(int64_t N) { return acq_grid(4 * N); }
+
+hipError_t launch_ehvi2d_argmax(hipStream_t stream, const double* mu, const double* var, int64_t ld, int64_t N,
+                                const double* pf, int P, double r0, double r1, double s00, double s01, int mode,
+                                const ArgmaxOut& am) {
+  size_t shm = sizeof(double) * (2 * P + 1);
+  hipLaunchKernelGGL(ehvi2d_argmax_kernel, dim3(acq_grid(4 * N)), dim3(kAcqThreads), shm, stream, mu, var, ld, N, pf,
+                     P, r0, r1, s00, s01, mode, am);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------------------------ EHVI 3-D
 // util_functions.py:170-214: samples s = cache·sqrt(σ²0) + μ (change, :217-237), then
 // mean_s max(0, Π_j(r_j − s_j) − HV(PF)).  pygmo raises ValueError when a sample is not inside

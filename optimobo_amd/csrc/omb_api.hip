@@ -87,7 +87,7 @@ struct omb_ctx {
   double* fit_dev = nullptr;
   int spin_limit = kDefaultSpinLimit;
   bool cov_table = false;   // OMB_DEBUG_COV_TABLE
-  int fused_chain = 1;      // OMB_DEBUG_FUSED_CHAIN (0 off; 1, 2 the kernel variant)
+  bool fused_chain = false;  // OMB_DEBUG_FUSED_CHAIN: EHVI-2D and the arg-max in one launch (off: measured slower)
 };
 
 namespace {
@@ -346,13 +346,12 @@ int run_chain(omb_ctx* ctx, const double* Xc, bool sobol, int64_t start, int64_t
   if ((N + 31) / 32 > 0x7fffffffLL) return fail(ctx, OMB_EUNSUP, "N=%lld too large", (long long)N);
   const int k = pl.k;
   const size_t nd = (size_t)N;
-  // the one-launch EHVI-2D chain (launch_fused_ehvi2d) where it applies; its per-workgroup pairs go to the chain
-  // workspace past the Sobol points when ctx->partials is too small
-  const bool one_launch = result_dev && !vals_out && N > 0 && ctx->fused_chain && pl.kind == PLAN_EHVI2D &&
-                          16 * max_R <= OMB_MAX_TRAIN && fused_ehvi2d_fits(k, max_R, args.DP, pl.P);
-  const int64_t fblocks = one_launch ? fused_ehvi2d_blocks(max_R, args.DP, N) : 0;
+  // EHVI-2D with the arg-max in one launch (launch_ehvi2d_argmax) when only the pair is wanted; its per-workgroup
+  // pairs go to the chain workspace past the Sobol points when ctx->partials is too small
+  const bool acq_argmax = result_dev && !vals_out && N > 0 && ctx->fused_chain && pl.kind == PLAN_EHVI2D;
+  const int64_t ablocks = acq_argmax ? ehvi2d_argmax_blocks(N) : 0;
   const size_t doubles = 2 * (size_t)k * nd + nd + (nd + 1) / 2 + (sobol ? nd * args.d : 0);
-  const size_t extra = fblocks > kArgmaxMaxBlocks ? 2 * (size_t)fblocks : 0;
+  const size_t extra = ablocks > kArgmaxMaxBlocks ? 2 * (size_t)ablocks : 0;
   if ((rc = grow_dev(ctx, &ctx->work, &ctx->work_cap, (doubles + extra ? doubles + extra : 1) * sizeof(double),
                      "chain workspace")))
     return rc;
@@ -387,17 +386,6 @@ int run_chain(omb_ctx* ctx, const double* Xc, bool sobol, int64_t start, int64_t
   if (e == hipSuccess && sobol && N > 0) e = launch_sobol(ctx->stream, ctx->sob, ctx->sob_d, ctx->sob_bits, start, N, Xs);
   if (sobol) Xc = Xs;
   if (e == hipSuccess) e = mark(1);
-  if (e == hipSuccess && one_launch) {
-    // posterior → EHVI-2D → arg-max in one launch; bitwise the separate launches' result.  The ticket lives after
-    // ctx->partials.
-    double* pairs = extra ? mu + doubles : ctx->partials;
-    FusedEhvi2d fe{pl.geo, pl.P, pl.mode, pl.r[0], pl.r[1], pl.s00, pl.s01, offset, pairs,
-                   reinterpret_cast<unsigned*>(ctx->partials + 2 * kArgmaxMaxBlocks), result_dev};
-    e = launch_fused_ehvi2d(ctx->stream, args, max_R, Xc, N, fe, ctx->fused_chain);
-    for (int i = 2; i <= 4 && e == hipSuccess; ++i) e = mark(i);
-    if (e != hipSuccess) return hip_fail(ctx, e, "fused chain");
-    return OMB_OK;
-  }
   const double* Ld[OMB_MAX_OBJ];
   gather_Ld(ctx, k, Ld);
   if (e == hipSuccess && N > 0) e = posterior_any(ctx, args, Ld, k, max_R, Xc, N, mu, var);
@@ -405,7 +393,14 @@ int run_chain(omb_ctx* ctx, const double* Xc, bool sobol, int64_t start, int64_t
   if (e == hipSuccess && N > 0) {
     switch (pl.kind) {
       case PLAN_EHVI2D:
-        e = launch_ehvi2d(ctx->stream, mu, var, N, N, pl.geo, pl.P, pl.r[0], pl.r[1], pl.s00, pl.s01, pl.mode, vals);
+        if (acq_argmax) {
+          const ArgmaxOut am{extra ? mu + doubles : ctx->partials,
+                             reinterpret_cast<unsigned*>(ctx->partials + 2 * kArgmaxMaxBlocks), result_dev, offset};
+          e = launch_ehvi2d_argmax(ctx->stream, mu, var, N, N, pl.geo, pl.P, pl.r[0], pl.r[1], pl.s00, pl.s01, pl.mode,
+                                   am);
+        } else {
+          e = launch_ehvi2d(ctx->stream, mu, var, N, N, pl.geo, pl.P, pl.r[0], pl.r[1], pl.s00, pl.s01, pl.mode, vals);
+        }
         break;
       case PLAN_EHVI3D_MC:
         e = launch_ehvi3d_mc(ctx->stream, mu, var, N, N, pl.geo, pl.M, pl.r, pl.hv, vals, raised);
@@ -427,7 +422,7 @@ int run_chain(omb_ctx* ctx, const double* Xc, bool sobol, int64_t start, int64_t
     }
   }
   if (e == hipSuccess) e = mark(3);
-  if (e == hipSuccess && result_dev) e = launch_argmax(ctx->stream, vals, N, offset, ctx->partials, result_dev);
+  if (e == hipSuccess && result_dev && !acq_argmax) e = launch_argmax(ctx->stream, vals, N, offset, ctx->partials, result_dev);
   if (e == hipSuccess) e = mark(4);
   if (e != hipSuccess) return hip_fail(ctx, e, "fused chain");
   return OMB_OK;
@@ -522,8 +517,7 @@ int omb_debug_set(omb_ctx* ctx, int what, int64_t value) {
     return OMB_OK;
   }
   if (what == OMB_DEBUG_FUSED_CHAIN) {
-    if (value < 0 || value > 2) return fail(ctx, OMB_EINVAL, "fused-chain setting %lld outside [0, 2]", (long long)value);
-    ctx->fused_chain = (int)value;
+    ctx->fused_chain = value != 0;
     return OMB_OK;
   }
   if (what == OMB_DEBUG_COV_TABLE) {

@@ -57,23 +57,19 @@ hipError_t launch_kernel_block(hipStream_t stream, const GPArgs& args, int obj, 
 hipError_t launch_posterior(hipStream_t stream, const GPArgs& args, int n_obj, int max_R, const double* Xc,
                             int64_t N, double* mu, double* var);
 
-// The fused 2-objective EHVI chain (posterior → EHVI-2D → arg-max in one launch; omb_posterior.hip).
-constexpr int kFusedMaxP = 128;    // stripes staged in LDS (the LDS left beside two packed L⁻¹ at n = 128)
-struct FusedEhvi2d {
-  const double* pf;       // (P, 2) stripes, sorted (the plan's geometry)
-  int P, mode;
-  double r0, r1, s00, s01;
-  int64_t offset;         // global index of candidate 0
-  double* partials;       // 2 doubles per workgroup (fused_ehvi2d_blocks)
-  unsigned* ticket;       // 0 between launches (the last workgroup resets it)
-  double* result;         // {value, global index}
+// EHVI-2D and the arg-max in one launch (omb_acquisition.hip): each workgroup's (value, index) pair goes to
+// `partials` (2 doubles per workgroup, ehvi2d_argmax_blocks(N)); the last workgroup to finish (an agent-scope
+// ticket, 0 between launches) reduces them and writes result = {value, index + offset}.
+struct ArgmaxOut {
+  double* partials;
+  unsigned* ticket;
+  double* result;
+  int64_t offset;
 };
-bool fused_ehvi2d_fits(int n_obj, int max_R, int DP, int P);
-// workgroups of the one-launch chain: FusedEhvi2d.partials must hold 2 doubles per workgroup
-int64_t fused_ehvi2d_blocks(int max_R, int DP, int64_t N);
-// variant 1: 16 waves per workgroup (4 per SIMD), 2: 8 waves
-hipError_t launch_fused_ehvi2d(hipStream_t stream, const GPArgs& args, int max_R, const double* Xc, int64_t N,
-                               const FusedEhvi2d& fe, int variant = 1);
+int64_t ehvi2d_argmax_blocks(int64_t N);
+hipError_t launch_ehvi2d_argmax(hipStream_t stream, const double* mu, const double* var, int64_t ld, int64_t N,
+                                const double* pf, int P, double r0, double r1, double s00, double s01, int mode,
+                                const ArgmaxOut& am);
 
 hipError_t launch_ehvi2d(hipStream_t stream, const double* mu, const double* var, int64_t ld, int64_t N,
                          const double* pf, int P, double r0, double r1, double s00, double s01, int mode,
@@ -153,9 +149,8 @@ hipError_t launch_add_diag(hipStream_t stream, double* S, int64_t N, int64_t lds
 constexpr int kCholWsDoubles = 64 * 64;
 constexpr int kCholSpinFault = -2147483647;
 // kCholBlocked (round 4): the diagonal blocks by tiles of 16 (chol64_blocked); kCholBlockedAcqRel: the same with
-// the fused step's flag as an agent-scope release / acquire, kCholBlockedMov: with the compiler's DPP moves in
-// place of the inline-asm v_fmac_f64_dpp (tools/ablate/ablate_chol)
-enum { kCholTwoLaunch = 0, kCholFused = 1, kCholBlocked = 2, kCholBlockedAcqRel = 3, kCholBlockedMov = 4 };
+// the fused step's flag as an agent-scope release / acquire (tools/ablate/ablate_chol)
+enum { kCholTwoLaunch = 0, kCholFused = 1, kCholBlocked = 2, kCholBlockedAcqRel = 3 };
 int64_t chol_ws_doubles(int64_t N);
 hipError_t launch_cholesky(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws,
                            int spin_limit = kDefaultSpinLimit);

@@ -478,27 +478,17 @@ __device__ __forceinline__ void lds_post_flag(int* f, int lane) {
 // orders one wave's LDS accesses across lanes for the compiler (LDS executes a wave's accesses in order)
 __device__ __forceinline__ void wave_lds_order() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 
-// a += L·na and x += L·nx with L = lane K's l (DPP row_newbcast folded into two v_fmac_f64_dpp: one instruction per
-// update instead of a v_mov_b64_dpp broadcast and two v_fma_f64).  The leading s_nop gives the 2 wait states a DPP
-// read needs after the VALU write of l: the compiler's hazard recognizer does not look inside inline asm.
-template <int K>
-__device__ __forceinline__ void fmac2_bcast(double& a, double& x, double l, double na, double nx) {
-  asm("s_nop 1\n\tv_fmac_f64_dpp %0, %2, %3 row_newbcast:%5 row_mask:0xf bank_mask:0xf\n\t"
-               "v_fmac_f64_dpp %1, %2, %4 row_newbcast:%5 row_mask:0xf bank_mask:0xf"
-               : "+v"(a), "+v"(x)
-               : "v"(l), "v"(na), "v"(nx), "n"(K));
-}
-
 // Cholesky of a 16×16 SPD tile held row-per-lane (lane → row r = lane & 15; the four 16-lane rows of the wave
 // hold the same copy), with W = L⁻¹ by column-oriented forward substitution of L x = e_r sharing the broadcasts:
 //   a[q] = D[r][q] (q ≤ r; entries above the diagonal start at 0 and are never broadcast) → L[r][q];
 //   x = e_r → x[m] = W[m][r].
 // Column j: inv_j = 1/√d_j (v_rsq + 2 Newton steps), L[r][j] = a[j]·inv_j; for k > j a[k] −= L[r][j]·L[k][j] and
-// x[k] −= x[j]·L[k][j], L[k][j] being lane k's value (fmac2_bcast: two v_fmac_f64_dpp row_newbcast per k).
+// x[k] −= x[j]·L[k][j], L[k][j] being lane k's value (one v_mov_b64_dpp row_newbcast per k, shared by both; folding
+// it into two inline-asm v_fmac_f64_dpp was slower: 3,784 against 3,188 cycles per factor,
+// profiles/r04_f_mb_chol16.txt).
 // The pivot chain runs ahead on wave-uniform values: d_{j+1} = a_{j+1}[j+1] − (a_{j+1}[j]·inv_j)² with both entries
 // read (v_readlane) before inv_j is known — bitwise the value the update leaves in lane j+1 (the same fma).
 // Returns 0 or the 1-based first column with a non-positive pivot (continued with 1.0: no NaNs; flagged).
-template <bool ASM>
 __device__ __forceinline__ int chol16_factor(double (&a)[16], double (&x)[16]) {
   int bad = 0;
   double dj = readlane_f64(a[0], 0);
@@ -528,13 +518,9 @@ __device__ __forceinline__ int chol16_factor(double (&a)[16], double (&x)[16]) {
     const double nl = -l, nx = -xj;
     static_for<j + 1, 16>([&](auto kc) {
       constexpr int k = decltype(kc)::value;
-      if constexpr (ASM) {
-        fmac2_bcast<k>(a[k], x[k], l, nl, nx);
-      } else {                                   // the compiler's form: v_mov_b64_dpp + two v_fma_f64
-        const double lk = __builtin_amdgcn_mov_dpp(l, 0x150 + k, 0xf, 0xf, true);
-        a[k] = fma(nl, lk, a[k]);
-        x[k] = fma(nx, lk, x[k]);
-      }
+      const double lk = __builtin_amdgcn_mov_dpp(l, 0x150 + k, 0xf, 0xf, true);   // v_mov_b64_dpp row_newbcast:k
+      a[k] = fma(nl, lk, a[k]);
+      x[k] = fma(nx, lk, x[k]);
     });
   });
   // the callers store a and x under a lane condition; without this the updates were sunk into that branch,
@@ -556,7 +542,7 @@ __device__ __forceinline__ void load_row16(const double* __restrict__ p, bool ok
 // (lower triangle of rows < nb), with W = L⁻¹'s MFMA fragments to Wf (the layout of chol64_inverse).  OUTER: A22_00
 // minus the product of the panel rows A[r0 + ·][c0 .. c0+63].  Ds, Wl, fl: LDS (fl zeroed by the caller and a
 // barrier passed).  The caller reads fl[20] (block-relative 1-based first bad column, 0 = none) after a barrier.
-template <bool OUTER, bool ASM = true>
+template <bool OUTER>
 __device__ __forceinline__ void chol64_blocked(double* __restrict__ A, int64_t lda, int64_t r0, int nb, int64_t c0,
                                                double* __restrict__ Wf, double* Ds, double* Wl, int* fl) {
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
@@ -669,7 +655,7 @@ __device__ __forceinline__ void chol64_blocked(double* __restrict__ A, int64_t l
 #pragma unroll
     for (int q = 0; q < 16; ++q) x[q] = (q == c) ? 1.0 : 0.0;
     OMB_CHOL_BTRACE(w, 8, lane == 0);
-    const int bad = chol16_factor<ASM>(a, x);
+    const int bad = chol16_factor(a, x);
     OMB_CHOL_BTRACE(w, 9, lane == 0);
     if (g == 0) {
       double2* drw = reinterpret_cast<double2*>(Ds + (16 * w + c) * kDP + 16 * w);
@@ -892,9 +878,8 @@ __device__ __forceinline__ void chol_tile_of(int b, int t, int& mt, int& nt) {
   nt = q - mp * (mp + 1) / 2 + 1;
 }
 
-// BLK: 0 round 3's diagonal workgroup, 1 chol64_blocked (the default), 2 chol64_blocked with the compiler's DPP moves
-// in place of the inline-asm v_fmac_f64_dpp (tools/ablate/ablate_chol)
-template <bool FUSE, int BLK>
+// BLK: the diagonal workgroup runs chol64_blocked (round 4, the default) instead of round 3's strip factor
+template <bool FUSE, bool BLK>
 __global__ __launch_bounds__(256, 3) void chol_update_kernel(double* __restrict__ A, int64_t N, int64_t lda, int step,
                                                           int t, double* __restrict__ ws, int* __restrict__ info,
                                                           int* __restrict__ flags, int spin_limit, int acq_rel) {
@@ -919,7 +904,7 @@ __global__ __launch_bounds__(256, 3) void chol_update_kernel(double* __restrict_
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const double* L21 = A + r0 * lda + c0;
-  if constexpr (BLK != 0) {
+  if constexpr (BLK) {
     // round 4: the next diagonal block factored by tiles of 16 (chol64_blocked), its product with the panel
     // formed by the waves that own the tiles
     if (mt == 0 && nt == 0) {
@@ -927,7 +912,7 @@ __global__ __launch_bounds__(256, 3) void chol_update_kernel(double* __restrict_
       __shared__ int fl[kBlkFlags];
       if (tid < kBlkFlags) fl[tid] = 0;
       __syncthreads();
-      chol64_blocked<true, BLK == 1>(A, lda, r0, (int)(M < kNB ? M : kNB), c0, ws, smem, Wl, fl);
+      chol64_blocked<true>(A, lda, r0, (int)(M < kNB ? M : kNB), c0, ws, smem, Wl, fl);
       __syncthreads();
       if (tid == 0 && (fl[20] || fl[21])) atomicCAS(info, 0, fl[21] ? kCholSpinFault : (int)(r0 + fl[20]));
       OMB_CHOL_STRACE(step, 1, tid == 0);
@@ -1203,7 +1188,7 @@ __global__ __launch_bounds__(256) void gp_grad_kernel(const double* __restrict__
       dot = fma(a[j], b[j], dot);
     }
     double r2 = (i == k) ? 0.0 : fma(-2.0, dot, aa + bb);
-    r2 = r2 > 0.0 ? r2 : 0.0;
+    r2 = r2_range<KIND>(r2);
     const double r = sqrt_nonneg(r2);
     double Kik, dkr;   // K and (dK/dr)/r
     if constexpr (KIND == OMB_KERNEL_MATERN52) {
@@ -1312,7 +1297,7 @@ __device__ __forceinline__ void fit_pair(const double* __restrict__ a, const dou
     dot = fma(a[j], b[j], dot);
   }
   double r2 = diag ? 0.0 : fma(-2.0, dot, aa + bb);
-  r2 = r2 > 0.0 ? r2 : 0.0;
+  r2 = r2_range<KIND>(r2);
   const double r = sqrt_nonneg(r2);
   if constexpr (KIND == OMB_KERNEL_MATERN52) {
     const double e = exp_nonpos(-(kSqrt5 * r));
@@ -2092,7 +2077,7 @@ constexpr size_t g_chol_update_lds = 0;
 
 // Round 4: the diagonal blocks by tiles of 16 (chol64_blocked), one launch per step with the next panel inside.
 static hipError_t launch_cholesky_blocked(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws,
-                                          int spin_limit, int acq_rel, bool mov) {
+                                          int spin_limit, int acq_rel) {
   const int steps = (int)((N + kNB - 1) / kNB);
   const bool vec = (lda % 2 == 0) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
   int* flags = reinterpret_cast<int*>(ws + kCholWsDoubles);
@@ -2105,12 +2090,8 @@ static hipError_t launch_cholesky_blocked(hipStream_t stream, double* A, int64_t
       e = chol_panel(stream, A, N, lda, k, ws, info, vec);
       if (e != hipSuccess) break;
     }
-    if (mov)
-      hipLaunchKernelGGL((chol_update_kernel<true, 2>), dim3((unsigned)(t * (t + 1) / 2)), dim3(256), g_chol_update_lds,
-                         stream, A, N, lda, k, t, ws, info, flags, spin_limit, acq_rel);
-    else
-      hipLaunchKernelGGL((chol_update_kernel<true, 1>), dim3((unsigned)(t * (t + 1) / 2)), dim3(256), g_chol_update_lds,
-                         stream, A, N, lda, k, t, ws, info, flags, spin_limit, acq_rel);
+    hipLaunchKernelGGL((chol_update_kernel<true, true>), dim3((unsigned)(t * (t + 1) / 2)), dim3(256), g_chol_update_lds,
+                       stream, A, N, lda, k, t, ws, info, flags, spin_limit, acq_rel);
     e = hipGetLastError();
   }
   return e;
@@ -2122,9 +2103,9 @@ hipError_t launch_cholesky_mode(hipStream_t stream, double* A, int64_t N, int64_
   const int steps = (int)((N + kNB - 1) / kNB);
   const bool vec = (lda % 2 == 0) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
   const bool fuse = mode == kCholFused;
-  const bool blk = mode == kCholBlocked || mode == kCholBlockedAcqRel || mode == kCholBlockedMov;
+  const bool blk = mode == kCholBlocked || mode == kCholBlockedAcqRel;
   const int acq_rel = mode == kCholBlockedAcqRel ? 1 : 0;
-  if (blk) return launch_cholesky_blocked(stream, A, N, lda, info, ws, spin_limit, acq_rel, mode == kCholBlockedMov);
+  if (blk) return launch_cholesky_blocked(stream, A, N, lda, info, ws, spin_limit, acq_rel);
   int* flags = reinterpret_cast<int*>(ws + kCholWsDoubles);
   hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), 0, stream, A, N, lda, ws, info, flags, fuse ? steps : 0);
   hipError_t e = hipGetLastError();
@@ -2138,10 +2119,10 @@ hipError_t launch_cholesky_mode(hipStream_t stream, double* A, int64_t N, int64_
     }
     const unsigned wgs = (unsigned)(t * (t + 1) / 2);
     if (fuse)
-      hipLaunchKernelGGL((chol_update_kernel<true, 0>), dim3(wgs), dim3(256), g_chol_update_lds, stream, A, N, lda, k,
+      hipLaunchKernelGGL((chol_update_kernel<true, false>), dim3(wgs), dim3(256), g_chol_update_lds, stream, A, N, lda, k,
                          t, ws, info, flags, spin_limit, 0);
     else
-      hipLaunchKernelGGL((chol_update_kernel<false, 0>), dim3(wgs), dim3(256), g_chol_update_lds, stream, A, N, lda,
+      hipLaunchKernelGGL((chol_update_kernel<false, false>), dim3(wgs), dim3(256), g_chol_update_lds, stream, A, N, lda,
                          k, t, ws, info, flags, spin_limit, 0);
     e = hipGetLastError();
   }

@@ -192,6 +192,16 @@ __device__ __forceinline__ double fma_vvs(double a, double b, double c) {
   return r;
 }
 
+constexpr double kMaternR2Max = 160000.0;   // r = 400: exp(−√5·400) = exp(−894.4) → 0
+constexpr double kRbfR2Max = 2048.0;        // exp(−1024) → 0
+// max(r², 0) with the same upper clamp, for the exp_nonpos paths (exp_nonpos itself saturates k
+// to INT_MIN and stays 0 up to r ~ 1e18, but its polynomial overflows past that).
+template <int KIND>
+__device__ __forceinline__ double r2_range(double r2) {
+  r2 = r2 > 0.0 ? r2 : 0.0;
+  return fmin(r2, KIND == OMB_KERNEL_MATERN52 ? kMaternR2Max : kRbfR2Max);
+}
+
 // exp_nonpos with its coefficients from `ec` (bit-identical results).
 __device__ __forceinline__ double exp_nonpos_k(double x, const ExpCoef& ec) {
   const double k = rint(x * 1.4426950408889634);
@@ -208,7 +218,7 @@ __device__ __forceinline__ double exp_nonpos_k(double x, const ExpCoef& ec) {
 // kernel_of_r2 (FAST form) with exp_nonpos_k.
 template <int KIND>
 __device__ __forceinline__ double kernel_of_r2_k(double r2, double variance, const ExpCoef& ec) {
-  r2 = r2 > 0.0 ? r2 : 0.0;
+  r2 = r2_range<KIND>(r2);
   const double r = sqrt_nonneg(r2);
   if constexpr (KIND == OMB_KERNEL_MATERN52) {
     const double poly = (1.0 + kSqrt5 * r) + kFiveThirds * (r * r);
@@ -224,8 +234,8 @@ __device__ __forceinline__ double kernel_of_r2_k(double r2, double variance, con
 template <int KIND>
 __device__ __forceinline__ void kernel_of_r2_k_x2(double r2a, double r2b, double variance, const ExpCoef& ec,
                                                   double& outa, double& outb) {
-  r2a = r2a > 0.0 ? r2a : 0.0;
-  r2b = r2b > 0.0 ? r2b : 0.0;
+  r2a = r2_range<KIND>(r2a);
+  r2b = r2_range<KIND>(r2b);
   // sqrt_nonneg ×2
   const double ya = __builtin_amdgcn_rsq(r2a), yb = __builtin_amdgcn_rsq(r2b);
   double ga = r2a * ya, gb = r2b * yb, ha = 0.5 * ya, hb = 0.5 * yb;
@@ -297,7 +307,17 @@ __device__ __forceinline__ void kernel_of_r2_k_x2(double r2a, double r2b, double
 // here; the compiler's hazard recognizer does not see inside inline asm, and as the first reader of
 // an FP64 MFMA result it could issue before the required wait states (found in r02 when a variant
 // with more registers scheduled it straight after the r²-MFMA and returned wrong moments).
-__device__ __forceinline__ double r2_clamp(double r2, double r2min) { return fabs(r2) + r2min; }
+//
+// Upper clamp (round 4): the table reductions round k = −√5·r·256/ln2 (or −r²/2·64/ln2) with the 1.5·2^52
+// shift, which is exact only for |k| < 2^51 — r > 2.7e12 (Matern) or r² > 2.4e13 (RBF).  A degenerate
+// lengthscale fit (ℓ = 2.3e-16 in a DTLZ2 run) puts r far past that and the low word of the
+// shifted sum is then garbage: K entries of ±inf/NaN instead of 0.  Clamping r² at the exp underflow
+// point (Matern √5·r > 894, RBF r²/2 > 1024: exp underflows to exactly 0 in double beyond either)
+// returns the reference's value, 0, for every larger r².  One v_min_f64 per element.
+__device__ __forceinline__ double r2_clamp(double r2, double r2min) {
+  return fmin(fabs(r2) + r2min, kMaternR2Max);
+}
+
 
 // Round-to-nearest-even of y with |y| < 2^51, as a double and as an int, from one add: the
 // 1.5·2^52 shift leaves the integer in the low word (replaces v_rndne + v_cvt_i32).
@@ -333,8 +353,8 @@ __device__ __forceinline__ void kernel_of_r2_tab_x2(double r2a, double r2b, cons
     ka_ = fma(ga, ec.t[0], 6755399441055744.0);     // −√5·r·64/ln2 + 1.5·2^52
     kb_ = fma(gb, ec.t[0], 6755399441055744.0);
   } else {
-    xa = -0.5 * fabs(r2a);                        // GPy clips r² < 0 (rounding, ~1e-16) to 0
-    xb = -0.5 * fabs(r2b);
+    xa = -0.5 * fmin(fabs(r2a), kRbfR2Max);       // GPy clips r² < 0 (rounding, ~1e-16) to 0
+    xb = -0.5 * fmin(fabs(r2b), kRbfR2Max);
     ka_ = fma(xa, -ec.t[0] / kSqrt5, 6755399441055744.0);
     kb_ = fma(xb, -ec.t[0] / kSqrt5, 6755399441055744.0);
   }
@@ -484,7 +504,7 @@ __device__ __forceinline__ double wf_load_f64(const double* p) {
                                                       __HIP_MEMORY_SCOPE_AGENT));
 }
 
-// Arg-max pair of the fused chains: higher value wins, the lower index on ties; index < 0 = none (NaN and −∞
+// Arg-max pair of the one-launch chains: higher value wins, the lower index on ties; index < 0 = none (NaN and −∞
 // never enter).  The same rule as omb_argmax.hip's `better`.
 __device__ __forceinline__ bool argmax_better(double av, long long ai, double bv, long long bi) {
   if (ai < 0) return false;
@@ -492,12 +512,38 @@ __device__ __forceinline__ bool argmax_better(double av, long long ai, double bv
   return (av > bv) || (av == bv && ai < bi);
 }
 
+// (v, i) of the whole workgroup into thread 0 (shuffles per wave, then wave 0's pairs from LDS in wave order);
+// red_v / red_i: one slot per wave.  Ends with a barrier passed by every thread.
+__device__ __forceinline__ void argmax_wave_block(double& v, long long& i, double* red_v, long long* red_i) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const double ov = __shfl_xor(v, off);
+    const long long oi = __shfl_xor(i, off);
+    if (argmax_better(ov, oi, v, i)) {
+      v = ov;
+      i = oi;
+    }
+  }
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red_v[wave] = v;
+    red_i[wave] = i;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0)
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w)
+      if (argmax_better(red_v[w], red_i[w], v, i)) {
+        v = red_v[w];
+        i = red_i[w];
+      }
+}
+
 // GPy Matern52.K_of_r: variance*(1+sqrt(5)*r+5/3*r**2)*exp(-sqrt(5)*r)  (r ≥ 0)
 // GPy RBF.K_of_r     : variance*exp(-r**2/2)
 // FAST selects exp_nonpos / sqrt_nonneg (default) or the libm functions (ablation reference).
 template <int KIND, bool FAST = true>
 __device__ __forceinline__ double kernel_of_r2(double r2, double variance) {
-  r2 = r2 > 0.0 ? r2 : 0.0;                 // np.clip(r2, 0, inf)
+  r2 = r2_range<KIND>(r2);                  // np.clip(r2, 0, inf); above the clamp K = 0 either way
   const double r = FAST ? sqrt_nonneg(r2) : sqrt(r2);
   if constexpr (KIND == OMB_KERNEL_MATERN52) {
     const double poly = (1.0 + kSqrt5 * r) + kFiveThirds * (r * r);

@@ -590,109 +590,6 @@ __global__ __launch_bounds__(512) void kernel_block_persist_kernel(GPDev g, int 
   }
 }
 
-// Epilogue of the fused EHVI-2D chains (posterior_kernel<…, EPI = 1>): the BN candidates' EHVI from their moments in
-// LDS (mom: μ0 | σ²0 | μ1 | σ²1), the block's arg-max (higher value, lower index; NaN and −∞ never win), its pair to
-// fe.partials[blockIdx.x] (agent-scope stores) and an agent-scope ticket; the last workgroup reduces every pair
-// and writes fe.result = {value, index + offset}, then resets the ticket.  geo: 2·kFusedMaxP + 1 doubles of LDS,
-// scratch: ≥ 2·(NT/64) doubles of LDS.
-template <int BN, int NT>
-__device__ __forceinline__ void fused_ehvi2d_epilogue(const FusedEhvi2d& fe, const double* mom, double* geo,
-                                                      int64_t N, int64_t c0, double* scratch) {
-  static_assert(BN % 16 == 0 && BN / 16 <= NT / 64, "16 candidates per wave");
-  constexpr int NW = NT / 64;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = tid >> 6;
-  const int P = fe.P;
-  double* y1 = geo;
-  double* y2 = geo + P + 1;
-  for (int i = tid; i < P; i += NT) {
-    y1[i + 1] = fe.pf[2 * i];
-    y2[i] = fe.pf[2 * i + 1];
-  }
-  if (tid == 0) y1[0] = fe.r0;
-  __syncthreads();
-  __shared__ int is_last;
-  long long* sbi = reinterpret_cast<long long*>(scratch + NW);
-  if (wave < BN / 16) {
-    // wave w: candidates 16w + (lane & 15), four lanes each (ehvi2d_point4)
-    double bv = -__builtin_inf();
-    long long bi = -1;
-    const int cl = 16 * wave + (lane & 15);
-    const int64_t c = c0 + cl;
-    const double v = ehvi2d_point4(mom[cl], mom[2 * BN + cl], mom[BN + cl],
-                                   fe.mode == OMB_EHVI_REFERENCE ? 0.0 : mom[3 * BN + cl], y1, y2, P, fe.r1, fe.s00,
-                                   fe.s01, fe.mode, lane >> 4);
-    if (lane < 16 && c < N && v == v && v > -__builtin_inf()) {
-      bv = v;
-      bi = c;
-    }
-#pragma unroll
-    for (int off = 8; off > 0; off >>= 1) {
-      const double ov = __shfl_xor(bv, off);
-      const long long oi = __shfl_xor(bi, off);
-      if (argmax_better(ov, oi, bv, bi)) {
-        bv = ov;
-        bi = oi;
-      }
-    }
-    if (lane == 0) {
-      scratch[wave] = bv;
-      sbi[wave] = bi;
-    }
-  }
-  __syncthreads();
-  if (tid == 0) {
-    double bv = scratch[0];
-    long long bi = sbi[0];
-    for (int w = 1; w < BN / 16; ++w)
-      if (argmax_better(scratch[w], sbi[w], bv, bi)) {
-        bv = scratch[w];
-        bi = sbi[w];
-      }
-    wf_store_f64(&fe.partials[2 * blockIdx.x], bv);
-    wf_store_f64(&fe.partials[2 * blockIdx.x + 1], __builtin_bit_cast(double, bi));
-    const unsigned prev = __hip_atomic_fetch_add(fe.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    is_last = prev == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!is_last) return;
-  double v = -__builtin_inf();
-  long long i = -1;
-  for (int b = tid; b < (int)gridDim.x; b += NT) {
-    const double bv = wf_load_f64(&fe.partials[2 * b]);
-    const long long bi = __builtin_bit_cast(long long, wf_load_f64(&fe.partials[2 * b + 1]));
-    if (argmax_better(bv, bi, v, i)) {
-      v = bv;
-      i = bi;
-    }
-  }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const double ov = __shfl_xor(v, off);
-    const long long oi = __shfl_xor(i, off);
-    if (argmax_better(ov, oi, v, i)) {
-      v = ov;
-      i = oi;
-    }
-  }
-  __syncthreads();                                       // the block pairs in scratch are read
-  if (lane == 0) {
-    scratch[wave] = v;
-    sbi[wave] = i;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    for (int w = 1; w < NW; ++w)
-      if (argmax_better(scratch[w], sbi[w], v, i)) {
-        v = scratch[w];
-        i = sbi[w];
-      }
-    fe.result[0] = i < 0 ? -__builtin_inf() : v;
-    fe.result[1] = i < 0 ? -1.0 : (double)(i + fe.offset);
-    __hip_atomic_store(fe.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
 // Per-workgroup phase timestamps of the posterior kernels for tools/ablate/ablate_posterior (empty here).
 #ifndef OMB_POST_TRACE
 #define OMB_POST_TRACE(id)
@@ -708,15 +605,10 @@ __device__ __forceinline__ void fused_ehvi2d_epilogue(const FusedEhvi2d& fe, con
 // chain at ‖x‖² + ‖x*‖² with −2x* pre-scaled (one fma fewer per element), bit 65536 forces a spin
 // bound of 0 on the counter-ring waits (the fault-word path).
 // NW = waves per workgroup (8 or 16): waves w, w+4, w+8, w+12 share a SIMD.
-// EPI = 1 (round 4, omb_eval_argmax with an EHVI-2D plan, n > 128): one workgroup computes BOTH objectives of its
-// BN candidates — the whole pipeline below runs once per objective, the moments go to LDS instead of HBM — and
-// then the epilogue evaluates the candidates' EHVI (ehvi2d_point4, util_functions.py:136-167), reduces the
-// block's arg-max and hands it to the last workgroup (fe.ticket), which writes {value, index + offset}: the
-// posterior → ehvi2d_kernel → argmax_pass1/2 chain in one launch, bit for bit.
-template <int RT, int CT, int DP, int KIND, int NW = 8, int ABL = 0, int EPI = 0>
+template <int RT, int CT, int DP, int KIND, int NW = 8, int ABL = 0>
 __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args, const double* __restrict__ Xc,
                                                                      int64_t N, double* __restrict__ mu_out,
-                                                                     double* __restrict__ var_out, FusedEhvi2d fe) {
+                                                                     double* __restrict__ var_out) {
   constexpr int NT = 64 * NW;                 // threads per workgroup
   constexpr int G = NW / 4;                   // waves sharing one SIMD
   constexpr int BN = 16 * CT;                 // candidates per workgroup
@@ -738,17 +630,14 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
   constexpr bool kTab256 = !(ABL & 16384) && KIND == OMB_KERNEL_MATERN52;
   constexpr int kTabN = kTab256 ? 256 : 64;
   __shared__ double kbuf[NBUF * CHUNK + kCtrDoubles + (kCandLds ? DP * BN : 0) + kTabN];
-  __shared__ double fe_mom[EPI ? 4 * BN : 1];            // EPI: μ0 | σ²0 | μ1 | σ²1 of the block's candidates
-  __shared__ double fe_geo[EPI ? 2 * kFusedMaxP + 1 : 1];
 
   OMB_POST_TRACE(0);
+  const int obj = blockIdx.y;
+  const GPDev g = args.gp[obj];
   const int d = args.d;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t c0 = (int64_t)blockIdx.x * BN;
-#pragma unroll 1
-  for (int obj = EPI ? 0 : (int)blockIdx.y; obj < (EPI ? 2 : (int)blockIdx.y + 1); ++obj) {
-  const GPDev g = args.gp[obj];
 
   // ---- this thread's generation candidate (fixed across chunks since BN | NT)
   const int cg = tid % BN;
@@ -1115,17 +1004,11 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args,
       for (int t = tid; t < NT; t += BN) m += redmu[t];
     }
     const int64_t c = c0 + tid;
-    if constexpr (EPI != 0) {
-      fe_mom[2 * obj * BN + tid] = m;
-      fe_mom[(2 * obj + 1) * BN + tid] = g.variance - s;
-    } else if (c < N) {
+    if (c < N) {
       mu_out[(int64_t)obj * N + c] = m;
       var_out[(int64_t)obj * N + c] = g.variance - s;
     }
   }
-  if constexpr (EPI != 0) __syncthreads();             // the K* ring and the reduction scratch are reused
-  }   // objectives
-  if constexpr (EPI != 0) fused_ehvi2d_epilogue<BN, 64 * NW>(fe, fe_mom, fe_geo, N, c0, kbuf);
   OMB_POST_TRACE(4);
 }
 
@@ -1366,91 +1249,6 @@ __global__ __launch_bounds__(512, 2) void posterior_tile_kernel(GPArgs args, con
 // Matern transform (K* = r²), bit 16 drops the sqrt's residual correction, bit 32 scales by 2^m with
 // an integer exponent add instead of v_ldexp_f64, bit 64 loads the next tile's coordinates during the current
 // tile (instead of at its start), bit 128 stages with the round-2 rolled loops and reloads ℓ per tile.
-// One 16-candidate tile of one objective in posterior_reg_ehvi_kernel (wave-level; posterior_reg_kernel below keeps
-// the same steps inline — through this function its RMAX = 8 instances spilled 2-10 VGPRs at the 128-VGPR bound): the
-// B fragment of the r²-MFMA from the raw coordinates, K* row tile by row tile (augmented r² on MFMA, the Matern
-// transform), μ = αᵀK* and ΣV² with V = L⁻¹K* accumulated in registers (row tile T retired after step T); μ and
-// ΣV² reduced over the wave's four row groups (every lane ends with its candidate's values).
-template <int RMAX, int DP, int KIND, bool XL, int ABL, int KSD>
-__device__ __forceinline__ void reg_tile_moments(const double* __restrict__ gls, int d, int R, const double (&raw)[KSD],
-                                                 const double (&lsr)[KSD], const d2* xf, const double* lds_L,
-                                                 const double* lds_alpha, const double* etab, const ExpCoef& ec,
-                                                 const double (&pm)[3], int lane, double& mu_out, double& s_out) {
-  constexpr int KSDP = (KSD + 1) / 2;
-  constexpr bool kTab256 = KIND == OMB_KERNEL_MATERN52;
-  // B fragment [−2·x*/ℓ, 1, ‖x*/ℓ‖²]: lane l needs dims 4s + (l>>4) only; ‖x*/ℓ‖² from the four
-  // lane groups by two shuffles
-  double xs[KSD], csq = 0.0;
-#pragma unroll
-  for (int q = 0; q < KSD; ++q) {
-    const int j = 4 * q + (lane >> 4);
-    if constexpr ((ABL & 128) != 0)
-      xs[q] = (j < d) ? raw[q] / gls[j] : 0.0;
-    else
-      xs[q] = (j < d) ? raw[q] / lsr[q] : 0.0;
-    csq = fma(xs[q], xs[q], csq);
-  }
-  csq += __shfl_xor(csq, 16);
-  csq += __shfl_xor(csq, 32);
-  double bfr[KSD];
-#pragma unroll
-  for (int s = 0; s < KSD; ++s) {
-    const int j = 4 * s + (lane >> 4);
-    bfr[s] = (j < d) ? -2.0 * xs[s] : (j == d ? 1.0 : (j == d + 1 ? csq : 0.0));
-  }
-
-  d4 acc[RMAX];
-  double mu_part = 0.0, s = 0.0;
-#pragma unroll
-  for (int T = 0; T < RMAX; ++T) {
-    const int Tl = XL ? T : min(T, R - 1);        // T ≥ R: finite stand-in rows (zero L⁻¹ / α)
-    d2 a[KSDP];
-#pragma unroll
-    for (int p = 0; p < KSDP; ++p) a[p] = xf[64 * (KSDP * Tl + p)];
-    d4 cr = d4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int q = 0; q < KSD; ++q)
-      cr = __builtin_amdgcn_mfma_f64_16x16x4f64((q & 1) ? a[q >> 1].y : a[q >> 1].x, bfr[q], cr, 0, 0, 0);
-    double kv[4];
-#pragma unroll
-    for (int e = 0; e < 4; e += 2) {
-      if constexpr ((ABL & 8) != 0) {
-        kv[e] = cr[e];
-        kv[e + 1] = cr[e + 1];
-      } else if constexpr (kTab256) {
-        matern_r2_tab256_x2<(ABL & 16) != 0, (ABL & 32) != 0>(cr[e], cr[e + 1], pm, ec, etab, kv[e], kv[e + 1]);
-      } else {
-        kernel_of_r2_tab_x2<KIND>(cr[e], cr[e + 1], pm, ec, etab, kv[e], kv[e + 1]);
-      }
-      mu_part = fma(lds_alpha[16 * T + 4 * e + (lane >> 4)], kv[e], mu_part);
-      mu_part = fma(lds_alpha[16 * T + 4 * e + 4 + (lane >> 4)], kv[e + 1], mu_part);
-    }
-    if constexpr (!(ABL & 2)) {
-#pragma unroll
-      for (int r = T; r < RMAX; ++r) {
-        const d2* A = reinterpret_cast<const d2*>(lds_L + 128 * r * (r + 1) + 256 * T) + lane;
-        const d2 a0 = A[0], a1 = A[64];
-        d4 v = (T == 0) ? d4{0.0, 0.0, 0.0, 0.0} : acc[r];
-        v = __builtin_amdgcn_mfma_f64_16x16x4f64(a0.x, kv[0], v, 0, 0, 0);
-        v = __builtin_amdgcn_mfma_f64_16x16x4f64(a0.y, kv[1], v, 0, 0, 0);
-        v = __builtin_amdgcn_mfma_f64_16x16x4f64(a1.x, kv[2], v, 0, 0, 0);
-        acc[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1.y, kv[3], v, 0, 0, 0);
-      }
-    } else {
-      acc[T] = d4{kv[0], kv[1], kv[2], kv[3]};
-    }
-    // row tile T has all its k-steps (T' ≤ T): retire its accumulator, so at most RMAX − T are live
-#pragma unroll
-    for (int i = 0; i < 4; ++i) s = fma(acc[T][i], acc[T][i], s);
-  }
-  s += __shfl_xor(s, 16);
-  s += __shfl_xor(s, 32);
-  mu_part += __shfl_xor(mu_part, 16);
-  mu_part += __shfl_xor(mu_part, 32);
-  mu_out = mu_part;
-  s_out = s;
-}
-
 template <int RMAX, int DP, int KIND, int NW = 8, bool XL = false, int ABL = 0>
 __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : NW / 4) void posterior_reg_kernel(
     GPArgs args, const double* __restrict__ Xc, int64_t N, double* __restrict__ mu_out, double* __restrict__ var_out) {
@@ -1660,265 +1458,6 @@ static dim3 reg_grid(int64_t N, int n_obj, int NW = 8, int per_cu = 2) {
   return dim3((unsigned)std::max<int64_t>(1, std::min(wgs, resident)), (unsigned)n_obj);
 }
 
-// ----------------------------------------------------------------------------- fused 2-objective EHVI chain
-// omb_eval_argmax with an EHVI-2D plan at n ≤ 128, n_var ≤ 8 (BASELINE config 2): posterior
-// of both objectives, EHVI (ehvi2d_point4, util_functions.py:136-167) and the arg-max in one persistent launch —
-// μ and σ² never leave the registers, and the acquisition values never reach HBM.
-//   * one 1024-thread workgroup per CU stages BOTH objectives' packed L⁻¹ and α (2 × 72 KiB at n = 128), the exp
-//     table and the EHVI stripes in LDS; the training-row fragments (Xf) are read from L2;
-//   * each wave loops over 16-candidate tiles: reg_tile_moments for objective 0, then 1 (bitwise the moments
-//     posterior_reg_kernel writes), then lanes 0..15 evaluate their candidate's EHVI and keep a running
-//     (value, index) best — higher value, lower index on ties, NaN and −∞ never win (omb_argmax.hip's rule);
-//   * the wave's best → LDS → the workgroup's pair → partials; the last workgroup to finish (an agent-scope
-//     ticket) reduces the pairs and writes {value, index + offset}, then resets the ticket for the next launch.
-// The result equals posterior → ehvi2d_kernel → argmax_pass1/2 bit for bit (tests/test_gpu_fused.py).
-// ehvi2d_point4 as a call: inlined into the tile loop, its ndtr coefficients were hoisted into VGPRs for the whole
-// loop (≈ 90 spilled VGPRs at the 128-VGPR bound)
-__device__ __noinline__ double ehvi2d_point4_call(double m0, double m1, double v0, double v1, const double* y1,
-                                                  const double* y2, int P, double r1, double s00, double s01, int mode,
-                                                  int g) {
-  return ehvi2d_point4(m0, m1, v0, v1, y1, y2, P, r1, s00, s01, mode, g);
-}
-
-template <int RMAX, int DP, int KIND, int NW>
-__global__ __launch_bounds__(64 * NW, 1) void posterior_reg_ehvi_kernel(GPArgs args, const double* __restrict__ Xc,
-                                                                        int64_t N, FusedEhvi2d fe) {
-  constexpr int NT = 64 * NW;
-  static_assert(DP <= 8, "augmented r² needs n_var ≤ 8");
-  constexpr int KSD = (DP + 5) / 4;
-  constexpr bool kTab256 = KIND == OMB_KERNEL_MATERN52;
-  constexpr int kTabN = kTab256 ? 256 : 64;
-  constexpr int kL2 = 64 * RMAX * (RMAX + 1);       // d2 elements of one packed L⁻¹
-  __shared__ double lds_L[2][2 * kL2];
-  __shared__ double lds_alpha[2][16 * RMAX];
-  __shared__ double etab[kTabN];
-  __shared__ double geo[2 * kFusedMaxP + 1];         // y1[0..P] | y2[0..P−1]
-  __shared__ double red_v[NW];
-  __shared__ long long red_i[NW];
-  __shared__ int is_last;
-  // per wave and candidate lane: objective 0's moments while objective 1's tile runs, and the running best
-  // (in LDS, not registers: the tile loop is at the 128-VGPR bound of 16 waves per CU)
-  __shared__ double st_mu[NW][16], st_var[NW][16], st_bv[NW][16];
-  __shared__ long long st_bi[NW][16];
-
-  const int d = args.d;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t ntiles = (N + 15) / 16;
-  const int64_t stride = (int64_t)gridDim.x * NW;
-  const int P = fe.P;
-  // ---- staging: both objectives' L⁻¹ and α, the exp table, the stripes
-#pragma unroll
-  for (int o = 0; o < 2; ++o) {
-    const GPDev& g = args.gp[o];
-    const int nL2 = 64 * g.R * (g.R + 1);
-    const d2* src = reinterpret_cast<const d2*>(g.Lp);
-    d2* dst = reinterpret_cast<d2*>(lds_L[o]);
-    for (int i = tid; i < kL2; i += NT) dst[i] = i < nL2 ? src[i] : d2{0.0, 0.0};
-    if (tid < 16 * RMAX) lds_alpha[o][tid] = tid < 16 * g.R ? g.alpha[tid] : 0.0;
-  }
-  for (int i = tid; i < kTabN; i += NT) etab[i] = kTab256 ? kExp2Tab256[i] : kExp2Tab64[i];
-  double* y1 = geo;
-  double* y2 = geo + P + 1;
-  for (int i = tid; i < P; i += NT) {
-    y1[i + 1] = fe.pf[2 * i];
-    y2[i] = fe.pf[2 * i + 1];
-  }
-  if (tid == 0) y1[0] = fe.r0;
-  __syncthreads();
-
-  if (lane < 16) {
-    st_bv[wave][lane] = -__builtin_inf();
-    st_bi[wave][lane] = -1;
-  }
-  for (int64_t t = (int64_t)blockIdx.x * NW + wave; t < ntiles; t += stride) {
-    const int64_t c = 16 * t + (lane & 15);
-    // the objectives one after the other (a rolled loop: unrolled, the compiler interleaved the two tiles' registers
-    // and spilled ≈ 200 VGPRs); the coordinates are reloaded for the second (L1/L2 hits)
-    double mu1 = 0.0, var1 = 0.0;
-#pragma unroll 1
-    for (int o = 0; o < 2; ++o) {
-      double raw[KSD];
-      {
-        const int64_t cc = c < N ? c : N - 1;
-#pragma unroll
-        for (int q = 0; q < KSD; ++q) {
-          const int j = 4 * q + (lane >> 4);
-          raw[q] = (j < d) ? Xc[cc * d + j] : 0.0;
-        }
-      }
-      const GPDev* g = o == 0 ? &args.gp[0] : &args.gp[1];
-      double lsr[KSD];
-#pragma unroll
-      for (int q = 0; q < KSD; ++q) {
-        const int j = 4 * q + (lane >> 4);
-        lsr[q] = (j < d) ? g->ls[j] : 1.0;
-      }
-      const double pm[3] = {g->variance, kSqrt5 * g->variance, kFiveThirds * g->variance};
-      double m, s;
-      // an opaque per-tile offset keeps LICM from hoisting the (tile-invariant) Xf fragments out of the tile loop
-      int xoff = lane;
-      asm volatile("" : "+v"(xoff));
-      reg_tile_moments<RMAX, DP, KIND, false, 0>(g->ls, d, g->R, raw, lsr, reinterpret_cast<const d2*>(g->Xf) + xoff,
-                                                 lds_L[o], lds_alpha[o], etab, args.ec, pm, lane, m, s);
-      if (o == 0) {
-        if (lane < 16) {
-          st_mu[wave][lane] = m;
-          st_var[wave][lane] = g->variance - s;
-        }
-      } else {
-        mu1 = m;
-        var1 = g->variance - s;
-      }
-    }
-    // every lane: its quarter of the candidate's stripes (ehvi2d_point4; the shuffles need the whole wave)
-    const double v = ehvi2d_point4_call(st_mu[wave][lane & 15], mu1, st_var[wave][lane & 15],
-                                        fe.mode == OMB_EHVI_REFERENCE ? 0.0 : var1, y1, y2, P, fe.r1, fe.s00, fe.s01,
-                                        fe.mode, lane >> 4);
-    if (lane < 16 && c < N) {
-      if (v == v && v > -__builtin_inf() && argmax_better(v, c, st_bv[wave][lane], st_bi[wave][lane])) {
-        st_bv[wave][lane] = v;
-        st_bi[wave][lane] = c;
-      }
-    }
-  }
-  // ---- the wave's best (lanes 0..15), the workgroup's, the grid's
-  double best_v = lane < 16 ? st_bv[wave][lane] : -__builtin_inf();
-  long long best_i = lane < 16 ? st_bi[wave][lane] : -1;
-#pragma unroll
-  for (int off = 8; off > 0; off >>= 1) {
-    const double ov = __shfl_xor(best_v, off);
-    const long long oi = __shfl_xor(best_i, off);
-    if (argmax_better(ov, oi, best_v, best_i)) {
-      best_v = ov;
-      best_i = oi;
-    }
-  }
-  if (lane == 0) {
-    red_v[wave] = best_v;
-    red_i[wave] = best_i;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    for (int w = 1; w < NW; ++w)
-      if (argmax_better(red_v[w], red_i[w], best_v, best_i)) {
-        best_v = red_v[w];
-        best_i = red_i[w];
-      }
-    wf_store_f64(&fe.partials[2 * blockIdx.x], best_v);
-    wf_store_f64(&fe.partials[2 * blockIdx.x + 1], __builtin_bit_cast(double, best_i));
-    const unsigned prev = __hip_atomic_fetch_add(fe.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    is_last = prev == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!is_last) return;
-  // the last workgroup: all pairs, in workgroup order (the rule is order-free; the scan is fixed anyway)
-  double v = -__builtin_inf();
-  long long i = -1;
-  for (int b = tid; b < (int)gridDim.x; b += NT) {
-    const double bv = wf_load_f64(&fe.partials[2 * b]);
-    const long long bi = __builtin_bit_cast(long long, wf_load_f64(&fe.partials[2 * b + 1]));
-    if (argmax_better(bv, bi, v, i)) {
-      v = bv;
-      i = bi;
-    }
-  }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const double ov = __shfl_xor(v, off);
-    const long long oi = __shfl_xor(i, off);
-    if (argmax_better(ov, oi, v, i)) {
-      v = ov;
-      i = oi;
-    }
-  }
-  __syncthreads();
-  if (lane == 0) {
-    red_v[wave] = v;
-    red_i[wave] = i;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    for (int w = 1; w < NW; ++w)
-      if (argmax_better(red_v[w], red_i[w], v, i)) {
-        v = red_v[w];
-        i = red_i[w];
-      }
-    fe.result[0] = i < 0 ? -__builtin_inf() : v;
-    fe.result[1] = i < 0 ? -1.0 : (double)(i + fe.offset);
-    __hip_atomic_store(fe.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// The one-launch EHVI-2D chain applies with two objectives, ≤ kFusedMaxP stripes and n_var ≤ 8, through
-// posterior_reg_ehvi_kernel (n ≤ 128) or posterior_kernel<…, EPI = 1> (128 < n ≤ 512).  Wider inputs and
-// n > 512 keep the separate launches: there the EPI = 1 ring kernels spilled 6-93 VGPRs.
-static bool fused_reg_path(int max_R, int DP) { return max_R <= 8 && DP <= 8; }
-static int ring_rt(int max_R) { return ((max_R + 3) / 4 + 1) / 2; }   // RTneed of launch_posterior_dp
-bool fused_ehvi2d_fits(int n_obj, int max_R, int DP, int P) {
-  if (n_obj != 2 || P < 1 || P > kFusedMaxP || DP > 8) return false;
-  return fused_reg_path(max_R, DP) || ring_rt(max_R) <= 4;
-}
-int64_t fused_ehvi2d_blocks(int max_R, int DP, int64_t N) {
-  if (fused_reg_path(max_R, DP)) return device_cu_count();                  // ≥ the persistent grid
-  const int rt = ring_rt(max_R);
-  const int64_t BN = rt <= 2 ? 32 : (rt <= 4 ? 64 : 32);
-  return (N + BN - 1) / BN;
-}
-
-template <int DP, int KIND, int NW>
-static hipError_t launch_fused_ehvi2d_nw(hipStream_t stream, const GPArgs& args, int max_R, const double* Xc,
-                                         int64_t N, const FusedEhvi2d& fe) {
-  const dim3 grid = reg_grid(N, 1, NW, 1);
-  const dim3 block(64 * NW);
-  if (max_R <= 2)
-    hipLaunchKernelGGL((posterior_reg_ehvi_kernel<2, DP, KIND, NW>), grid, block, 0, stream, args, Xc, N, fe);
-  else if (max_R <= 4)
-    hipLaunchKernelGGL((posterior_reg_ehvi_kernel<4, DP, KIND, NW>), grid, block, 0, stream, args, Xc, N, fe);
-  else
-    hipLaunchKernelGGL((posterior_reg_ehvi_kernel<8, DP, KIND, NW>), grid, block, 0, stream, args, Xc, N, fe);
-  return hipGetLastError();
-}
-
-template <int DP, int KIND>
-static hipError_t launch_fused_ehvi2d_dp(hipStream_t stream, const GPArgs& args, int max_R, const double* Xc,
-                                         int64_t N, const FusedEhvi2d& fe, int variant) {
-  if constexpr (DP <= 8) {
-    if (fused_reg_path(max_R, DP))
-      return variant == 2 ? launch_fused_ehvi2d_nw<DP, KIND, 8>(stream, args, max_R, Xc, N, fe)
-                          : launch_fused_ehvi2d_nw<DP, KIND, 16>(stream, args, max_R, Xc, N, fe);
-    // the ring kernels of launch_posterior_dp, both objectives per workgroup (EPI = 1)
-    const int rt = ring_rt(max_R);
-    const unsigned blocks = (unsigned)fused_ehvi2d_blocks(max_R, DP, N);
-    if (rt <= 2)
-      hipLaunchKernelGGL((posterior_kernel<2, 2, DP, KIND, 8, 0, 1>), dim3(blocks), dim3(kBlockThreads), 0, stream,
-                         args, Xc, N, nullptr, nullptr, fe);
-    else if (rt <= 4)
-      hipLaunchKernelGGL((posterior_kernel<4, 4, DP, KIND, 8, 0, 1>), dim3(blocks), dim3(kBlockThreads), 0, stream,
-                         args, Xc, N, nullptr, nullptr, fe);
-    else
-      return hipErrorInvalidValue;
-    return hipGetLastError();
-  }
-  return hipErrorInvalidValue;
-}
-
-hipError_t launch_fused_ehvi2d(hipStream_t stream, const GPArgs& args_in, int max_R, const double* Xc, int64_t N,
-                               const FusedEhvi2d& fe, int variant) {
-  GPArgs args = args_in;
-  args.ec = exp_coef();
-  const bool rbf = args.gp[0].kind == OMB_KERNEL_RBF;
-  switch (args.DP) {
-#define OMB_FE(DPV)                                                                                       \
-  case DPV:                                                                                               \
-    return rbf ? launch_fused_ehvi2d_dp<DPV, OMB_KERNEL_RBF>(stream, args, max_R, Xc, N, fe, variant)    \
-               : launch_fused_ehvi2d_dp<DPV, OMB_KERNEL_MATERN52>(stream, args, max_R, Xc, N, fe, variant);
-    OMB_FE(2) OMB_FE(4) OMB_FE(6) OMB_FE(8)
-#undef OMB_FE
-    default: return hipErrorInvalidValue;
-  }
-}
-
 // ----------------------------------------------------------------------------- dispatch
 template <int DP, int KIND>
 static hipError_t launch_posterior_dp(hipStream_t stream, const GPArgs& args, int n_obj, int max_R,
@@ -1950,16 +1489,13 @@ static hipError_t launch_posterior_dp(hipStream_t stream, const GPArgs& args, in
     // tools/ablate at n = 256, 3 objectives, 2^17 candidates: 0.709 ms (CT 4, barrier) → 0.641 ms;
     // the whole-tile kernel (RMAX 16, CT 2) takes 0.688 ms there (profiles/r02_v2_ablate_c4.txt)
     dim3 grid((unsigned)((N + 31) / 32), n_obj);
-    hipLaunchKernelGGL((posterior_kernel<2, 2, DP, KIND, 8, 0>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var,
-                       FusedEhvi2d{});
+    hipLaunchKernelGGL((posterior_kernel<2, 2, DP, KIND, 8, 0>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var);
   } else if (RTneed <= 4) {
     dim3 grid((unsigned)((N + 63) / 64), n_obj);
-    hipLaunchKernelGGL((posterior_kernel<4, 4, DP, KIND>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var,
-                       FusedEhvi2d{});
+    hipLaunchKernelGGL((posterior_kernel<4, 4, DP, KIND>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var);
   } else if (RTneed <= 8) {
     dim3 grid((unsigned)((N + 31) / 32), n_obj);
-    hipLaunchKernelGGL((posterior_kernel<8, 2, DP, KIND>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var,
-                       FusedEhvi2d{});
+    hipLaunchKernelGGL((posterior_kernel<8, 2, DP, KIND>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var);
   } else {
     return hipErrorInvalidValue;
   }

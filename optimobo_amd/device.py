@@ -69,8 +69,8 @@ class AcqContext:
 
     def debug_set(self, what, value):
         """omb_debug_set: ("spin_limit", polls) bounds the posterior's LDS-counter waits; ("cov_table", 0/1)
-        builds K(X, X) / K(X*, X*) with the posterior's table-driven Matern transform; ("fused_chain", 0/1) turns
-        the one-launch posterior → EHVI → arg-max chain off / on."""
+        builds K(X, X) / K(X*, X*) with the posterior's table-driven Matern transform; ("fused_chain", 0/1) runs
+        EHVI-2D and the arg-max as separate launches / as one."""
         code = {"spin_limit": _lib.DEBUG_SPIN_LIMIT, "cov_table": _lib.DEBUG_COV_TABLE,
                 "fused_chain": _lib.DEBUG_FUSED_CHAIN}[what]
         self._check(self.lib.omb_debug_set(self._h, code, int(value)), "omb_debug_set")

@@ -102,3 +102,121 @@ def test_table_transform_matches_libm_on_readme_states():
           f"near-duplicate pairs (r² < 1e-6) {worst_near:.2e}")
     assert worst <= 3e-14
     assert worst_diag <= 2.3e-16
+
+
+def test_covariance_kernel_table_vs_polynomial_on_readme_states():
+    """K(X*, X*) from the covariance kernel with the table transform against its polynomial-exp form, on the README
+    run's states (omb_posterior_cov with one far-away training point, so Σ = K(X*, X*) to rounding): the two
+    transforms must agree to the table's accuracy entrywise — and with it the fit-state install must succeed."""
+    import os
+    from optimobo_amd.device import AcqContext
+    from optimobo_amd.gp import DeviceGPState
+    rec = []
+    _run_readme(False, rec)
+    ctx = AcqContext(0)
+    worst = (0.0, None)
+    dump = os.environ.get("OMB_TEST_RECORD")
+    try:
+        for si, (X, y, ls, sf2, _) in enumerate(rec[::5]):
+            far = np.full((1, X.shape[1]), 1e4)
+            ctx.set_gp_state(0, DeviceGPState(far, np.zeros(1), ls, sf2))
+            out = {}
+            for tab in (0, 1):
+                ctx.debug_set("cov_table", tab)
+                _, S = ctx.posterior_cov(0, X)
+                out[tab] = S.cpu().numpy()
+            ctx.debug_set("cov_table", 0)
+            Kl = ogp.matern52_K(X, X, ls, sf2)
+            L0, L1 = np.tril(out[0]), np.tril(out[1])
+            e_poly = np.abs(L0 - np.tril(Kl)).max() / sf2
+            e_tab = np.abs(L1 - np.tril(Kl)).max() / sf2
+            if e_tab > worst[0]:
+                i, j = np.unravel_index(np.argmax(np.abs(L1 - np.tril(Kl))), L1.shape)
+                worst = (e_tab, dict(state=si, n=len(X), i=int(i), j=int(j), K_tab=float(L1[i, j]),
+                                     K_poly=float(L0[i, j]), K_libm=float(Kl[i, j]), sf2=sf2, e_poly=e_poly))
+                if dump and e_tab > 1e-12:
+                    np.savez(dump, X=X, y=y, ls=ls, sf2=sf2, K_tab=out[1], K_poly=out[0])
+    finally:
+        ctx.debug_set("cov_table", 0)
+        ctx.close()
+    print("worst table-path entry:", worst)
+    assert worst[0] <= 3e-14, worst
+
+
+def _degenerate_state():
+    """The state whose install failed with the table covariance in round 4 (gpurun_out/r04_i, saved by the
+    README run on the GPU: n 23, ℓ = [2.3e-16, 360.6], σ_f² 1.0e5) — a degenerate lengthscale fit."""
+    import os
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "degenerate_ls_state.npz"))
+    return d["X"], d["y"], d["ls"], float(d["sf2"])
+
+
+def test_degenerate_lengthscale_state_installs_on_table_path():
+    """Root cause of the r03/r04 table-covariance install failures: ℓ_0 = 2.3e-16 puts r ≈ 4e15 past the range
+    (r < 2.7e12) where the 1.5·2^52 shift rounds k = −√5·r·256/ln2 exactly, so K had ±inf/NaN entries in place
+    of 0 and no jitter could help.  With the r² clamp at the exp underflow point (omb_math.h r2_clamp) the
+    table path gives the reference's 0 there: K(X, X) finite, equal to the polynomial path and the libm
+    restatement, and the install succeeds."""
+    from optimobo_amd.device import AcqContext
+    from optimobo_amd.gp import DeviceGPState
+    X, y, ls, sf2 = _degenerate_state()
+    n = len(X)
+    ctx = AcqContext(0)
+    try:
+        far = np.full((1, X.shape[1]), 1e4)
+        ctx.set_gp_state(0, DeviceGPState(far, np.zeros(1), ls, sf2))
+        Kl = ogp.matern52_K(X, X, ls, sf2)
+        for tab in (0, 1):
+            ctx.debug_set("cov_table", tab)
+            _, S = ctx.posterior_cov(0, X)
+            K = np.tril(S.cpu().numpy())
+            K = K + np.tril(K, -1).T
+            assert np.isfinite(K).all(), tab
+            assert np.abs(K - Kl).max() <= 3e-14 * sf2, (tab, np.abs(K - Kl).max() / sf2)
+        # install (K + 1e-8 I factorised on the device) with either covariance transform; the posterior at
+        # X* = X + 1e-3 (r ≥ 4e12 from every training point) is the prior: K* exactly 0
+        orc = ogp.ExactGP(X, y, ls, sf2)
+        mu_o, var_o = orc.predict(X + 1e-3)
+        for tab in (0, 1):
+            ctx.debug_set("cov_table", tab)
+            ctx.set_gp_state(0, DeviceGPState(X, y, ls, sf2))
+            Kt = ctx.kernel_block(0, X + 1e-3).cpu().numpy()
+            assert np.isfinite(Kt).all()
+            assert np.abs(Kt - ogp.matern52_K(X, X + 1e-3, ls, sf2)).max() <= 3e-14 * sf2
+            mu, var = (t.cpu().numpy()[0] for t in ctx.posterior(X + 1e-3, n_obj=1))
+            np.testing.assert_allclose(mu, mu_o[:, 0], rtol=0, atol=1e-9 * np.abs(y).max())
+            np.testing.assert_allclose(var, var_o[:, 0], rtol=1e-12, atol=1e-9 * sf2)
+    finally:
+        ctx.debug_set("cov_table", 0)
+        ctx.close()
+
+
+@pytest.mark.parametrize("kernel", ["matern52", "rbf"])
+def test_kernel_transform_over_lengthscale_sweep(kernel):
+    """K(X*, X) from the posterior transform against the libm restatement for ℓ from 1 down to 1e-100: past the
+    exp underflow point every entry is exactly the reference's 0 (before the clamp, ℓ ≤ 1e-13 gave inf/NaN)."""
+    from optimobo_amd.device import AcqContext
+    from optimobo_amd.gp import DeviceGPState
+    rng = np.random.default_rng(5)
+    X = rng.uniform(-1, 1, (40, 3))
+    Xc = rng.uniform(-1, 1, (300, 3))
+    ref = ogp.matern52_K if kernel == "matern52" else ogp.rbf_K
+    ctx = AcqContext(0)
+    try:
+        for ls0 in (1.0, 1e-2, 1e-6, 1e-10, 1e-13, 1e-16, 1e-40, 1e-100):
+            ls = np.array([ls0, 0.7, 1.3])
+            ctx.set_gp_state(0, DeviceGPState(X, rng.standard_normal(40), ls, 2.5, kernel=kernel))
+            Kt = ctx.kernel_block(0, Xc).cpu().numpy()
+            Kl = ref(X, Xc, ls, 2.5)
+            assert np.isfinite(Kt).all(), ls0
+            if ls0 <= 1e-10:
+                # r ≥ 1e6 for every pair: exactly the reference's 0 (the clamp's own range, r > 400, included)
+                assert (Kl == 0).all() and (Kt == 0).all(), ls0
+            else:
+                # r² = |a|² + |b|² − 2a·b on the MFMA (GPy's _unscaled_dist form): its rounding is ~eps·|a|², so
+                # the bound scales with the largest squared scaled coordinate norm (1e4 at ℓ_0 = 1e-2)
+                sq = max(((X / ls) ** 2).sum(1).max(), ((Xc / ls) ** 2).sum(1).max())
+                tol = 2.5 * max(3e-14, 16 * np.finfo(float).eps * sq)
+                assert np.abs(Kt - Kl).max() <= tol, (ls0, np.abs(Kt - Kl).max(), tol)
+    finally:
+        ctx.close()

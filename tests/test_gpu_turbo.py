@@ -91,6 +91,33 @@ def test_cholesky_info_matches_dpotrf(ctx, N, bad):
     assert info == info_ref == bad + 1
 
 
+def test_cholesky_randomized_stress(ctx):
+    """the fused steps hand W_{k+1} from the diagonal workgroup to the panel workgroups through
+    agent-scope relaxed fragment stores / loads and a flag ordered by a vmcnt wait and compiler fences, not by a
+    release / acquire pair (whose L2 write-back costs 3%).  A wrong order would show as a silently
+    wrong panel with info = 0: many sizes, repeated back to back in one process, each against LAPACK."""
+    rng = np.random.default_rng(2024)
+    sizes = list(rng.integers(1, 700, 40)) + [1500, 2048, 3000, 4097]
+    for rep, N in enumerate(sizes):
+        N = int(N)
+        A = spd(N, 1000 + rep)
+        At = dev(A)
+        assert ctx.cholesky(At, jitter=0.0) == 0, N
+        got = np.tril(At.cpu().numpy())
+        ref = np.linalg.cholesky(A)
+        np.testing.assert_allclose(got, ref, rtol=1e-10, atol=1e-12, err_msg=f"N={N} rep={rep}")
+    # the same matrix factored 25 times in a row: bitwise the same factor every time
+    A = spd(1300, 7)
+    first = None
+    for _ in range(25):
+        At = dev(A)
+        assert ctx.cholesky(At) == 0
+        got = At.cpu().numpy()
+        if first is None:
+            first = got
+        assert np.array_equal(got, first)
+
+
 def test_cholesky_step_wait_timeout_is_reported(ctx):
     """The fused Cholesky step (the next panel formed in the update launch) waits for the diagonal
     workgroup's flag with a bounded poll; omb_debug_set(SPIN_LIMIT, 0) makes the first unset poll run

@@ -12,7 +12,8 @@ using namespace omb;
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); exit(1);} } while (0)
 
-// VAR 0: compiler DPP moves + 2 fma; 1: inline-asm v_fmac_f64_dpp (non-volatile); 2: as 0 without the inverse
+// Round 4 measured VAR 0 (the compiler's v_mov_b64_dpp + 2 fma, kept in omb_linalg.hip) against an inline-asm
+// v_fmac_f64_dpp form (3,188 vs 3,784 cycles, profiles/r04_f_mb_chol16.txt); the asm form was removed from the library.
 template <int VAR>
 __global__ __launch_bounds__(64) void f16_kernel(const double* __restrict__ D, double* __restrict__ out, int reps,
                                                  unsigned long long* cyc) {
@@ -29,16 +30,7 @@ __global__ __launch_bounds__(64) void f16_kernel(const double* __restrict__ D, d
     for (int q = 0; q < 16; ++q) b[q] = a[q];
     __builtin_amdgcn_s_waitcnt(0);
     if (r == reps - 1) t0 = __builtin_readcyclecounter();
-    if constexpr (VAR == 1) {
-      bad += chol16_factor<true>(b, x);
-    } else if constexpr (VAR == 0) {
-      bad += chol16_factor<false>(b, x);
-    } else {
-      double y[16];
-#pragma unroll
-      for (int q = 0; q < 16; ++q) y[q] = 0.0;
-      bad += chol16_factor<false>(b, y);      // same work (x is updated too; kept for the count)
-    }
+    bad += chol16_factor(b, x);
 #pragma unroll
     for (int q = 0; q < 16; ++q) asm volatile("" : "+v"(b[q]), "+v"(x[q]));
     if (r == reps - 1) t1 = __builtin_readcyclecounter();
@@ -65,12 +57,10 @@ int main() {
   CK(hipMalloc(&out, 2 * n * n * 8));
   CK(hipMalloc(&cyc, 16));
   CK(hipMemcpy(D, h.data(), n * n * 8, hipMemcpyHostToDevice));
-  const char* names[3] = {"DPP mov + 2 fma (compiler)", "v_fmac_f64_dpp (inline asm)", "mov form again"};
+  const char* names[1] = {"chol16_factor (DPP mov + 2 fma)"};
   for (int rep = 0; rep < 2; ++rep)
-    for (int v = 0; v < 3; ++v) {
-      if (v == 0) hipLaunchKernelGGL(f16_kernel<0>, dim3(1), dim3(64), 0, 0, D, out, 20, cyc);
-      if (v == 1) hipLaunchKernelGGL(f16_kernel<1>, dim3(1), dim3(64), 0, 0, D, out, 20, cyc);
-      if (v == 2) hipLaunchKernelGGL(f16_kernel<2>, dim3(1), dim3(64), 0, 0, D, out, 20, cyc);
+    for (int v = 0; v < 1; ++v) {
+      hipLaunchKernelGGL(f16_kernel<0>, dim3(1), dim3(64), 0, 0, D, out, 20, cyc);
       CK(hipDeviceSynchronize());
       unsigned long long c[2];
       CK(hipMemcpy(c, cyc, 16, hipMemcpyDeviceToHost));

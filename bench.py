@@ -422,6 +422,8 @@ def main():
     ap.add_argument("--one-launch", type=int, default=None, choices=[0, 1],
                     help="omb_debug_set(FUSED_CHAIN): 0 EHVI-2D and the arg-max as separate launches, 1 as one "
                          "(default: the library's, 0 — the one launch measured slower)")
+    ap.add_argument("--argmax-passes", type=int, default=None, choices=[1, 2],
+                    help="omb_debug_set(ARGMAX_PASSES): the arg-max as one launch or two (default: the library's, 1)")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks and the process group only, print what torch.distributed saw")
     ap.add_argument("--cache-seed", type=int, default=1,
@@ -483,6 +485,8 @@ def main():
     ctx = AcqContext(local_rank)
     if args.one_launch is not None:
         ctx.debug_set("fused_chain", args.one_launch)
+    if args.argmax_passes is not None:
+        ctx.debug_set("argmax_passes", args.argmax_passes)
     if acq_kind == "ei_tch":
         # ParEGO-style mono surrogate: Tchebicheff-aggregate the objectives (parego.py:212-219)
         tch = sc.Tchebicheff(Y.min(axis=0), Y.max(axis=0))

@@ -21,6 +21,7 @@ EA_EI, EA_PARETO_EI = 0, 1
 DEBUG_SPIN_LIMIT = 1
 DEBUG_COV_TABLE = 2
 DEBUG_FUSED_CHAIN = 3
+DEBUG_ARGMAX_PASSES = 4
 MAX_OBJ, MAX_DIM, MAX_TRAIN, MAX_TRAIN_DENSE = 8, 64, 1024, 16384
 
 _p = ctypes.c_void_p

@@ -88,6 +88,7 @@ struct omb_ctx {
   int spin_limit = kDefaultSpinLimit;
   bool cov_table = false;   // OMB_DEBUG_COV_TABLE
   bool fused_chain = false;  // OMB_DEBUG_FUSED_CHAIN: EHVI-2D and the arg-max in one launch (off: measured slower)
+  bool argmax_one_pass = true;  // OMB_DEBUG_ARGMAX_PASSES: 1 (one launch) or 2
 };
 
 namespace {
@@ -422,7 +423,8 @@ int run_chain(omb_ctx* ctx, const double* Xc, bool sobol, int64_t start, int64_t
     }
   }
   if (e == hipSuccess) e = mark(3);
-  if (e == hipSuccess && result_dev && !acq_argmax) e = launch_argmax(ctx->stream, vals, N, offset, ctx->partials, result_dev);
+  if (e == hipSuccess && result_dev && !acq_argmax)
+    e = launch_argmax(ctx->stream, vals, N, offset, ctx->partials, result_dev, ctx->argmax_one_pass);
   if (e == hipSuccess) e = mark(4);
   if (e != hipSuccess) return hip_fail(ctx, e, "fused chain");
   return OMB_OK;
@@ -518,6 +520,11 @@ int omb_debug_set(omb_ctx* ctx, int what, int64_t value) {
   }
   if (what == OMB_DEBUG_FUSED_CHAIN) {
     ctx->fused_chain = value != 0;
+    return OMB_OK;
+  }
+  if (what == OMB_DEBUG_ARGMAX_PASSES) {
+    if (value != 1 && value != 2) return fail(ctx, OMB_EINVAL, "arg-max passes %lld (1 or 2)", (long long)value);
+    ctx->argmax_one_pass = value == 1;
     return OMB_OK;
   }
   if (what == OMB_DEBUG_COV_TABLE) {
@@ -718,7 +725,7 @@ int omb_argmax_dev(omb_ctx* ctx, const double* vals_dev, int64_t N, int64_t offs
   int rc = enter(ctx);
   if (rc) return rc;
   if (!result_dev || N < 0 || (N > 0 && !vals_dev)) return fail(ctx, OMB_EINVAL, "bad arg-max arguments");
-  hipError_t e = launch_argmax(ctx->stream, vals_dev, N, offset, ctx->partials, result_dev);
+  hipError_t e = launch_argmax(ctx->stream, vals_dev, N, offset, ctx->partials, result_dev, ctx->argmax_one_pass);
   if (e != hipSuccess) return hip_fail(ctx, e, "argmax");
   return OMB_OK;
 }

@@ -103,10 +103,11 @@ hipError_t launch_expdec(hipStream_t stream, const ScalParams& sp, const double*
 hipError_t launch_ei(hipStream_t stream, int kind, int k, const double* mu, const double* var, int64_t ld, int64_t N,
                      double best, double var_eps, double pof_eps, double* out);
 
-// Two-pass deterministic arg-max; `partials` must hold kArgmaxMaxBlocks (val, idx) pairs.
+// Deterministic arg-max; `partials` must hold kArgmaxMaxBlocks (val, idx) pairs followed by one zeroed ticket word
+// (one_pass: both passes in one launch, the last workgroup to arrive reducing; it leaves the word zeroed again).
 constexpr int kArgmaxMaxBlocks = 1024;
 hipError_t launch_argmax(hipStream_t stream, const double* vals, int64_t N, int64_t offset, double* partials,
-                         double* result);
+                         double* result, bool one_pass = true);
 
 // Scrambled Sobol' generation (omb_sobol.hip).  The packed state holds the direction
 // numbers, shift and box of one engine; sobol_pack_state fills a host buffer of
@@ -150,7 +151,9 @@ constexpr int kCholWsDoubles = 64 * 64;
 constexpr int kCholSpinFault = -2147483647;
 // kCholBlocked (round 4): the diagonal blocks by tiles of 16 (chol64_blocked); kCholBlockedAcqRel: the same with
 // the fused step's flag as an agent-scope release / acquire (tools/ablate/ablate_chol)
-enum { kCholTwoLaunch = 0, kCholFused = 1, kCholBlocked = 2, kCholBlockedAcqRel = 3 };
+// kCholPersistent (round 4): the whole factorisation in one launch (chol_persist_kernel; kCholBlocked when A is too
+// large for its 32-bit buffer offsets)
+enum { kCholTwoLaunch = 0, kCholFused = 1, kCholBlocked = 2, kCholBlockedAcqRel = 3, kCholPersistent = 4 };
 int64_t chol_ws_doubles(int64_t N);
 hipError_t launch_cholesky(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws,
                            int spin_limit = kDefaultSpinLimit);

@@ -542,6 +542,8 @@ __device__ __forceinline__ void load_row16(const double* __restrict__ p, bool ok
 // (lower triangle of rows < nb), with W = L⁻¹'s MFMA fragments to Wf (the layout of chol64_inverse).  OUTER: A22_00
 // minus the product of the panel rows A[r0 + ·][c0 .. c0+63].  Ds, Wl, fl: LDS (fl zeroed by the caller and a
 // barrier passed).  The caller reads fl[20] (block-relative 1-based first bad column, 0 = none) after a barrier.
+__device__ __forceinline__ void chol64_blocked_core(double* __restrict__ A, int64_t lda, int64_t r0, int nb,
+                                                    double* __restrict__ Wf, double* Ds, double* Wl, int* fl);
 template <bool OUTER>
 __device__ __forceinline__ void chol64_blocked(double* __restrict__ A, int64_t lda, int64_t r0, int nb, int64_t c0,
                                                double* __restrict__ Wf, double* Ds, double* Wl, int* fl) {
@@ -600,6 +602,16 @@ __device__ __forceinline__ void chol64_blocked(double* __restrict__ A, int64_t l
     }
   }
   OMB_CHOL_BTRACE(w, 1, lane == 0);
+  chol64_blocked_core(A, lda, r0, nb, Wf, Ds, Wl, fl);
+}
+
+// chol64_blocked after its D tiles: each wave has written its own tiles (w, j ≤ w) of D to Ds (no barrier needed:
+// a wave reads another wave's rows only behind that wave's LDS flag).  Also the diagonal step of the persistent
+// factorisation (chol_persist_kernel), which forms D from the previous step's panel tile held in LDS.
+__device__ __forceinline__ void chol64_blocked_core(double* __restrict__ A, int64_t lda, int64_t r0, int nb,
+                                                    double* __restrict__ Wf, double* Ds, double* Wl, int* fl) {
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // ---- P_b, U_b for b < w
   for (int b = 0; b < w; ++b) {
     double dop[4];                                                    // D_wb[c][4s + g], read before the wait
@@ -1112,6 +1124,284 @@ __global__ __launch_bounds__(256, 3) void chol_update_kernel(double* __restrict_
   __syncthreads();
   if (tid == 0 && bad_lds[0]) atomicCAS(info, 0, (int)(r0 + bad_lds[0]));
   if constexpr (FUSE) chol_publish_w(flags + step, tid, acq_rel);
+}
+
+// ----------------------------------------------------------------------------- Cholesky, one persistent launch
+// Round 4.  The per-step launches above pay a kernel boundary on the step's serial chain (≈ 5.7 µs of the ≈ 29-µs
+// step at N = 3000: the end of the update launch to the next diagonal workgroup's start, profiles/r04_h_ablate_chol.txt)
+// and the diagonal workgroup's first loads compete with the whole grid's.  Here the factorisation is ONE launch of one
+// workgroup per CU:
+//   * workgroup 0 walks the diagonal: at step k it forms D_kk = A_kk − L_{k,k−1} L_{k,k−1}ᵀ from the panel tile it
+//     made itself one step earlier (kept in LDS), factors it (chol64_blocked_core: L_kk, W_k = L_kk⁻¹ fragments),
+//     publishes W_k, then forms the next panel tile L_{k+1,k} = A_{k+1,k} W_kᵀ into LDS (and A) — the chain of a step
+//     is the 64-column factor plus one 64×64×64 product, no launch and no hand-off to another workgroup;
+//   * the other workgroups draw tasks from one ticket counter, in an order in which every task depends only on
+//     tasks drawn before it (so the grid needs no co-residency and cannot deadlock):
+//       step k:  P(i, k), i ≥ k + 2   L_ik = A_ik W_kᵀ                      (W_k flag, A_ik updated through step k−1)
+//                U(i, j, k), k+1 ≤ j ≤ i, (i, j) ≠ (k+1, k+1), by columns j  A_ij −= L_ik L_jkᵀ  (the two panel flags,
+//                                                                         A_ij updated through step k−1)
+//     U(k+1, k+1, k) is the diagonal workgroup's own D product.
+// Cross-workgroup data (panel tiles, A tiles between updates, W fragments) is written with sc1 (write-through) stores
+// after which every storing wave waits vmcnt(0), the workgroup passes a barrier and one lane stores the flag or tile
+// counter (relaxed, agent scope); readers poll relaxed, pass a barrier and read those bytes with sc1 loads only
+// (MI355X_MICROARCH.md § inter-workgroup visibility, the sc1 valid form; one workgroup per CU as measured there:
+// 227 VGPRs + 32 AGPRs, and static + dynamic LDS above half a CU's).  Tile counters cnt(i, j) = number of updates applied: each update waits for
+// cnt = k, so the updates of one tile, possibly on different XCDs, never overlap.  Every wait is bounded (spin_limit
+// polls), after which an abort word stops all waits and info = kCholSpinFault.
+// dynamic LDS added at the launch (never read) so that static + dynamic > 80 KB: one workgroup per CU
+constexpr int kPersistLdsPad = 8 * 1024;
+
+// sc1 loads through a buffer descriptor over A (loads past num_records return 0: rows ≥ N read as zeros)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t chol_rsrc(const double* base, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), (short)0,
+                                           (int)(bytes < 0x7fffffff ? bytes : 0x7fffffff), 0x00020000);
+}
+typedef int i4v __attribute__((ext_vector_type(4)));
+typedef double d2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ d2v ld2_sc1(__amdgpu_buffer_rsrc_t r, int64_t elem) {
+  return __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(elem * 8), 0, 16));
+}
+// v[4q + u] = A[row][c0 + 16q + u] (the k permutation of load_row16; elem = row·lda + c0, c0 ≡ 4g)
+__device__ __forceinline__ void load_row16_sc1(__amdgpu_buffer_rsrc_t r, int64_t elem, double (&v)[16]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const d2v lo = ld2_sc1(r, elem + 16 * q), hi = ld2_sc1(r, elem + 16 * q + 2);
+    v[4 * q] = lo.x;
+    v[4 * q + 1] = lo.y;
+    v[4 * q + 2] = hi.x;
+    v[4 * q + 3] = hi.y;
+  }
+}
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+struct CholSync {
+  int* wflag;   // [t]      W_k published
+  int* pflag;   // [t·t]    panel tile (i, k) published
+  int* cnt;     // [t·t]    updates applied to tile (i, j)
+  int* ticket;  // task counter of the worker workgroups
+  int* abort;   // set by the first wait that runs out
+};
+
+// thread 0: wait until *p ≥ v (relaxed polls); false after an abort or spin_limit polls (then abort = the word's
+// offset in the sync block + 1, for tools/ablate, and info = kCholSpinFault)
+__device__ __forceinline__ bool chol_poll_ge(const int* p, int v, const CholSync& s, int spin_limit, int* info) {
+  int polls = 0;
+  while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < v) {
+    if (((polls & 63) == 0 && __hip_atomic_load(s.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) ||
+        ++polls > spin_limit) {
+      atomicCAS(s.abort, 0, (int)(p - s.wflag) + 1);
+      atomicCAS(info, 0, kCholSpinFault);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return true;
+}
+
+// every storing wave drains its sc1 stores, the workgroup meets, thread 0 raises the flag
+__device__ __forceinline__ void chol_signal(int* flag, int value) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Panel tile L_ik = A_ik W_kᵀ (chol_panel_kernel's product, 4 waves × 16 rows): W from the fragments Wk (sc1), the
+// result to A (sc1) and, for the diagonal workgroup, into Lp (LDS, pitch kDP).
+__device__ __forceinline__ void chol_persist_panel(__amdgpu_buffer_rsrc_t ra, double* __restrict__ A, int64_t N,
+                                                   int64_t lda, int i, int k, const double* __restrict__ Wk, double* Lp) {
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t row = (int64_t)i * kNB + 16 * w + c;
+  double x[16];
+  load_row16_sc1(ra, row * lda + (int64_t)k * kNB + 4 * g, x);
+  if (row >= N) {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) x[s] = 0.0;
+  }
+#pragma unroll
+  for (int jb = 0; jb < 4; ++jb) {
+    const double* wf = Wk + jb * 16 * 64 + lane;
+    d4 pa = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+      if (s < 4 * (jb + 1)) pa = __builtin_amdgcn_mfma_f64_16x16x4f64(x[s], ld_sc1(wf + s * 64), pa, 0, 0, 0);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t orow = (int64_t)i * kNB + 16 * w + 4 * e + g;
+      if (orow < N) st_sc1(A + orow * lda + (int64_t)k * kNB + 16 * jb + c, pa[e]);
+      if (Lp) Lp[(16 * w + 4 * e + g) * kDP + 16 * jb + c] = pa[e];
+    }
+  }
+}
+
+// U(i, j, k): A_ij −= L_ik L_jkᵀ, wave (wm, wn) the 32 × 32 quadrant (the upper-right one skipped on a diagonal tile,
+// whose strict upper triangle is never written)
+__device__ __forceinline__ void chol_persist_update(__amdgpu_buffer_rsrc_t ra, double* __restrict__ A, int64_t N,
+                                                    int64_t lda, int i, int j, int k) {
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  if (i == j && wm < wn) return;
+  const int64_t ri = (int64_t)i * kNB + 32 * wm, rj = (int64_t)j * kNB + 32 * wn, ck = (int64_t)k * kNB + 4 * g;
+  double av[2][2][4];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t row = ri + 16 * rb + 4 * e + g, col = rj + 16 * cb + c;
+        av[rb][cb][e] = (row < N && col < N) ? ld_sc1(A + row * lda + col) : 0.0;
+      }
+  double a0[16], a1[16], b0[16], b1[16];
+  load_row16_sc1(ra, (ri + c) * lda + ck, a0);
+  load_row16_sc1(ra, (ri + 16 + c) * lda + ck, a1);
+  load_row16_sc1(ra, (rj + c) * lda + ck, b0);
+  load_row16_sc1(ra, (rj + 16 + c) * lda + ck, b1);
+  d4 acc[2][2];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) acc[rb][cb] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[s], b0[s], acc[0][0], 0, 0, 0);
+    acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[s], b1[s], acc[0][1], 0, 0, 0);
+    acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[s], b0[s], acc[1][0], 0, 0, 0);
+    acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[s], b1[s], acc[1][1], 0, 0, 0);
+  }
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t row = ri + 16 * rb + 4 * e + g, col = rj + 16 * cb + c;
+        if (row < N && col < N && (i != j || col <= row)) st_sc1(A + row * lda + col, av[rb][cb][e] - acc[rb][cb][e]);
+      }
+}
+
+// bulk tasks of step k (see above): P(i, k) for i = k+2 .. t−1, then the update tiles by columns
+__device__ __forceinline__ int chol_persist_step_tasks(int t, int k) {
+  const int m = t - k - 1;
+  const int np = t - k - 2 > 0 ? t - k - 2 : 0;
+  const int nu = m > 1 ? m * (m + 1) / 2 - 1 : 0;
+  return np + nu;
+}
+
+__global__ __launch_bounds__(256, 1) void chol_persist_kernel(double* __restrict__ A, int64_t N, int64_t lda, int t,
+                                                              int total, double* __restrict__ Wf, CholSync sync,
+                                                              int* __restrict__ info, int spin_limit) {
+  __shared__ __attribute__((aligned(16))) double Ds[kNB * kDP];
+  __shared__ __attribute__((aligned(16))) double Lp[kNB * kDP];
+  __shared__ __attribute__((aligned(16))) double Wl[4 * kWlP];
+  __shared__ int fl[kBlkFlags];
+  __shared__ int s_task[2];
+  const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const __amdgpu_buffer_rsrc_t ra = chol_rsrc(A, ((N - 1) * lda + N) * 8);
+  if (blockIdx.x == 0) {
+    // ---------------- the diagonal walk
+    double av[16];                                              // A_kk[16w + 4e + g][16j + c], index 4j + e
+    auto load_av = [&](int k) {
+      const int64_t r0 = (int64_t)k * kNB;
+      const int nb = (int)(N - r0 < kNB ? N - r0 : kNB);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int row = 16 * w + 4 * e + g, col = 16 * j + c;
+          av[4 * j + e] = (j <= w && row < nb && col <= row) ? ld_sc1(A + (r0 + row) * lda + r0 + col)
+                                                             : (row == col ? 1.0 : 0.0);
+        }
+    };
+    load_av(0);
+    for (int k = 0; k < t; ++k) {
+      const int64_t r0 = (int64_t)k * kNB;
+      const int nb = (int)(N - r0 < kNB ? N - r0 : kNB);
+      if (tid < kBlkFlags) fl[tid] = 0;
+      // D tiles (w, j ≤ w) = A_kk − L_{k,k−1} L_{k,k−1}ᵀ (Lp: written before the previous step's last barrier)
+      {
+        double xa[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) xa[4 * q + u] = k > 0 ? Lp[(16 * w + c) * kDP + 16 * q + 4 * g + u] : 0.0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (j <= w) {
+            d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+            if (k > 0) {
+#pragma unroll
+              for (int s = 0; s < 16; ++s) {
+                const double xb = Lp[(16 * j + c) * kDP + 16 * (s >> 2) + 4 * g + (s & 3)];
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[s], xb, acc, 0, 0, 0);
+              }
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) Ds[(16 * w + 4 * e + g) * kDP + 16 * j + c] = av[4 * j + e] - acc[e];
+          }
+        }
+      }
+      __syncthreads();                                          // fl zeroed; every wave past its Lp reads
+      chol64_blocked_core(A, lda, r0, nb, Wf + (int64_t)k * kCholWsDoubles, Ds, Wl, fl);
+      chol_signal(sync.wflag + k, 1);                           // W_k's fragments (wf_store: sc1) drained
+      if (tid == 0 && (fl[20] || fl[21])) atomicCAS(info, 0, fl[21] ? kCholSpinFault : (int)(r0 + fl[20]));
+      if (k + 1 < t) {
+        // the next panel tile and the next diagonal tile: both updated through step k − 1 by the workers
+        if (tid == 0) {
+          const int i1 = (k + 1) * t;
+          if (chol_poll_ge(sync.cnt + i1 + k, k, sync, spin_limit, info))
+            chol_poll_ge(sync.cnt + i1 + k + 1, k, sync, spin_limit, info);
+        }
+        __syncthreads();
+        load_av(k + 1);
+        chol_persist_panel(ra, A, N, lda, k + 1, k, Wf + (int64_t)k * kCholWsDoubles, Lp);
+        chol_signal(sync.pflag + (k + 1) * t + k, 1);
+      }
+    }
+    return;
+  }
+  // ---------------- workers
+  for (;;) {
+    if (tid == 0) s_task[0] = __hip_atomic_fetch_add(sync.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    int q = s_task[0];
+    if (q >= total) return;
+    int k = 0;
+    for (; k < t; ++k) {
+      const int nk = chol_persist_step_tasks(t, k);
+      if (q < nk) break;
+      q -= nk;
+    }
+    const int np = t - k - 2 > 0 ? t - k - 2 : 0;
+    if (q < np) {
+      const int i = k + 2 + q;
+      if (tid == 0 && chol_poll_ge(sync.wflag + k, 1, sync, spin_limit, info))
+        chol_poll_ge(sync.cnt + i * t + k, k, sync, spin_limit, info);
+      __syncthreads();
+      chol_persist_panel(ra, A, N, lda, i, k, Wf + (int64_t)k * kCholWsDoubles, nullptr);
+      chol_signal(sync.pflag + i * t + k, 1);
+    } else {
+      int u = q - np + 1, j = k + 1;                            // + 1: (k+1, k+1) is the diagonal workgroup's
+      while (u >= t - j) {
+        u -= t - j;
+        ++j;
+      }
+      const int i = j + u;
+      if (tid == 0 && chol_poll_ge(sync.pflag + i * t + k, 1, sync, spin_limit, info) &&
+          chol_poll_ge(sync.pflag + j * t + k, 1, sync, spin_limit, info))
+        chol_poll_ge(sync.cnt + i * t + j, k, sync, spin_limit, info);
+      __syncthreads();
+      chol_persist_update(ra, A, N, lda, i, j, k);
+      chol_signal(sync.cnt + i * t + j, k + 1);
+    }
+  }
 }
 
 // ----------------------------------------------------------------------------- triangular inverse
@@ -2052,7 +2342,10 @@ hipError_t launch_add_diag(hipStream_t stream, double* S, int64_t N, int64_t lds
 
 int64_t chol_ws_doubles(int64_t N) {
   const int64_t steps = (N + kNB - 1) / kNB;
-  return (int64_t)kCholWsDoubles + (steps + 1) / 2 + 2;     // W fragments | one int flag per step
+  const int64_t launches = (int64_t)kCholWsDoubles + (steps + 1) / 2 + 2;     // W fragments | one int flag per step
+  // chol_persist_kernel: W fragments of every step | wflag[t] | pflag[t·t] | cnt[t·t] | ticket | abort
+  const int64_t persist = steps * kCholWsDoubles + (steps + 2 * steps * steps + 2 + 1) / 2 + 2;
+  return launches > persist ? launches : persist;
 }
 
 static hipError_t chol_panel(hipStream_t stream, double* A, int64_t N, int64_t lda, int k, const double* ws,
@@ -2097,9 +2390,51 @@ static hipError_t launch_cholesky_blocked(hipStream_t stream, double* A, int64_t
   return e;
 }
 
+// Round 4: one persistent launch (chol_persist_kernel), one workgroup per CU.
+static int device_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cus[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+
+static bool chol_persist_fits(int64_t N, int64_t lda) {
+  return ((N + kNB) * lda + kNB) * 8 < 0x7fffffff;   // 32-bit buffer offsets (rows past N included)
+}
+
+static hipError_t launch_cholesky_persist(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws,
+                                          int spin_limit) {
+  const int t = (int)((N + kNB - 1) / kNB);
+  int total = 0;
+  for (int k = 0; k < t; ++k) {
+    const int m = t - k - 1;
+    total += (t - k - 2 > 0 ? t - k - 2 : 0) + (m > 1 ? m * (m + 1) / 2 - 1 : 0);
+  }
+  double* Wf = ws;
+  int* ints = reinterpret_cast<int*>(ws + (int64_t)t * kCholWsDoubles);
+  const size_t nints = (size_t)t + 2 * (size_t)t * t + 2;
+  CholSync sync{ints, ints + t, ints + t + t * t, ints + t + 2 * t * t, ints + t + 2 * t * t + 1};
+  hipError_t e = hipMemsetAsync(ints, 0, nints * sizeof(int), stream);
+  if (e == hipSuccess) e = hipMemsetAsync(info, 0, sizeof(int), stream);
+  if (e != hipSuccess) return e;
+  const int grid = 1 + (total < device_cus() - 1 ? total : device_cus() - 1);
+  hipLaunchKernelGGL(chol_persist_kernel, dim3((unsigned)grid), dim3(256), kPersistLdsPad, stream, A, N, lda, t, total, Wf,
+                     sync, info, spin_limit);
+  return hipGetLastError();
+}
+
 hipError_t launch_cholesky_mode(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws, int mode,
                                 int spin_limit) {
   if (N <= 0) return hipSuccess;
+  if (mode == kCholPersistent) {
+    if (chol_persist_fits(N, lda)) return launch_cholesky_persist(stream, A, N, lda, info, ws, spin_limit);
+    mode = kCholBlocked;
+  }
   const int steps = (int)((N + kNB - 1) / kNB);
   const bool vec = (lda % 2 == 0) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
   const bool fuse = mode == kCholFused;

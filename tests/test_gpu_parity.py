@@ -284,6 +284,29 @@ def test_argmax_rules(ctx):
     assert r[0] == 5.0 and r[1] == 4.0
 
 
+def test_argmax_one_launch_equals_two_launches(ctx):
+    """argmax_onepass (the last workgroup at the ticket reduces; the default) against argmax_pass1/2: the same pair,
+    call after call (the ticket is left at zero), at grid sizes 1 .. kArgmaxMaxBlocks and past it (grid stride)."""
+    rng = np.random.default_rng(10)
+    try:
+        for N in [1, 2, 255, 256, 257, 65536, 256 * 1024, 256 * 1024 + 1, 3 << 20]:
+            v = rng.standard_normal(N)
+            v[rng.integers(0, N, max(1, N // 1000))] = np.nan
+            if N > 3:
+                v[N - 1] = v[1] = np.nanmax(v) + 2.0               # tie across workgroups → lowest index
+            pairs = []
+            for passes in (1, 2, 1, 1):
+                ctx.debug_set("argmax_passes", passes)
+                pairs.append(ctx.argmax_dev(dev(v), offset=5).cpu().numpy())
+            ov, oi = oacq.argmax(v, offset=5)
+            for p in pairs:
+                assert (p[0], int(p[1])) == (ov, oi), (N, p, ov, oi)
+        ctx.debug_set("argmax_passes", 1)
+        assert ctx.argmax(dev(np.full(70000, np.nan))) == (-np.inf, -1)
+    finally:
+        ctx.debug_set("argmax_passes", 1)
+
+
 @pytest.mark.parametrize("cache_seed", [0, 1])
 def test_chain_posterior_ehvi_argmax(ctx, cache_seed):
     """End to end at BASELINE config 2 (n=128, d=6, N=2^16): posterior → reference EHVI → arg-max vs

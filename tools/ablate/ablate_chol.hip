@@ -260,8 +260,8 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     // the launch schedules interleaved: kCholTwoLaunch (round 2), kCholFused (round 3), kCholBlocked (round 4),
-    // kCholBlockedAcqRel (round 4 with the agent-scope release / acquire flag)
-    const int modes[5] = {kCholTwoLaunch, kCholFused, kCholBlocked, kCholBlockedAcqRel, kCholBlocked};
+    // kCholBlockedAcqRel (round 4 with the agent-scope release / acquire flag), kCholPersistent (round 4, one launch)
+    const int modes[5] = {kCholTwoLaunch, kCholFused, kCholBlocked, kCholBlockedAcqRel, kCholPersistent};
     float msum[5] = {0, 0, 0, 0, 0}, mbest[5] = {1e30f, 1e30f, 1e30f, 1e30f, 1e30f};
     const int reps = 10;
     std::vector<double> Lref(N * N), Lm(N * N);
@@ -291,7 +291,7 @@ int main(int argc, char** argv) {
       }
     }
     printf("N=%lld  two-launch %.3f (best %.3f) | fused %.3f (%.3f) | blocked %.3f (%.3f) | blocked acq/rel %.3f (%.3f) | "
-           "blocked again %.3f (%.3f) ms; info %d %d %d %d %d; max |L - L_twolaunch|/sqrt(A_ii) %.1e %.1e %.1e %.1e\n",
+           "persistent %.3f (%.3f) ms; info %d %d %d %d %d; max |L - L_twolaunch|/sqrt(A_ii) %.1e %.1e %.1e %.1e\n",
            (long long)N, msum[0] / reps, mbest[0], msum[1] / reps, mbest[1], msum[2] / reps, mbest[2], msum[3] / reps,
            mbest[3], msum[4] / reps, mbest[4], minfo[0], minfo[1], minfo[2], minfo[3], minfo[4], mdiff[1], mdiff[2],
            mdiff[3], mdiff[4]);

@@ -423,7 +423,7 @@ def main():
                     help="omb_debug_set(FUSED_CHAIN): 0 EHVI-2D and the arg-max as separate launches, 1 as one "
                          "(default: the library's, 0 — the one launch measured slower)")
     ap.add_argument("--argmax-passes", type=int, default=None, choices=[1, 2],
-                    help="omb_debug_set(ARGMAX_PASSES): the arg-max as one launch or two (default: the library's, 1)")
+                    help="omb_debug_set(ARGMAX_PASSES): the arg-max as one launch or two (default: the library's, 2)")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks and the process group only, print what torch.distributed saw")
     ap.add_argument("--cache-seed", type=int, default=1,

@@ -95,8 +95,9 @@ const char* omb_last_error(const omb_ctx* ctx);
  * omb_debug_set(ctx, OMB_DEBUG_FUSED_CHAIN, 1) makes omb_eval_argmax[_sobol] with an EHVI-2D plan run the
  * acquisition and the arg-max in one launch instead of two (bit-identical pair; default 0: the one launch measured
  * 1.9 % / 0.6 % slower on configs 2 / 3, gpurun_out/r04_j).
- * omb_debug_set(ctx, OMB_DEBUG_ARGMAX_PASSES, 2) runs the arg-max as two launches (per-workgroup pairs, then one
- * workgroup reducing them) instead of one (the last workgroup to finish reduces; default 1; bit-identical pair). */
+ * omb_debug_set(ctx, OMB_DEBUG_ARGMAX_PASSES, 1) runs the arg-max as one launch (the last workgroup to finish
+ * reduces the per-workgroup pairs) instead of two (default 2: config 2 measured 719.6 vs 719.5 M candidates/s,
+ * gpurun_out/r04_l; bit-identical pair). */
 enum { OMB_DEBUG_SPIN_LIMIT = 1, OMB_DEBUG_COV_TABLE = 2, OMB_DEBUG_FUSED_CHAIN = 3, OMB_DEBUG_ARGMAX_PASSES = 4 };
 int omb_debug_set(omb_ctx* ctx, int what, int64_t value);
 

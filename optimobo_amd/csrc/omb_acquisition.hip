@@ -106,7 +106,7 @@ __global__ __launch_bounds__(kAcqThreads) void ehvi2d_argmax_kernel(const double
     is_last = prev == gridDim.x - 1;
   }
   __syncthreads();
-  if (!is_last) return;
+  if (!__builtin_amdgcn_readfirstlane(is_last)) return;   // uniform: the reduction below has barriers
   double v = -__builtin_inf();
   long long i = -1;
   for (int b = threadIdx.x; b < (int)gridDim.x; b += blockDim.x) {

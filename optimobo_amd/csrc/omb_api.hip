@@ -88,7 +88,7 @@ struct omb_ctx {
   int spin_limit = kDefaultSpinLimit;
   bool cov_table = false;   // OMB_DEBUG_COV_TABLE
   bool fused_chain = false;  // OMB_DEBUG_FUSED_CHAIN: EHVI-2D and the arg-max in one launch (off: measured slower)
-  bool argmax_one_pass = true;  // OMB_DEBUG_ARGMAX_PASSES: 1 (one launch) or 2
+  bool argmax_one_pass = false;  // OMB_DEBUG_ARGMAX_PASSES: 1 (one launch) or 2 (default: measured level)
 };
 
 namespace {

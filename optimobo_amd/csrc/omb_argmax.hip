@@ -103,7 +103,7 @@ __global__ __launch_bounds__(256) void argmax_onepass(const double* __restrict__
     is_last = prev == gridDim.x - 1;
   }
   __syncthreads();
-  if (!is_last) return;
+  if (!__builtin_amdgcn_readfirstlane(is_last)) return;   // uniform: the reduction below has barriers
   VI x{-__builtin_inf(), -1};
   for (int b = threadIdx.x; b < (int)gridDim.x; b += blockDim.x) {
     VI y{wf_load_f64(&partials[2 * b]), (int64_t)__builtin_bit_cast(long long, wf_load_f64(&partials[2 * b + 1]))};

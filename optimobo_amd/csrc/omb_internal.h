@@ -107,7 +107,7 @@ hipError_t launch_ei(hipStream_t stream, int kind, int k, const double* mu, cons
 // (one_pass: both passes in one launch, the last workgroup to arrive reducing; it leaves the word zeroed again).
 constexpr int kArgmaxMaxBlocks = 1024;
 hipError_t launch_argmax(hipStream_t stream, const double* vals, int64_t N, int64_t offset, double* partials,
-                         double* result, bool one_pass = true);
+                         double* result, bool one_pass = false);
 
 // Scrambled Sobol' generation (omb_sobol.hip).  The packed state holds the direction
 // numbers, shift and box of one engine; sobol_pack_state fills a host buffer of

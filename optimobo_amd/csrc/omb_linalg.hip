@@ -444,7 +444,7 @@ __device__ __forceinline__ void chol64_factor(double (&a)[16], int w, int r, int
 // 16-column factors and three 8-MFMA hand-offs.  Round 3 ran one wave per 16-column strip of all 64 rows
 // (≈ 470 cycles per column on the owner, ≈ 40k cycles for the block, profiles/r03_v38_chol_trace_pipelined_inverse.txt).
 // The waves synchronise through LDS flags (wready: W_bb in Wl; lready: L_ib in D); no barrier inside.
-// OUTER (the diagonal workgroup of chol_update_kernel): D = A22_00 − L21_0 L21_0ᵀ, wave w forming its own tiles
+// kCholDOuter (the diagonal workgroup of chol_update_kernel): D = A22_00 − L21_0 L21_0ᵀ, wave w forming its own tiles
 // (16 MFMAs each, K = 64, the k index permuted so a lane reads 4 contiguous doubles per 16-column group), so wave
 // 0 starts F_0 after one tile instead of after the whole 64×64 product.
 // per-wave phase timestamps of chol64_blocked, and step-level timestamps of chol_update_kernel (workgroup 0,
@@ -539,12 +539,13 @@ __device__ __forceinline__ void load_row16(const double* __restrict__ p, bool ok
 }
 
 // The diagonal block at rows / columns r0 .. r0+63 of A (nb ≤ 64 real rows; the rest identity), factored in place
-// (lower triangle of rows < nb), with W = L⁻¹'s MFMA fragments to Wf (the layout of chol64_inverse).  OUTER: A22_00
+// (lower triangle of rows < nb), with W = L⁻¹'s MFMA fragments to Wf (the layout of chol64_inverse).  kCholDOuter: A22_00
 // minus the product of the panel rows A[r0 + ·][c0 .. c0+63].  Ds, Wl, fl: LDS (fl zeroed by the caller and a
 // barrier passed).  The caller reads fl[20] (block-relative 1-based first bad column, 0 = none) after a barrier.
-__device__ __forceinline__ void chol64_blocked_core(double* __restrict__ A, int64_t lda, int64_t r0, int nb,
-                                                    double* __restrict__ Wf, double* Ds, double* Wl, int* fl);
-template <bool OUTER>
+// MODE kCholDLoad (step 0 / chol_diag_blk_kernel): D = A_kk; kCholDOuter (chol_update_kernel): D = A22_00 − L21_0
+// L21_0ᵀ from global; kCholDReady (chol_persist_kernel): each wave has already written its D tiles (w, j ≤ w) to Ds.
+enum { kCholDLoad = 0, kCholDOuter = 1, kCholDReady = 2 };
+template <int MODE>
 __device__ __forceinline__ void chol64_blocked(double* __restrict__ A, int64_t lda, int64_t r0, int nb, int64_t c0,
                                                double* __restrict__ Wf, double* Ds, double* Wl, int* fl) {
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
@@ -552,7 +553,7 @@ __device__ __forceinline__ void chol64_blocked(double* __restrict__ A, int64_t l
   OMB_CHOL_BTRACE(w, 0, lane == 0);
   // ---- D tiles (w, j), j ≤ w (accumulator layout: lane (g, c) → rows 4e + g, column c); tile j + 1's loads are
   // issued before tile j's product (one load latency per wave instead of one per tile)
-  {
+  if constexpr (MODE != kCholDReady) {
     auto load_a22 = [&](int j, double (&av)[4]) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -561,7 +562,7 @@ __device__ __forceinline__ void chol64_blocked(double* __restrict__ A, int64_t l
       }
     };
     double xa[16], xb[16], av[4];
-    if constexpr (OUTER) {
+    if constexpr (MODE == kCholDOuter) {
       load_row16(A + (r0 + 16 * w + c) * lda + c0 + 4 * g, 16 * w + c < nb, xa);
       if (w > 0) {
         load_row16(A + (r0 + c) * lda + c0 + 4 * g, c < nb, xb);
@@ -574,7 +575,7 @@ __device__ __forceinline__ void chol64_blocked(double* __restrict__ A, int64_t l
     for (int j = 0; j <= w; ++j) {
       double nxb[16], nav[4];
       if (j < w) {
-        if constexpr (OUTER) {
+        if constexpr (MODE == kCholDOuter) {
           if (j + 1 < w) {
             load_row16(A + (r0 + 16 * (j + 1) + c) * lda + c0 + 4 * g, 16 * (j + 1) + c < nb, nxb);
           } else {
@@ -585,7 +586,7 @@ __device__ __forceinline__ void chol64_blocked(double* __restrict__ A, int64_t l
         load_a22(j + 1, nav);
       }
       d4 acc = d4{0.0, 0.0, 0.0, 0.0};
-      if constexpr (OUTER) {
+      if constexpr (MODE == kCholDOuter) {
 #pragma unroll
         for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[s], xb[s], acc, 0, 0, 0);
       }
@@ -594,7 +595,7 @@ __device__ __forceinline__ void chol64_blocked(double* __restrict__ A, int64_t l
       if (j < w) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) av[e] = nav[e];
-        if constexpr (OUTER) {
+        if constexpr (MODE == kCholDOuter) {
 #pragma unroll
           for (int q = 0; q < 16; ++q) xb[q] = nxb[q];
         }
@@ -602,16 +603,6 @@ __device__ __forceinline__ void chol64_blocked(double* __restrict__ A, int64_t l
     }
   }
   OMB_CHOL_BTRACE(w, 1, lane == 0);
-  chol64_blocked_core(A, lda, r0, nb, Wf, Ds, Wl, fl);
-}
-
-// chol64_blocked after its D tiles: each wave has written its own tiles (w, j ≤ w) of D to Ds (no barrier needed:
-// a wave reads another wave's rows only behind that wave's LDS flag).  Also the diagonal step of the persistent
-// factorisation (chol_persist_kernel), which forms D from the previous step's panel tile held in LDS.
-__device__ __forceinline__ void chol64_blocked_core(double* __restrict__ A, int64_t lda, int64_t r0, int nb,
-                                                    double* __restrict__ Wf, double* Ds, double* Wl, int* fl) {
-  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // ---- P_b, U_b for b < w
   for (int b = 0; b < w; ++b) {
     double dop[4];                                                    // D_wb[c][4s + g], read before the wait
@@ -737,7 +728,7 @@ __global__ __launch_bounds__(256) void chol_diag_blk_kernel(double* __restrict__
   __shared__ int fl[kBlkFlags];
   if (threadIdx.x < kBlkFlags) fl[threadIdx.x] = 0;
   __syncthreads();
-  chol64_blocked<false>(A, lda, 0, (int)(N < kNB ? N : kNB), 0, ws, Ds, Wl, fl);
+  chol64_blocked<kCholDLoad>(A, lda, 0, (int)(N < kNB ? N : kNB), 0, ws, Ds, Wl, fl);
   __syncthreads();
   if (threadIdx.x == 0 && (fl[20] || fl[21])) atomicCAS(info, 0, fl[21] ? kCholSpinFault : fl[20]);
 }
@@ -894,8 +885,12 @@ __device__ __forceinline__ void chol_tile_of(int b, int t, int& mt, int& nt) {
 template <bool FUSE, bool BLK>
 __global__ __launch_bounds__(256, 3) void chol_update_kernel(double* __restrict__ A, int64_t N, int64_t lda, int step,
                                                           int t, double* __restrict__ ws, int* __restrict__ info,
-                                                          int* __restrict__ flags, int spin_limit, int acq_rel) {
+                                                          int* __restrict__ flags, int spin_limit, int acq_rel,
+                                                          int delay = 0) {
   OMB_CHOL_STRACE(step, blockIdx.x == 0 ? 0 : 3, threadIdx.x == 0 && blockIdx.x <= 1);
+  // delay (tools/ablate knob): every workgroup but the diagonal one sleeps delay × 32·64 cycles (≈ 0.85 µs) first,
+  // so the diagonal workgroup's loads meet an idle memory system
+  for (int i = 0; i < delay && blockIdx.x != 0; ++i) __builtin_amdgcn_s_sleep(32);
   if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
   int mt, nt;
   chol_tile_of((int)blockIdx.x, t, mt, nt);
@@ -924,7 +919,7 @@ __global__ __launch_bounds__(256, 3) void chol_update_kernel(double* __restrict_
       __shared__ int fl[kBlkFlags];
       if (tid < kBlkFlags) fl[tid] = 0;
       __syncthreads();
-      chol64_blocked<true>(A, lda, r0, (int)(M < kNB ? M : kNB), c0, ws, smem, Wl, fl);
+      chol64_blocked<kCholDOuter>(A, lda, r0, (int)(M < kNB ? M : kNB), c0, ws, smem, Wl, fl);
       __syncthreads();
       if (tid == 0 && (fl[20] || fl[21])) atomicCAS(info, 0, fl[21] ? kCholSpinFault : (int)(r0 + fl[20]));
       OMB_CHOL_STRACE(step, 1, tid == 0);
@@ -1132,7 +1127,7 @@ __global__ __launch_bounds__(256, 3) void chol_update_kernel(double* __restrict_
 // and the diagonal workgroup's first loads compete with the whole grid's.  Here the factorisation is ONE launch of one
 // workgroup per CU:
 //   * workgroup 0 walks the diagonal: at step k it forms D_kk = A_kk − L_{k,k−1} L_{k,k−1}ᵀ from the panel tile it
-//     made itself one step earlier (kept in LDS), factors it (chol64_blocked_core: L_kk, W_k = L_kk⁻¹ fragments),
+//     made itself one step earlier (kept in LDS), factors it (chol64_blocked<kCholDReady>: L_kk, W_k = L_kk⁻¹ fragments),
 //     publishes W_k, then forms the next panel tile L_{k+1,k} = A_{k+1,k} W_kᵀ into LDS (and A) — the chain of a step
 //     is the 64-column factor plus one 64×64×64 product, no launch and no hand-off to another workgroup;
 //   * the other workgroups draw tasks from one ticket counter, in an order in which every task depends only on
@@ -1150,6 +1145,15 @@ __global__ __launch_bounds__(256, 3) void chol_update_kernel(double* __restrict_
 // polls), after which an abort word stops all waits and info = kCholSpinFault.
 // dynamic LDS added at the launch (never read) so that static + dynamic > 80 KB: one workgroup per CU
 constexpr int kPersistLdsPad = 8 * 1024;
+
+// progress words for tools/ablate/chol_persist_check (host-mapped memory; empty here)
+#ifndef OMB_PDBG
+#define OMB_PDBG(word, value)
+#endif
+// timestamps (s_memrealtime) of the diagonal walk's phases and of every worker task (tools/ablate; empty here)
+#ifndef OMB_PTIME
+#define OMB_PTIME(slot)
+#endif
 
 // sc1 loads through a buffer descriptor over A (loads past num_records return 0: rows ≥ N read as zeros)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t chol_rsrc(const double* base, int64_t bytes) {
@@ -1187,13 +1191,19 @@ struct CholSync {
   int* abort;   // set by the first wait that runs out
 };
 
-// thread 0: wait until *p ≥ v (relaxed polls); false after an abort or spin_limit polls (then abort = the word's
-// offset in the sync block + 1, for tools/ablate, and info = kCholSpinFault)
+// Wave 0 waits (every lane of it, on wave-uniform values) until *p ≥ v: relaxed polls; false after an abort or
+// spin_limit polls (then abort = the word's offset in the sync block + 1, for tools/ablate, and info =
+// kCholSpinFault).  The waits, flags and the ticket are whole-wave operations on purpose: with them under
+// `threadIdx.x == 0` the compiler merged the flag store, the loop back edge and the next ticket into one divergent
+// region and let wave 0's other lanes run ahead into the next task's barrier with the old ticket (the launch hung
+// at N = 130, gpurun_out/r04_o; the ISA showed the barrier inside a loop entered without the ticket).
 __device__ __forceinline__ bool chol_poll_ge(const int* p, int v, const CholSync& s, int spin_limit, int* info) {
   int polls = 0;
-  while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < v) {
-    if (((polls & 63) == 0 && __hip_atomic_load(s.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) ||
-        ++polls > spin_limit) {
+  while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < v) {
+    const int ab = (polls & 63) == 0
+                       ? __builtin_amdgcn_readfirstlane(__hip_atomic_load(s.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                       : 0;
+    if (ab != 0 || ++polls > spin_limit) {
       atomicCAS(s.abort, 0, (int)(p - s.wflag) + 1);
       atomicCAS(info, 0, kCholSpinFault);
       return false;
@@ -1203,11 +1213,13 @@ __device__ __forceinline__ bool chol_poll_ge(const int* p, int v, const CholSync
   return true;
 }
 
-// every storing wave drains its sc1 stores, the workgroup meets, thread 0 raises the flag
+// every storing wave drains its sc1 stores, the workgroup meets, wave 0 raises the flag (all its lanes store the
+// same value to the same word: one uniform store)
 __device__ __forceinline__ void chol_signal(int* flag, int value) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0)
+    __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Panel tile L_ik = A_ik W_kᵀ (chol_panel_kernel's product, 4 waves × 16 rows): W from the fragments Wk (sc1), the
@@ -1322,6 +1334,8 @@ __global__ __launch_bounds__(256, 1) void chol_persist_kernel(double* __restrict
     };
     load_av(0);
     for (int k = 0; k < t; ++k) {
+      OMB_PDBG(0, 1000 * k + 1);
+      OMB_PTIME(8 * k + 0);
       const int64_t r0 = (int64_t)k * kNB;
       const int nb = (int)(N - r0 < kNB ? N - r0 : kNB);
       if (tid < kBlkFlags) fl[tid] = 0;
@@ -1349,30 +1363,50 @@ __global__ __launch_bounds__(256, 1) void chol_persist_kernel(double* __restrict
         }
       }
       __syncthreads();                                          // fl zeroed; every wave past its Lp reads
-      chol64_blocked_core(A, lda, r0, nb, Wf + (int64_t)k * kCholWsDoubles, Ds, Wl, fl);
+      OMB_PDBG(0, 1000 * k + 2);
+      OMB_PTIME(8 * k + 1);
+      chol64_blocked<kCholDReady>(A, lda, r0, nb, 0, Wf + (int64_t)k * kCholWsDoubles, Ds, Wl, fl);
+      OMB_PDBG(1 + w, 1000 * k + 3);
       chol_signal(sync.wflag + k, 1);                           // W_k's fragments (wf_store: sc1) drained
-      if (tid == 0 && (fl[20] || fl[21])) atomicCAS(info, 0, fl[21] ? kCholSpinFault : (int)(r0 + fl[20]));
+      OMB_PDBG(0, 1000 * k + 4);
+      if (w == 0 && (fl[20] || fl[21])) atomicCAS(info, 0, fl[21] ? kCholSpinFault : (int)(r0 + fl[20]));
+      OMB_PTIME(8 * k + 2);
       if (k + 1 < t) {
         // the next panel tile and the next diagonal tile: both updated through step k − 1 by the workers
-        if (tid == 0) {
+        if (w == 0) {
           const int i1 = (k + 1) * t;
           if (chol_poll_ge(sync.cnt + i1 + k, k, sync, spin_limit, info))
             chol_poll_ge(sync.cnt + i1 + k + 1, k, sync, spin_limit, info);
         }
         __syncthreads();
+        OMB_PDBG(0, 1000 * k + 5);
+        OMB_PTIME(8 * k + 3);
         load_av(k + 1);
         chol_persist_panel(ra, A, N, lda, k + 1, k, Wf + (int64_t)k * kCholWsDoubles, Lp);
         chol_signal(sync.pflag + (k + 1) * t + k, 1);
+        OMB_PDBG(0, 1000 * k + 6);
+        OMB_PTIME(8 * k + 4);
       }
     }
     return;
   }
   // ---------------- workers
   for (;;) {
-    if (tid == 0) s_task[0] = __hip_atomic_fetch_add(sync.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (w == 0) {                 // the whole wave adds 1 (lane 0) + 0 (the rest): lane 0's old value is the ticket
+      const int old = __hip_atomic_fetch_add(sync.ticket, lane == 0 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_task[0] = __builtin_amdgcn_readfirstlane(old);   // every lane: the same value, no divergent store
+    }
     __syncthreads();
-    int q = s_task[0];
-    if (q >= total) return;
+    // read as a wave-uniform value: loaded per lane, the compiler treats every branch on q as divergent and
+    // restructures the loop around the barriers below (it sank the flag stores out of the task code, and the
+    // launch hung at N = 130, gpurun_out/r04_o)
+    int q = __builtin_amdgcn_readfirstlane(s_task[0]);
+    OMB_PDBG(8 * blockIdx.x, q + 1);
+    OMB_PTIME(8 * t + 4 * q);
+    if (q >= total) {
+      OMB_PDBG(8 * blockIdx.x + 1, 99);
+      return;
+    }
     int k = 0;
     for (; k < t; ++k) {
       const int nk = chol_persist_step_tasks(t, k);
@@ -1382,11 +1416,16 @@ __global__ __launch_bounds__(256, 1) void chol_persist_kernel(double* __restrict
     const int np = t - k - 2 > 0 ? t - k - 2 : 0;
     if (q < np) {
       const int i = k + 2 + q;
-      if (tid == 0 && chol_poll_ge(sync.wflag + k, 1, sync, spin_limit, info))
+      if (w == 0 && chol_poll_ge(sync.wflag + k, 1, sync, spin_limit, info))
         chol_poll_ge(sync.cnt + i * t + k, k, sync, spin_limit, info);
       __syncthreads();
+      OMB_PDBG(8 * blockIdx.x + 1, 1);
+      OMB_PTIME(8 * t + 4 * s_task[0] + 1);
       chol_persist_panel(ra, A, N, lda, i, k, Wf + (int64_t)k * kCholWsDoubles, nullptr);
+      OMB_PDBG(8 * blockIdx.x + 2 + w, 2);
       chol_signal(sync.pflag + i * t + k, 1);
+      OMB_PDBG(8 * blockIdx.x + 1, 3);
+      OMB_PTIME(8 * t + 4 * s_task[0] + 2);
     } else {
       int u = q - np + 1, j = k + 1;                            // + 1: (k+1, k+1) is the diagonal workgroup's
       while (u >= t - j) {
@@ -1394,12 +1433,17 @@ __global__ __launch_bounds__(256, 1) void chol_persist_kernel(double* __restrict
         ++j;
       }
       const int i = j + u;
-      if (tid == 0 && chol_poll_ge(sync.pflag + i * t + k, 1, sync, spin_limit, info) &&
+      if (w == 0 && chol_poll_ge(sync.pflag + i * t + k, 1, sync, spin_limit, info) &&
           chol_poll_ge(sync.pflag + j * t + k, 1, sync, spin_limit, info))
         chol_poll_ge(sync.cnt + i * t + j, k, sync, spin_limit, info);
       __syncthreads();
+      OMB_PDBG(8 * blockIdx.x + 1, 11);
+      OMB_PTIME(8 * t + 4 * s_task[0] + 1);
       chol_persist_update(ra, A, N, lda, i, j, k);
+      OMB_PDBG(8 * blockIdx.x + 2 + w, 12);
       chol_signal(sync.cnt + i * t + j, k + 1);
+      OMB_PDBG(8 * blockIdx.x + 1, 13);
+      OMB_PTIME(8 * t + 4 * s_task[0] + 2);
     }
   }
 }
@@ -2364,8 +2408,11 @@ static hipError_t chol_panel(hipStream_t stream, double* A, int64_t N, int64_t l
 #ifdef OMB_TOOLS_KNOBS
 static size_t g_chol_update_lds = 0;
 void set_chol_update_lds(size_t bytes) { g_chol_update_lds = bytes; }
+static int g_chol_update_delay = 0;
+void set_chol_update_delay(int n) { g_chol_update_delay = n; }
 #else
 constexpr size_t g_chol_update_lds = 0;
+constexpr int g_chol_update_delay = 0;
 #endif
 
 // Round 4: the diagonal blocks by tiles of 16 (chol64_blocked), one launch per step with the next panel inside.
@@ -2384,7 +2431,7 @@ static hipError_t launch_cholesky_blocked(hipStream_t stream, double* A, int64_t
       if (e != hipSuccess) break;
     }
     hipLaunchKernelGGL((chol_update_kernel<true, true>), dim3((unsigned)(t * (t + 1) / 2)), dim3(256), g_chol_update_lds,
-                       stream, A, N, lda, k, t, ws, info, flags, spin_limit, acq_rel);
+                       stream, A, N, lda, k, t, ws, info, flags, spin_limit, acq_rel, g_chol_update_delay);
     e = hipGetLastError();
   }
   return e;
@@ -2455,10 +2502,10 @@ hipError_t launch_cholesky_mode(hipStream_t stream, double* A, int64_t N, int64_
     const unsigned wgs = (unsigned)(t * (t + 1) / 2);
     if (fuse)
       hipLaunchKernelGGL((chol_update_kernel<true, false>), dim3(wgs), dim3(256), g_chol_update_lds, stream, A, N, lda, k,
-                         t, ws, info, flags, spin_limit, 0);
+                         t, ws, info, flags, spin_limit, 0, 0);
     else
       hipLaunchKernelGGL((chol_update_kernel<false, false>), dim3(wgs), dim3(256), g_chol_update_lds, stream, A, N, lda,
-                         k, t, ws, info, flags, spin_limit, 0);
+                         k, t, ws, info, flags, spin_limit, 0, 0);
     e = hipGetLastError();
   }
   return e;

@@ -285,7 +285,7 @@ def test_argmax_rules(ctx):
 
 
 def test_argmax_one_launch_equals_two_launches(ctx):
-    """argmax_onepass (the last workgroup at the ticket reduces; the default) against argmax_pass1/2: the same pair,
+    """argmax_onepass (the last workgroup at the ticket reduces) against argmax_pass1/2 (the default): the same pair,
     call after call (the ticket is left at zero), at grid sizes 1 .. kArgmaxMaxBlocks and past it (grid stride)."""
     rng = np.random.default_rng(10)
     try:
@@ -304,7 +304,7 @@ def test_argmax_one_launch_equals_two_launches(ctx):
         ctx.debug_set("argmax_passes", 1)
         assert ctx.argmax(dev(np.full(70000, np.nan))) == (-np.inf, -1)
     finally:
-        ctx.debug_set("argmax_passes", 1)
+        ctx.debug_set("argmax_passes", 2)
 
 
 @pytest.mark.parametrize("cache_seed", [0, 1])

@@ -236,12 +236,11 @@ static void trace_steps(int64_t N, int st) {
 }
 
 int main(int argc, char** argv) {
+  setvbuf(stdout, nullptr, _IOLBF, 0);
   trace_diag();
   trace_diag_blocked();
   trace_steps(3000, 20);
   trace_steps(3000, 2);
-  // extra dynamic LDS per update workgroup: 0 (3 workgroups per CU by VGPRs), 16 KB (2), 48 KB (1)
-  const size_t extra[3] = {0, 16 << 10, 48 << 10};
   std::vector<int64_t> sizes;
   for (int i = 1; i < argc; ++i) sizes.push_back(atoll(argv[i]));
   if (sizes.empty()) sizes = {512, 1024, 3000};
@@ -298,22 +297,24 @@ int main(int argc, char** argv) {
     float best = mbest[1], sum = msum[1], best2 = mbest[0], sum2 = msum[0];
     printf("N=%lld  two launches per step %.3f ms (best %.3f)\n", (long long)N, sum2 / reps, best2);
     {
-      float sx[3] = {0.f, 0.f, 0.f};
+      // round 4: the non-diagonal workgroups of each blocked step start after delay × ≈ 0.85 µs
+      const int delays[5] = {0, 1, 2, 4, 6};
+      float sx[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
       for (int r = 0; r < reps + 1; ++r)
-        for (int v = 0; v < 3; ++v) {
-          set_chol_update_lds(extra[v]);
+        for (int v = 0; v < 5; ++v) {
+          set_chol_update_delay(delays[v]);
           CK(hipMemcpy(A, A0, N * N * 8, hipMemcpyDeviceToDevice));
           CK(hipEventRecord(e0));
-          CK(launch_cholesky(0, A, N, N, info, ws));
+          CK(launch_cholesky_mode(0, A, N, N, info, ws, kCholBlocked));
           CK(hipEventRecord(e1));
           CK(hipEventSynchronize(e1));
           float ms;
           CK(hipEventElapsedTime(&ms, e0, e1));
           if (r > 0) sx[v] += ms;
         }
-      set_chol_update_lds(0);
-      printf("N=%lld  fused, extra LDS per update workgroup 0 / 16 KB / 48 KB: %.3f / %.3f / %.3f ms\n", (long long)N,
-             sx[0] / reps, sx[1] / reps, sx[2] / reps);
+      set_chol_update_delay(0);
+      printf("N=%lld  blocked, other workgroups delayed by 0 / 0.85 / 1.7 / 3.4 / 5.1 us: %.3f / %.3f / %.3f / %.3f / %.3f ms\n",
+             (long long)N, sx[0] / reps, sx[1] / reps, sx[2] / reps, sx[3] / reps, sx[4] / reps);
     }
     // the same launch sequence captured once into a hipGraph and replayed (launch-gap ablation)
     float gbest = 1e30f, gsum = 0.f;

@@ -240,6 +240,8 @@ def run_thompson(args, cfg, world_size, rank, device, backend):
     yagg = tch(Y, np.array([0.5, 0.5]))
     var = float(np.var(yagg))
     ctx = AcqContext(device.index)
+    if args.chol_mode is not None:
+        ctx.debug_set("chol_mode", args.chol_mode)
     ctx.set_gp_state(0, GPState(X, yagg, ls, var))
     rng = np.random.default_rng(100 + rank)
     # a trust region of side 0.2 around a training point (turbo.py:82-111), one per rank
@@ -424,6 +426,8 @@ def main():
                          "(default: the library's, 0 — the one launch measured slower)")
     ap.add_argument("--argmax-passes", type=int, default=None, choices=[1, 2],
                     help="omb_debug_set(ARGMAX_PASSES): the arg-max as one launch or two (default: the library's, 2)")
+    ap.add_argument("--chol-mode", type=int, default=None, choices=[0, 1, 2],
+                    help="omb_debug_set(CHOL_MODE): Cholesky auto / per-step launches / one persistent launch")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks and the process group only, print what torch.distributed saw")
     ap.add_argument("--cache-seed", type=int, default=1,
@@ -487,6 +491,8 @@ def main():
         ctx.debug_set("fused_chain", args.one_launch)
     if args.argmax_passes is not None:
         ctx.debug_set("argmax_passes", args.argmax_passes)
+    if args.chol_mode is not None:
+        ctx.debug_set("chol_mode", args.chol_mode)
     if acq_kind == "ei_tch":
         # ParEGO-style mono surrogate: Tchebicheff-aggregate the objectives (parego.py:212-219)
         tch = sc.Tchebicheff(Y.min(axis=0), Y.max(axis=0))

@@ -97,8 +97,17 @@ const char* omb_last_error(const omb_ctx* ctx);
  * 1.9 % / 0.6 % slower on configs 2 / 3, gpurun_out/r04_j).
  * omb_debug_set(ctx, OMB_DEBUG_ARGMAX_PASSES, 1) runs the arg-max as one launch (the last workgroup to finish
  * reduces the per-workgroup pairs) instead of two (default 2: config 2 measured 719.6 vs 719.5 M candidates/s,
- * gpurun_out/r04_l; bit-identical pair). */
-enum { OMB_DEBUG_SPIN_LIMIT = 1, OMB_DEBUG_COV_TABLE = 2, OMB_DEBUG_FUSED_CHAIN = 3, OMB_DEBUG_ARGMAX_PASSES = 4 };
+ * gpurun_out/r04_l; bit-identical pair).
+ * omb_debug_set(ctx, OMB_DEBUG_CHOL_MODE, m) picks the Cholesky schedule of omb_cholesky / omb_posterior_samples /
+ * omb_gp_fit_state: 0 auto (default: one persistent launch up to N = 3584, per-step launches above), 1 per-step
+ * launches, 2 one persistent launch (where A fits its 32-bit buffer offsets).  Same factor to rounding. */
+enum {
+  OMB_DEBUG_SPIN_LIMIT = 1,
+  OMB_DEBUG_COV_TABLE = 2,
+  OMB_DEBUG_FUSED_CHAIN = 3,
+  OMB_DEBUG_ARGMAX_PASSES = 4,
+  OMB_DEBUG_CHOL_MODE = 5
+};
 int omb_debug_set(omb_ctx* ctx, int what, int64_t value);
 
 /* Fitted-GP state of objective `obj` — replaces the fitted GPy model

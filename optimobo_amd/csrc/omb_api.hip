@@ -89,6 +89,7 @@ struct omb_ctx {
   bool cov_table = false;   // OMB_DEBUG_COV_TABLE
   bool fused_chain = false;  // OMB_DEBUG_FUSED_CHAIN: EHVI-2D and the arg-max in one launch (off: measured slower)
   bool argmax_one_pass = false;  // OMB_DEBUG_ARGMAX_PASSES: 1 (one launch) or 2 (default: measured level)
+  int chol_mode = kCholAuto;     // OMB_DEBUG_CHOL_MODE
 };
 
 namespace {
@@ -529,6 +530,13 @@ int omb_debug_set(omb_ctx* ctx, int what, int64_t value) {
   }
   if (what == OMB_DEBUG_COV_TABLE) {
     ctx->cov_table = value != 0;
+    return OMB_OK;
+  }
+  if (what == OMB_DEBUG_CHOL_MODE) {
+    if (value != 0 && value != 1 && value != 2)
+      return fail(ctx, OMB_EINVAL, "Cholesky mode %lld (0 auto, 1 per-step launches, 2 one persistent launch)",
+                  (long long)value);
+    ctx->chol_mode = value == 0 ? kCholAuto : (value == 1 ? kCholBlocked : kCholPersistent);
     return OMB_OK;
   }
   return fail(ctx, OMB_EINVAL, "unknown debug setting %d", what);
@@ -1011,7 +1019,7 @@ static int run_cholesky(omb_ctx* ctx, double* A, int64_t N, int64_t lda, double 
   int* dinfo = static_cast<int*>(ctx->ichol);
   double* ws = reinterpret_cast<double*>(static_cast<char*>(ctx->ichol) + 16);
   OMB_HIP(ctx, launch_add_diag(ctx->stream, A, N, lda, jitter));
-  OMB_HIP(ctx, launch_cholesky(ctx->stream, A, N, lda, dinfo, ws, ctx->spin_limit));
+  OMB_HIP(ctx, launch_cholesky_mode(ctx->stream, A, N, lda, dinfo, ws, ctx->chol_mode, ctx->spin_limit));
   int h = 0;
   OMB_HIP(ctx, hipMemcpyAsync(&h, dinfo, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   OMB_HIP(ctx, hipStreamSynchronize(ctx->stream));

@@ -461,9 +461,10 @@ constexpr int kBlkFlags = 4 + 16 + 2;      // wready[4] | lready[4i + b] | bad |
 
 // bounded (2^20 polls ≈ 30 ms): a wait that runs out marks fl[kBlkFlags − 1] (→ info = kCholSpinFault) and
 // goes on, so a wrong flag protocol ends the kernel instead of hanging it
-__device__ __forceinline__ void lds_wait_flag(int* f, int* fault) {
+// epoch: the value a post writes (chol_persist_kernel posts step + 1, so its flags need no reset between steps)
+__device__ __forceinline__ void lds_wait_flag(int* f, int* fault, int epoch = 1) {
   int polls = 0;
-  while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) {
+  while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < epoch) {
     if (++polls > (1 << 20)) {
       *fault = 1;
       break;
@@ -472,8 +473,8 @@ __device__ __forceinline__ void lds_wait_flag(int* f, int* fault) {
   }
 }
 // lane 0 posts; the release orders the whole wave's earlier LDS stores before the flag
-__device__ __forceinline__ void lds_post_flag(int* f, int lane) {
-  if (lane == 0) __hip_atomic_store(f, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+__device__ __forceinline__ void lds_post_flag(int* f, int lane, int epoch = 1) {
+  if (lane == 0) __hip_atomic_store(f, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 // orders one wave's LDS accesses across lanes for the compiler (LDS executes a wave's accesses in order)
 __device__ __forceinline__ void wave_lds_order() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
@@ -547,7 +548,7 @@ __device__ __forceinline__ void load_row16(const double* __restrict__ p, bool ok
 enum { kCholDLoad = 0, kCholDOuter = 1, kCholDReady = 2 };
 template <int MODE>
 __device__ __forceinline__ void chol64_blocked(double* __restrict__ A, int64_t lda, int64_t r0, int nb, int64_t c0,
-                                               double* __restrict__ Wf, double* Ds, double* Wl, int* fl) {
+                                               double* __restrict__ Wf, double* Ds, double* Wl, int* fl, int epoch = 1) {
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   OMB_CHOL_BTRACE(w, 0, lane == 0);
@@ -608,7 +609,7 @@ __device__ __forceinline__ void chol64_blocked(double* __restrict__ A, int64_t l
     double dop[4];                                                    // D_wb[c][4s + g], read before the wait
 #pragma unroll
     for (int s = 0; s < 4; ++s) dop[s] = Ds[(16 * w + c) * kDP + 16 * b + 4 * s + g];
-    lds_wait_flag(&fl[b], &fl[21]);
+    lds_wait_flag(&fl[b], &fl[21], epoch);
     OMB_CHOL_BTRACE(w, 2 + 2 * b, lane == 0);
     const double* Wb = Wl + b * kWlP;
     d4 lt = d4{0.0, 0.0, 0.0, 0.0};
@@ -617,7 +618,7 @@ __device__ __forceinline__ void chol64_blocked(double* __restrict__ A, int64_t l
       lt = __builtin_amdgcn_mfma_f64_16x16x4f64(Wb[(4 * s + g) * 18 + c], dop[s], lt, 0, 0, 0);   // W_bb[c][4s + g]
 #pragma unroll
     for (int e = 0; e < 4; ++e) Ds[(16 * w + c) * kDP + 16 * b + 4 * e + g] = lt[e];     // L_wb[c][4e + g]
-    lds_post_flag(&fl[4 + 4 * w + b], lane);
+    lds_post_flag(&fl[4 + 4 * w + b], lane, epoch);
     // U_b: the own diagonal tile first (on the chain when b = w − 1), then the tiles (w, j), b < j < w
     for (int j = w; j > b; --j) {
       d4 u = d4{0.0, 0.0, 0.0, 0.0};
@@ -625,7 +626,7 @@ __device__ __forceinline__ void chol64_blocked(double* __restrict__ A, int64_t l
 #pragma unroll
         for (int s = 0; s < 4; ++s) u = __builtin_amdgcn_mfma_f64_16x16x4f64(lt[s], lt[s], u, 0, 0, 0);
       } else {
-        lds_wait_flag(&fl[4 + 4 * j + b], &fl[21]);
+        lds_wait_flag(&fl[4 + 4 * j + b], &fl[21], epoch);
 #pragma unroll
         for (int s = 0; s < 4; ++s)
           u = __builtin_amdgcn_mfma_f64_16x16x4f64(lt[s], Ds[(16 * j + c) * kDP + 16 * b + 4 * s + g], u, 0, 0, 0);
@@ -670,7 +671,7 @@ __device__ __forceinline__ void chol64_blocked(double* __restrict__ A, int64_t l
       }
       if (c == 0 && bad != 0 && fl[20] == 0) fl[20] = 16 * w + bad;
     }
-    lds_post_flag(&fl[w], lane);
+    lds_post_flag(&fl[w], lane, epoch);
     OMB_CHOL_BTRACE(w, 10, lane == 0);
     if (g == 0 && 16 * w + c < nb) {
 #pragma unroll
@@ -694,7 +695,7 @@ __device__ __forceinline__ void chol64_blocked(double* __restrict__ A, int64_t l
       static_for<0, i>([&](auto kc) {
         constexpr int k = decltype(kc)::value;
         if (k >= w) {
-          lds_wait_flag(&fl[4 + 4 * i + k], &fl[21]);                                             // L_ik final
+          lds_wait_flag(&fl[4 + 4 * i + k], &fl[21], epoch);                                      // L_ik final
 #pragma unroll
           for (int s = 0; s < 4; ++s) {
             const double av = Ds[(16 * i + c) * kDP + 16 * k + 4 * s + g];              // L_ik[c][4s + g]
@@ -703,7 +704,7 @@ __device__ __forceinline__ void chol64_blocked(double* __restrict__ A, int64_t l
           }
         }
       });
-      lds_wait_flag(&fl[i], &fl[21]);                                                             // W_ii in Wl
+      lds_wait_flag(&fl[i], &fl[21], epoch);                                                      // W_ii in Wl
       d4 R = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int s = 0; s < 4; ++s)
@@ -1139,11 +1140,13 @@ __global__ __launch_bounds__(256, 3) void chol_update_kernel(double* __restrict_
 // Cross-workgroup data (panel tiles, A tiles between updates, W fragments) is written with sc1 (write-through) stores
 // after which every storing wave waits vmcnt(0), the workgroup passes a barrier and one lane stores the flag or tile
 // counter (relaxed, agent scope); readers poll relaxed, pass a barrier and read those bytes with sc1 loads only
-// (MI355X_MICROARCH.md § inter-workgroup visibility, the sc1 valid form; one workgroup per CU as measured there:
-// 227 VGPRs + 32 AGPRs, and static + dynamic LDS above half a CU's).  Tile counters cnt(i, j) = number of updates applied: each update waits for
+// (MI355X_MICROARCH.md § inter-workgroup visibility, the sc1 valid form; one workgroup per CU as measured there).  Tile counters cnt(i, j) = number of updates applied: each update waits for
 // cnt = k, so the updates of one tile, possibly on different XCDs, never overlap.  Every wait is bounded (spin_limit
 // polls), after which an abort word stops all waits and info = kCholSpinFault.
-// dynamic LDS added at the launch (never read) so that static + dynamic > 80 KB: one workgroup per CU
+// one workgroup per CU: the launch bounds (228 VGPRs + 32 AGPRs) and dynamic LDS added at the launch (never read)
+// so that static + dynamic > 80 KB.  Two per CU (225 VGPRs, no pad) was slower — N = 3000 1.64 against 1.11 ms: a
+// worker sharing the diagonal workgroup's CU stretches its factor and panel (gpurun_out/r04_r).
+constexpr int kPersistWgPerCu = 1;
 constexpr int kPersistLdsPad = 8 * 1024;
 
 // progress words for tools/ablate/chol_persist_check (host-mapped memory; empty here)
@@ -1306,7 +1309,7 @@ __device__ __forceinline__ int chol_persist_step_tasks(int t, int k) {
   return np + nu;
 }
 
-__global__ __launch_bounds__(256, 1) void chol_persist_kernel(double* __restrict__ A, int64_t N, int64_t lda, int t,
+__global__ __launch_bounds__(256, kPersistWgPerCu) void chol_persist_kernel(double* __restrict__ A, int64_t N, int64_t lda, int t,
                                                               int total, double* __restrict__ Wf, CholSync sync,
                                                               int* __restrict__ info, int spin_limit) {
   __shared__ __attribute__((aligned(16))) double Ds[kNB * kDP];
@@ -1333,13 +1336,16 @@ __global__ __launch_bounds__(256, 1) void chol_persist_kernel(double* __restrict
         }
     };
     load_av(0);
+    if (tid < kBlkFlags) fl[tid] = 0;
+    __syncthreads();
     for (int k = 0; k < t; ++k) {
       OMB_PDBG(0, 1000 * k + 1);
       OMB_PTIME(8 * k + 0);
       const int64_t r0 = (int64_t)k * kNB;
       const int nb = (int)(N - r0 < kNB ? N - r0 : kNB);
-      if (tid < kBlkFlags) fl[tid] = 0;
-      // D tiles (w, j ≤ w) = A_kk − L_{k,k−1} L_{k,k−1}ᵀ (Lp: written before the previous step's last barrier)
+      // D tiles (w, j ≤ w) = A_kk − L_{k,k−1} L_{k,k−1}ᵀ (Lp: written before the previous step's last barrier).  No
+      // barrier after them: the core's LDS flags carry the step (epoch k + 1), so wave 0 starts its first tile's
+      // factor while the later waves still form theirs.
       {
         double xa[16];
 #pragma unroll
@@ -1362,14 +1368,14 @@ __global__ __launch_bounds__(256, 1) void chol_persist_kernel(double* __restrict
           }
         }
       }
-      __syncthreads();                                          // fl zeroed; every wave past its Lp reads
       OMB_PDBG(0, 1000 * k + 2);
       OMB_PTIME(8 * k + 1);
-      chol64_blocked<kCholDReady>(A, lda, r0, nb, 0, Wf + (int64_t)k * kCholWsDoubles, Ds, Wl, fl);
+      chol64_blocked<kCholDReady>(A, lda, r0, nb, 0, Wf + (int64_t)k * kCholWsDoubles, Ds, Wl, fl, k + 1);
       OMB_PDBG(1 + w, 1000 * k + 3);
       chol_signal(sync.wflag + k, 1);                           // W_k's fragments (wf_store: sc1) drained
       OMB_PDBG(0, 1000 * k + 4);
       if (w == 0 && (fl[20] || fl[21])) atomicCAS(info, 0, fl[21] ? kCholSpinFault : (int)(r0 + fl[20]));
+      if (w == 0) fl[20] = 0;           // read above (wave 0, in order); the next step's writes follow a barrier
       OMB_PTIME(8 * k + 2);
       if (k + 1 < t) {
         // the next panel tile and the next diagonal tile: both updated through step k − 1 by the workers
@@ -2437,7 +2443,7 @@ static hipError_t launch_cholesky_blocked(hipStream_t stream, double* A, int64_t
   return e;
 }
 
-// Round 4: one persistent launch (chol_persist_kernel), one workgroup per CU.
+// Round 4: one persistent launch (chol_persist_kernel), kPersistWgPerCu workgroups per CU.
 static int device_cus() {
   static int cus[64] = {0};
   int dev = 0;
@@ -2469,15 +2475,17 @@ static hipError_t launch_cholesky_persist(hipStream_t stream, double* A, int64_t
   hipError_t e = hipMemsetAsync(ints, 0, nints * sizeof(int), stream);
   if (e == hipSuccess) e = hipMemsetAsync(info, 0, sizeof(int), stream);
   if (e != hipSuccess) return e;
-  const int grid = 1 + (total < device_cus() - 1 ? total : device_cus() - 1);
-  hipLaunchKernelGGL(chol_persist_kernel, dim3((unsigned)grid), dim3(256), kPersistLdsPad, stream, A, N, lda, t, total, Wf,
-                     sync, info, spin_limit);
+  const int slots = kPersistWgPerCu * device_cus() - 1;
+  const int grid = 1 + (total < slots ? total : slots);
+  hipLaunchKernelGGL(chol_persist_kernel, dim3((unsigned)grid), dim3(256), kPersistLdsPad, stream, A, N, lda, t, total,
+                     Wf, sync, info, spin_limit);
   return hipGetLastError();
 }
 
 hipError_t launch_cholesky_mode(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws, int mode,
                                 int spin_limit) {
   if (N <= 0) return hipSuccess;
+  if (mode == kCholAuto) mode = N <= kCholPersistMaxN ? kCholPersistent : kCholBlocked;
   if (mode == kCholPersistent) {
     if (chol_persist_fits(N, lda)) return launch_cholesky_persist(stream, A, N, lda, info, ws, spin_limit);
     mode = kCholBlocked;
@@ -2512,7 +2520,7 @@ hipError_t launch_cholesky_mode(hipStream_t stream, double* A, int64_t N, int64_
 }
 
 hipError_t launch_cholesky(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws, int spin_limit) {
-  return launch_cholesky_mode(stream, A, N, lda, info, ws, kCholBlocked, spin_limit);
+  return launch_cholesky_mode(stream, A, N, lda, info, ws, kCholAuto, spin_limit);
 }
 
 hipError_t launch_trinv(hipStream_t stream, const double* L, int64_t n, int64_t lda, double* X, int64_t ldx,

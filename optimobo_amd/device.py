@@ -71,9 +71,10 @@ class AcqContext:
         """omb_debug_set: ("spin_limit", polls) bounds the posterior's LDS-counter waits; ("cov_table", 0/1)
         builds K(X, X) / K(X*, X*) with the posterior's table-driven Matern transform; ("fused_chain", 0/1) runs
         EHVI-2D and the arg-max as separate launches / as one; ("argmax_passes", 1/2) runs the arg-max as one
-        launch / as two."""
+        launch / as two; ("chol_mode", 0/1/2) factors auto / by per-step launches / in one persistent launch."""
         code = {"spin_limit": _lib.DEBUG_SPIN_LIMIT, "cov_table": _lib.DEBUG_COV_TABLE,
-                "fused_chain": _lib.DEBUG_FUSED_CHAIN, "argmax_passes": _lib.DEBUG_ARGMAX_PASSES}[what]
+                "fused_chain": _lib.DEBUG_FUSED_CHAIN, "argmax_passes": _lib.DEBUG_ARGMAX_PASSES,
+                "chol_mode": _lib.DEBUG_CHOL_MODE}[what]
         self._check(self.lib.omb_debug_set(self._h, code, int(value)), "omb_debug_set")
 
     # ------------------------------------------------------------------ GP state

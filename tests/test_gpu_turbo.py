@@ -67,8 +67,16 @@ def spd(N, seed):
     return G @ G.T / N + 0.5 * np.eye(N)
 
 
+@pytest.fixture(params=[0, 1, 2], ids=["auto", "steps", "persistent"])
+def chol_mode(ctx, request):
+    """omb_debug_set(CHOL_MODE): the default schedule, the per-step launches and the one persistent launch."""
+    ctx.debug_set("chol_mode", request.param)
+    yield request.param
+    ctx.debug_set("chol_mode", 0)
+
+
 @pytest.mark.parametrize("N", [1, 2, 63, 64, 65, 130, 192, 193, 333, 1000, 3000])
-def test_cholesky_vs_lapack(ctx, N):
+def test_cholesky_vs_lapack(ctx, chol_mode, N):
     A = spd(N, N)
     wide = np.full((N, N + 5), 7.0)                  # lda > N: the extra columns are never touched
     wide[:, :N] = np.triu(np.full((N, N), -3.0), 1) + np.tril(A)   # upper triangle holds junk
@@ -83,7 +91,7 @@ def test_cholesky_vs_lapack(ctx, N):
 
 
 @pytest.mark.parametrize("N,bad", [(200, 0), (200, 70), (200, 199), (700, 300), (700, 650), (700, 699)])
-def test_cholesky_info_matches_dpotrf(ctx, N, bad):
+def test_cholesky_info_matches_dpotrf(ctx, chol_mode, N, bad):
     A = spd(N, 5)
     A[bad, bad] = -1.0
     _, info_ref = linalg.lapack.dpotrf(A, lower=1)
@@ -91,7 +99,7 @@ def test_cholesky_info_matches_dpotrf(ctx, N, bad):
     assert info == info_ref == bad + 1
 
 
-def test_cholesky_randomized_stress(ctx):
+def test_cholesky_randomized_stress(ctx, chol_mode):
     """the fused steps hand W_{k+1} from the diagonal workgroup to the panel workgroups through
     agent-scope relaxed fragment stores / loads and a flag ordered by a vmcnt wait and compiler fences, not by a
     release / acquire pair (whose L2 write-back costs 3%).  A wrong order would show as a silently
@@ -118,7 +126,7 @@ def test_cholesky_randomized_stress(ctx):
         assert np.array_equal(got, first)
 
 
-def test_cholesky_step_wait_timeout_is_reported(ctx):
+def test_cholesky_step_wait_timeout_is_reported(ctx, chol_mode):
     """The fused Cholesky step (the next panel formed in the update launch) waits for the diagonal
     workgroup's flag with a bounded poll; omb_debug_set(SPIN_LIMIT, 0) makes the first unset poll run
     out, and the call returns OMB_EHIP instead of an info or a wrong factor.  The default bound then

@@ -546,9 +546,11 @@ __device__ __forceinline__ void load_row16(const double* __restrict__ p, bool ok
 // MODE kCholDLoad (step 0 / chol_diag_blk_kernel): D = A_kk; kCholDOuter (chol_update_kernel): D = A22_00 − L21_0
 // L21_0ᵀ from global; kCholDReady (chol_persist_kernel): each wave has already written its D tiles (w, j ≤ w) to Ds.
 enum { kCholDLoad = 0, kCholDOuter = 1, kCholDReady = 2 };
+// kCholDReady also leaves W's fragments in Wfl (LDS, the layout of Wf) for the walker's own panel tile.
 template <int MODE>
 __device__ __forceinline__ void chol64_blocked(double* __restrict__ A, int64_t lda, int64_t r0, int nb, int64_t c0,
-                                               double* __restrict__ Wf, double* Ds, double* Wl, int* fl, int epoch = 1) {
+                                               double* __restrict__ Wf, double* Ds, double* Wl, int* fl, int epoch = 1,
+                                               double* Wfl = nullptr) {
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   OMB_CHOL_BTRACE(w, 0, lane == 0);
@@ -682,7 +684,11 @@ __device__ __forceinline__ void chol64_blocked(double* __restrict__ A, int64_t l
   // W_ww's fragments: block (w, w), k-step 4w + u: W[16w + c][16w + 4g + u]
   wave_lds_order();
 #pragma unroll
-  for (int u = 0; u < 4; ++u) wf_store(&Wf[(w * 16 + 4 * w + u) * 64 + 16 * g + c], Wl[w * kWlP + (4 * g + u) * 18 + c]);
+  for (int u = 0; u < 4; ++u) {
+    const double v = Wl[w * kWlP + (4 * g + u) * 18 + c];
+    wf_store(&Wf[(w * 16 + 4 * w + u) * 64 + 16 * g + c], v);
+    if constexpr (MODE == kCholDReady) Wfl[(w * 16 + 4 * w + u) * 64 + 16 * g + c] = v;   // the walker's LDS copy
+  }
   // ---- W's column block w: W_iw = −W_ii Σ_{k=w}^{i−1} L_ik W_kw, i = w+1 .. 3 (Wc[k] = W_kw, accumulator layout,
   // is the B operand of the next product: lane (g, c) holds W_kw[4s + g][c] in register s)
   d4 Wc[4];
@@ -712,7 +718,10 @@ __device__ __forceinline__ void chol64_blocked(double* __restrict__ A, int64_t l
       Wc[i] = -R;
       // W[16i + 4e + g][16w + c]: row block i, k-step 4w + (c & 3), lane 4e + g + 16 (c >> 2)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) wf_store(&Wf[(i * 16 + 4 * w + (c & 3)) * 64 + 4 * e + g + 16 * (c >> 2)], Wc[i][e]);
+      for (int e = 0; e < 4; ++e) {
+        wf_store(&Wf[(i * 16 + 4 * w + (c & 3)) * 64 + 4 * e + g + 16 * (c >> 2)], Wc[i][e]);
+        if constexpr (MODE == kCholDReady) Wfl[(i * 16 + 4 * w + (c & 3)) * 64 + 4 * e + g + 16 * (c >> 2)] = Wc[i][e];
+      }
       OMB_CHOL_BTRACE(w, 10 + i, lane == 0);
     }
   });
@@ -1143,11 +1152,10 @@ __global__ __launch_bounds__(256, 3) void chol_update_kernel(double* __restrict_
 // (MI355X_MICROARCH.md § inter-workgroup visibility, the sc1 valid form; one workgroup per CU as measured there).  Tile counters cnt(i, j) = number of updates applied: each update waits for
 // cnt = k, so the updates of one tile, possibly on different XCDs, never overlap.  Every wait is bounded (spin_limit
 // polls), after which an abort word stops all waits and info = kCholSpinFault.
-// one workgroup per CU: the launch bounds (228 VGPRs + 32 AGPRs) and dynamic LDS added at the launch (never read)
-// so that static + dynamic > 80 KB.  Two per CU (225 VGPRs, no pad) was slower — N = 3000 1.64 against 1.11 ms: a
+// one workgroup per CU: the launch bounds (≈ 228 VGPRs + 32 AGPRs) and > 80 KB of static LDS (D, the panel tile,
+// W_bb and the walker's W fragments).  Two per CU (225 VGPRs, 77 KB) was slower — N = 3000 1.64 against 1.11 ms: a
 // worker sharing the diagonal workgroup's CU stretches its factor and panel (gpurun_out/r04_r).
 constexpr int kPersistWgPerCu = 1;
-constexpr int kPersistLdsPad = 8 * 1024;
 
 // progress words for tools/ablate/chol_persist_check (host-mapped memory; empty here)
 #ifndef OMB_PDBG
@@ -1188,7 +1196,7 @@ __device__ __forceinline__ void st_sc1(double* p, double v) {
 
 struct CholSync {
   int* wflag;   // [t]      W_k published
-  int* pflag;   // [t·t]    panel tile (i, k) published
+  int* pflag;   // [t·t]    panel tile (i, k) published: 4 (per-wave adds for the walker's tiles)
   int* cnt;     // [t·t]    updates applied to tile (i, j)
   int* ticket;  // task counter of the worker workgroups
   int* abort;   // set by the first wait that runs out
@@ -1225,8 +1233,9 @@ __device__ __forceinline__ void chol_signal(int* flag, int value) {
     __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Panel tile L_ik = A_ik W_kᵀ (chol_panel_kernel's product, 4 waves × 16 rows): W from the fragments Wk (sc1), the
-// result to A (sc1) and, for the diagonal workgroup, into Lp (LDS, pitch kDP).
+// Panel tile L_ik = A_ik W_kᵀ (chol_panel_kernel's product, 4 waves × 16 rows): W from the fragments Wk (global,
+// sc1; for the diagonal workgroup, Lp set, its LDS copy), the result to A (sc1) and, for the diagonal workgroup,
+// into Lp (LDS, pitch kDP).
 __device__ __forceinline__ void chol_persist_panel(__amdgpu_buffer_rsrc_t ra, double* __restrict__ A, int64_t N,
                                                    int64_t lda, int i, int k, const double* __restrict__ Wk, double* Lp) {
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
@@ -1244,12 +1253,15 @@ __device__ __forceinline__ void chol_persist_panel(__amdgpu_buffer_rsrc_t ra, do
     d4 pa = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int s = 0; s < 16; ++s)
-      if (s < 4 * (jb + 1)) pa = __builtin_amdgcn_mfma_f64_16x16x4f64(x[s], ld_sc1(wf + s * 64), pa, 0, 0, 0);
+      if (s < 4 * (jb + 1))
+        pa = __builtin_amdgcn_mfma_f64_16x16x4f64(x[s], Lp ? wf[s * 64] : ld_sc1(wf + s * 64), pa, 0, 0, 0);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int64_t orow = (int64_t)i * kNB + 16 * w + 4 * e + g;
-      if (orow < N) st_sc1(A + orow * lda + (int64_t)k * kNB + 16 * jb + c, pa[e]);
-      if (Lp) Lp[(16 * w + 4 * e + g) * kDP + 16 * jb + c] = pa[e];
+      if (Lp)
+        Lp[(16 * w + 4 * e + g) * kDP + 16 * jb + c] = pa[e];   // the walker: waves 2 and 3 store it (below)
+      else if (orow < N)
+        st_sc1(A + orow * lda + (int64_t)k * kNB + 16 * jb + c, pa[e]);
     }
   }
 }
@@ -1315,6 +1327,7 @@ __global__ __launch_bounds__(256, kPersistWgPerCu) void chol_persist_kernel(doub
   __shared__ __attribute__((aligned(16))) double Ds[kNB * kDP];
   __shared__ __attribute__((aligned(16))) double Lp[kNB * kDP];
   __shared__ __attribute__((aligned(16))) double Wl[4 * kWlP];
+  __shared__ __attribute__((aligned(16))) double Wfl[kCholWsDoubles];   // the walker's W fragments
   __shared__ int fl[kBlkFlags];
   __shared__ int s_task[2];
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4;
@@ -1368,9 +1381,13 @@ __global__ __launch_bounds__(256, kPersistWgPerCu) void chol_persist_kernel(doub
           }
         }
       }
+      if (k > 0 && w >= 2) {   // the previous step's panel tile (k, k − 1): this wave's rows drained, its share
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(sync.pflag + k * t + k - 1, lane == 0 ? 2 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       OMB_PDBG(0, 1000 * k + 2);
       OMB_PTIME(8 * k + 1);
-      chol64_blocked<kCholDReady>(A, lda, r0, nb, 0, Wf + (int64_t)k * kCholWsDoubles, Ds, Wl, fl, k + 1);
+      chol64_blocked<kCholDReady>(A, lda, r0, nb, 0, Wf + (int64_t)k * kCholWsDoubles, Ds, Wl, fl, k + 1, Wfl);
       OMB_PDBG(1 + w, 1000 * k + 3);
       chol_signal(sync.wflag + k, 1);                           // W_k's fragments (wf_store: sc1) drained
       OMB_PDBG(0, 1000 * k + 4);
@@ -1388,8 +1405,19 @@ __global__ __launch_bounds__(256, kPersistWgPerCu) void chol_persist_kernel(doub
         OMB_PDBG(0, 1000 * k + 5);
         OMB_PTIME(8 * k + 3);
         load_av(k + 1);
-        chol_persist_panel(ra, A, N, lda, k + 1, k, Wf + (int64_t)k * kCholWsDoubles, Lp);
-        chol_signal(sync.pflag + (k + 1) * t + k, 1);
+        chol_persist_panel(ra, A, N, lda, k + 1, k, Wfl, Lp);
+        // Lp visible to every wave; waves 2 and 3 store the tile to A (32 rows each, sc1) and signal it in the next
+        // step, after their D tiles, where they wait for W_00 anyway: the stores' drain (≈ 2.4 µs) stays off the
+        // chain that waves 0 and 1 run (consumers wait for 4 = 2 + 2)
+        __syncthreads();
+        if (w >= 2) {
+          const int64_t rbase = (int64_t)(k + 1) * kNB;
+#pragma unroll 4
+          for (int q = 0; q < 32; ++q) {
+            const int lr = 32 * (w - 2) + q;
+            if (rbase + lr < N) st_sc1(A + (rbase + lr) * lda + (int64_t)k * kNB + lane, Lp[lr * kDP + lane]);
+          }
+        }
         OMB_PDBG(0, 1000 * k + 6);
         OMB_PTIME(8 * k + 4);
       }
@@ -1429,7 +1457,7 @@ __global__ __launch_bounds__(256, kPersistWgPerCu) void chol_persist_kernel(doub
       OMB_PTIME(8 * t + 4 * s_task[0] + 1);
       chol_persist_panel(ra, A, N, lda, i, k, Wf + (int64_t)k * kCholWsDoubles, nullptr);
       OMB_PDBG(8 * blockIdx.x + 2 + w, 2);
-      chol_signal(sync.pflag + i * t + k, 1);
+      chol_signal(sync.pflag + i * t + k, 4);
       OMB_PDBG(8 * blockIdx.x + 1, 3);
       OMB_PTIME(8 * t + 4 * s_task[0] + 2);
     } else {
@@ -1439,8 +1467,8 @@ __global__ __launch_bounds__(256, kPersistWgPerCu) void chol_persist_kernel(doub
         ++j;
       }
       const int i = j + u;
-      if (w == 0 && chol_poll_ge(sync.pflag + i * t + k, 1, sync, spin_limit, info) &&
-          chol_poll_ge(sync.pflag + j * t + k, 1, sync, spin_limit, info))
+      if (w == 0 && chol_poll_ge(sync.pflag + i * t + k, 4, sync, spin_limit, info) &&
+          chol_poll_ge(sync.pflag + j * t + k, 4, sync, spin_limit, info))
         chol_poll_ge(sync.cnt + i * t + j, k, sync, spin_limit, info);
       __syncthreads();
       OMB_PDBG(8 * blockIdx.x + 1, 11);
@@ -2477,8 +2505,8 @@ static hipError_t launch_cholesky_persist(hipStream_t stream, double* A, int64_t
   if (e != hipSuccess) return e;
   const int slots = kPersistWgPerCu * device_cus() - 1;
   const int grid = 1 + (total < slots ? total : slots);
-  hipLaunchKernelGGL(chol_persist_kernel, dim3((unsigned)grid), dim3(256), kPersistLdsPad, stream, A, N, lda, t, total,
-                     Wf, sync, info, spin_limit);
+  hipLaunchKernelGGL(chol_persist_kernel, dim3((unsigned)grid), dim3(256), 0, stream, A, N, lda, t, total, Wf, sync,
+                     info, spin_limit);
   return hipGetLastError();
 }
 

@@ -99,8 +99,9 @@ const char* omb_last_error(const omb_ctx* ctx);
  * reduces the per-workgroup pairs) instead of two (default 2: config 2 measured 719.6 vs 719.5 M candidates/s,
  * gpurun_out/r04_l; bit-identical pair).
  * omb_debug_set(ctx, OMB_DEBUG_CHOL_MODE, m) picks the Cholesky schedule of omb_cholesky / omb_posterior_samples /
- * omb_gp_fit_state: 0 auto (default: one persistent launch up to N = 3584, per-step launches above), 1 per-step
- * launches, 2 one persistent launch (where A fits its 32-bit buffer offsets).  Same factor to rounding. */
+ * omb_gp_fit_state: 0 auto (default: = 2 where A fits the persistent launch's 32-bit buffer offsets, else 1),
+ * 1 one launch per 64-column step, 2 the last min(steps, 32) steps in one persistent launch after per-step
+ * launches for the others.  Same factor to rounding. */
 enum {
   OMB_DEBUG_SPIN_LIMIT = 1,
   OMB_DEBUG_COV_TABLE = 2,

@@ -153,11 +153,11 @@ constexpr int kCholSpinFault = -2147483647;
 // the fused step's flag as an agent-scope release / acquire (tools/ablate/ablate_chol)
 // kCholPersistent (round 4): the whole factorisation in one launch (chol_persist_kernel; kCholBlocked when A is too
 // large for its 32-bit buffer offsets)
-// kCholAuto (launch_cholesky): kCholPersistent up to kCholPersistMaxN, kCholBlocked above (the persistent launch's
-// ticketed trailing updates fall behind the per-step launches' when the trailing matrix is large:
-// N = 3000 1.154 vs 1.215 ms, N = 5000 3.77 vs 2.67 ms, gpurun_out/r04_o2)
+// kCholPersistent: the last min(t, 32) of the t 64-column steps in one persistent launch, the steps before it as
+// per-step launches (their trailing updates are faster while the trailing matrix is large; omb_linalg.hip
+// chol_hybrid_k0).  kCholAuto (launch_cholesky) = kCholPersistent where A fits its 32-bit buffer offsets, else
+// kCholBlocked.
 enum { kCholTwoLaunch = 0, kCholFused = 1, kCholBlocked = 2, kCholBlockedAcqRel = 3, kCholPersistent = 4, kCholAuto = 5 };
-constexpr int64_t kCholPersistMaxN = 3584;
 int64_t chol_ws_doubles(int64_t N);
 hipError_t launch_cholesky(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws,
                            int spin_limit = kDefaultSpinLimit);

@@ -1314,16 +1314,40 @@ __device__ __forceinline__ void chol_persist_update(__amdgpu_buffer_rsrc_t ra, d
 }
 
 // bulk tasks of step k (see above): P(i, k) for i = k+2 .. t−1, then the update tiles by columns
-__device__ __forceinline__ int chol_persist_step_tasks(int t, int k) {
+// k0 > 0 (chol_persist_kernel after k0 per-step launches): step k0's panel column is already in A, so step k0 has
+// only its update tasks
+__host__ __device__ __forceinline__ int chol_persist_np(int t, int k, int k0) {
+  return (k0 > 0 && k == k0) ? 0 : (t - k - 2 > 0 ? t - k - 2 : 0);
+}
+__host__ __device__ __forceinline__ int chol_persist_step_tasks(int t, int k, int k0 = 0) {
   const int m = t - k - 1;
-  const int np = t - k - 2 > 0 ? t - k - 2 : 0;
   const int nu = m > 1 ? m * (m + 1) / 2 - 1 : 0;
-  return np + nu;
+  return chol_persist_np(t, k, k0) + nu;
+}
+
+// The sync words of one persistent launch: all zero, except (k0 > 0) the state the per-step launches leave — step
+// k0's panel tiles published (pflag(i, k0) = 4) and every trailing tile updated through step k0 − 1 (cnt = k0).
+// One launch in place of a memset; k0 = 0 also zeroes info (the per-step path's first kernel does that otherwise).
+__global__ __launch_bounds__(256) void chol_persist_init_kernel(int* __restrict__ ints, int t, int k0,
+                                                                int* __restrict__ info) {
+  const int n = t + 2 * t * t + 2;
+  for (int x = threadIdx.x; x < n; x += 256) {
+    int v = 0;
+    if (k0 > 0 && x >= t && x < t + t * t) {
+      const int i = (x - t) / t, k = (x - t) % t;
+      v = (k == k0 && i > k0) ? 4 : 0;
+    } else if (k0 > 0 && x >= t + t * t && x < t + 2 * t * t) {
+      const int i = (x - t - t * t) / t, j = (x - t - t * t) % t;
+      v = (j > k0 && j <= i) ? k0 : 0;
+    }
+    ints[x] = v;
+  }
+  if (threadIdx.x == 0 && k0 == 0) *info = 0;
 }
 
 __global__ __launch_bounds__(256, kPersistWgPerCu) void chol_persist_kernel(double* __restrict__ A, int64_t N, int64_t lda, int t,
                                                               int total, double* __restrict__ Wf, CholSync sync,
-                                                              int* __restrict__ info, int spin_limit) {
+                                                              int* __restrict__ info, int spin_limit, int k0) {
   __shared__ __attribute__((aligned(16))) double Ds[kNB * kDP];
   __shared__ __attribute__((aligned(16))) double Lp[kNB * kDP];
   __shared__ __attribute__((aligned(16))) double Wl[4 * kWlP];
@@ -1348,10 +1372,20 @@ __global__ __launch_bounds__(256, kPersistWgPerCu) void chol_persist_kernel(doub
                                                              : (row == col ? 1.0 : 0.0);
         }
     };
-    load_av(0);
+    // k0 > 0: the per-step launches factored blocks 0 .. k0 and formed panel column k0; the walk starts at k0 + 1
+    // from the panel tile (k0 + 1, k0) in A
+    const int kstart = k0 > 0 ? k0 + 1 : 0;
+    if (kstart > 0) {
+      const int64_t rb = (int64_t)kstart * kNB, cb = (int64_t)k0 * kNB;
+      for (int x = tid; x < kNB * kNB; x += 256) {
+        const int r = x >> 6, cc = x & 63;
+        Lp[r * kDP + cc] = rb + r < N ? ld_sc1(A + (rb + r) * lda + cb + cc) : 0.0;
+      }
+    }
+    load_av(kstart);
     if (tid < kBlkFlags) fl[tid] = 0;
     __syncthreads();
-    for (int k = 0; k < t; ++k) {
+    for (int k = kstart; k < t; ++k) {
       OMB_PDBG(0, 1000 * k + 1);
       OMB_PTIME(8 * k + 0);
       const int64_t r0 = (int64_t)k * kNB;
@@ -1381,7 +1415,7 @@ __global__ __launch_bounds__(256, kPersistWgPerCu) void chol_persist_kernel(doub
           }
         }
       }
-      if (k > 0 && w >= 2) {   // the previous step's panel tile (k, k − 1): this wave's rows drained, its share
+      if (k > kstart && w >= 2) {   // the previous step's panel tile (k, k − 1): this wave's rows drained, its share
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_fetch_add(sync.pflag + k * t + k - 1, lane == 0 ? 2 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
@@ -1441,13 +1475,13 @@ __global__ __launch_bounds__(256, kPersistWgPerCu) void chol_persist_kernel(doub
       OMB_PDBG(8 * blockIdx.x + 1, 99);
       return;
     }
-    int k = 0;
+    int k = k0;
     for (; k < t; ++k) {
-      const int nk = chol_persist_step_tasks(t, k);
+      const int nk = chol_persist_step_tasks(t, k, k0);
       if (q < nk) break;
       q -= nk;
     }
-    const int np = t - k - 2 > 0 ? t - k - 2 : 0;
+    const int np = chol_persist_np(t, k, k0);
     if (q < np) {
       const int i = k + 2 + q;
       if (w == 0 && chol_poll_ge(sync.wflag + k, 1, sync, spin_limit, info))
@@ -2451,8 +2485,10 @@ constexpr int g_chol_update_delay = 0;
 
 // Round 4: the diagonal blocks by tiles of 16 (chol64_blocked), one launch per step with the next panel inside.
 static hipError_t launch_cholesky_blocked(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws,
-                                          int spin_limit, int acq_rel) {
-  const int steps = (int)((N + kNB - 1) / kNB);
+                                          int spin_limit, int acq_rel, int steps_limit) {
+  int steps = (int)((N + kNB - 1) / kNB);
+  // steps_limit k0 ≥ 1: only the launches that factor blocks 0 .. k0 and form panel columns 0 .. k0
+  if (steps_limit > 0 && steps_limit + 1 < steps) steps = steps_limit + 1;
   const bool vec = (lda % 2 == 0) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
   int* flags = reinterpret_cast<int*>(ws + kCholWsDoubles);
   hipLaunchKernelGGL(chol_diag_blk_kernel, dim3(1), dim3(256), 0, stream, A, N, lda, ws, info, flags, steps);
@@ -2469,6 +2505,25 @@ static hipError_t launch_cholesky_blocked(hipStream_t stream, double* A, int64_t
     e = hipGetLastError();
   }
   return e;
+}
+
+// Per-step launches before the persistent one (k0, launch_cholesky_persist); tools/ablate sets it, the library
+// picks it from the number of 64-column steps t.
+#ifdef OMB_TOOLS_KNOBS
+static int g_chol_hybrid_k0 = -1;
+void set_chol_hybrid_k0(int k0) { g_chol_hybrid_k0 = k0; }
+#else
+constexpr int g_chol_hybrid_k0 = -1;
+#endif
+// The persistent launch's trailing updates keep up with the walk once ≤ ≈ 32 block columns remain; before that the
+// per-step launches' (three workgroups per CU, LDS-staged) are faster.  GPU-side times, k0 swept
+// (tools/ablate/chol_hybrid_sweep, gpurun_out/r04_w): N = 3000 per-step 1.093, persistent 1.092, k0 = 12-16
+// 0.996-0.999 ms; N = 4000 1.701 / 2.166 / k0 = 24-32 1.583-1.586; N = 5000 2.566 / 3.889 / k0 = 48 2.487; N ≤ 2000
+// (t ≤ 32) the persistent launch alone.
+constexpr int kCholPersistSteps = 32;
+static int chol_hybrid_k0(int t) {
+  if (g_chol_hybrid_k0 >= 0) return g_chol_hybrid_k0;
+  return t > kCholPersistSteps ? t - kCholPersistSteps : 0;
 }
 
 // Round 4: one persistent launch (chol_persist_kernel), kPersistWgPerCu workgroups per CU.
@@ -2488,34 +2543,39 @@ static bool chol_persist_fits(int64_t N, int64_t lda) {
   return ((N + kNB) * lda + kNB) * 8 < 0x7fffffff;   // 32-bit buffer offsets (rows past N included)
 }
 
+static hipError_t launch_cholesky_blocked(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws,
+                                          int spin_limit, int acq_rel, int steps_limit = -1);
+
+// k0 > 0: steps 0 .. k0 − 1 as per-step launches (their bulk trailing updates run at three workgroups per CU), the
+// rest in one persistent launch (the diagonal walk without kernel boundaries once the trailing matrix is small).
 static hipError_t launch_cholesky_persist(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws,
-                                          int spin_limit) {
+                                          int spin_limit, int k0 = 0) {
   const int t = (int)((N + kNB - 1) / kNB);
+  if (k0 > t - 2) k0 = 0;
+  hipError_t e = hipSuccess;
+  if (k0 > 0) e = launch_cholesky_blocked(stream, A, N, lda, info, ws, spin_limit, 0, k0);
+  if (e != hipSuccess) return e;
   int total = 0;
-  for (int k = 0; k < t; ++k) {
-    const int m = t - k - 1;
-    total += (t - k - 2 > 0 ? t - k - 2 : 0) + (m > 1 ? m * (m + 1) / 2 - 1 : 0);
-  }
+  for (int k = k0; k < t; ++k) total += chol_persist_step_tasks(t, k, k0);
   double* Wf = ws;
   int* ints = reinterpret_cast<int*>(ws + (int64_t)t * kCholWsDoubles);
-  const size_t nints = (size_t)t + 2 * (size_t)t * t + 2;
   CholSync sync{ints, ints + t, ints + t + t * t, ints + t + 2 * t * t, ints + t + 2 * t * t + 1};
-  hipError_t e = hipMemsetAsync(ints, 0, nints * sizeof(int), stream);
-  if (e == hipSuccess) e = hipMemsetAsync(info, 0, sizeof(int), stream);
-  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(chol_persist_init_kernel, dim3(1), dim3(256), 0, stream, ints, t, k0, info);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
   const int slots = kPersistWgPerCu * device_cus() - 1;
   const int grid = 1 + (total < slots ? total : slots);
   hipLaunchKernelGGL(chol_persist_kernel, dim3((unsigned)grid), dim3(256), 0, stream, A, N, lda, t, total, Wf, sync,
-                     info, spin_limit);
+                     info, spin_limit, k0);
   return hipGetLastError();
 }
 
 hipError_t launch_cholesky_mode(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws, int mode,
                                 int spin_limit) {
   if (N <= 0) return hipSuccess;
-  if (mode == kCholAuto) mode = N <= kCholPersistMaxN ? kCholPersistent : kCholBlocked;
+  if (mode == kCholAuto) mode = kCholPersistent;
   if (mode == kCholPersistent) {
-    if (chol_persist_fits(N, lda)) return launch_cholesky_persist(stream, A, N, lda, info, ws, spin_limit);
+    if (chol_persist_fits(N, lda))
+      return launch_cholesky_persist(stream, A, N, lda, info, ws, spin_limit, chol_hybrid_k0((int)((N + kNB - 1) / kNB)));
     mode = kCholBlocked;
   }
   const int steps = (int)((N + kNB - 1) / kNB);

@@ -337,11 +337,13 @@ int main(int argc, char** argv) {
       {"tile RMAX8 CT4", run_tile<8, 4, 0>},
   };
   const Variant small256[] = {
-      {"tile RMAX16 CT2 (library n<=256)", run_tile<16, 2, 0>},
-      {"RT2 CT2 counter ring (r01 library)", run<2, 2, 8, 0>},
-      {"tile RMAX16 CT2 gen only (2)", run_tile<16, 2, 2>},
-      {"tile RMAX16 CT2 const A (4)", run_tile<16, 2, 4>},
-      {"RT2 CT4 barrier", run<2, 4, 8, 32>},
+      {"RT2 CT2 counter ring (library n<=256)", run<2, 2, 8, 0>},
+      {"RT2 CT4 counter ring", run<2, 4, 8, 0>},
+      {"RT1 CT2 16 waves ring", run<1, 2, 16, 0>},
+      {"RT1 CT4 16 waves ring", run<1, 4, 16, 0>},
+      {"RT2 CT2 16 waves ring", run<2, 2, 16, 0>},
+      {"tile RMAX16 CT2", run_tile<16, 2, 0>},
+      {"RT2 CT2 counter ring again", run<2, 2, 8, 0>},
   };
   const Variant small[] = {
       {"RT2 CT4 barrier (library n<=256)", run<2, 4, 8, 32>},

@@ -75,7 +75,9 @@ def chol_mode(ctx, request):
     ctx.debug_set("chol_mode", 0)
 
 
-@pytest.mark.parametrize("N", [1, 2, 63, 64, 65, 130, 192, 193, 333, 1000, 3000])
+# 2048 / 2049 / 2112 / 2113: 32, 33, 33 and 34 steps — the default schedule's hand-over from per-step launches to the
+# persistent launch at k0 = 0, 1, 1, 2 (max(0, steps − 32))
+@pytest.mark.parametrize("N", [1, 2, 63, 64, 65, 130, 192, 193, 333, 1000, 2048, 2049, 2112, 2113, 3000])
 def test_cholesky_vs_lapack(ctx, chol_mode, N):
     A = spd(N, N)
     wide = np.full((N, N + 5), 7.0)                  # lda > N: the extra columns are never touched

@@ -434,6 +434,12 @@ __device__ __forceinline__ void matern_r2_tab256_x2(double r2a, double r2b, cons
 // division (≈ 10 instructions), so within 2 ulp of npdf; −t²/2 below −746 (t = ±inf from a zero σ) is clamped
 // there, where exp is 0 either way, and NaN stays NaN.
 constexpr double kInvSqrt2Pi = 0.3989422804014327;      // 1/√(2π) rounded
+// Φ for EHVI-2D's stripes: 0.5·erfc(−a/√2) on every range (cephes' ndtr switches to 0.5 + 0.5·erf inside
+// |a| < 1, and lanes on both sides of the switch run both paths); within a few ulp of ndtr.
+__device__ __forceinline__ double ndtr_fast(double a) {
+#pragma clang fp contract(off)
+  return 0.5 * erfc(-(a * kSqrt1_2));
+}
 __device__ __forceinline__ double npdf_fast(double t) {
 #pragma clang fp contract(off)
   double x = -(t * t) * 0.5;
@@ -477,13 +483,13 @@ __device__ __forceinline__ double ehvi2d_point4(double m0, double m1, double v0,
     // x·(1/0) agree, ±inf or NaN)
     const double iA = 1.0 / sA, iB = 1.0 / sB;
     const double tp = (y1[i0 - 1] - m0) * iA;
-    double cdf_p = ndtr(tp), pdf_p = npdf_fast(tp);
+    double cdf_p = ndtr_fast(tp), pdf_p = npdf_fast(tp);
     for (int i = i0; i <= i1; ++i) {
       const double y1p = y1[i - 1], y1i = y1[i], y2i = y2[i - 1];
       const double t = (y1i - m0) * iA;
-      const double cdf_t = ndtr(t), pdf_t = npdf_fast(t);
+      const double cdf_t = ndtr_fast(t), pdf_t = npdf_fast(t);
       const double u = (y2i - m1) * iB;
-      const double p2 = sB * npdf_fast(u) + (y2i - m1) * ndtr(u);     // ψ(y2i, y2i, μ1, σB)
+      const double p2 = sB * npdf_fast(u) + (y2i - m1) * ndtr_fast(u);     // ψ(y2i, y2i, μ1, σB)
       sum1 = sum1 + (y1p - y1i) * cdf_t * p2;
       const double psi_pp = sA * pdf_p + (y1p - m0) * cdf_p;          // ψ(y1[i−1], y1[i−1], μ0, σA)
       const double psi_pi = sA * pdf_t + (y1p - m0) * cdf_t;          // ψ(y1[i−1], y1[i],   μ0, σA)
@@ -501,9 +507,9 @@ __device__ __forceinline__ double ehvi2d_point4(double m0, double m1, double v0,
   if (mode == OMB_EHVI_TEXTBOOK) {
     // the stripe i = P+1 that range(1, n+1) leaves out (quirk 3): ψ(y1P,y1P,μ0,σA)·ψ(r1,r1,μ1,σB)
     const double tP = (y1[P] - m0) / sA;
-    const double psiA = sA * npdf_fast(tP) + (y1[P] - m0) * ndtr(tP);
+    const double psiA = sA * npdf_fast(tP) + (y1[P] - m0) * ndtr_fast(tP);
     const double u = (r1 - m1) / sB;
-    res += psiA * (sB * npdf_fast(u) + (r1 - m1) * ndtr(u));
+    res += psiA * (sB * npdf_fast(u) + (r1 - m1) * ndtr_fast(u));
   }
   return res;
 }

@@ -421,9 +421,14 @@ def main():
     ap.add_argument("--no-kblock", action="store_true")
     ap.add_argument("--chain", default="fused", choices=["fused", "separate", "sobol"])
     ap.add_argument("--stage-timing", action="store_true", help="events around every stage (adds ~5 us/stage)")
-    ap.add_argument("--one-launch", type=int, default=None, choices=[0, 1],
+    ap.add_argument("--timing-stride", type=int, default=8,
+                    help="record the timing events on every s-th step of the timed loop only (each record adds "
+                         "~2.5 us of GPU time to its step: config 2 82.8 us per step with events on every step, "
+                         "77.3-77.8 on every 8th, gpurun_out/r04_ae)")
+    ap.add_argument("--one-launch", type=int, default=None, choices=[0, 1, 2],
                     help="omb_debug_set(FUSED_CHAIN): 0 EHVI-2D and the arg-max as separate launches, 1 as one "
-                         "(default: the library's, 0 — the one launch measured slower)")
+                         "ticketed launch, 2 EHVI-2D reducing to per-workgroup pairs + the arg-max's second pass "
+                         "(default: the library's)")
     ap.add_argument("--argmax-passes", type=int, default=None, choices=[1, 2],
                     help="omb_debug_set(ARGMAX_PASSES): the arg-max as one launch or two (default: the library's, 2)")
     ap.add_argument("--chol-mode", type=int, default=None, choices=[0, 1, 2],
@@ -569,6 +574,7 @@ def main():
     torch.cuda.synchronize()
     if args.chain != "separate":
         # HIP events on the chain's stream: around the posterior (level 1) or every stage (2)
+        ctx.debug_set("timing_stride", args.timing_stride)
         ctx.timing(2 if args.stage_timing else 1)
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -578,6 +584,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     stage_ms = None
+    chains = args.steps
     if args.chain != "separate":
         stage_sum, chains = ctx.timing_read()
         ctx.timing(0)
@@ -641,7 +648,11 @@ def main():
     roofline = {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": load_traffic(n, N),
                 "kernel": f"posterior_kernel (omb_posterior, {n_obj} objective(s), n_train={n}, n_var={d})",
-                "ms_per_launch": post_ms}
+                "ms_per_launch": post_ms,
+                "launches_timed": int(chains),
+                "timing": "HIP events on the chain's stream around the posterior launch"
+                          + (f" of every {args.timing_stride}th timed step" if args.chain != "separate"
+                             and args.timing_stride > 1 else " of every timed step")}
 
     cpu = None
     if rank == 0 and world_size == 1 and not args.no_cpu_baseline:

@@ -92,22 +92,26 @@ const char* omb_last_error(const omb_ctx* ctx);
  * omb_debug_set(ctx, OMB_DEBUG_COV_TABLE, 1) builds K(X, X) / K(X*, X*) (GP-fit state, posterior covariance) with
  * the posterior kernels' table-driven Matern transform instead of the polynomial exp (a parity check of that
  * transform near r = 0; default 0).
- * omb_debug_set(ctx, OMB_DEBUG_FUSED_CHAIN, 1) makes omb_eval_argmax[_sobol] with an EHVI-2D plan run the
- * acquisition and the arg-max in one launch instead of two (bit-identical pair; default 0: the one launch measured
- * 1.9 % / 0.6 % slower on configs 2 / 3, gpurun_out/r04_j).
+ * omb_debug_set(ctx, OMB_DEBUG_FUSED_CHAIN, m) picks how omb_eval_argmax[_sobol] with an EHVI-2D plan runs the
+ * acquisition and the arg-max: 0 the EHVI launch, then the arg-max's passes; 1 one launch (the last workgroup at
+ * an agent-scope ticket reduces: the ticket's same-address atomics serialise, 23 vs 13.5 µs at config 2);
+ * 2 the EHVI launch reducing to one pair per workgroup, then the arg-max's second pass.  Bit-identical pair.
  * omb_debug_set(ctx, OMB_DEBUG_ARGMAX_PASSES, 1) runs the arg-max as one launch (the last workgroup to finish
  * reduces the per-workgroup pairs) instead of two (default 2: config 2 measured 719.6 vs 719.5 M candidates/s,
  * gpurun_out/r04_l; bit-identical pair).
  * omb_debug_set(ctx, OMB_DEBUG_CHOL_MODE, m) picks the Cholesky schedule of omb_cholesky / omb_posterior_samples /
  * omb_gp_fit_state: 0 auto (default: = 2 where A fits the persistent launch's 32-bit buffer offsets, else 1),
  * 1 one launch per 64-column step, 2 the last min(steps, 32) steps in one persistent launch after per-step
- * launches for the others.  Same factor to rounding. */
+ * launches for the others.  Same factor to rounding.
+ * omb_debug_set(ctx, OMB_DEBUG_TIMING_STRIDE, s) records omb_timing's events on every s-th chain only (default 1;
+ * omb_timing_read then averages over the recorded chains), so that a timed loop carries fewer event records. */
 enum {
   OMB_DEBUG_SPIN_LIMIT = 1,
   OMB_DEBUG_COV_TABLE = 2,
   OMB_DEBUG_FUSED_CHAIN = 3,
   OMB_DEBUG_ARGMAX_PASSES = 4,
-  OMB_DEBUG_CHOL_MODE = 5
+  OMB_DEBUG_CHOL_MODE = 5,
+  OMB_DEBUG_TIMING_STRIDE = 6
 };
 int omb_debug_set(omb_ctx* ctx, int what, int64_t value);
 

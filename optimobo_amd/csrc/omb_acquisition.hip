@@ -60,7 +60,11 @@ hipError_t launch_ehvi2d(hipStream_t stream, const double* mu, const double* var
 // EHVI-2D with the arg-max (omb_eval_argmax[_sobol] with an EHVI-2D plan): the values of ehvi2d_kernel, bit for bit,
 // are reduced in the same launch — per wave by shuffles, per workgroup in LDS, per grid by the last workgroup to
 // take the ticket — by the rule of argmax_pass1/2 (higher value, lower index; NaN and −∞ never win).  Two launches
-// (the arg-max's) and the values' round trip through HBM leave the chain.
+// (the arg-max's) and the values' round trip through HBM leave the chain.  With am.ticket == nullptr the launch
+// stops at the per-workgroup pairs (argmax_pass1's output) and argmax_pass2 reduces them: the ticket's
+// same-address agent-scope atomics serialise (≈ 10 ns each, 1024 of them at config 2: 23.3 µs for the one launch
+// against 13.5 µs for the EHVI alone, rocprofv3, gpurun_out/r04_ac).  The grid is at most kArgmaxMaxBlocks
+// workgroups (grid-stride), so the pairs fit the context's arg-max buffer.
 __global__ __launch_bounds__(kAcqThreads) void ehvi2d_argmax_kernel(const double* __restrict__ mu,
                                                                     const double* __restrict__ var, int64_t ld,
                                                                     int64_t N, const double* __restrict__ pf, int P,
@@ -93,6 +97,13 @@ __global__ __launch_bounds__(kAcqThreads) void ehvi2d_argmax_kernel(const double
     }
   }
   argmax_wave_block(bv, bi, red_v, red_i);          // thread 0: the workgroup's pair
+  if (!am.ticket) {                                  // kernel argument: uniform
+    if (threadIdx.x == 0) {
+      am.partials[2 * blockIdx.x] = bv;
+      am.partials[2 * blockIdx.x + 1] = __builtin_bit_cast(double, bi);
+    }
+    return;
+  }
   if (threadIdx.x == 0) {
     // the pair as agent-scope (sc1) stores, complete (vmcnt 0) before the ticket: the ordering the Cholesky's W
     // hand-off uses (chol_publish_w).  An acquire-release ticket made every workgroup write back its XCD's L2
@@ -126,15 +137,21 @@ __global__ __launch_bounds__(kAcqThreads) void ehvi2d_argmax_kernel(const double
   }
 }
 
-int64_t ehvi2d_argmax_blocks(int64_t N) { return acq_grid(4 * N); }
+int64_t ehvi2d_argmax_blocks(int64_t N) {
+  const int64_t b = acq_grid(4 * N);
+  return b < kArgmaxMaxBlocks ? b : kArgmaxMaxBlocks;
+}
 
 hipError_t launch_ehvi2d_argmax(hipStream_t stream, const double* mu, const double* var, int64_t ld, int64_t N,
                                 const double* pf, int P, double r0, double r1, double s00, double s01, int mode,
                                 const ArgmaxOut& am) {
   size_t shm = sizeof(double) * (2 * P + 1);
-  hipLaunchKernelGGL(ehvi2d_argmax_kernel, dim3(acq_grid(4 * N)), dim3(kAcqThreads), shm, stream, mu, var, ld, N, pf,
-                     P, r0, r1, s00, s01, mode, am);
-  return hipGetLastError();
+  const int64_t nb = ehvi2d_argmax_blocks(N);
+  hipLaunchKernelGGL(ehvi2d_argmax_kernel, dim3((unsigned)nb), dim3(kAcqThreads), shm, stream, mu, var, ld, N, pf, P,
+                     r0, r1, s00, s01, mode, am);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || am.ticket) return e;
+  return launch_argmax_reduce(stream, am.partials, (int)nb, am.offset, am.result);
 }
 
 // ------------------------------------------------------------------------------ EHVI 3-D

@@ -59,6 +59,8 @@ struct omb_ctx {
   int sob_d = 0, sob_bits = 0;
   // timing of the fused chain: 5 events per chain (level 2) or 2 around the posterior (level 1)
   int timing = 0;
+  int timing_stride = 1;     // OMB_DEBUG_TIMING_STRIDE: events on every stride-th chain only
+  int64_t timing_calls = 0;  // chains since omb_timing
   std::vector<hipEvent_t> ev;
   size_t ev_used = 0;
   // Thompson sampling: K* | V | μ | σ² | Σ workspace, and Cholesky info + step counters
@@ -87,7 +89,8 @@ struct omb_ctx {
   double* fit_dev = nullptr;
   int spin_limit = kDefaultSpinLimit;
   bool cov_table = false;   // OMB_DEBUG_COV_TABLE
-  bool fused_chain = false;  // OMB_DEBUG_FUSED_CHAIN: EHVI-2D and the arg-max in one launch (off: measured slower)
+  int fused_chain = 0;  // OMB_DEBUG_FUSED_CHAIN: 0 EHVI-2D then the arg-max's passes, 1 one ticketed launch, 2 EHVI
+                        // with the per-workgroup pairs, then the arg-max's second pass
   bool argmax_one_pass = false;  // OMB_DEBUG_ARGMAX_PASSES: 1 (one launch) or 2 (default: measured level)
   int chol_mode = kCholAuto;     // OMB_DEBUG_CHOL_MODE
 };
@@ -348,14 +351,11 @@ int run_chain(omb_ctx* ctx, const double* Xc, bool sobol, int64_t start, int64_t
   if ((N + 31) / 32 > 0x7fffffffLL) return fail(ctx, OMB_EUNSUP, "N=%lld too large", (long long)N);
   const int k = pl.k;
   const size_t nd = (size_t)N;
-  // EHVI-2D with the arg-max in one launch (launch_ehvi2d_argmax) when only the pair is wanted; its per-workgroup
-  // pairs go to the chain workspace past the Sobol points when ctx->partials is too small
+  // EHVI-2D with the arg-max's first pass in its launch (launch_ehvi2d_argmax) when only the pair is wanted; its
+  // per-workgroup pairs (≤ kArgmaxMaxBlocks) go to ctx->partials
   const bool acq_argmax = result_dev && !vals_out && N > 0 && ctx->fused_chain && pl.kind == PLAN_EHVI2D;
-  const int64_t ablocks = acq_argmax ? ehvi2d_argmax_blocks(N) : 0;
   const size_t doubles = 2 * (size_t)k * nd + nd + (nd + 1) / 2 + (sobol ? nd * args.d : 0);
-  const size_t extra = ablocks > kArgmaxMaxBlocks ? 2 * (size_t)ablocks : 0;
-  if ((rc = grow_dev(ctx, &ctx->work, &ctx->work_cap, (doubles + extra ? doubles + extra : 1) * sizeof(double),
-                     "chain workspace")))
+  if ((rc = grow_dev(ctx, &ctx->work, &ctx->work_cap, (doubles ? doubles : 1) * sizeof(double), "chain workspace")))
     return rc;
   double* mu = static_cast<double*>(ctx->work);
   double* var = mu + (size_t)k * nd;
@@ -364,7 +364,7 @@ int run_chain(omb_ctx* ctx, const double* Xc, bool sobol, int64_t start, int64_t
   double* Xs = var + (size_t)k * nd + nd + (nd + 1) / 2;
 
   hipEvent_t* ev = nullptr;
-  if (ctx->timing) {
+  if (ctx->timing && ctx->timing_calls++ % ctx->timing_stride == 0) {
     if (ctx->ev_used + 5 > ctx->ev.size() && ctx->ev.size() < 5 * 4096) {
       for (int i = 0; i < 5 * 64; ++i) {
         hipEvent_t e;
@@ -396,8 +396,9 @@ int run_chain(omb_ctx* ctx, const double* Xc, bool sobol, int64_t start, int64_t
     switch (pl.kind) {
       case PLAN_EHVI2D:
         if (acq_argmax) {
-          const ArgmaxOut am{extra ? mu + doubles : ctx->partials,
-                             reinterpret_cast<unsigned*>(ctx->partials + 2 * kArgmaxMaxBlocks), result_dev, offset};
+          unsigned* ticket = ctx->fused_chain == 1 ? reinterpret_cast<unsigned*>(ctx->partials + 2 * kArgmaxMaxBlocks)
+                                                   : nullptr;
+          const ArgmaxOut am{ctx->partials, ticket, result_dev, offset};
           e = launch_ehvi2d_argmax(ctx->stream, mu, var, N, N, pl.geo, pl.P, pl.r[0], pl.r[1], pl.s00, pl.s01, pl.mode,
                                    am);
         } else {
@@ -520,7 +521,8 @@ int omb_debug_set(omb_ctx* ctx, int what, int64_t value) {
     return OMB_OK;
   }
   if (what == OMB_DEBUG_FUSED_CHAIN) {
-    ctx->fused_chain = value != 0;
+    if (value < 0 || value > 2) return fail(ctx, OMB_EINVAL, "fused chain %lld (0, 1 or 2)", (long long)value);
+    ctx->fused_chain = (int)value;
     return OMB_OK;
   }
   if (what == OMB_DEBUG_ARGMAX_PASSES) {
@@ -530,6 +532,11 @@ int omb_debug_set(omb_ctx* ctx, int what, int64_t value) {
   }
   if (what == OMB_DEBUG_COV_TABLE) {
     ctx->cov_table = value != 0;
+    return OMB_OK;
+  }
+  if (what == OMB_DEBUG_TIMING_STRIDE) {
+    if (value < 1 || value > 0x7fffffff) return fail(ctx, OMB_EINVAL, "timing stride %lld < 1", (long long)value);
+    ctx->timing_stride = (int)value;
     return OMB_OK;
   }
   if (what == OMB_DEBUG_CHOL_MODE) {
@@ -940,6 +947,7 @@ int omb_timing(omb_ctx* ctx, int enable) {
   OMB_HIP(ctx, hipStreamSynchronize(ctx->stream));
   if (enable < 0 || enable > 2) return fail(ctx, OMB_EINVAL, "timing level %d outside [0, 2]", enable);
   ctx->timing = enable;
+  ctx->timing_calls = 0;
   ctx->ev_used = 0;
   // create the events of the first 256 chains now, not inside the timed chains
   while (enable && ctx->ev.size() < 5 * 256) {

@@ -117,6 +117,11 @@ __global__ __launch_bounds__(256) void argmax_onepass(const double* __restrict__
   }
 }
 
+hipError_t launch_argmax_reduce(hipStream_t stream, const double* partials, int nb, int64_t offset, double* result) {
+  hipLaunchKernelGGL(argmax_pass2, dim3(1), dim3(256), 0, stream, partials, nb, offset, result);
+  return hipGetLastError();
+}
+
 hipError_t launch_argmax(hipStream_t stream, const double* vals, int64_t N, int64_t offset, double* partials,
                          double* result, bool one_pass) {
   int64_t nb = (N + 255) / 256;

@@ -58,8 +58,9 @@ hipError_t launch_posterior(hipStream_t stream, const GPArgs& args, int n_obj, i
                             int64_t N, double* mu, double* var);
 
 // EHVI-2D and the arg-max in one launch (omb_acquisition.hip): each workgroup's (value, index) pair goes to
-// `partials` (2 doubles per workgroup, ehvi2d_argmax_blocks(N)); the last workgroup to finish (an agent-scope
-// ticket, 0 between launches) reduces them and writes result = {value, index + offset}.
+// `partials` (2 doubles per workgroup, ehvi2d_argmax_blocks(N) ≤ kArgmaxMaxBlocks); the last workgroup to finish (an
+// agent-scope ticket, 0 between launches) reduces them and writes result = {value, index + offset} — or, with
+// ticket == nullptr, a second launch (argmax_pass2) does.
 struct ArgmaxOut {
   double* partials;
   unsigned* ticket;
@@ -108,6 +109,8 @@ hipError_t launch_ei(hipStream_t stream, int kind, int k, const double* mu, cons
 constexpr int kArgmaxMaxBlocks = 1024;
 hipError_t launch_argmax(hipStream_t stream, const double* vals, int64_t N, int64_t offset, double* partials,
                          double* result, bool one_pass = false);
+// argmax_pass2 alone: nb (value, index) pairs → result {value, index + offset}
+hipError_t launch_argmax_reduce(hipStream_t stream, const double* partials, int nb, int64_t offset, double* result);
 
 // Scrambled Sobol' generation (omb_sobol.hip).  The packed state holds the direction
 // numbers, shift and box of one engine; sobol_pack_state fills a host buffer of

@@ -223,9 +223,14 @@ def test_fused_empty_batch_and_errors(ctx, gp3):
     with pytest.raises(_lib.OMBError) as e:
         ctx.eval_argmax_sobol(0, 16)                            # Sobol d=3 vs n_var=4
     assert e.value.code == _lib.OMB_EINVAL
+    for bad in (-1, 3):
+        with pytest.raises(_lib.OMBError) as e:
+            ctx.debug_set("fused_chain", bad)                   # chain modes are 0, 1, 2
+        assert e.value.code == _lib.OMB_EINVAL
 
 
 def test_stage_timing(ctx, gp3):
+    from optimobo_amd import _lib
     Y = gp3[0]
     _plans(ctx, Y)[0][2]()
     ctx.set_sobol(4, np.zeros(4), np.ones(4), seed=0)
@@ -239,8 +244,18 @@ def test_stage_timing(ctx, gp3):
     for _ in range(2):
         ctx.eval_argmax_sobol(0, 1 << 14)
     ms, n = ctx.timing_read()
-    ctx.timing(0)
     assert n == 2 and ms["posterior"] > 0 and ms["acquisition"] == 0 and ms["sobol"] == 0
+    ctx.debug_set("timing_stride", 3)                # events on chains 0, 3, 6 of 7
+    ctx.timing(1)
+    for _ in range(7):
+        ctx.eval_argmax_sobol(0, 1 << 14)
+    ms, n = ctx.timing_read()
+    ctx.debug_set("timing_stride", 1)
+    ctx.timing(0)
+    assert n == 3 and ms["posterior"] > 0
+    with pytest.raises(_lib.OMBError) as e:
+        ctx.debug_set("timing_stride", 0)
+    assert e.value.code == _lib.OMB_EINVAL
 
 
 # ----------------------------------------------------------------------------- one-launch EHVI-2D chain
@@ -264,8 +279,9 @@ def _ehvi2d_problem(n, d, seed):
     (128, 6, 1 << 16, "reference", 1), (128, 8, 4099, "sigma", 1), (97, 4, 30000, "reference", 0),
     (33, 3, 17, "textbook", 1)])
 def test_one_launch_ehvi2d_chain_equals_separate_launches(n, d, N, mode, cseed):
-    """ehvi2d_argmax_kernel (EHVI-2D and the arg-max in one launch) returns bit for bit the pair of ehvi2d_kernel →
-    argmax_pass1/2 (cache seed 0: s01 < 0, EHVI ≤ 0, ties at 0 decided by the lowest index)."""
+    """ehvi2d_argmax_kernel (EHVI-2D and the arg-max in one launch; or reducing to per-workgroup pairs, then
+    argmax_pass2) returns bit for bit the pair of ehvi2d_kernel → argmax_pass1/2 (cache seed 0: s01 < 0, EHVI ≤ 0,
+    ties at 0 decided by the lowest index)."""
     from optimobo_amd import pareto
     from optimobo_amd.device import AcqContext
     ctx = AcqContext(0)
@@ -277,31 +293,31 @@ def test_one_launch_ehvi2d_chain_equals_separate_launches(n, d, N, mode, cseed):
         ctx.plan_ehvi2d(stripes, r, s00, s01, mode=mode)
         Xc = dev(np.random.default_rng(n + N).uniform(0, 1, (N, d)))
         pairs = {}
-        for variant in (0, 1):
+        for variant in (0, 1, 2):
             ctx.debug_set("fused_chain", variant)
             pairs[variant] = ctx.eval_argmax(Xc, offset=123).cpu().numpy()
         ctx.debug_set("fused_chain", 0)
         vals = ctx.eval(Xc).cpu().numpy()
         ctx.debug_set("fused_chain", 1)
         v, i = oacq.argmax(vals, offset=123)
-        for variant in (0, 1):
+        for variant in (0, 1, 2):
             assert (pairs[variant][0], int(pairs[variant][1])) == (v, i), (variant, pairs[variant], v, i)
         if cseed == 0:
             assert v == 0.0 and i == 123 + int(np.flatnonzero(vals == 0.0)[0])
         # the Sobol entry point takes the same one-launch path
         ctx.set_sobol(d, np.zeros(d), np.ones(d), seed=3)
-        ctx.debug_set("fused_chain", 1)
-        p1 = ctx.eval_argmax_sobol(11, N).cpu().numpy()
-        ctx.debug_set("fused_chain", 0)
-        p0 = ctx.eval_argmax_sobol(11, N).cpu().numpy()
-        assert np.array_equal(p0, p1)
+        ps = []
+        for variant in (1, 2, 0):
+            ctx.debug_set("fused_chain", variant)
+            ps.append(ctx.eval_argmax_sobol(11, N).cpu().numpy())
+        assert np.array_equal(ps[2], ps[0]) and np.array_equal(ps[2], ps[1])
     finally:
         ctx.close()
 
 
 def test_one_launch_ehvi2d_many_stripes_and_blocks():
-    """Many stripes (P = 200) and more workgroups than ctx->partials holds (N = 2^20: the pairs go to the chain
-    workspace): the one-launch pair equals the separate launches'."""
+    """Many stripes (P = 200) and the grid-stride loop (N = 2^20: 16 candidate blocks per workgroup): the one-launch
+    and the pairs-then-reduce pairs equal the separate launches'."""
     from optimobo_amd import pareto
     from optimobo_amd.device import AcqContext
     ctx = AcqContext(0)
@@ -315,11 +331,10 @@ def test_one_launch_ehvi2d_many_stripes_and_blocks():
         ctx.plan_ehvi2d(pareto.stripes_2d(pf), r, s00, s01, mode="textbook")
         for N in (5000, 1 << 20):
             Xc = dev(np.random.default_rng(N).uniform(0, 1, (N, 4)))
-            ctx.debug_set("fused_chain", 1)
-            pair = ctx.eval_argmax(Xc).cpu().numpy()
             v, i = oacq.argmax(ctx.eval(Xc).cpu().numpy())
-            assert (pair[0], int(pair[1])) == (v, i), N
-            ctx.debug_set("fused_chain", 0)
-            assert np.array_equal(ctx.eval_argmax(Xc).cpu().numpy(), pair)
+            for variant in (1, 2, 0):
+                ctx.debug_set("fused_chain", variant)
+                pair = ctx.eval_argmax(Xc).cpu().numpy()
+                assert (pair[0], int(pair[1])) == (v, i), (N, variant)
     finally:
         ctx.close()

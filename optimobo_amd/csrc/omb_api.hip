@@ -47,6 +47,7 @@ struct omb_ctx {
   double* partials = nullptr;  // argmax pass-1 output
   double* result_dev = nullptr;
   double* result_host = nullptr;  // pinned
+  int* info_host = nullptr;       // pinned: the Cholesky status read back by run_cholesky / chol_wait
   // fused chain
   Plan plan;
   void* geo = nullptr;    // device: plan geometry
@@ -452,6 +453,7 @@ int omb_create(int device, omb_ctx** out) {
       hipMemset(ctx->partials, 0, sizeof(double) * (2 * kArgmaxMaxBlocks + 2)) != hipSuccess ||
       hipMalloc(&ctx->result_dev, sizeof(double) * 2) != hipSuccess ||
       hipHostMalloc(&ctx->result_host, sizeof(double) * 2, hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc(&ctx->info_host, sizeof(int) * 4, hipHostMallocDefault) != hipSuccess ||
       hipMalloc(&ctx->sob, sobol_state_bytes(OMB_MAX_DIM, 32)) != hipSuccess ||
       hipHostMalloc(&ctx->fault_host, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->fault_dev), ctx->fault_host, 0) != hipSuccess ||
@@ -476,6 +478,7 @@ int omb_destroy(omb_ctx* ctx) {
   if (ctx->partials) (void)hipFree(ctx->partials);
   if (ctx->result_dev) (void)hipFree(ctx->result_dev);
   if (ctx->result_host) (void)hipHostFree(ctx->result_host);
+  if (ctx->info_host) (void)hipHostFree(ctx->info_host);
   if (ctx->geo) (void)hipFree(ctx->geo);
   if (ctx->stage) (void)hipHostFree(ctx->stage);
   if (ctx->work) (void)hipFree(ctx->work);
@@ -1020,7 +1023,10 @@ static hipError_t cov_build(omb_ctx* ctx, const ObjState& s, const double* Xc, i
 }
 
 // In-place lower Cholesky of A + jitter·I; synchronises and returns LAPACK's info in *info.
-static int run_cholesky(omb_ctx* ctx, double* A, int64_t N, int64_t lda, double jitter, int* info) {
+// The factorisation in two halves, so that a caller can queue work that reads the factor before it waits for the
+// status: chol_enqueue queues A += jitter·I, the factor and the status's copy into pinned memory; chol_wait
+// synchronises and reads it.
+static int chol_enqueue(omb_ctx* ctx, double* A, int64_t N, int64_t lda, double jitter) {
   // [info int | pad to 16 B | factor workspace (chol_ws_doubles)]
   int rc = grow_dev(ctx, &ctx->ichol, &ctx->ichol_cap, 16 + sizeof(double) * chol_ws_doubles(N), "Cholesky workspace");
   if (rc) return rc;
@@ -1028,14 +1034,23 @@ static int run_cholesky(omb_ctx* ctx, double* A, int64_t N, int64_t lda, double 
   double* ws = reinterpret_cast<double*>(static_cast<char*>(ctx->ichol) + 16);
   OMB_HIP(ctx, launch_add_diag(ctx->stream, A, N, lda, jitter));
   OMB_HIP(ctx, launch_cholesky_mode(ctx->stream, A, N, lda, dinfo, ws, ctx->chol_mode, ctx->spin_limit));
-  int h = 0;
-  OMB_HIP(ctx, hipMemcpyAsync(&h, dinfo, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  OMB_HIP(ctx, hipMemcpyAsync(ctx->info_host, dinfo, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  return OMB_OK;
+}
+
+static int chol_wait(omb_ctx* ctx, int* info) {
   OMB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  const int h = *ctx->info_host;
   if (h == kCholSpinFault)
     return fail(ctx, OMB_EHIP, "Cholesky: a workgroup's wait for the diagonal block exceeded %d polls; the factor is "
                                "invalid", ctx->spin_limit);
   *info = h;
   return OMB_OK;
+}
+
+static int run_cholesky(omb_ctx* ctx, double* A, int64_t N, int64_t lda, double jitter, int* info) {
+  int rc = chol_enqueue(ctx, A, N, lda, jitter);
+  return rc ? rc : chol_wait(ctx, info);
 }
 
 int omb_posterior_cov(omb_ctx* ctx, int obj, const double* Xc_dev, int64_t N, double* mu_dev, double* cov_dev) {
@@ -1099,14 +1114,17 @@ int omb_posterior_samples(omb_ctx* ctx, int obj, const double* Xc_dev, int64_t N
   for (; t < max_tries; ++t, jit *= 10.0) {
     if ((e = cov_build(ctx, s, Xc_dev, N, V, S, N, cws, jit)) != hipSuccess)   // Σ + jit·I
       return hip_fail(ctx, e, "posterior_samples (cov)");
-    if ((rc = run_cholesky(ctx, S, N, N, 0.0, &info))) return rc;
+    if ((rc = chol_enqueue(ctx, S, N, N, 0.0))) return rc;
+    // the draws are queued before the status is read (no idle GPU between the factor and them); a failed factor's
+    // draws are overwritten by the next try's
+    if ((e = launch_chol_samples(ctx->stream, S, N, N, mu, Zt_dev, B, Y_dev, cws)) != hipSuccess)
+      return hip_fail(ctx, e, "posterior_samples (samples)");
+    if ((rc = chol_wait(ctx, &info))) return rc;
     if (info == 0) break;
   }
   if (info != 0)
     return fail(ctx, OMB_ENOTPD, "posterior covariance + %g I is not positive definite (column %d) after %d tries",
                 jit / 10.0, info, max_tries);
-  if ((e = launch_chol_samples(ctx->stream, S, N, N, mu, Zt_dev, B, Y_dev, cws)) != hipSuccess)
-    return hip_fail(ctx, e, "posterior_samples (samples)");
   if (jitter_used) *jitter_used = jit;
   return OMB_OK;
 }

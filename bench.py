@@ -433,6 +433,9 @@ def main():
                     help="omb_debug_set(ARGMAX_PASSES): the arg-max as one launch or two (default: the library's, 2)")
     ap.add_argument("--chol-mode", type=int, default=None, choices=[0, 1, 2],
                     help="omb_debug_set(CHOL_MODE): Cholesky auto / per-step launches / one persistent launch")
+    ap.add_argument("--uniform-train", action="store_true",
+                    help="train on X uniform in [0, 1]^d (SURVEY 8d) instead of the config's mid-run BO box "
+                         "(configs 2-5); the step's work is the same, the arg-max lands on the unexplored corner")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks and the process group only, print what torch.distributed saw")
     ap.add_argument("--cache-seed", type=int, default=1,
@@ -484,6 +487,8 @@ def main():
 
     n, d, acq_kind = cfg["n"], cfg["d"], cfg["acq"]
     N = 1 << (args.log2_cand if args.log2_cand is not None else cfg["log2"])
+    if args.uniform_train:                           # SURVEY §8(d)'s training set: X uniform in [0, 1]^d
+        cfg = {k: v for k, v in cfg.items() if k not in ("x_lo", "tail_hi")}
     X, Y, ls, variances = setup_problem(n, d, problem=cfg["problem"], x_lo=cfg.get("x_lo", 0.0),
                                         tail_hi=cfg.get("tail_hi", 1.0))
     k_obj = Y.shape[1]
@@ -718,7 +723,8 @@ def main():
             out["best"]["note"] = ("reference-mode EHVI passes sigma_B = var_0*s01 (util_functions.py:163-167); this "
                                    f"cache has s01 = {s01:.4g} < 0, so the acquisition is <= 0 everywhere and the "
                                    "arg-max is the lowest index among its maxima (DESIGN.md section 2, quirk 2)")
-        if acq_kind == "ehvi3d":
+        out["config"]["train_box"] = f"[0, 1]^{d} (uniform, SURVEY 8d)"
+        if "x_lo" in cfg:
             out["config"]["train_box"] = f"[{cfg['x_lo']}, 1]^{d}"
         if "tail_hi" in cfg:
             out["config"]["train_box"] = f"x_1 in [0, 1], x_2..x_{d} in [0, {cfg['tail_hi']}]"

@@ -1,0 +1,22 @@
+# Round 4, call ak: persistent Cholesky workers poll a task's flags together (no ticket prefetch)
+# (Measured slower and reverted; see DESIGN §9a "Worker latency".)
+# together: check tool (bitwise vs per-step, watchdog), phases at N = 3000, hybrid k0 sweep, turbo tests, config 6
+# A/B against the previous commit's library (tools/ablate/prev, swapped on the box's copy only).
+set -e
+O=gpurun_out/${1:-r04_ak}
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 60 ./tools/ablate/chol_persist_check 65536 130 200 1000 2000 3000 3500 5000 > $O/check.txt 2>&1
+
+CHOL_K0S=8,15 timeout -k 10 200 ./tools/ablate/chol_hybrid_sweep 3000 5000 > $O/sweep.txt 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_gpu_turbo.py -x -q --timeout 300 --timeout-method thread > $O/turbo_tests.txt 2>&1
+cp optimobo_amd/liboptimobo_hip.so $O/../new_lib.so.tmp
+for r in a b; do
+  cp $O/../new_lib.so.tmp optimobo_amd/liboptimobo_hip.so
+  timeout -k 10 200 python -u bench.py --config 6 --steps 100 --warmup 10 --no-cpu-baseline > $O/c6_new_$r.json 2>&1
+  cp tools/ablate/prev/liboptimobo_hip.so optimobo_amd/liboptimobo_hip.so
+  timeout -k 10 200 python -u bench.py --config 6 --steps 100 --warmup 10 --no-cpu-baseline > $O/c6_prev_$r.json 2>&1
+done
+cp $O/../new_lib.so.tmp optimobo_amd/liboptimobo_hip.so
+rm -f $O/../new_lib.so.tmp
+echo done

@@ -20,9 +20,12 @@ static unsigned acq_grid(int64_t N) {
 }
 
 // ------------------------------------------------------------------------------ EHVI 2-D
-// Four lanes per candidate (ehvi2d_point4, omb_math.h — shared with the one-launch chains, so both give bitwise the
-// same values and the same arg-max): wave w of a workgroup takes 16 candidates, lane group g = lane >> 4 a quarter of
-// their stripes.
+// L lanes per candidate (ehvi2d_point<L>, omb_math.h — shared with the one-launch chain, so both give bitwise the
+// same values and the same arg-max): wave w of a workgroup takes 64/L candidates, lane group g = lane / (64/L) an
+// L-th of their stripes.  L by batch size (ehvi2d_lanes): four lanes while the batch leaves SIMDs short of waves.
+int ehvi2d_lanes(int64_t N) { return N >= (1 << 19) ? 1 : (N >= (1 << 18) ? 2 : 4); }
+
+template <int L>
 __global__ __launch_bounds__(kAcqThreads) void ehvi2d_kernel(const double* __restrict__ mu,
                                                              const double* __restrict__ var, int64_t ld, int64_t N,
                                                              const double* __restrict__ pf, int P, double r0,
@@ -37,13 +40,14 @@ __global__ __launch_bounds__(kAcqThreads) void ehvi2d_kernel(const double* __res
   }
   if (threadIdx.x == 0) y1[0] = r0;
   __syncthreads();
-  const int lane = threadIdx.x & 63, g = lane >> 4;
-  const int64_t per_block = kAcqThreads / 4;
+  constexpr int CPW = 64 / L;                            // candidates per wave
+  const int lane = threadIdx.x & 63, g = lane / CPW;
+  const int64_t per_block = kAcqThreads / L;
   for (int64_t base = (int64_t)blockIdx.x * per_block; base < N; base += (int64_t)gridDim.x * per_block) {
-    const int64_t c = base + 16 * (threadIdx.x >> 6) + (lane & 15);
+    const int64_t c = base + CPW * (threadIdx.x >> 6) + (lane % CPW);
     const int64_t cc = c < N ? c : N - 1;                // every lane of the wave takes part in the shuffles
-    const double v = ehvi2d_point4(mu[cc], mu[ld + cc], var[cc], mode == OMB_EHVI_REFERENCE ? 0.0 : var[ld + cc], y1,
-                                   y2, P, r1, s00, s01, mode, g);
+    const double v = ehvi2d_point<L>(mu[cc], mu[ld + cc], var[cc], mode == OMB_EHVI_REFERENCE ? 0.0 : var[ld + cc],
+                                     y1, y2, P, r1, s00, s01, mode, g);
     if (g == 0 && c < N) out[c] = v;
   }
 }
@@ -52,8 +56,16 @@ hipError_t launch_ehvi2d(hipStream_t stream, const double* mu, const double* var
                          const double* pf, int P, double r0, double r1, double s00, double s01, int mode,
                          double* out) {
   size_t shm = sizeof(double) * (2 * P + 1);
-  hipLaunchKernelGGL(ehvi2d_kernel, dim3(acq_grid(4 * N)), dim3(kAcqThreads), shm, stream, mu, var, ld, N, pf, P, r0,
-                     r1, s00, s01, mode, out);
+  const int L = ehvi2d_lanes(N);
+  if (L == 4)
+    hipLaunchKernelGGL(ehvi2d_kernel<4>, dim3(acq_grid(4 * N)), dim3(kAcqThreads), shm, stream, mu, var, ld, N, pf, P,
+                       r0, r1, s00, s01, mode, out);
+  else if (L == 2)
+    hipLaunchKernelGGL(ehvi2d_kernel<2>, dim3(acq_grid(2 * N)), dim3(kAcqThreads), shm, stream, mu, var, ld, N, pf, P,
+                       r0, r1, s00, s01, mode, out);
+  else
+    hipLaunchKernelGGL(ehvi2d_kernel<1>, dim3(acq_grid(N)), dim3(kAcqThreads), shm, stream, mu, var, ld, N, pf, P, r0,
+                       r1, s00, s01, mode, out);
   return hipGetLastError();
 }
 
@@ -65,6 +77,7 @@ hipError_t launch_ehvi2d(hipStream_t stream, const double* mu, const double* var
 // same-address agent-scope atomics serialise (≈ 10 ns each, 1024 of them at config 2: 23.3 µs for the one launch
 // against 13.5 µs for the EHVI alone, rocprofv3, gpurun_out/r04_ac).  The grid is at most kArgmaxMaxBlocks
 // workgroups (grid-stride), so the pairs fit the context's arg-max buffer.
+template <int L>
 __global__ __launch_bounds__(kAcqThreads) void ehvi2d_argmax_kernel(const double* __restrict__ mu,
                                                                     const double* __restrict__ var, int64_t ld,
                                                                     int64_t N, const double* __restrict__ pf, int P,
@@ -82,15 +95,16 @@ __global__ __launch_bounds__(kAcqThreads) void ehvi2d_argmax_kernel(const double
   }
   if (threadIdx.x == 0) y1[0] = r0;
   __syncthreads();
-  const int lane = threadIdx.x & 63, g = lane >> 4, wave = threadIdx.x >> 6;
-  const int64_t per_block = kAcqThreads / 4;
+  constexpr int CPW = 64 / L;
+  const int lane = threadIdx.x & 63, g = lane / CPW, wave = threadIdx.x >> 6;
+  const int64_t per_block = kAcqThreads / L;
   double bv = -__builtin_inf();
   long long bi = -1;
   for (int64_t base = (int64_t)blockIdx.x * per_block; base < N; base += (int64_t)gridDim.x * per_block) {
-    const int64_t c = base + 16 * wave + (lane & 15);
+    const int64_t c = base + CPW * wave + (lane % CPW);
     const int64_t cc = c < N ? c : N - 1;
-    const double v = ehvi2d_point4(mu[cc], mu[ld + cc], var[cc], mode == OMB_EHVI_REFERENCE ? 0.0 : var[ld + cc], y1,
-                                   y2, P, r1, s00, s01, mode, g);
+    const double v = ehvi2d_point<L>(mu[cc], mu[ld + cc], var[cc], mode == OMB_EHVI_REFERENCE ? 0.0 : var[ld + cc],
+                                     y1, y2, P, r1, s00, s01, mode, g);
     if (g == 0 && c < N && v == v && v > -__builtin_inf() && argmax_better(v, c, bv, bi)) {
       bv = v;
       bi = c;
@@ -138,7 +152,7 @@ __global__ __launch_bounds__(kAcqThreads) void ehvi2d_argmax_kernel(const double
 }
 
 int64_t ehvi2d_argmax_blocks(int64_t N) {
-  const int64_t b = acq_grid(4 * N);
+  const int64_t b = acq_grid(ehvi2d_lanes(N) * N);
   return b < kArgmaxMaxBlocks ? b : kArgmaxMaxBlocks;
 }
 
@@ -147,8 +161,16 @@ hipError_t launch_ehvi2d_argmax(hipStream_t stream, const double* mu, const doub
                                 const ArgmaxOut& am) {
   size_t shm = sizeof(double) * (2 * P + 1);
   const int64_t nb = ehvi2d_argmax_blocks(N);
-  hipLaunchKernelGGL(ehvi2d_argmax_kernel, dim3((unsigned)nb), dim3(kAcqThreads), shm, stream, mu, var, ld, N, pf, P,
-                     r0, r1, s00, s01, mode, am);
+  const int L = ehvi2d_lanes(N);
+  if (L == 4)
+    hipLaunchKernelGGL(ehvi2d_argmax_kernel<4>, dim3((unsigned)nb), dim3(kAcqThreads), shm, stream, mu, var, ld, N, pf,
+                       P, r0, r1, s00, s01, mode, am);
+  else if (L == 2)
+    hipLaunchKernelGGL(ehvi2d_argmax_kernel<2>, dim3((unsigned)nb), dim3(kAcqThreads), shm, stream, mu, var, ld, N, pf,
+                       P, r0, r1, s00, s01, mode, am);
+  else
+    hipLaunchKernelGGL(ehvi2d_argmax_kernel<1>, dim3((unsigned)nb), dim3(kAcqThreads), shm, stream, mu, var, ld, N, pf,
+                       P, r0, r1, s00, s01, mode, am);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || am.ticket) return e;
   return launch_argmax_reduce(stream, am.partials, (int)nb, am.offset, am.result);

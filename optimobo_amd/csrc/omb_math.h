@@ -447,18 +447,20 @@ __device__ __forceinline__ double npdf_fast(double t) {
   return exp_nonpos(x) * kInvSqrt2Pi;
 }
 
-// EHVI-2D of one candidate over four lanes: util_functions.py:81-128 (EHVI_2D_aux) with the stripe array
-// S = [(r0,−∞), PF↑f2, (−∞,r1)] of :93-109; y1[0] = r0, y1[i] / y2[i−1] = stripe i's f1 / f2 (i = 1..P).
-// Lane g (0..3; the candidate's four lanes are l, l^16, l^32, l^48 of one wave) sums the stripes of the g-th
-// contiguous quarter of 1..P; within a quarter φ/Φ of t_i = (y1[i]−μ0)/σA are reused by stripe i+1 (the
+// EHVI-2D of one candidate over L lanes (L = 1, 2, 4): util_functions.py:81-128 (EHVI_2D_aux) with the stripe
+// array S = [(r0,−∞), PF↑f2, (−∞,r1)] of :93-109; y1[0] = r0, y1[i] / y2[i−1] = stripe i's f1 / f2 (i = 1..P).
+// Lane g (0..L−1; the candidate's lanes are l, l + 64/L, … of one wave) sums the stripes of the g-th
+// contiguous L-th of 1..P; within a quarter φ/Φ of t_i = (y1[i]−μ0)/σA are reused by stripe i+1 (the
 // reference evaluates ψ(y1[i−1], y1[i−1]) from the same t), so a stripe costs 2 Φ + 2 φ instead of 7 calls, and a
 // quarter one Φ + φ more for its first t.  The quarters' partial sums meet by two xor-shuffles: every lane of the
 // candidate returns the same value, identical in every kernel that calls this (ehvi2d_kernel and the one-launch
-// chains), which is what makes their arg-max bitwise the same.  One lane per candidate (the round-3 kernel) summed
-// all P stripes serially: 4× the latency for the same issue count.
-__device__ __forceinline__ double ehvi2d_point4(double m0, double m1, double v0, double v1, const double* y1,
-                                                const double* y2, int P, double r1, double s00, double s01, int mode,
-                                                int g) {
+// chains), which is what makes their arg-max bitwise the same.  One lane per candidate (the round-3 kernel) sums
+// all P stripes serially: 4× the latency, but no lane idles on a short last quarter and no quarter pays its own
+// first Φ + φ — the kernels take L = 1 for batches large enough to fill every SIMD with waves (ehvi2d_lanes).
+template <int L>
+__device__ __forceinline__ double ehvi2d_point(double m0, double m1, double v0, double v1, const double* y1,
+                                               const double* y2, int P, double r1, double s00, double s01, int mode,
+                                               int g) {
 #pragma clang fp contract(off)
   double sA, sB;
   bool nan = false;
@@ -475,7 +477,7 @@ __device__ __forceinline__ double ehvi2d_point4(double m0, double m1, double v0,
     sA = v0;
     sB = v1;
   }
-  const int chunk = (P + 3) >> 2;
+  const int chunk = (P + L - 1) / L;
   const int i0 = 1 + g * chunk, i1 = min(P, (g + 1) * chunk);
   double sum1 = 0.0, sum2 = 0.0;
   if (!nan && i0 <= i1) {
@@ -498,10 +500,15 @@ __device__ __forceinline__ double ehvi2d_point4(double m0, double m1, double v0,
       pdf_p = pdf_t;
     }
   }
-  sum1 += __shfl_xor(sum1, 16);
-  sum1 += __shfl_xor(sum1, 32);
-  sum2 += __shfl_xor(sum2, 16);
-  sum2 += __shfl_xor(sum2, 32);
+  if constexpr (L == 4) {
+    sum1 += __shfl_xor(sum1, 16);
+    sum1 += __shfl_xor(sum1, 32);
+    sum2 += __shfl_xor(sum2, 16);
+    sum2 += __shfl_xor(sum2, 32);
+  } else if constexpr (L == 2) {
+    sum1 += __shfl_xor(sum1, 32);
+    sum2 += __shfl_xor(sum2, 32);
+  }
   if (nan) return __builtin_nan("");
   double res = sum1 + sum2;
   if (mode == OMB_EHVI_TEXTBOOK) {

@@ -22,8 +22,9 @@ static unsigned acq_grid(int64_t N) {
 // ------------------------------------------------------------------------------ EHVI 2-D
 // L lanes per candidate (ehvi2d_point<L>, omb_math.h — shared with the one-launch chain, so both give bitwise the
 // same values and the same arg-max): wave w of a workgroup takes 64/L candidates, lane group g = lane / (64/L) an
-// L-th of their stripes.  L by batch size (ehvi2d_lanes): four lanes while the batch leaves SIMDs short of waves.
-int ehvi2d_lanes(int64_t N) { return N >= (1 << 19) ? 1 : (N >= (1 << 18) ? 2 : 4); }
+// L-th of their stripes.  L by batch size (ehvi2d_lanes): more lanes per candidate only while the batch leaves SIMDs
+// short of waves (config 3's 2^20: one lane, EHVI 197 → 135 µs; config 2's 2^16: two lanes, 15.6 → 14.0 µs).
+int ehvi2d_lanes(int64_t N) { return N >= (1 << 19) ? 1 : (N >= (1 << 16) ? 2 : 4); }
 
 template <int L>
 __global__ __launch_bounds__(kAcqThreads) void ehvi2d_kernel(const double* __restrict__ mu,

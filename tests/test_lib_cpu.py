@@ -63,3 +63,14 @@ def test_host_limits_match_header():
     assert val["MAX_DIM"] == _lib.MAX_DIM
     assert val["MAX_TRAIN"] == _lib.MAX_TRAIN
     assert val["MAX_TRAIN_DENSE"] == _lib.MAX_TRAIN_DENSE
+
+
+def test_debug_knob_codes_match_header():
+    """The ctypes layer's omb_debug_set codes are the header's OMB_DEBUG_* enum values."""
+    import re
+
+    from optimobo_amd import _lib
+    src = open(os.path.join(REPO, "include", "optimobo_hip.h")).read()
+    val = {m.group(1): int(m.group(2)) for m in re.finditer(r"OMB_(DEBUG_\w+)\s*=\s*(\d+)", src)}
+    assert val and all(getattr(_lib, k) == v for k, v in val.items()), val
+    assert {"DEBUG_FUSED_CHAIN", "DEBUG_TIMING_STRIDE", "DEBUG_CHOL_MODE"} <= set(val)

@@ -45,6 +45,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t Nc, int64_
   const int64_t kbeg = (int64_t)blockIdx.z * kchunk;
   if (gridDim.z > 1) {
     kend = kend < kbeg + kchunk ? kend : kbeg + kchunk;
+    if (BTRI && kend <= kbeg) return;   // a slice past the tile's last column: zero, never read (splitk_reduce_kernel)
     C += (int64_t)blockIdx.z * zstride;
   }
 
@@ -174,15 +175,24 @@ static hipError_t gemm(hipStream_t stream, int64_t M, int64_t Nc, int64_t K, dou
   return hipGetLastError();
 }
 
-// C (M, Nc) = bias + Σ_z P[z] in slice order (deterministic), P[z] (M, Nc) dense at P + z·zstride.
+// C (M, Nc) = bias + Σ_z P[z] in slice order (deterministic), P[z] (M, Nc) dense at P + z·zstride.  With kchunk > 0
+// (op(B) lower-triangular, BTRI), column c sums only the slices that start below its tile's last row, the others
+// being zero and left unwritten by gemm_kernel.
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const double* __restrict__ P, int S, int64_t zstride,
                                                             int64_t M, int64_t Nc, const double* __restrict__ bias,
-                                                            double* __restrict__ C, int64_t ldc) {
+                                                            double* __restrict__ C, int64_t ldc, int64_t kchunk) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= M * Nc) return;
   const int64_t r = i / Nc, c = i - r * Nc;
+  int Sc = S;
+  if (kchunk > 0) {                               // the product's K is Nc here (Y = Z·Lᵀ, L square)
+    int64_t kend = (c / kGT + 1) * kGT;
+    kend = kend < Nc ? kend : Nc;
+    const int64_t a = (kend + kchunk - 1) / kchunk;
+    Sc = a < S ? (int)a : S;
+  }
   double v = 0.0;
-  for (int z = 0; z < S; ++z) v += P[z * zstride + i];
+  for (int z = 0; z < Sc; ++z) v += P[z * zstride + i];
   C[r * ldc + c] = v + (bias ? bias[c] : 0.0);
 }
 
@@ -203,15 +213,16 @@ hipError_t launch_gemm_tn_lower(hipStream_t s, int64_t N, int64_t K, double alph
   return gemm<true, false, false, true>(s, N, N, K, alpha, A, lda, A, lda, beta, C, ldc, nullptr);
 }
 
-// K slices of the sample product: enough (tile, slice) workgroups to fill the chip (≥ 1024), slices of
-// ≥ 256 columns.  At B = 64 draws of N = 3000 candidates the unsplit product has 47 workgroups
-// (208 µs, profiles/r02_v21_c6_kernel_stats.csv).
+// K slices of the sample product: enough (tile, slice) workgroups to fill the chip (≥ 2048), slices of
+// ≥ 96 columns.  At B = 64 draws of N = 3000 candidates the unsplit product has 47 workgroups
+// (208 µs, profiles/r02_v21_c6_kernel_stats.csv); 16 slices of 192 columns 33.9 + 5.7 µs (product + reduction),
+// 32 slices of 96 with the zero slices neither written nor read 22.3 + 10.9 µs (profiles/r04_ar_*).
 static int samples_split(int64_t N, int B) {
   const int64_t tiles = ((B + kGT - 1) / kGT) * ((N + kGT - 1) / kGT);
-  int64_t S = (1024 + tiles - 1) / tiles;
-  const int64_t smax = (N + 255) / 256;
+  int64_t S = (2048 + tiles - 1) / tiles;
+  const int64_t smax = (N + 95) / 96;
   if (S > smax) S = smax;
-  if (S > 16) S = 16;
+  if (S > 32) S = 32;
   return S < 1 ? 1 : (int)S;
 }
 
@@ -234,7 +245,7 @@ hipError_t launch_chol_samples(hipStream_t stream, const double* L, int64_t N, i
   if (e != hipSuccess) return e;
   const int64_t tot = (int64_t)B * N;
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, ws, S, zstride,
-                     (int64_t)B, N, mu, Y, N);
+                     (int64_t)B, N, mu, Y, N, kchunk);
   return hipGetLastError();
 }
 

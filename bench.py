@@ -421,10 +421,11 @@ def main():
     ap.add_argument("--no-kblock", action="store_true")
     ap.add_argument("--chain", default="fused", choices=["fused", "separate", "sobol"])
     ap.add_argument("--stage-timing", action="store_true", help="events around every stage (adds ~5 us/stage)")
-    ap.add_argument("--timing-stride", type=int, default=8,
+    ap.add_argument("--timing-stride", type=int, default=None,
                     help="record the timing events on every s-th step of the timed loop only (each record adds "
                          "~2.5 us of GPU time to its step: config 2 82.8 us per step with events on every step, "
-                         "77.3-77.8 on every 8th, gpurun_out/r04_ae)")
+                         "77.3-77.8 on every 8th, gpurun_out/r04_ae).  Default: from the warm-up's step length, "
+                         "1 for steps >= 1 ms (configs 3-5: 2.5 us is < 0.05%), else 8")
     ap.add_argument("--one-launch", type=int, default=None, choices=[0, 1, 2],
                     help="omb_debug_set(FUSED_CHAIN): 0 EHVI-2D and the arg-max as separate launches, 1 as one "
                          "ticketed launch, 2 EHVI-2D reducing to per-workgroup pairs + the arg-max's second pass "
@@ -570,38 +571,49 @@ def main():
             ctx.argmax_dev(acq, offset=start, out=pair)
         return global_argmax(pair)
 
+    torch.cuda.synchronize()
+    t_w = time.perf_counter()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    warm_ms = (time.perf_counter() - t_w) / args.warmup * 1e3 if args.warmup else None
+    stride = args.timing_stride
+    if stride is None:            # every launch when an event pair is noise against the step
+        stride = 1 if warm_ms is None or warm_ms >= 1.0 else 8
 
     if world_size > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    if args.chain != "separate":
-        # HIP events on the chain's stream: around the posterior (level 1) or every stage (2)
-        ctx.debug_set("timing_stride", args.timing_stride)
-        ctx.timing(2 if args.stage_timing else 1)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        best = step(i)
+        if i == 1 and args.chain != "separate":
+            # HIP events on the chain's stream: around the posterior (level 1) or every stage (2).  Switched on
+            # after step 0 is queued: step 0 follows the synchronize on an idle GPU and is not a steady-state
+            # launch, so the average covers steps 1, 1 + stride, ...
+            ctx.debug_set("timing_stride", stride)
+            ctx.timing(2 if args.stage_timing else 1)
+        best = step(i if i >= 1 else None)
     torch.cuda.synchronize()
     if world_size > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     stage_ms = None
     chains = args.steps
-    if args.chain != "separate":
+    if args.chain != "separate" and args.steps > 1:
         stage_sum, chains = ctx.timing_read()
         ctx.timing(0)
         stage_ms = {k: v / chains for k, v in stage_sum.items() if args.stage_timing or k == "posterior"}
+    elif args.chain != "separate":
+        stage_ms, chains = {"posterior": float("nan")}, 0
     if world_size > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     if stage_ms is not None:
-        post_ms = stage_ms["posterior"]
+        post_ms = stage_ms["posterior"] if chains else float("nan")
     else:
-        post_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+        post_ms = float(np.mean([a.elapsed_time(b) for a, b in ev[1:]])) if args.steps > 1 else float("nan")
+        chains = max(args.steps - 1, 0)
     best = best.cpu().numpy()
 
     # standalone K(X, X*) block: the HBM-bound kernel of the north star
@@ -650,14 +662,19 @@ def main():
 
     flops = n_obj * posterior_flops_per_candidate(n, d) * N
     achieved = flops / (post_ms * 1e-3) / 1e12
+    step_ms = elapsed / args.steps * 1e3
+    # the posterior is one launch inside every step, so its event-timed average cannot exceed the step
+    check = bool(post_ms <= step_ms)
     roofline = {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": load_traffic(n, N),
                 "kernel": f"posterior_kernel (omb_posterior, {n_obj} objective(s), n_train={n}, n_var={d})",
                 "ms_per_launch": post_ms,
                 "launches_timed": int(chains),
+                "timing_stride": stride,
+                "check": check,
                 "timing": "HIP events on the chain's stream around the posterior launch"
-                          + (f" of every {args.timing_stride}th timed step" if args.chain != "separate"
-                             and args.timing_stride > 1 else " of every timed step")}
+                          + (f" of every {stride}th timed step from step 1" if args.chain != "separate"
+                             and stride > 1 else " of every timed step but the first")}
 
     cpu = None
     if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
@@ -728,11 +745,14 @@ def main():
             out["config"]["train_box"] = f"[{cfg['x_lo']}, 1]^{d}"
         if "tail_hi" in cfg:
             out["config"]["train_box"] = f"x_1 in [0, 1], x_2..x_{d} in [0, {cfg['tail_hi']}]"
-        print(json.dumps(out))
+        print(json.dumps(out), flush=True)
     if world_size > 1:
         dist.barrier()
         dist.destroy_process_group()
     ctx.close()
+    if not check:
+        raise SystemExit(f"bench.py: roofline check failed: posterior {post_ms:.4f} ms per launch > "
+                         f"{step_ms:.4f} ms per step (the event timing is not measuring the launch)")
 
 
 if __name__ == "__main__":

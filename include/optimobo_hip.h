@@ -32,7 +32,8 @@ extern "C" {
 
 #define OMB_ABI_VERSION 1
 #define OMB_MAX_OBJ 8      /* objectives held by one context */
-#define OMB_MAX_DIM 64     /* n_var */
+#define OMB_MAX_DIM 256    /* n_var.  Up to 64 the fused / register-fragment kernels; 65..256 the wide path
+                              (DP 128 / 256: GEMM-tiled cross terms over 16-dim slabs, the dense posterior) */
 #define OMB_MAX_TRAIN 1024 /* n_train handled by the fused posterior kernel */
 #define OMB_MAX_TRAIN_DENSE 16384 /* n_train of the GEMM-based posterior path used above OMB_MAX_TRAIN */
 
@@ -100,18 +101,23 @@ const char* omb_last_error(const omb_ctx* ctx);
  * reduces the per-workgroup pairs) instead of two (default 2: config 2 measured 719.6 vs 719.5 M candidates/s,
  * gpurun_out/r04_l; bit-identical pair).
  * omb_debug_set(ctx, OMB_DEBUG_CHOL_MODE, m) picks the Cholesky schedule of omb_cholesky / omb_posterior_samples /
- * omb_gp_fit_state: 0 auto (default: = 2 where A fits the persistent launch's 32-bit buffer offsets, else 1),
- * 1 one launch per 64-column step, 2 the last min(steps, 32) steps in one persistent launch after per-step
- * launches for the others.  Same factor to rounding.
+ * omb_gp_fit_state: 0 auto (default: where A fits the persistent launch's 32-bit buffer offsets, per-step launches for
+ * all but the last min(steps, 32) 64-column steps and one persistent launch for those; else 1), 1 one launch per
+ * step, 2 the whole factorisation in one persistent launch; m + 4 runs schedule m with every cross-workgroup hand-off
+ * an agent-scope release / acquire pair (the HIP memory model's guarantee; the default form — sc1 payloads, a vmcnt
+ * wait and relaxed flags — is measured valid on gfx950), bitwise the same factor as schedule m.
  * omb_debug_set(ctx, OMB_DEBUG_TIMING_STRIDE, s) records omb_timing's events on every s-th chain only (default 1;
- * omb_timing_read then averages over the recorded chains), so that a timed loop carries fewer event records. */
+ * omb_timing_read then averages over the recorded chains), so that a timed loop carries fewer event records. *
+ * omb_debug_set(ctx, OMB_DEBUG_POSTERIOR_PERSIST, p) picks the fused posterior kernel for n_train > 128: 1 the persistent
+ * ring (resident workgroups, ring chunks numbered across candidate blocks), 0 one workgroup per candidate block. */
 enum {
   OMB_DEBUG_SPIN_LIMIT = 1,
   OMB_DEBUG_COV_TABLE = 2,
   OMB_DEBUG_FUSED_CHAIN = 3,
   OMB_DEBUG_ARGMAX_PASSES = 4,
   OMB_DEBUG_CHOL_MODE = 5,
-  OMB_DEBUG_TIMING_STRIDE = 6
+  OMB_DEBUG_TIMING_STRIDE = 6,
+  OMB_DEBUG_POSTERIOR_PERSIST = 7
 };
 int omb_debug_set(omb_ctx* ctx, int what, int64_t value);
 
@@ -276,7 +282,8 @@ int omb_cholesky(omb_ctx* ctx, double* A_dev, int64_t N, int64_t lda, double jit
 /* B joint posterior samples of objective `obj` at Xc_dev (N, d) (GPy posterior_samples_f):
  *   Y_dev (B, N) row b = μ + L z_b,  L = chol(Σ + j I),  Zt_dev (B, N) standard normals z_b.
  * Try t = 0 .. max_tries-1 uses j = jitter_rel · σ_f² · 10^t until the factorisation succeeds
- * (OMB_ENOTPD otherwise); *jitter_used (may be NULL) receives the j used.  Synchronises. */
+ * (OMB_ENOTPD otherwise); *jitter_used (may be NULL) receives the j used.  Synchronises.  When the call fails after
+ * the draws were queued (OMB_ENOTPD, or OMB_EHIP from a factor wait that ran out), Y_dev is filled with NaN. */
 int omb_posterior_samples(omb_ctx* ctx, int obj, const double* Xc_dev, int64_t N, const double* Zt_dev, int B,
                           double jitter_rel, int max_tries, double* Y_dev, double* jitter_used);
 /* Greedy selection of TuRBO_1.select_candidates (turbo.py:142-153) / TuRBO_M._select_candidates

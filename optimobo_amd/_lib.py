@@ -24,7 +24,8 @@ DEBUG_FUSED_CHAIN = 3
 DEBUG_ARGMAX_PASSES = 4
 DEBUG_CHOL_MODE = 5
 DEBUG_TIMING_STRIDE = 6
-MAX_OBJ, MAX_DIM, MAX_TRAIN, MAX_TRAIN_DENSE = 8, 64, 1024, 16384
+DEBUG_POSTERIOR_PERSIST = 7
+MAX_OBJ, MAX_DIM, MAX_TRAIN, MAX_TRAIN_DENSE = 8, 256, 1024, 16384
 
 _p = ctypes.c_void_p
 _d = ctypes.c_double

@@ -192,6 +192,10 @@ class AcquisitionEngine:
         self.ctx.set_sobol(d, lower, upper, seed=seed)
         vals = self.ctx.eval(self.ctx.sobol(start, count)) if acq_fn is None else acq_fn(self.ctx.sobol(start, count))
         v = torch.nan_to_num(vals, nan=-float("inf"))
+        # start 0 is round 0's arg-max by the device rule (value desc, lowest index; NaN never wins): torch.topk does
+        # not promise which of several equal values it returns, so the pool alone could miss it on a flat
+        # region (e.g. reference-mode EHVI <= 0 with many ties at 0)
+        best = global_argmax(self.ctx.argmax_dev(vals, offset=start)).cpu().numpy()
         top = torch.topk(v, min(pool, count))
         pairs = torch.stack([top.values, top.indices.to(torch.float64) + start], 1)
         if W > 1:
@@ -206,6 +210,8 @@ class AcquisitionEngine:
         P = pairs.cpu().numpy()
         P = P[(P[:, 1] >= 0) & np.isfinite(P[:, 0])]
         P = P[np.lexsort((P[:, 1], -P[:, 0]))]
+        if best[1] >= 0 and np.isfinite(best[0]):
+            P = np.concatenate([best[None, :], P[P[:, 1] != best[1]]])
         span = np.maximum(upper - lower, 1e-300)
         out = []
         for val, idx in P:

@@ -93,7 +93,9 @@ struct omb_ctx {
   int fused_chain = 0;  // OMB_DEBUG_FUSED_CHAIN: 0 EHVI-2D then the arg-max's passes, 1 one ticketed launch, 2 EHVI
                         // with the per-workgroup pairs, then the arg-max's second pass
   bool argmax_one_pass = false;  // OMB_DEBUG_ARGMAX_PASSES: 1 (one launch) or 2 (default: measured level)
-  int chol_mode = kCholAuto;     // OMB_DEBUG_CHOL_MODE
+  int posterior_persist = 0;     // OMB_DEBUG_POSTERIOR_PERSIST
+  int chol_mode = kCholAuto;     // OMB_DEBUG_CHOL_MODE (value & 3)
+  int chol_acq_rel = 0;          // OMB_DEBUG_CHOL_MODE (value & 4): release / acquire hand-offs
 };
 
 namespace {
@@ -125,7 +127,7 @@ constexpr int kMaxLdsDoubles = 8192;
 constexpr int kMaxStripes = (kMaxLdsDoubles - 1) / 2;
 
 int pad_dim(int d) {
-  const int opts[] = {2, 4, 6, 8, 16, 32, 64};
+  const int opts[] = {2, 4, 6, 8, 16, 32, 64, 128, 256};   // > 64: the wide path (omb_wide.hip)
   for (int o : opts)
     if (d <= o) return o;
   return -1;
@@ -152,6 +154,7 @@ void init_args(omb_ctx* ctx, GPArgs* args) {
   memset(args, 0, sizeof(*args));
   args->fault = ctx->fault_dev;
   args->spin_limit = ctx->spin_limit;
+  args->persist = ctx->posterior_persist;
 }
 
 // GP state of objectives 0..n_obj-1, all set, sharing d.
@@ -302,7 +305,9 @@ int plan_begin(omb_ctx* ctx, size_t bytes, void** host) {
 // column reduction.
 hipError_t posterior_any(omb_ctx* ctx, const GPArgs& args, const double* const* Ld, int n_obj, int max_R,
                          const double* Xc, int64_t N, double* mu, double* var) {
-  if (16 * max_R <= OMB_MAX_TRAIN) return launch_posterior(ctx->stream, args, n_obj, max_R, Xc, N, mu, var);
+  // the fused kernel keeps the candidates' B fragments in registers: n_var ≤ 64 (kMaxFusedDP)
+  if (16 * max_R <= OMB_MAX_TRAIN && args.DP <= kMaxFusedDP)
+    return launch_posterior(ctx->stream, args, n_obj, max_R, Xc, N, mu, var);
   for (int o = 0; o < n_obj; ++o) {
     const int64_t n = args.gp[o].n;
     int64_t Nc = (int64_t)(((size_t)256 << 20) / (16 * (size_t)n));   // K* and V chunks of 128 MiB each
@@ -542,11 +547,18 @@ int omb_debug_set(omb_ctx* ctx, int what, int64_t value) {
     ctx->timing_stride = (int)value;
     return OMB_OK;
   }
+  if (what == OMB_DEBUG_POSTERIOR_PERSIST) {
+    if (value != 0 && value != 1) return fail(ctx, OMB_EINVAL, "posterior persist %lld (0 or 1)", (long long)value);
+    ctx->posterior_persist = (int)value;
+    return OMB_OK;
+  }
   if (what == OMB_DEBUG_CHOL_MODE) {
-    if (value != 0 && value != 1 && value != 2)
-      return fail(ctx, OMB_EINVAL, "Cholesky mode %lld (0 auto, 1 per-step launches, 2 one persistent launch)",
-                  (long long)value);
-    ctx->chol_mode = value == 0 ? kCholAuto : (value == 1 ? kCholBlocked : kCholPersistent);
+    if ((value & 3) == 3 || value < 0 || value > 6)
+      return fail(ctx, OMB_EINVAL, "Cholesky mode %lld (0 auto, 1 per-step launches, 2 one persistent launch; + 4: "
+                  "release / acquire hand-offs)", (long long)value);
+    const int modes[3] = {kCholAuto, kCholBlocked, kCholPersistOnly};
+    ctx->chol_mode = modes[value & 3];
+    ctx->chol_acq_rel = (value & 4) ? 1 : 0;
     return OMB_OK;
   }
   return fail(ctx, OMB_EINVAL, "unknown debug setting %d", what);
@@ -1033,7 +1045,8 @@ static int chol_enqueue(omb_ctx* ctx, double* A, int64_t N, int64_t lda, double 
   int* dinfo = static_cast<int*>(ctx->ichol);
   double* ws = reinterpret_cast<double*>(static_cast<char*>(ctx->ichol) + 16);
   OMB_HIP(ctx, launch_add_diag(ctx->stream, A, N, lda, jitter));
-  OMB_HIP(ctx, launch_cholesky_mode(ctx->stream, A, N, lda, dinfo, ws, ctx->chol_mode, ctx->spin_limit));
+  OMB_HIP(ctx, launch_cholesky_mode(ctx->stream, A, N, lda, dinfo, ws, ctx->chol_mode, ctx->spin_limit,
+                                    ctx->chol_acq_rel));
   OMB_HIP(ctx, hipMemcpyAsync(ctx->info_host, dinfo, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   return OMB_OK;
 }
@@ -1085,6 +1098,13 @@ int omb_cholesky(omb_ctx* ctx, double* A_dev, int64_t N, int64_t lda, double jit
   return run_cholesky(ctx, A_dev, N, lda, jitter, info);
 }
 
+// The draws are queued before the factor's status is read (omb_posterior_samples), so a failed call would leave
+// draws from an invalid factor in Y: they are overwritten with NaN (all-ones bit patterns) instead.
+static void poison_draws(omb_ctx* ctx, double* Y, size_t count) {
+  (void)hipMemsetAsync(Y, 0xff, count * sizeof(double), ctx->stream);
+  (void)hipStreamSynchronize(ctx->stream);
+}
+
 int omb_posterior_samples(omb_ctx* ctx, int obj, const double* Xc_dev, int64_t N, const double* Zt_dev, int B,
                           double jitter_rel, int max_tries, double* Y_dev, double* jitter_used) {
   int rc = enter(ctx);
@@ -1119,12 +1139,17 @@ int omb_posterior_samples(omb_ctx* ctx, int obj, const double* Xc_dev, int64_t N
     // draws are overwritten by the next try's
     if ((e = launch_chol_samples(ctx->stream, S, N, N, mu, Zt_dev, B, Y_dev, cws)) != hipSuccess)
       return hip_fail(ctx, e, "posterior_samples (samples)");
-    if ((rc = chol_wait(ctx, &info))) return rc;
+    if ((rc = chol_wait(ctx, &info))) {
+      poison_draws(ctx, Y_dev, (size_t)B * N);
+      return rc;
+    }
     if (info == 0) break;
   }
-  if (info != 0)
+  if (info != 0) {
+    poison_draws(ctx, Y_dev, (size_t)B * N);
     return fail(ctx, OMB_ENOTPD, "posterior covariance + %g I is not positive definite (column %d) after %d tries",
                 jit / 10.0, info, max_tries);
+  }
   if (jitter_used) *jitter_used = jit;
   return OMB_OK;
 }

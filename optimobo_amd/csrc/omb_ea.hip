@@ -55,8 +55,13 @@ __device__ double ea_moments(const GPDev& g, const double* __restrict__ LdT, con
   for (int i = tid; i < g.n; i += kEAThreads) {
     const double* xr = g.Xs + (int64_t)i * DP;
     double dot = 0.0;
+    if constexpr (DP <= kMaxFusedDP) {
 #pragma unroll
-    for (int j = 0; j < DP; ++j) dot = fma(xr[j], ab[j], dot);
+      for (int j = 0; j < DP; ++j) dot = fma(xr[j], ab[j], dot);
+    } else {   // wide inputs: unrolled, the row's loads would take every register (392 spilled at DP = 256)
+#pragma unroll 8
+      for (int j = 0; j < DP; ++j) dot = fma(xr[j], ab[j], dot);
+    }
     const double r2 = fma(-2.0, dot, g.xsq[i] + asq);              // −2a·b + (‖a‖² + ‖b‖²)
     const double k = (g.kind == OMB_KERNEL_RBF) ? kernel_of_r2<OMB_KERNEL_RBF>(r2, g.variance)
                                                 : kernel_of_r2<OMB_KERNEL_MATERN52>(r2, g.variance);
@@ -241,7 +246,7 @@ hipError_t launch_ea_search(hipStream_t stream, const EASearch& s, double* ldt_w
     hipLaunchKernelGGL((ea_search_kernel<DPV>), dim3(1), dim3(kEAThreads), 0, stream, A);            \
     break;
   switch (s.DP) {
-    OMB_EA(2) OMB_EA(4) OMB_EA(6) OMB_EA(8) OMB_EA(16) OMB_EA(32) OMB_EA(64)
+    OMB_EA(2) OMB_EA(4) OMB_EA(6) OMB_EA(8) OMB_EA(16) OMB_EA(32) OMB_EA(64) OMB_EA(128) OMB_EA(256)
     default: return hipErrorInvalidValue;
   }
 #undef OMB_EA

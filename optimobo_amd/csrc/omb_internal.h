@@ -37,6 +37,7 @@ struct GPArgs {
   ExpCoef ec;      // exp_nonpos coefficients as kernel arguments (set by launch_posterior)
   int* fault;      // context fault word (pinned host memory): bit 0 = an LDS-counter wait ran out
   int spin_limit;  // polls per LDS-counter wait before the fault word is marked
+  int persist;     // OMB_DEBUG_POSTERIOR_PERSIST: 1 = the persistent ring (posterior_persist_kernel) where it applies
 };
 
 constexpr int kFaultSpin = 1;          // fault word bit: posterior counter-ring wait exhausted
@@ -160,12 +161,16 @@ constexpr int kCholSpinFault = -2147483647;
 // per-step launches (their trailing updates are faster while the trailing matrix is large; omb_linalg.hip
 // chol_hybrid_k0).  kCholAuto (launch_cholesky) = kCholPersistent where A fits its 32-bit buffer offsets, else
 // kCholBlocked.
-enum { kCholTwoLaunch = 0, kCholFused = 1, kCholBlocked = 2, kCholBlockedAcqRel = 3, kCholPersistent = 4, kCholAuto = 5 };
+// kCholPersistOnly: the whole factorisation in one persistent launch (k0 = 0; kCholBlocked when A is too large).
+enum { kCholTwoLaunch = 0, kCholFused = 1, kCholBlocked = 2, kCholBlockedAcqRel = 3, kCholPersistent = 4, kCholAuto = 5,
+       kCholPersistOnly = 6 };
 int64_t chol_ws_doubles(int64_t N);
 hipError_t launch_cholesky(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws,
                            int spin_limit = kDefaultSpinLimit);
+// acq_rel = 1: every cross-workgroup hand-off of the schedule as an agent-scope release / acquire pair (the HIP memory
+// model's form; the default relaxed / sc1 form is measured valid on gfx950 and checked bitwise against this one)
 hipError_t launch_cholesky_mode(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws, int mode,
-                                int spin_limit = kDefaultSpinLimit);
+                                int spin_limit = kDefaultSpinLimit, int acq_rel = 0);
 // Y (B, N) = μ + Zt Lᵀ (L lower, N×N): row b of Y is the sample μ + L z_b.
 // ws: chol_samples_ws_doubles(N, B) device doubles (split-K partial products; 0 when unsplit).
 int64_t chol_samples_ws_doubles(int64_t N, int B);
@@ -223,6 +228,26 @@ struct EASearch {
   double* out;
 };
 hipError_t launch_ea_search(hipStream_t stream, const EASearch& s, double* ldt_ws);
+
+// ---------------------------------------------------------------------------------------
+// Wide inputs (omb_wide.hip): n_var 65 .. OMB_MAX_DIM, DP = 128 or 256.  The fused posterior kernel and the
+// register-fragment K-block / covariance / gradient kernels hold a candidate's coordinates in registers, which
+// is only affordable up to kMaxFusedDP; above it the cross terms run as GEMM tiles with the k loop over slabs of
+// kWideSlab dimensions staged in LDS, and the posterior takes the dense path (K block → V = L⁻¹K* → column
+// reduction, posterior_any).  Every entry point keeps its meaning and its parity bar.
+constexpr int kMaxFusedDP = 64;
+constexpr int kWideSlab = 16;
+// K (M, N) row-major, pitch ldk: K[i][c] = k(X_i, X*_c) for the training rows of g (pre-scaled g.Xs, g.xsq, pitch
+// DP) against the raw candidates Xc (N, d), divided by ℓ as they are staged.
+hipError_t launch_kernel_block_wide(hipStream_t stream, const GPDev& g, int d, int DP, const double* Xc, int64_t N,
+                                    double* K, int64_t ldk);
+// launch_cand_cov for DP > kMaxFusedDP (same arguments and workspace, cand_cov_ws_doubles(N, DP))
+hipError_t launch_cand_cov_wide(hipStream_t stream, const GPDev& g, int d, int DP, const double* Xc, int64_t N,
+                                double* S, int64_t lds, double* ws, double diag_add);
+// gp_grad_kernel's partial sums for DP > kMaxFusedDP (the same layout: gp_grad_blocks(n) blocks × (DP + 1))
+hipError_t launch_gp_grad_partials_wide(hipStream_t stream, int kind, int DP, const double* X, int d, int64_t n,
+                                        const double* ls, double variance, const double* alpha, const double* Kinv,
+                                        int64_t ldk, double* partials);
 
 // Packed-L^-1 size in doubles for R row tiles: Σ_{r<R} 4(r+1)·64 = 128·R·(R+1).
 inline int64_t packed_L_size(int R) { return 128ll * R * (R + 1); }

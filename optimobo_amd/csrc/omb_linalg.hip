@@ -1208,6 +1208,9 @@ struct CholSync {
 // `threadIdx.x == 0` the compiler merged the flag store, the loop back edge and the next ticket into one divergent
 // region and let wave 0's other lanes run ahead into the next task's barrier with the old ticket (the launch hung
 // at N = 130, gpurun_out/r04_o; the ISA showed the barrier inside a loop entered without the ticket).
+// AR (chol_mode bit 4, tests): an agent-scope acquire fence after the poll — the HIP memory model's form of the
+// hand-off, against which the default relaxed form is checked bitwise (tests/test_gpu_turbo.py stress test).
+template <bool AR = false>
 __device__ __forceinline__ bool chol_poll_ge(const int* p, int v, const CholSync& s, int spin_limit, int* info) {
   int polls = 0;
   while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < v) {
@@ -1221,16 +1224,22 @@ __device__ __forceinline__ bool chol_poll_ge(const int* p, int v, const CholSync
     }
     __builtin_amdgcn_s_sleep(1);
   }
+  if constexpr (AR) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   return true;
 }
 
 // every storing wave drains its sc1 stores, the workgroup meets, wave 0 raises the flag (all its lanes store the
-// same value to the same word: one uniform store)
+// same value to the same word: one uniform store).  AR: the flag store is an agent-scope release.
+template <bool AR = false>
 __device__ __forceinline__ void chol_signal(int* flag, int value) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0)
-    __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0) {
+    if constexpr (AR)
+      __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // Panel tile L_ik = A_ik W_kᵀ (chol_panel_kernel's product, 4 waves × 16 rows): W from the fragments Wk (global,
@@ -1345,6 +1354,7 @@ __global__ __launch_bounds__(256) void chol_persist_init_kernel(int* __restrict_
   if (threadIdx.x == 0 && k0 == 0) *info = 0;
 }
 
+template <bool AR>
 __global__ __launch_bounds__(256, kPersistWgPerCu) void chol_persist_kernel(double* __restrict__ A, int64_t N, int64_t lda, int t,
                                                               int total, double* __restrict__ Wf, CholSync sync,
                                                               int* __restrict__ info, int spin_limit, int k0) {
@@ -1417,13 +1427,16 @@ __global__ __launch_bounds__(256, kPersistWgPerCu) void chol_persist_kernel(doub
       }
       if (k > kstart && w >= 2) {   // the previous step's panel tile (k, k − 1): this wave's rows drained, its share
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(sync.pflag + k * t + k - 1, lane == 0 ? 2 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if constexpr (AR)
+          __hip_atomic_fetch_add(sync.pflag + k * t + k - 1, lane == 0 ? 2 : 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        else
+          __hip_atomic_fetch_add(sync.pflag + k * t + k - 1, lane == 0 ? 2 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       OMB_PDBG(0, 1000 * k + 2);
       OMB_PTIME(8 * k + 1);
       chol64_blocked<kCholDReady>(A, lda, r0, nb, 0, Wf + (int64_t)k * kCholWsDoubles, Ds, Wl, fl, k + 1, Wfl);
       OMB_PDBG(1 + w, 1000 * k + 3);
-      chol_signal(sync.wflag + k, 1);                           // W_k's fragments (wf_store: sc1) drained
+      chol_signal<AR>(sync.wflag + k, 1);                           // W_k's fragments (wf_store: sc1) drained
       OMB_PDBG(0, 1000 * k + 4);
       if (w == 0 && (fl[20] || fl[21])) atomicCAS(info, 0, fl[21] ? kCholSpinFault : (int)(r0 + fl[20]));
       if (w == 0) fl[20] = 0;           // read above (wave 0, in order); the next step's writes follow a barrier
@@ -1432,8 +1445,8 @@ __global__ __launch_bounds__(256, kPersistWgPerCu) void chol_persist_kernel(doub
         // the next panel tile and the next diagonal tile: both updated through step k − 1 by the workers
         if (w == 0) {
           const int i1 = (k + 1) * t;
-          if (chol_poll_ge(sync.cnt + i1 + k, k, sync, spin_limit, info))
-            chol_poll_ge(sync.cnt + i1 + k + 1, k, sync, spin_limit, info);
+          if (chol_poll_ge<AR>(sync.cnt + i1 + k, k, sync, spin_limit, info))
+            chol_poll_ge<AR>(sync.cnt + i1 + k + 1, k, sync, spin_limit, info);
         }
         __syncthreads();
         OMB_PDBG(0, 1000 * k + 5);
@@ -1484,14 +1497,14 @@ __global__ __launch_bounds__(256, kPersistWgPerCu) void chol_persist_kernel(doub
     const int np = chol_persist_np(t, k, k0);
     if (q < np) {
       const int i = k + 2 + q;
-      if (w == 0 && chol_poll_ge(sync.wflag + k, 1, sync, spin_limit, info))
-        chol_poll_ge(sync.cnt + i * t + k, k, sync, spin_limit, info);
+      if (w == 0 && chol_poll_ge<AR>(sync.wflag + k, 1, sync, spin_limit, info))
+        chol_poll_ge<AR>(sync.cnt + i * t + k, k, sync, spin_limit, info);
       __syncthreads();
       OMB_PDBG(8 * blockIdx.x + 1, 1);
       OMB_PTIME(8 * t + 4 * s_task[0] + 1);
       chol_persist_panel(ra, A, N, lda, i, k, Wf + (int64_t)k * kCholWsDoubles, nullptr);
       OMB_PDBG(8 * blockIdx.x + 2 + w, 2);
-      chol_signal(sync.pflag + i * t + k, 4);
+      chol_signal<AR>(sync.pflag + i * t + k, 4);
       OMB_PDBG(8 * blockIdx.x + 1, 3);
       OMB_PTIME(8 * t + 4 * s_task[0] + 2);
     } else {
@@ -1501,15 +1514,15 @@ __global__ __launch_bounds__(256, kPersistWgPerCu) void chol_persist_kernel(doub
         ++j;
       }
       const int i = j + u;
-      if (w == 0 && chol_poll_ge(sync.pflag + i * t + k, 4, sync, spin_limit, info) &&
-          chol_poll_ge(sync.pflag + j * t + k, 4, sync, spin_limit, info))
-        chol_poll_ge(sync.cnt + i * t + j, k, sync, spin_limit, info);
+      if (w == 0 && chol_poll_ge<AR>(sync.pflag + i * t + k, 4, sync, spin_limit, info) &&
+          chol_poll_ge<AR>(sync.pflag + j * t + k, 4, sync, spin_limit, info))
+        chol_poll_ge<AR>(sync.cnt + i * t + j, k, sync, spin_limit, info);
       __syncthreads();
       OMB_PDBG(8 * blockIdx.x + 1, 11);
       OMB_PTIME(8 * t + 4 * s_task[0] + 1);
       chol_persist_update(ra, A, N, lda, i, j, k);
       OMB_PDBG(8 * blockIdx.x + 2 + w, 12);
-      chol_signal(sync.cnt + i * t + j, k + 1);
+      chol_signal<AR>(sync.cnt + i * t + j, k + 1);
       OMB_PDBG(8 * blockIdx.x + 1, 13);
       OMB_PTIME(8 * t + 4 * s_task[0] + 2);
     }
@@ -1683,8 +1696,11 @@ constexpr int kSmallFitThreads = 512;
 constexpr int kSmallFitMax = 128;
 constexpr int kSmallFitXs = 1024;   // LDS doubles for X/ℓ: n·DP ≤ 1024 (d ≤ 8 at n = 128)
 
+// the one-workgroup fit takes n_var ≤ 8 (gp_lml_small_fits), so its lengthscale argument is 8 doubles
+// (an OMB_MAX_DIM-wide one would be a 2-KiB kernel argument and a 2-KiB local array in the batch kernel)
+constexpr int kSmallFitMaxDP = 8;
 struct FitLs {
-  double v[OMB_MAX_DIM];
+  double v[kSmallFitMaxDP];
 };
 
 // K and (dK/dr)/r of scaled rows a (LDS, wave-uniform row) and b (registers): gp_grad_kernel's arithmetic
@@ -2070,7 +2086,7 @@ __global__ __launch_bounds__(kSmallFitThreads) void gp_lml_small_batch_kernel(co
   const int p = blockIdx.x;
   FitLs ls;
 #pragma unroll
-  for (int j = 0; j < OMB_MAX_DIM; ++j) ls.v[j] = j < 8 ? b.ls[p][j] : 1.0;
+  for (int j = 0; j < kSmallFitMaxDP; ++j) ls.v[j] = b.ls[p][j];
   gp_lml_small_body<DP, KIND, ABL>(X, d, n, ls, b.variance[p], base, b.y[p], b.out[p]);
 }
 
@@ -2081,9 +2097,9 @@ bool gp_lml_small_fits(int n, int DP) { return n >= 1 && n <= kSmallFitMax && DP
 
 hipError_t launch_gp_lml_small(hipStream_t stream, int kind, int DP, const double* X, int d, int n,
                                const double* ls_host, double variance, double base, const double* y, double* out) {
-  if (!gp_lml_small_fits(n, DP) || d < 1 || d > DP || DP > OMB_MAX_DIM) return hipErrorInvalidValue;
+  if (!gp_lml_small_fits(n, DP) || d < 1 || d > DP || DP > kSmallFitMaxDP) return hipErrorInvalidValue;
   FitLs ls{};
-  for (int j = 0; j < OMB_MAX_DIM; ++j) ls.v[j] = (j < d) ? ls_host[j] : 1.0;
+  for (int j = 0; j < kSmallFitMaxDP; ++j) ls.v[j] = (j < d) ? ls_host[j] : 1.0;
 #define OMB_GS(DPV)                                                                                              \
   case DPV:                                                                                                      \
     if (kind == OMB_KERNEL_RBF)                                                                                  \
@@ -2412,6 +2428,7 @@ int64_t cand_cov_ws_doubles(int64_t N, int DP) { return N * ((DP + 3) / 4 * 4) +
 hipError_t launch_cand_cov(hipStream_t stream, const GPDev& g, int d, int DP, const double* Xc, int64_t N, double* S,
                            int64_t lds, double* ws, double diag_add, bool table) {
   if (N <= 0) return hipSuccess;
+  if (DP > kMaxFusedDP) return launch_cand_cov_wide(stream, g, d, DP, Xc, N, S, lds, ws, diag_add);
   const ExpCoef ec = exp_coef();
   const int KP = (DP + 3) / 4 * 4;
   double* Xs = ws;
@@ -2549,11 +2566,11 @@ static hipError_t launch_cholesky_blocked(hipStream_t stream, double* A, int64_t
 // k0 > 0: steps 0 .. k0 − 1 as per-step launches (their bulk trailing updates run at three workgroups per CU), the
 // rest in one persistent launch (the diagonal walk without kernel boundaries once the trailing matrix is small).
 static hipError_t launch_cholesky_persist(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws,
-                                          int spin_limit, int k0 = 0) {
+                                          int spin_limit, int k0 = 0, int acq_rel = 0) {
   const int t = (int)((N + kNB - 1) / kNB);
   if (k0 > t - 2) k0 = 0;
   hipError_t e = hipSuccess;
-  if (k0 > 0) e = launch_cholesky_blocked(stream, A, N, lda, info, ws, spin_limit, 0, k0);
+  if (k0 > 0) e = launch_cholesky_blocked(stream, A, N, lda, info, ws, spin_limit, acq_rel, k0);
   if (e != hipSuccess) return e;
   int total = 0;
   for (int k = k0; k < t; ++k) total += chol_persist_step_tasks(t, k, k0);
@@ -2564,26 +2581,35 @@ static hipError_t launch_cholesky_persist(hipStream_t stream, double* A, int64_t
   if ((e = hipGetLastError()) != hipSuccess) return e;
   const int slots = kPersistWgPerCu * device_cus() - 1;
   const int grid = 1 + (total < slots ? total : slots);
-  hipLaunchKernelGGL(chol_persist_kernel, dim3((unsigned)grid), dim3(256), 0, stream, A, N, lda, t, total, Wf, sync,
-                     info, spin_limit, k0);
+  if (acq_rel)
+    hipLaunchKernelGGL(chol_persist_kernel<true>, dim3((unsigned)grid), dim3(256), 0, stream, A, N, lda, t, total, Wf,
+                       sync, info, spin_limit, k0);
+  else
+    hipLaunchKernelGGL(chol_persist_kernel<false>, dim3((unsigned)grid), dim3(256), 0, stream, A, N, lda, t, total, Wf,
+                       sync, info, spin_limit, k0);
   return hipGetLastError();
 }
 
 hipError_t launch_cholesky_mode(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws, int mode,
-                                int spin_limit) {
+                                int spin_limit, int acq_rel) {
   if (N <= 0) return hipSuccess;
   if (mode == kCholAuto) mode = kCholPersistent;
-  if (mode == kCholPersistent) {
-    if (chol_persist_fits(N, lda))
-      return launch_cholesky_persist(stream, A, N, lda, info, ws, spin_limit, chol_hybrid_k0((int)((N + kNB - 1) / kNB)));
+  if (mode == kCholPersistOnly) {
+    if (chol_persist_fits(N, lda)) return launch_cholesky_persist(stream, A, N, lda, info, ws, spin_limit, 0, acq_rel);
     mode = kCholBlocked;
   }
+  if (mode == kCholPersistent) {
+    if (chol_persist_fits(N, lda))
+      return launch_cholesky_persist(stream, A, N, lda, info, ws, spin_limit, chol_hybrid_k0((int)((N + kNB - 1) / kNB)),
+                                     acq_rel);
+    mode = kCholBlocked;
+  }
+  if (acq_rel && mode == kCholBlocked) mode = kCholBlockedAcqRel;
   const int steps = (int)((N + kNB - 1) / kNB);
   const bool vec = (lda % 2 == 0) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
   const bool fuse = mode == kCholFused;
   const bool blk = mode == kCholBlocked || mode == kCholBlockedAcqRel;
-  const int acq_rel = mode == kCholBlockedAcqRel ? 1 : 0;
-  if (blk) return launch_cholesky_blocked(stream, A, N, lda, info, ws, spin_limit, acq_rel);
+  if (blk) return launch_cholesky_blocked(stream, A, N, lda, info, ws, spin_limit, mode == kCholBlockedAcqRel ? 1 : 0);
   int* flags = reinterpret_cast<int*>(ws + kCholWsDoubles);
   hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), 0, stream, A, N, lda, ws, info, flags, fuse ? steps : 0);
   hipError_t e = hipGetLastError();
@@ -2636,6 +2662,13 @@ hipError_t launch_gp_grad(hipStream_t stream, int kind, int DP, const double* X,
                           const double* L, int64_t lda, const double* y, double* out) {
   const unsigned t = (unsigned)((n + 15) / 16);
   dim3 grid(t, t);
+  if (DP > kMaxFusedDP) {   // n_var > 64 (omb_wide.hip): the same partial sums, one thread per dimension
+    hipError_t e = launch_gp_grad_partials_wide(stream, kind, DP, X, d, n, ls, variance, alpha, Kinv, ldk, partials);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(gp_reduce_kernel, dim3(1), dim3(256), 0, stream, partials, (int64_t)t * t, DP + 1, L, n, lda, y,
+                       alpha, out);
+    return hipGetLastError();
+  }
 #define OMB_GG(DPV)                                                                                              \
   case DPV:                                                                                                      \
     if (kind == OMB_KERNEL_RBF)                                                                                  \

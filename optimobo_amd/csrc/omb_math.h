@@ -449,14 +449,14 @@ __device__ __forceinline__ double npdf_fast(double t) {
 
 // EHVI-2D of one candidate over L lanes (L = 1, 2, 4): util_functions.py:81-128 (EHVI_2D_aux) with the stripe
 // array S = [(r0,−∞), PF↑f2, (−∞,r1)] of :93-109; y1[0] = r0, y1[i] / y2[i−1] = stripe i's f1 / f2 (i = 1..P).
-// Lane g (0..L−1; the candidate's lanes are l, l + 64/L, … of one wave) sums the stripes of the g-th
-// contiguous L-th of 1..P; within a quarter φ/Φ of t_i = (y1[i]−μ0)/σA are reused by stripe i+1 (the
+// The stripes 1..P form four contiguous quarters; lane g (0..L−1; the candidate's lanes are l, l + 64/L, … of one
+// wave) sums quarter g (L = 4), quarters 2g and 2g + 1 (L = 2) or all four (L = 1); within a quarter φ/Φ of t_i = (y1[i]−μ0)/σA are reused by stripe i+1 (the
 // reference evaluates ψ(y1[i−1], y1[i−1]) from the same t), so a stripe costs 2 Φ + 2 φ instead of 7 calls, and a
-// quarter one Φ + φ more for its first t.  The quarters' partial sums meet by two xor-shuffles: every lane of the
-// candidate returns the same value, identical in every kernel that calls this (ehvi2d_kernel and the one-launch
-// chains), which is what makes their arg-max bitwise the same.  One lane per candidate (the round-3 kernel) sums
-// all P stripes serially: 4× the latency, but no lane idles on a short last quarter and no quarter pays its own
-// first Φ + φ — the kernels take L = 1 for batches large enough to fill every SIMD with waves (ehvi2d_lanes).
+// quarter one Φ + φ more for its first t.  The quarters' partial sums meet in one fixed order for every L: every lane
+// of the candidate returns the same value, identical in every kernel that calls this (ehvi2d_kernel and the one-launch
+// chains) and at every batch size, which is what makes their arg-max bitwise the same.  One lane per candidate sums
+// the four quarters serially (4× the latency, but no lane idles on a short last quarter): the kernels take L = 1 for
+// batches large enough to fill every SIMD with waves (ehvi2d_lanes).
 template <int L>
 __device__ __forceinline__ double ehvi2d_point(double m0, double m1, double v0, double v1, const double* y1,
                                                const double* y2, int P, double r1, double s00, double s01, int mode,
@@ -477,13 +477,24 @@ __device__ __forceinline__ double ehvi2d_point(double m0, double m1, double v0, 
     sA = v0;
     sB = v1;
   }
-  const int chunk = (P + L - 1) / L;
-  const int i0 = 1 + g * chunk, i1 = min(P, (g + 1) * chunk);
-  double sum1 = 0.0, sum2 = 0.0;
-  if (!nan && i0 <= i1) {
+  // The stripes are always summed as four fixed quarters (chunk = ⌈P/4⌉), each from 0 with its own first t, and
+  // the quarters meet as ((q0 + q1) + (q2 + q3)) whatever L is: L only decides which lane sums which quarters (L = 4:
+  // one each, met by two xor-shuffles; L = 2: two each, then one shuffle; L = 1: all four).  So a candidate's value
+  // does not depend on the batch size its lane count came from (polish compared a 4-lane single-point
+  // score against 1- or 2-lane batch values).
+  const int chunk = (P + 3) / 4;
+  double iA = 0.0, iB = 0.0;
+  if (!nan) {
     // (b − m)/s as (b − m)·(1/s): one division per candidate instead of two per stripe (≤ 1 ulp in t; x/0 and
     // x·(1/0) agree, ±inf or NaN)
-    const double iA = 1.0 / sA, iB = 1.0 / sB;
+    iA = 1.0 / sA;
+    iB = 1.0 / sB;
+  }
+  auto quarter = [&](int q, double& s1, double& s2) {
+    const int i0 = 1 + q * chunk, i1 = min(P, (q + 1) * chunk);
+    s1 = 0.0;
+    s2 = 0.0;
+    if (nan || i0 > i1) return;
     const double tp = (y1[i0 - 1] - m0) * iA;
     double cdf_p = ndtr_fast(tp), pdf_p = npdf_fast(tp);
     for (int i = i0; i <= i1; ++i) {
@@ -492,22 +503,35 @@ __device__ __forceinline__ double ehvi2d_point(double m0, double m1, double v0, 
       const double cdf_t = ndtr_fast(t), pdf_t = npdf_fast(t);
       const double u = (y2i - m1) * iB;
       const double p2 = sB * npdf_fast(u) + (y2i - m1) * ndtr_fast(u);     // ψ(y2i, y2i, μ1, σB)
-      sum1 = sum1 + (y1p - y1i) * cdf_t * p2;
+      s1 = s1 + (y1p - y1i) * cdf_t * p2;
       const double psi_pp = sA * pdf_p + (y1p - m0) * cdf_p;          // ψ(y1[i−1], y1[i−1], μ0, σA)
       const double psi_pi = sA * pdf_t + (y1p - m0) * cdf_t;          // ψ(y1[i−1], y1[i],   μ0, σA)
-      sum2 = sum2 + (psi_pp - psi_pi) * p2;
+      s2 = s2 + (psi_pp - psi_pi) * p2;
       cdf_p = cdf_t;
       pdf_p = pdf_t;
     }
-  }
+  };
+  double sum1, sum2;
   if constexpr (L == 4) {
+    quarter(g, sum1, sum2);
     sum1 += __shfl_xor(sum1, 16);
     sum1 += __shfl_xor(sum1, 32);
     sum2 += __shfl_xor(sum2, 16);
     sum2 += __shfl_xor(sum2, 32);
   } else if constexpr (L == 2) {
+    double a1, a2, b1, b2;
+    quarter(2 * g, a1, a2);
+    quarter(2 * g + 1, b1, b2);
+    sum1 = a1 + b1;
+    sum2 = a2 + b2;
     sum1 += __shfl_xor(sum1, 32);
     sum2 += __shfl_xor(sum2, 32);
+  } else {
+    double q1[4], q2[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) quarter(q, q1[q], q2[q]);
+    sum1 = (q1[0] + q1[1]) + (q1[2] + q1[3]);
+    sum2 = (q2[0] + q2[1]) + (q2[2] + q2[3]);
   }
   if (nan) return __builtin_nan("");
   double res = sum1 + sum2;

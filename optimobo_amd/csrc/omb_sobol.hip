@@ -23,13 +23,16 @@ constexpr int kSobolMaxBlocks = 16384;
 
 // Device layout of SobolDev (see omb_set_sobol): sv (d·bits uint32) | shift (d uint32) |
 // lo (d f64) | width (d f64); `words` = d·bits + d rounded up to an even count.
+// MAXD: the LDS copy's capacity in dimensions (64 for the usual n_var, so the workgroup's LDS stays at 10 KiB;
+// OMB_MAX_DIM above that)
+template <int MAXD>
 __global__ __launch_bounds__(kSobolThreads) void sobol_kernel(const uint32_t* __restrict__ state, int d, int bits,
                                                              int64_t start, int64_t total, double scale,
                                                              double* __restrict__ X) {
 #pragma clang fp contract(off)
-  __shared__ uint32_t sv[OMB_MAX_DIM * 32];
-  __shared__ uint32_t shift[OMB_MAX_DIM];
-  __shared__ double lo[OMB_MAX_DIM], width[OMB_MAX_DIM];
+  __shared__ uint32_t sv[MAXD * 32];
+  __shared__ uint32_t shift[MAXD];
+  __shared__ double lo[MAXD], width[MAXD];
   const int words = d * bits + d;
   const double* fstate = reinterpret_cast<const double*>(state + ((words + 1) & ~1));
   for (int t = threadIdx.x; t < d * bits; t += blockDim.x) sv[t] = state[t];
@@ -84,8 +87,12 @@ hipError_t launch_sobol(hipStream_t stream, const void* state_dev, int d, int bi
   int64_t nb = (total + kSobolThreads - 1) / kSobolThreads;
   if (nb > kSobolMaxBlocks) nb = kSobolMaxBlocks;
   const double scale = 1.0 / (double)(1ull << bits);
-  hipLaunchKernelGGL(sobol_kernel, dim3((unsigned)nb), dim3(kSobolThreads), 0, stream,
-                     static_cast<const uint32_t*>(state_dev), d, bits, start, total, scale, X);
+  if (d <= 64)
+    hipLaunchKernelGGL(sobol_kernel<64>, dim3((unsigned)nb), dim3(kSobolThreads), 0, stream,
+                       static_cast<const uint32_t*>(state_dev), d, bits, start, total, scale, X);
+  else
+    hipLaunchKernelGGL(sobol_kernel<OMB_MAX_DIM>, dim3((unsigned)nb), dim3(kSobolThreads), 0, stream,
+                       static_cast<const uint32_t*>(state_dev), d, bits, start, total, scale, X);
   return hipGetLastError();
 }
 

@@ -72,11 +72,13 @@ class AcqContext:
         builds K(X, X) / K(X*, X*) with the posterior's table-driven Matern transform; ("fused_chain", 0/1/2) runs
         EHVI-2D and the arg-max as separate launches / as one ticketed launch / as EHVI with per-workgroup pairs
         and the arg-max's second pass; ("argmax_passes", 1/2) runs the arg-max as one
-        launch / as two; ("chol_mode", 0/1/2) factors auto / by per-step launches / in one persistent launch;
+        launch / as two; ("chol_mode", 0/1/2 [+ 4]) factors auto / by per-step launches / in one persistent launch
+        [with release-acquire hand-offs];
         ("timing_stride", s) records the timing events on every s-th chain only."""
         code = {"spin_limit": _lib.DEBUG_SPIN_LIMIT, "cov_table": _lib.DEBUG_COV_TABLE,
                 "fused_chain": _lib.DEBUG_FUSED_CHAIN, "argmax_passes": _lib.DEBUG_ARGMAX_PASSES,
-                "chol_mode": _lib.DEBUG_CHOL_MODE, "timing_stride": _lib.DEBUG_TIMING_STRIDE}[what]
+                "chol_mode": _lib.DEBUG_CHOL_MODE, "timing_stride": _lib.DEBUG_TIMING_STRIDE,
+                "posterior_persist": _lib.DEBUG_POSTERIOR_PERSIST}[what]
         self._check(self.lib.omb_debug_set(self._h, code, int(value)), "omb_debug_set")
 
     # ------------------------------------------------------------------ GP state

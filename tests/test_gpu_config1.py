@@ -109,11 +109,12 @@ def test_readme_run_full_size():
         assert abs(r["v"] - r["v_dev_at_x"]) <= 1e-12 * abs(r["v"]) + 1e-300   # the returned value is the value at x
         # on a singular surrogate (cond(K + 1e-8 I) ~ 1e16-1e18 at every checkpoint) the acquisition is itself
         # determined only loosely: DE's ~10^4 single-point calls find rounding ripples, the device search (Sobol
-        # grid + polish) does not — measured gaps 1.35e-4 (single start) and 2.3e-4 (four starts) at iteration 99
-        # (gpurun_out/r04_n), where the oracle's own surface differs from the device's by 25% (cond·eps ≫ 1).  So
-        # the singular checkpoints are recorded (printed above) and only held to 1e-3; value parity is asserted
-        # on the conditioned run (test_readme_shaped_run_on_a_conditioned_surrogate) and by test_gpu_polish at 1e-6.
-        tol = 1e-6 if r["cond"] <= 1e10 else 1e-3
+        # grid + polish) does not — measured gap 1.35e-4 at iteration 99 (gpurun_out/r04_n), where the oracle's own
+        # surface differs from the device's by 25% (cond·eps ≫ 1).  So the bar is tiered by cond·eps:
+        # 1e-6 where cond ≤ 1e10, 3e-4 (twice the measured gap) while cond·eps < 1, and 1e-3 only where cond·eps ≥ 1
+        # makes the surface itself ambiguous; value parity is asserted on the conditioned run
+        # (test_readme_shaped_run_on_a_conditioned_surrogate) and by test_gpu_polish at 1e-6.
+        tol = 1e-6 if r["cond"] <= 1e10 else (3e-4 if r["cond"] * np.finfo(float).eps < 1.0 else 1e-3)
         assert r["v"] >= r["v_de"] - tol * abs(r["v_de"]), (k, r)
         if r["cond"] <= 1e10:
             assert abs(r["v_oracle"] - r["v"]) <= 1e-6 * abs(r["v_oracle"]) + 1e-14, (k, r)
@@ -165,9 +166,28 @@ def test_readme_shaped_run_on_a_conditioned_surrogate():
         it[0] += 1
         return x, negv, rd
     opt._get_proposed_scalarisation = recording
+    # the multi-start search (4 starts at n_var 6) against the single-start search on the same surface,
+    # same seed: start 0 is the single-start search's incumbent, so the result is never worse
+    from optimobo_amd.acquisition import engine_for
+    orig_max, pairs = opt._maximise, []
+
+    def recording_max(models, acq_fn):
+        itn = opt._iteration
+        x, v = orig_max(models, acq_fn)
+        if itn in (0, 12, 29):
+            eng = engine_for(models, opt.device)
+            _, v1 = eng.maximise(acq_fn, opt.test_problem.xl, opt.test_problem.xu, n_candidates=opt.n_candidates,
+                                 seed=opt.seed + 7919 * itn, refine_rounds=opt.refine_rounds, starts=1)
+            pairs.append((itn, v, v1))
+        return x, v
+    opt._maximise = recording_max
     res = opt.solve(budget=30, n_init_samples=20, sample_exponent=3,
                     acquisition_func=sc.Tchebicheff([0, 0], [2.5, 2.5]))
     assert len(res.ysample) == 50 and len(rows) == 30
+    assert len(pairs) == 3
+    for itn, v_multi, v_single in pairs:
+        print("multi-start vs single-start", itn, v_multi, v_single)
+        assert v_multi >= v_single - 1e-12 * abs(v_single), (itn, v_multi, v_single)
     for r in rows:
         print(r)
         assert r["cond"] <= 1e10, r

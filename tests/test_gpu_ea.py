@@ -59,7 +59,7 @@ def test_device_search_random_tapes_match_oracle():
     from optimobo_amd import ea
     from optimobo_amd.device import AcqContext
     from optimobo_amd.gp import GPState
-    for seed, d, n in [(11, 3, 40), (12, 7, 150), (13, 5, 90)]:
+    for seed, d, n in [(11, 3, 40), (12, 7, 150), (13, 5, 90), (14, 100, 60), (15, 256, 30)]:
         rng = np.random.default_rng(seed)
         X = rng.uniform(0, 1, (n, d))
         y = np.sin(4 * X).sum(1) + X[:, 0]

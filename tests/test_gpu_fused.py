@@ -36,7 +36,8 @@ def host_points(d, seed, scramble, lo, hi, start, N):
 
 # ----------------------------------------------------------------------------- Sobol'
 @pytest.mark.parametrize("d,seed,scramble", [(1, 0, True), (2, 5, True), (6, 11, True), (30, 3, True),
-                                             (32, 9, True), (6, None, False)])
+                                             (32, 9, True), (6, None, False), (100, 4, True), (256, 8, True),
+                                             (65, None, False)])
 def test_sobol_bit_exact_vs_scipy(ctx, d, seed, scramble):
     rng = np.random.default_rng(d)
     lo = rng.uniform(-3, 0, d)

@@ -42,7 +42,8 @@ def sklearn_lml_grad(X, y, ls, var, nu=2.5):
 
 
 @pytest.mark.parametrize("n,d", [(1, 1), (20, 2), (96, 8), (97, 2), (100, 6), (64, 9), (129, 3), (300, 6),
-                                 (257, 30), (700, 4), (150, 50)])
+                                 (257, 30), (700, 4), (150, 50),
+                                 (12, 100), (150, 100), (70, 256)])   # n_var > 64: wide K and gradient kernels
 def test_lml_grad_vs_sklearn(ctx, n, d):
     X, y, ls, var = data(n, d, n + d)
     lml, g, jit = ctx.gp_lml_grad(X, y, ls, var)
@@ -75,11 +76,14 @@ def test_lml_grad_matches_host_fit(ctx):
     np.testing.assert_allclose(g_d, g_h, rtol=1e-5, atol=1e-5 * np.max(np.abs(g_h)))
 
 
-def test_fit_state_posterior_matches_oracle(ctx):
-    X, y, ls, var = data(400, 6, 13)
+@pytest.mark.parametrize("n,d", [(400, 6), (200, 100)])
+def test_fit_state_posterior_matches_oracle(ctx, n, d):
+    X, y, ls, var = data(n, d, 13)
+    if d > 8:
+        ls = ls * np.sqrt(d)                 # a correlated surface at n_var = 100
     jit = ctx.gp_fit_state(0, X, y, ls, var)
     assert jit == 0.0
-    Xc = np.random.default_rng(14).uniform(0, 1, (3000, 6))
+    Xc = np.random.default_rng(14).uniform(0, 1, (3000, d))
     Xc[:5] = X[:5]
     mu, v = ctx.posterior(torch.as_tensor(Xc, device="cuda:0"), n_obj=1)
     mo, vo = ogp.ExactGP(X, y, ls, var).predict(Xc)

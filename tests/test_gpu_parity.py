@@ -85,7 +85,10 @@ def test_posterior_vs_golden(ctx, golden_dir, name):
                                    (200, 8, 100), (150, 7, 99), (90, 5, 33), (1000, 8, 65),
                                    (200, 30, 97), (256, 17, 65), (129, 3, 31),
                                    (100, 40, 70), (300, 50, 100), (500, 64, 65), (700, 50, 65),
-                                   (200, 64, 97), (100, 64, 130), (1100, 40, 65), (1030, 64, 33)])
+                                   (200, 64, 97), (100, 64, 130), (1100, 40, 65), (1030, 64, 33),
+                                   # n_var > 64: the wide path (omb_wide.hip K block → V = L⁻¹K* → column reduction)
+                                   (64, 65, 100), (100, 100, 300), (129, 128, 97), (300, 200, 130), (40, 256, 50),
+                                   (1100, 100, 65)])
 def test_posterior_sizes(ctx, n, d, N):
     rng = np.random.default_rng(n * 1000 + d)
     X = rng.uniform(0, 1, (n, d))
@@ -126,6 +129,42 @@ def test_posterior_small_n_persistent(ctx, n, d, N, n_obj, kernel):
     assert_posterior(mu[:, idx], var[:, idx], mu_o, var_o, variances)
 
 
+@pytest.mark.parametrize("n,d,N,n_obj,kernel", [
+    (130, 6, 5000, 2, "matern52"), (200, 3, 777, 3, "rbf"), (256, 6, 131072, 3, "matern52"),   # RT 2 (config 4)
+    (257, 6, 65, 1, "matern52"), (400, 17, 3001, 2, "matern52"), (512, 6, 70001, 2, "matern52"),   # RT 4 (config 3)
+    (300, 32, 1000, 1, "rbf"), (256, 30, 33, 2, "matern52")])
+def test_posterior_persistent_ring(ctx, n, d, N, n_obj, kernel):
+    """posterior_persist_kernel (omb_debug_set POSTERIOR_PERSIST): resident workgroups whose LDS ring runs across
+    candidate blocks.  Against the oracle on a sample (whole batch finite) and against posterior_kernel on the same
+    inputs (1e-12: only ‖x*/ℓ‖²'s summation order differs)."""
+    rng = np.random.default_rng(n + d + N)
+    X = rng.uniform(0, 1, (n, d))
+    Y = np.column_stack([np.sin(3 * X).sum(1), np.cos(2 * X).prod(1), (X ** 2).sum(1)])[:, :n_obj]
+    ls = rng.uniform(0.2, 2.0, d) * np.sqrt(d)
+    variances = [float(np.var(Y[:, o]) + 0.1) for o in range(n_obj)]
+    set_gps(ctx, X, Y, ls, variances, kernel=kernel)
+    Xc = rng.uniform(0, 1, (N, d))
+    Xc[: min(3, N)] = X[: min(3, N)]
+    Xd = dev(Xc)
+    mu0, var0 = ctx.posterior(Xd, n_obj=n_obj)
+    ctx.debug_set("posterior_persist", 1)
+    try:
+        mu, var = ctx.posterior(Xd, n_obj=n_obj)
+        mu2, var2 = ctx.posterior(Xd, n_obj=n_obj)
+    finally:
+        ctx.debug_set("posterior_persist", 0)
+    mu, var, mu0, var0 = (t.cpu().numpy() for t in (mu, var, mu0, var0))
+    assert np.array_equal(mu, mu2.cpu().numpy()) and np.array_equal(var, var2.cpu().numpy())   # deterministic
+    assert np.isfinite(mu).all() and np.isfinite(var).all()
+    for o in range(n_obj):
+        np.testing.assert_allclose(mu[o], mu0[o], rtol=1e-12, atol=1e-13 * np.sqrt(variances[o]))
+        np.testing.assert_allclose(var[o], var0[o], rtol=1e-10, atol=1e-13 * variances[o])
+    idx = np.unique(np.concatenate([np.arange(min(N, 40)), np.arange(max(0, N - 40), N),
+                                    rng.choice(N, min(N, 1500), replace=False)]))
+    mu_o, var_o = oracle_posterior(X, Y, ls, variances, Xc[idx], kernel=kernel)
+    assert_posterior(mu[:, idx], var[:, idx], mu_o, var_o, variances)
+
+
 @pytest.mark.parametrize("n", [96, 200, 400, 900])   # every posterior dispatch shape (RT 1/2/4/8)
 def test_posterior_rbf_kernel(ctx, n):
     rng = np.random.default_rng(5)
@@ -141,7 +180,8 @@ def test_posterior_rbf_kernel(ctx, n):
 
 
 @pytest.mark.parametrize("n,d,N", [(20, 2, 100), (512, 6, 4099), (100, 30, 77), (300, 64, 129), (150, 12, 333),
-                                   (257, 8, 1000), (1030, 30, 260)])
+                                   (257, 8, 1000), (1030, 30, 260),
+                                   (65, 65, 1), (100, 100, 300), (300, 200, 129), (64, 256, 70)])
 def test_kernel_block(ctx, n, d, N):
     rng = np.random.default_rng(n + d)
     X = rng.uniform(0, 1, (n, d))

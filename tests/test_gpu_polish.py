@@ -85,3 +85,33 @@ def test_polish_improves_or_keeps(golden_dir):
     assert v1 >= v0
     assert np.all(x1 >= z[f"{k}_xl"]) and np.all(x1 <= z[f"{k}_xu"])
     eng.ctx.close()
+
+
+@pytest.mark.parametrize("flat", ["all_zero", "plateau"])
+def test_multistart_start0_is_argmax_on_ties(flat):
+    """with values tied at the maximum, start 0 of the multi-start search is the lowest-index arg-max
+    (the device rule), not whichever tied entry torch.topk returns; and the multi-start result is never worse than
+    the single-start search's on the same surface."""
+    import torch
+    from optimobo_amd.acquisition import AcquisitionEngine
+    eng = AcquisitionEngine(0)
+    d, N = 3, 1 << 12
+    lo, hi = np.zeros(d), np.ones(d)
+
+    def acq(Xd):
+        if flat == "all_zero":
+            return torch.zeros(Xd.shape[0], dtype=torch.float64, device=Xd.device)
+        # a plateau of value 1 over x_0 < 0.5 (about half the points tie), lower elsewhere
+        return torch.where(Xd[:, 0] < 0.5, torch.ones_like(Xd[:, 0]), Xd[:, 1] * 0.5)
+
+    starts = eng._starts(acq, lo, hi, N, seed=4, k=4)
+    eng.ctx.set_sobol(d, lo, hi, seed=4)
+    U = eng.ctx.sobol(0, N).cpu().numpy()
+    vals = acq(torch.as_tensor(U, device="cuda:0")).cpu().numpy()
+    i0 = int(np.flatnonzero(vals == vals.max())[0])
+    np.testing.assert_array_equal(starts[0][0], U[i0])
+    assert starts[0][1] == vals.max()
+    x1, v1 = eng.maximise(acq, lo, hi, n_candidates=N, seed=4, starts=1, polish=False)
+    x4, v4 = eng.maximise(acq, lo, hi, n_candidates=N, seed=4, starts=4, polish=False)
+    assert v4 >= v1
+    eng.ctx.close()

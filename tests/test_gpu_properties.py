@@ -124,3 +124,28 @@ def test_thompson_select_random_values(N, B, data):
     Y = np.array(vals, np.float64).reshape(B, N)
     got = ctx().thompson_select(dev(Y)).cpu().numpy()
     np.testing.assert_array_equal(got, oturbo.select(Y.T))
+
+
+@pytest.mark.parametrize("P", [1, 3, 17, 30])
+@pytest.mark.parametrize("mode", ["reference", "textbook"])
+def test_ehvi2d_value_independent_of_batch_size(P, mode):
+    """EHVI-2D takes 1, 2 or 4 lanes per candidate by batch size (ehvi2d_lanes); the stripes are summed in
+    four fixed quarters met in one order for every lane count, so the same candidate scores bitwise the same at
+    N = 1 (4 lanes), 2^16 (2 lanes) and 2^19 (1 lane)."""
+    rng = np.random.default_rng(P)
+    f1 = np.sort(rng.uniform(0, 1, P))
+    pf = np.column_stack([f1, 1.0 - np.sqrt(f1)])
+    pf = pf[np.argsort(pf[:, 1], kind="stable")]
+    r = np.array([1.1, 1.1])
+    cache = np.random.default_rng(1).standard_normal((64, 2))
+    s00, s01 = oacq.cache_stats(cache)
+    probe_mu = rng.uniform(0, 1, (2, 8))
+    probe_var = rng.uniform(0.01, 0.2, (2, 8))
+    vals = {}
+    for N in (1, 1 << 16, 1 << 19):
+        mu = np.tile(probe_mu, (1, (N + 7) // 8))[:, :N]
+        var = np.tile(probe_var, (1, (N + 7) // 8))[:, :N]
+        out = ctx().ehvi2d(dev(mu), dev(var), pf, r, s00, s01, mode=mode).cpu().numpy()
+        vals[N] = out[: min(N, 8)]
+    assert np.array_equal(vals[1], vals[1 << 16][:1]) and np.array_equal(vals[1], vals[1 << 19][:1])
+    assert np.array_equal(vals[1 << 16], vals[1 << 19])

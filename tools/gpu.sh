@@ -9,6 +9,7 @@
 #   "prof NAME ARGS..."    rocprofv3 --kernel-trace --stats of bench.py ARGS (OUT/NAME/…, line in OUT/NAME.json)
 #   "pmc NAME ARGS..."     PMC passes (tools/pmc_run.sh) of bench.py ARGS into OUT/NAME
 #   "test NAME PYTEST..."  python -m pytest -m gpu PYTEST > OUT/NAME.txt
+#   "testk NAME K1,K2 FILES..."  the same with -k "K1 or K2" (commas: a step is split on whitespace)
 #   "smoke"                __graft_entry__.smoke() > OUT/smoke.txt
 #   "py NAME SCRIPT ARGS..." python -u SCRIPT ARGS > OUT/NAME.txt
 #   "bin NAME SECS EXE ARGS..." a built tool binary under timeout SECS > OUT/NAME.txt
@@ -38,6 +39,11 @@ for step in "$@"; do
     test)
       name=$1; shift
       timeout -k 10 1000 python -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread "$@" \
+        > "$OUT/$name.txt" 2>&1
+      tail -3 "$OUT/$name.txt" ;;
+    testk)
+      name=$1; kexpr=${2//,/ or }; shift 2
+      timeout -k 10 1000 python -u -m pytest -m gpu --maxfail 20 -v --timeout 300 --timeout-method thread -k "$kexpr" "$@" \
         > "$OUT/$name.txt" 2>&1
       tail -3 "$OUT/$name.txt" ;;
     smoke)

@@ -13,7 +13,10 @@
 //   select_kernel      the greedy per-sample arg-min (np.argmin order) with an LDS exclusion bitmap.
 // The factor is chol(Σ + jitter·I): numpy factors Σ by SVD instead; both draw from N(μ, Σ) up to
 // the jitter, which the caller bounds (omb_posterior_samples).
+#include <algorithm>
+#include <mutex>
 #include <type_traits>
+#include <vector>
 
 #include "omb_internal.h"
 #include "omb_math.h"
@@ -1200,6 +1203,7 @@ struct CholSync {
   int* cnt;     // [t·t]    updates applied to tile (i, j)
   int* ticket;  // task counter of the worker workgroups
   int* abort;   // set by the first wait that runs out
+  const int* tab;   // the workers' task order (chol_task_table), or null for the step-major arithmetic order
 };
 
 // Wave 0 waits (every lane of it, on wave-uniform values) until *p ≥ v: relaxed polls; false after an abort or
@@ -1488,15 +1492,36 @@ __global__ __launch_bounds__(256, kPersistWgPerCu) void chol_persist_kernel(doub
       OMB_PDBG(8 * blockIdx.x + 1, 99);
       return;
     }
-    int k = k0;
-    for (; k < t; ++k) {
-      const int nk = chol_persist_step_tasks(t, k, k0);
-      if (q < nk) break;
-      q -= nk;
+    // the task: from the table (round 5, lookahead order) or the step-major arithmetic order
+    int k = k0, i = 0, j = 0;
+    bool panel;
+    if (sync.tab) {
+      const int e = __builtin_amdgcn_readfirstlane(sync.tab[q]);
+      panel = (e >> 30) == 0;
+      k = (e >> 20) & 1023;
+      i = (e >> 10) & 1023;
+      j = e & 1023;
+    } else {
+      for (; k < t; ++k) {
+        const int nk = chol_persist_step_tasks(t, k, k0);
+        if (q < nk) break;
+        q -= nk;
+      }
+      const int np = chol_persist_np(t, k, k0);
+      panel = q < np;
+      if (panel) {
+        i = k + 2 + q;
+      } else {
+        int u = q - np + 1;                                     // + 1: (k+1, k+1) is the diagonal workgroup's
+        j = k + 1;
+        while (u >= t - j) {
+          u -= t - j;
+          ++j;
+        }
+        i = j + u;
+      }
     }
-    const int np = chol_persist_np(t, k, k0);
-    if (q < np) {
-      const int i = k + 2 + q;
+    if (panel) {
       if (w == 0 && chol_poll_ge<AR>(sync.wflag + k, 1, sync, spin_limit, info))
         chol_poll_ge<AR>(sync.cnt + i * t + k, k, sync, spin_limit, info);
       __syncthreads();
@@ -1508,12 +1533,6 @@ __global__ __launch_bounds__(256, kPersistWgPerCu) void chol_persist_kernel(doub
       OMB_PDBG(8 * blockIdx.x + 1, 3);
       OMB_PTIME(8 * t + 4 * s_task[0] + 2);
     } else {
-      int u = q - np + 1, j = k + 1;                            // + 1: (k+1, k+1) is the diagonal workgroup's
-      while (u >= t - j) {
-        u -= t - j;
-        ++j;
-      }
-      const int i = j + u;
       if (w == 0 && chol_poll_ge<AR>(sync.pflag + i * t + k, 4, sync, spin_limit, info) &&
           chol_poll_ge<AR>(sync.pflag + j * t + k, 4, sync, spin_limit, info))
         chol_poll_ge<AR>(sync.cnt + i * t + j, k, sync, spin_limit, info);
@@ -2563,6 +2582,70 @@ static bool chol_persist_fits(int64_t N, int64_t lda) {
 static hipError_t launch_cholesky_blocked(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws,
                                           int spin_limit, int acq_rel, int steps_limit = -1);
 
+// Round 5: the persistent launch's task order.  Step-major tickets put step k's critical tasks (its panel tiles, the
+// next column's updates) behind every far-column update of step k − 1, and the diagonal walk waited for them.  Here
+// the host sorts the tasks by
+//     P(i, k): (k + 1, k, 0, ·, i)        U(i, j, k): (min(j, k + L), k, 1, j, i)
+// — step k's update of column j no later than "step" k + L, the near columns by their deadline j (the step whose
+// panel needs them).  Every task's inputs (U(i, j, k − 1), P(i, k), P(j, k); P(i, k)'s U(i, k, k − 1)) sort before
+// it, and everything the walk waits for at step k (tiles (k + 1, k), (k + 1, k + 1) through step k − 1) sorts before
+// every task that needs W_k, so the order stays topological and the grid needs no co-residency.  The table (one int
+// per task: panel flag, k, i, j in 10-bit fields) is built once per (device, t, k0, L) and kept.
+#ifdef OMB_TOOLS_KNOBS
+static int g_chol_lookahead = -1;
+void set_chol_lookahead(int L) { g_chol_lookahead = L; }
+#else
+constexpr int g_chol_lookahead = -1;
+#endif
+constexpr int kCholLookahead = 3;
+
+struct CholTaskTab {
+  int dev, t, k0, L;
+  int* d;
+};
+
+static const int* chol_task_table(int t, int k0, int L, int total) {
+  static std::mutex mu;
+  static std::vector<CholTaskTab> tabs;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  for (const CholTaskTab& e : tabs)
+    if (e.dev == dev && e.t == t && e.k0 == k0 && e.L == L) return e.d;
+  struct Key {
+    int a, b, c, d, e, code;
+  };
+  std::vector<Key> keys;
+  keys.reserve(total);
+  for (int k = k0; k < t; ++k) {
+    if (!(k0 > 0 && k == k0))
+      for (int i = k + 2; i < t; ++i) keys.push_back({k + 1, k, 0, 0, i, (k << 20) | (i << 10)});
+    for (int j = k + 1; j < t; ++j)
+      for (int i = j; i < t; ++i) {
+        if (i == k + 1 && j == k + 1) continue;                 // the walker's own D product
+        keys.push_back({std::min(j, k + L), k, 1, j, i, (1 << 30) | (k << 20) | (i << 10) | j});
+      }
+  }
+  if ((int)keys.size() != total || t > 1024) return nullptr;
+  std::sort(keys.begin(), keys.end(), [](const Key& x, const Key& y) {
+    if (x.a != y.a) return x.a < y.a;
+    if (x.b != y.b) return x.b < y.b;
+    if (x.c != y.c) return x.c < y.c;
+    if (x.d != y.d) return x.d < y.d;
+    return x.e < y.e;
+  });
+  std::vector<int> codes(total);
+  for (int q = 0; q < total; ++q) codes[q] = keys[q].code;
+  int* d = nullptr;
+  if (hipMalloc(&d, sizeof(int) * (size_t)std::max(total, 1)) != hipSuccess) return nullptr;
+  if (hipMemcpy(d, codes.data(), sizeof(int) * (size_t)total, hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(d);
+    return nullptr;
+  }
+  tabs.push_back({dev, t, k0, L, d});
+  return d;
+}
+
 // k0 > 0: steps 0 .. k0 − 1 as per-step launches (their bulk trailing updates run at three workgroups per CU), the
 // rest in one persistent launch (the diagonal walk without kernel boundaries once the trailing matrix is small).
 static hipError_t launch_cholesky_persist(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws,
@@ -2576,7 +2659,10 @@ static hipError_t launch_cholesky_persist(hipStream_t stream, double* A, int64_t
   for (int k = k0; k < t; ++k) total += chol_persist_step_tasks(t, k, k0);
   double* Wf = ws;
   int* ints = reinterpret_cast<int*>(ws + (int64_t)t * kCholWsDoubles);
-  CholSync sync{ints, ints + t, ints + t + t * t, ints + t + 2 * t * t, ints + t + 2 * t * t + 1};
+  const int L = g_chol_lookahead >= 0 ? g_chol_lookahead : kCholLookahead;
+  // L = 0 (tools): the step-major arithmetic order of round 4
+  const int* tab = L > 0 ? chol_task_table(t, k0, L, total) : nullptr;
+  CholSync sync{ints, ints + t, ints + t + t * t, ints + t + 2 * t * t, ints + t + 2 * t * t + 1, tab};
   hipLaunchKernelGGL(chol_persist_init_kernel, dim3(1), dim3(256), 0, stream, ints, t, k0, info);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   const int slots = kPersistWgPerCu * device_cus() - 1;

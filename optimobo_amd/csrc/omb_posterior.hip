@@ -605,8 +605,9 @@ __global__ __launch_bounds__(512) void kernel_block_persist_kernel(GPDev g, int 
 // chain at ‖x‖² + ‖x*‖² with −2x* pre-scaled (one fma fewer per element), bit 65536 forces a spin
 // bound of 0 on the counter-ring waits (the fault-word path).
 // NW = waves per workgroup (8 or 16): waves w, w+4, w+8, w+12 share a SIMD.
-template <int RT, int CT, int DP, int KIND, int NW = 8, int ABL = 0>
-__global__ __launch_bounds__(64 * NW, NW / 4) void posterior_kernel(GPArgs args, const double* __restrict__ Xc,
+// WPE: minimum waves per SIMD the register allocation must allow (launch bounds); default NW / 4 (one workgroup)
+template <int RT, int CT, int DP, int KIND, int NW = 8, int ABL = 0, int WPE = NW / 4>
+__global__ __launch_bounds__(64 * NW, WPE) void posterior_kernel(GPArgs args, const double* __restrict__ Xc,
                                                                      int64_t N, double* __restrict__ mu_out,
                                                                      double* __restrict__ var_out) {
   constexpr int NT = 64 * NW;                 // threads per workgroup
@@ -1132,13 +1133,12 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_persist_kernel(GPAr
     }
     mu_part = 0.0;
   };
-  auto gen_chunk = [&](int64_t c) {
-    const int64_t i = c / Q;
-    const int kc = (int)(c - i * Q);
+  // chunk (unit i, kc) into ring slot `slot` (cursors are advanced by the caller: no 64-bit divisions per chunk)
+  auto gen_chunk = [&](int64_t i, int kc, int slot) {
     if (kc == 0) start_gen_unit(i);
     if (kc == Q - 1 && i + 1 < nu) load_raw(i + 1);     // the next unit's coordinates, in flight from here
     const GPDev& g = args.gp[gen_obj];
-    double* buf = ring + (c % 3) * CHUNK;
+    double* buf = ring + slot * CHUNK;
     const double pm[3] = {g.variance, kSqrt5 * g.variance, kFiveThirds * g.variance};
     if (!(NW > TPC && (wave / TPC) != kc % (NW / TPC))) {
 #pragma unroll
@@ -1208,11 +1208,9 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_persist_kernel(GPAr
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) acc[j][ct] = d4{0.0, 0.0, 0.0, 0.0};
   };
-  auto mul_chunk = [&](int64_t c) {
-    const int64_t i = c / Q;
-    const int kc = (int)(c - i * Q);
+  auto mul_chunk = [&](int64_t i, int kc, int slot) {
     if (kc == 0) start_mul_unit(i);
-    const double* buf = ring + (c % 3) * CHUNK;
+    const double* buf = ring + slot * CHUNK;
     int nS[RT];
 #pragma unroll
     for (int j = 0; j < RT; ++j)
@@ -1289,22 +1287,43 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_persist_kernel(GPAr
     }
   };
 
-  // ---- the ring over the workgroup's chunks
+  // ---- the ring over the workgroup's chunks.  Cursors: the multiplied chunk c (unit mi, chunk mk, slot ms, round mr:
+  // ready[ms] reaches NW·(mr + 1) when every wave has generated it), chunk c − 1 (slot ps, round pr) and the
+  // generated chunk c + 2 (unit gi, chunk gk) — all advanced incrementally.
+  int64_t gi = 0, mi = 0;
+  int gk = 0, mk = 0;
+  auto adv = [&](int64_t& ui, int& kk) {
+    if (++kk == Q) {
+      kk = 0;
+      ++ui;
+    }
+  };
   load_raw(0);
-  gen_chunk(0);
+  gen_chunk(gi, gk, 0);
+  adv(gi, gk);
   signal(&ready[0]);
   if (C > 1) {
-    gen_chunk(1);
+    gen_chunk(gi, gk, 1);
+    adv(gi, gk);
     signal(&ready[1]);
   }
+  int ms = 0, mr = 0, ps = 2, pr = -1;
   for (int64_t c = 0; c < C; ++c) {
-    wait_ge(&ready[c % 3], NW * (int)(c / 3 + 1));
-    mul_chunk(c);
-    signal(&done[c % 3]);
+    wait_ge(&ready[ms], NW * (mr + 1));
+    mul_chunk(mi, mk, ms);
+    adv(mi, mk);
+    signal(&done[ms]);
     if (c + 2 < C) {
-      if (c >= 1) wait_ge(&done[(c - 1) % 3], NW * (int)((c - 1) / 3 + 1));
-      gen_chunk(c + 2);
-      signal(&ready[(c + 2) % 3]);
+      if (c >= 1) wait_ge(&done[ps], NW * (pr + 1));   // slot ps held chunk c − 1; chunk c + 2 goes there
+      gen_chunk(gi, gk, ps);
+      adv(gi, gk);
+      signal(&ready[ps]);
+    }
+    ps = ms;
+    pr = mr;
+    if (++ms == 3) {
+      ms = 0;
+      ++mr;
     }
   }
 }

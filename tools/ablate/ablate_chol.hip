@@ -47,6 +47,7 @@ __device__ unsigned long long g_strace[2][8];
 
 #define OMB_TOOLS_KNOBS
 #include "../../optimobo_amd/csrc/omb_linalg.hip"
+#include "../../optimobo_amd/csrc/omb_wide.hip"
 #include "../../optimobo_amd/csrc/omb_gemm.hip"
 
 using namespace omb;

@@ -16,6 +16,7 @@ __device__ unsigned long long g_ftrace[2][8][8];
 
 #include "../../optimobo_amd/csrc/omb_posterior.hip"
 #include "../../optimobo_amd/csrc/omb_linalg.hip"
+#include "../../optimobo_amd/csrc/omb_wide.hip"
 #include "../../optimobo_amd/csrc/omb_gemm.hip"
 
 using namespace omb;

@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../../optimobo_amd/csrc/omb_posterior.hip"
+#include "../../optimobo_amd/csrc/omb_wide.hip"
 
 using namespace omb;
 

@@ -10,6 +10,7 @@
 #include <algorithm>
 
 #include "../../optimobo_amd/csrc/omb_posterior.hip"
+#include "../../optimobo_amd/csrc/omb_wide.hip"
 
 using namespace omb;
 

@@ -29,6 +29,7 @@ __device__ unsigned long long g_ptrace[4096][8];
   } while (0)
 
 #include "../../optimobo_amd/csrc/omb_posterior.hip"
+#include "../../optimobo_amd/csrc/omb_wide.hip"
 
 using namespace omb;
 
@@ -42,16 +43,17 @@ struct Bench {
   double *mu, *var;
 };
 
-template <int RT, int CT, int NW, int ABL, int DP = 6>
+template <int RT, int CT, int NW, int ABL, int DP = 6, int WPE = NW / 4>
 float run(const Bench& b, int reps) {
   dim3 grid((unsigned)((b.N + 16 * CT - 1) / (16 * CT)), b.n_obj);
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  hipLaunchKernelGGL((posterior_kernel<RT, CT, DP, 0, NW, ABL>), grid, dim3(64 * NW), 0, 0, b.a, b.Xc, b.N, b.mu, b.var);
+  hipLaunchKernelGGL((posterior_kernel<RT, CT, DP, 0, NW, ABL, WPE>), grid, dim3(64 * NW), 0, 0, b.a, b.Xc, b.N, b.mu,
+                     b.var);
   CK(hipEventRecord(e0));
   for (int i = 0; i < reps; ++i)
-    hipLaunchKernelGGL((posterior_kernel<RT, CT, DP, 0, NW, ABL>), grid, dim3(64 * NW), 0, 0, b.a, b.Xc, b.N, b.mu,
+    hipLaunchKernelGGL((posterior_kernel<RT, CT, DP, 0, NW, ABL, WPE>), grid, dim3(64 * NW), 0, 0, b.a, b.Xc, b.N, b.mu,
                        b.var);
   CK(hipEventRecord(e1));
   CK(hipEventSynchronize(e1));
@@ -338,6 +340,8 @@ int main(int argc, char** argv) {
   };
   const Variant small256[] = {
       {"RT2 CT2 counter ring (library n<=256)", run<2, 2, 8, 0>},
+      {"RT2 CT2 ring, 5 waves/SIMD bound", run<2, 2, 8, 0, 6, 5>},
+      {"RT2 CT2 ring, 6 waves/SIMD bound", run<2, 2, 8, 0, 6, 6>},
       {"RT2 CT4 counter ring", run<2, 4, 8, 0>},
       {"RT1 CT2 16 waves ring", run<1, 2, 16, 0>},
       {"RT1 CT4 16 waves ring", run<1, 4, 16, 0>},

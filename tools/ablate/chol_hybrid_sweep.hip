@@ -1,7 +1,8 @@
 // Per-step launches for the first k0 steps, then the persistent launch (launch_cholesky_persist's k0): time and
 // factor against the per-step launches alone, for a list of k0 (tools only).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/ablate/chol_hybrid_sweep tools/ablate/chol_hybrid_sweep.hip
-// Run:   ./tools/ablate/chol_hybrid_sweep N [N ...]   (k0 list from CHOL_K0S, default 0,4,8,12,16,24,32)
+// Run:   ./tools/ablate/chol_hybrid_sweep N [N ...]   (k0 list from CHOL_K0S, default 0,4,8,12,16,24,32; the
+//        persistent launch's lookahead L list from CHOL_LS, default 3 — 0 = round 4's step-major task order)
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -12,6 +13,7 @@
 
 #define OMB_TOOLS_KNOBS
 #include "../../optimobo_amd/csrc/omb_linalg.hip"
+#include "../../optimobo_amd/csrc/omb_wide.hip"
 #include "../../optimobo_amd/csrc/omb_gemm.hip"
 
 using namespace omb;
@@ -36,6 +38,18 @@ int main(int argc, char** argv) {
       size_t q = s.find(',', p);
       if (q == std::string::npos) q = s.size();
       k0s.push_back(atoi(s.substr(p, q - p).c_str()));
+      p = q + 1;
+    }
+  }
+  std::vector<int> Ls = {3};
+  if (const char* e = getenv("CHOL_LS")) {
+    Ls.clear();
+    std::string s(e);
+    size_t p = 0;
+    while (p < s.size()) {
+      size_t q = s.find(',', p);
+      if (q == std::string::npos) q = s.size();
+      Ls.push_back(atoi(s.substr(p, q - p).c_str()));
       p = q + 1;
     }
   }
@@ -80,15 +94,18 @@ int main(int argc, char** argv) {
     int ib = run(kCholBlocked, -1, tb);
     CK(hipMemcpy(R.data(), A, N * N * 8, hipMemcpyDeviceToHost));
     printf("N=%lld per-step launches %.3f ms info %d\n", (long long)N, tb, ib);
+    for (int la : Ls)
     for (int k0 : k0s) {
+      set_chol_lookahead(la);
       float tp;
       const int ip = run(kCholPersistent, k0, tp);
       CK(hipMemcpy(L.data(), A, N * N * 8, hipMemcpyDeviceToHost));
       double md = 0.0;
       for (int64_t i = 0; i < N; ++i)
         for (int64_t j = 0; j <= i; ++j) md = std::max(md, std::abs(L[i * N + j] - R[i * N + j]) / std::sqrt(h[i * N + i]));
-      printf("N=%lld k0=%d: %.3f ms info %d max |L - L_steps|/sqrt(A_ii) %.2e\n", (long long)N, k0, tp, ip, md);
+      printf("N=%lld L=%d k0=%d: %.3f ms info %d max |L - L_steps|/sqrt(A_ii) %.2e\n", (long long)N, la, k0, tp, ip, md);
     }
+    set_chol_lookahead(-1);
     set_chol_hybrid_k0(-1);
     CK(hipFree(A0)); CK(hipFree(A)); CK(hipFree(ws)); CK(hipFree(info));
   }

@@ -6,6 +6,7 @@
 #include <vector>
 
 #include "../../optimobo_amd/csrc/omb_linalg.hip"
+#include "../../optimobo_amd/csrc/omb_wide.hip"
 
 using namespace omb;
 

@@ -9,8 +9,8 @@ export TMPDIR=/tmp
 ARGS="bench.py --steps 3 --warmup 1 --no-cpu-baseline ${PMC_BENCH_ARGS:-}"
 i=0
 # PMC_GROUPS: ';'-separated counter groups (one rocprofv3 pass each) in place of the default four
-GROUPS=${PMC_GROUPS:-"FETCH_SIZE;WRITE_SIZE;SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE;TCC_HIT_sum TCC_MISS_sum"}
-IFS=';' read -r -a GROUP_LIST <<< "$GROUPS"
+PGROUPS=${PMC_GROUPS:-"FETCH_SIZE;WRITE_SIZE;SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE;TCC_HIT_sum TCC_MISS_sum"}
+IFS=';' read -r -a GROUP_LIST <<< "$PGROUPS"
 for grp in "${GROUP_LIST[@]}"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $grp -d "$GRAFT_REPO_ROOT/$OUT" -o pass$i --output-format csv -- python3 $ARGS > "$OUT/pass$i.log" 2>&1

@@ -356,6 +356,22 @@ def load_traffic(n, N, kernel="posterior"):
         return None
 
 
+def load_pipe(config, kernel):
+    """FP64-pipe occupancy of a kernel from the committed PMC summary (tools/pmc_pipe.py → profiles/r05_h_pmc_pipe.json):
+    MFMA-busy and VALU-issue fractions per SIMD (they never co-execute on gfx950), or None."""
+    path = os.path.join(REPO, "profiles", "r05_h_pmc_pipe.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    for k, v in t.items():
+        if k.startswith(f"pmc_c{config}:") and kernel in k:
+            return {x: v[x] for x in ("mfma_busy_frac", "valu_issue_frac", "fp64_pipe_busy_frac") if x in v} | \
+                {"source": "profiles/r05_h_pmc_pipe.json (rocprofv3 --pmc, separate passes)"}
+    return None
+
+
 def _free_port():
     import socket
     with socket.socket() as sk:
@@ -647,8 +663,11 @@ def main():
                   "frac": kb_bytes / (kb_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": load_traffic(n, N, "kblock"),
                   "fp64_frac": kb_fp64, "fp64_tflops": kb_flops / (kb_ms * 1e-3) / 1e12,
                   "ms": kb_ms,
+                  "pipe": load_pipe(args.config, "kernel_block"),
                   "note": f"omb_kernel_block writes K ({n}, {N}) fp64 to HBM; frac = HBM fraction, fp64_frac = "
-                          f"{n * (2 * d + 12)} flop per candidate / time / {FP64_MFMA_PEAK_TFLOPS} TFLOP/s"}
+                          f"{n * (2 * d + 12)} flop per candidate / time / {FP64_MFMA_PEAK_TFLOPS} TFLOP/s; pipe = the "
+                          f"FP64 pipe's MFMA + VALU occupancy from PMC (the Matern transform's VALU work and the "
+                          f"cross-term MFMAs share it)"}
         del K
 
     # per-iteration model-state install, outside `value`: what a BO iteration does before its
@@ -676,6 +695,7 @@ def main():
                 "kernel": f"posterior_kernel (omb_posterior, {n_obj} objective(s), n_train={n}, n_var={d})",
                 "ms_per_launch": post_ms,
                 "launches_timed": int(chains),
+                "pipe": load_pipe(args.config, "posterior_kernel"),
                 "timing_stride": stride,
                 "check": check,
                 "timing": "HIP events on the chain's stream around the posterior launch"

@@ -90,6 +90,7 @@ struct omb_ctx {
   double* fit_dev = nullptr;
   int spin_limit = kDefaultSpinLimit;
   bool cov_table = false;   // OMB_DEBUG_COV_TABLE
+  bool cov_fused = true;    // OMB_DEBUG_COV_FUSED: K(X*, X*) in the covariance SYRK's epilogue
   int fused_chain = 0;  // OMB_DEBUG_FUSED_CHAIN: 0 EHVI-2D then the arg-max's passes, 1 one ticketed launch, 2 EHVI
                         // with the per-workgroup pairs, then the arg-max's second pass
   bool argmax_one_pass = false;  // OMB_DEBUG_ARGMAX_PASSES: 1 (one launch) or 2 (default: measured level)
@@ -545,6 +546,10 @@ int omb_debug_set(omb_ctx* ctx, int what, int64_t value) {
   if (what == OMB_DEBUG_TIMING_STRIDE) {
     if (value < 1 || value > 0x7fffffff) return fail(ctx, OMB_EINVAL, "timing stride %lld < 1", (long long)value);
     ctx->timing_stride = (int)value;
+    return OMB_OK;
+  }
+  if (what == OMB_DEBUG_COV_FUSED) {
+    ctx->cov_fused = value != 0;
     return OMB_OK;
   }
   if (what == OMB_DEBUG_POSTERIOR_PERSIST) {
@@ -1029,6 +1034,14 @@ static hipError_t cov_prepare(omb_ctx* ctx, const ObjState& s, const double* Xc,
 // cand_cov_ws_doubles(N, DP) doubles.
 static hipError_t cov_build(omb_ctx* ctx, const ObjState& s, const double* Xc, int64_t N, const double* V, double* S,
                             int64_t lds, double* cws, double jitter = 0.0) {
+  if (!ctx->cov_table && ctx->cov_fused && s.DP <= kMaxFusedDP) {
+    // K(X*, X*) formed in the SYRK's epilogue (launch_cov_syrk): the two-launch result below to the ulp
+    hipError_t e = hipSuccess;
+    const int kp = launch_cand_scale(ctx->stream, s.dev, s.d, s.DP, Xc, N, cws, &e);
+    if (e == hipSuccess && kp > 0)
+      return launch_cov_syrk(ctx->stream, N, s.n, V, N, S, lds, cws, cws + N * kp, kp, s.kind, s.variance, jitter);
+    if (e != hipSuccess) return e;
+  }
   hipError_t e = launch_cand_cov(ctx->stream, s.dev, s.d, s.DP, Xc, N, S, lds, cws, jitter, ctx->cov_table);
   if (e == hipSuccess) e = launch_gemm_tn_lower(ctx->stream, N, s.n, -1.0, V, N, 1.0, S, lds);
   return e;

@@ -23,13 +23,29 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 // ATRI (round 3): op(A) is lower-triangular (op(A)(m, k) = 0 for k > m, e.g. the dense L⁻¹ of V = L⁻¹K*):
 // slabs past the tile's last row are skipped and the entries above the diagonal read as zero, so the
 // upper triangle is never read (as the packed posterior path never reads it) and half the work goes.
-template <bool TA, bool TB, bool BTRI, bool LOWER, bool ATRI = false>
+// KSS (round 5, the posterior covariance): C = K(X*, X*) − op(A)·op(B) on the lower triangle, the kernel block of
+// the tile formed in the epilogue from the scaled candidates (CovEpi: X*/ℓ rows of kp doubles and ‖·‖², as
+// cand_scale_kernel writes them) — cand_cov_kernel's arithmetic in its order (the cross term on MFMA over k-steps of
+// 4 ascending, r² = −2·a·b + (‖a‖² + ‖b‖²) with the diagonal forced to 0, kernel_of_r2, + diag_add on the
+// diagonal), so C is what cand_cov_kernel then gemm_kernel(β = 1, α = −1) store — to the ulp of the Matern
+// polynomial, whose FMA contraction the compiler picks per kernel (measured ≤ 6e-17 absolute at σ_f² ≈ 0.5, the
+// diagonal bitwise; gpurun_out/r05_j) — without the 8N² bytes of K(X*, X*) written and read back and its launch.
+struct CovEpi {
+  const double* xs;
+  const double* xsq;
+  int kp;
+  int kind;
+  double variance;
+  double diag_add;
+};
+
+template <bool TA, bool TB, bool BTRI, bool LOWER, bool ATRI = false, bool KSS = false>
 __global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t Nc, int64_t K, double alpha,
                                                    const double* __restrict__ A, int64_t lda,
                                                    const double* __restrict__ B, int64_t ldb, double beta,
                                                    double* __restrict__ C, int64_t ldc,
                                                    const double* __restrict__ col_bias, int64_t kchunk,
-                                                   int64_t zstride) {
+                                                   int64_t zstride, CovEpi ce) {
   // ATRI: the last row tiles carry the most slabs, so they are dispatched first
   const int64_t m0 = (int64_t)(ATRI ? gridDim.y - 1 - blockIdx.y : blockIdx.y) * kGT, n0 = (int64_t)blockIdx.x * kGT;
   if (LOWER && n0 > m0) return;   // tile strictly above the diagonal
@@ -146,6 +162,57 @@ __global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t Nc, int64_
     multiply(buf);
   }
 
+  if constexpr (KSS) {
+    // the tile of K(X*, X*): cross term over kp dimensions in slabs of 16 through As[0] / Bs[0]
+    d4 cr[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) cr[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int k0 = 0; k0 < ce.kp; k0 += kGK) {
+      __syncthreads();                                       // the product's last slab is read by every wave
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int idx = tid + 256 * e, r = idx >> 4, k = idx & 15;
+        const int64_t ra = m0 + r < M ? m0 + r : M - 1, rb = n0 + r < Nc ? n0 + r : Nc - 1;
+        As[0][k][r] = k0 + k < ce.kp ? ce.xs[ra * ce.kp + k0 + k] : 0.0;
+        Bs[0][k][r] = k0 + k < ce.kp ? ce.xs[rb * ce.kp + k0 + k] : 0.0;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int ks = 0; ks < kGK / 4; ++ks) {
+        const int kk = 4 * ks + (lane >> 4);
+        const double a0 = As[0][kk][32 * wm + (lane & 15)];
+        const double a1 = As[0][kk][32 * wm + 16 + (lane & 15)];
+        const double b0 = Bs[0][kk][32 * wn + (lane & 15)];
+        const double b1 = Bs[0][kk][32 * wn + 16 + (lane & 15)];
+        cr[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, cr[0][0], 0, 0, 0);
+        cr[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, cr[0][1], 0, 0, 0);
+        cr[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, cr[1][0], 0, 0, 0);
+        cr[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, cr[1][1], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const int64_t col = n0 + 32 * wn + 16 * cb + (lane & 15);
+      const double bsq = col < Nc ? ce.xsq[col] : 0.0;
+#pragma unroll
+      for (int rb2 = 0; rb2 < 2; ++rb2)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int64_t row = m0 + 32 * wm + 16 * rb2 + (lane >> 4) + 4 * i;
+          if (row < M && col < Nc && col <= row) {
+            const double r2 = (row == col) ? 0.0 : fma(-2.0, cr[rb2][cb][i], ce.xsq[row] + bsq);
+            double kv = ce.kind == OMB_KERNEL_RBF ? kernel_of_r2<OMB_KERNEL_RBF>(r2, ce.variance)
+                                                  : kernel_of_r2<OMB_KERNEL_MATERN52>(r2, ce.variance);
+            if (row == col) kv = kv + ce.diag_add;
+            C[row * ldc + col] = fma(1.0, kv, alpha * acc[rb2][cb][i]);
+          }
+        }
+    }
+    return;
+  }
+
   // C/D map of v_mfma_f64_16x16x4f64: col = lane & 15, row = (lane >> 4) + 4·i
 #pragma unroll
   for (int rb2 = 0; rb2 < 2; ++rb2)
@@ -171,7 +238,7 @@ static hipError_t gemm(hipStream_t stream, int64_t M, int64_t Nc, int64_t K, dou
   if (M <= 0 || Nc <= 0) return hipSuccess;
   dim3 grid((unsigned)((Nc + kGT - 1) / kGT), (unsigned)((M + kGT - 1) / kGT));
   hipLaunchKernelGGL((gemm_kernel<TA, TB, BTRI, LOWER, ATRI>), grid, dim3(256), 0, stream, M, Nc, K, alpha, A, lda, B,
-                     ldb, beta, C, ldc, col_bias, (int64_t)0, (int64_t)0);
+                     ldb, beta, C, ldc, col_bias, (int64_t)0, (int64_t)0, CovEpi{});
   return hipGetLastError();
 }
 
@@ -240,12 +307,22 @@ hipError_t launch_chol_samples(hipStream_t stream, const double* L, int64_t N, i
   const int64_t zstride = (int64_t)B * N;
   dim3 grid((unsigned)((N + kGT - 1) / kGT), (unsigned)((B + kGT - 1) / kGT), (unsigned)S);
   hipLaunchKernelGGL((gemm_kernel<false, true, true, false>), grid, dim3(256), 0, stream, (int64_t)B, N, N, 1.0, Zt,
-                     N, L, ldl, 0.0, ws, N, (const double*)nullptr, kchunk, zstride);
+                     N, L, ldl, 0.0, ws, N, (const double*)nullptr, kchunk, zstride, CovEpi{});
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int64_t tot = (int64_t)B * N;
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, ws, S, zstride,
                      (int64_t)B, N, mu, Y, N, kchunk);
+  return hipGetLastError();
+}
+
+hipError_t launch_cov_syrk(hipStream_t s, int64_t N, int64_t K, const double* V, int64_t ldv, double* S, int64_t lds,
+                           const double* xs, const double* xsq, int kp, int kind, double variance, double diag_add) {
+  if (N <= 0) return hipSuccess;
+  const dim3 grid((unsigned)((N + kGT - 1) / kGT), (unsigned)((N + kGT - 1) / kGT));
+  hipLaunchKernelGGL((gemm_kernel<true, false, false, true, false, true>), grid, dim3(256), 0, s, N, N, K, -1.0, V, ldv,
+                     V, ldv, 0.0, S, lds, (const double*)nullptr, (int64_t)0, (int64_t)0,
+                     CovEpi{xs, xsq, kp, kind, variance, diag_add});
   return hipGetLastError();
 }
 

@@ -145,6 +145,14 @@ hipError_t launch_gemm_tn_lower(hipStream_t s, int64_t N, int64_t K, double alph
 int64_t cand_cov_ws_doubles(int64_t N, int DP);
 hipError_t launch_cand_cov(hipStream_t stream, const GPDev& g, int d, int DP, const double* Xc, int64_t N, double* S,
                            int64_t lds, double* ws, double diag_add = 0.0, bool table = false);
+// X*/ℓ rows (kp = ⌈DP/4⌉·4 doubles, written to ws) and their squared norms (ws + N·kp), as launch_cand_cov stages
+// them; returns kp (0 for DP > kMaxFusedDP: the wide path has its own staging)
+int launch_cand_scale(hipStream_t stream, const GPDev& g, int d, int DP, const double* Xc, int64_t N, double* ws,
+                      hipError_t* err);
+// lower triangle of S = K(X*, X*) + diag_add·I − VᵀV, V (K, N): the covariance SYRK with K(X*, X*) formed in its
+// epilogue from launch_cand_scale's rows (omb_gemm.hip gemm_kernel<…, KSS>)
+hipError_t launch_cov_syrk(hipStream_t s, int64_t N, int64_t K, const double* V, int64_t ldv, double* S, int64_t lds,
+                           const double* xs, const double* xsq, int kp, int kind, double variance, double diag_add);
 hipError_t launch_mirror_lower(hipStream_t stream, double* S, int64_t N, int64_t lds);
 hipError_t launch_add_diag(hipStream_t stream, double* S, int64_t N, int64_t lds, double v);
 // in-place lower Cholesky; info (device int, zeroed by the first kernel) = first bad column (1-based);

@@ -2476,6 +2476,26 @@ hipError_t launch_cand_cov(hipStream_t stream, const GPDev& g, int d, int DP, co
   return hipGetLastError();
 }
 
+int launch_cand_scale(hipStream_t stream, const GPDev& g, int d, int DP, const double* Xc, int64_t N, double* ws,
+                      hipError_t* err) {
+  *err = hipSuccess;
+  if (N <= 0 || DP > kMaxFusedDP) return 0;
+  const int KP = (DP + 3) / 4 * 4;
+  const unsigned sb = (unsigned)((N * KP + 255) / 256);
+  switch (DP) {
+#define OMB_CS(DPV)                                                                                               \
+  case DPV:                                                                                                       \
+    hipLaunchKernelGGL((cand_scale_kernel<DPV>), dim3(sb), dim3(256), 0, stream, Xc, d, N, g.ls, ws, ws + N * KP); \
+    break;
+    OMB_CS(2) OMB_CS(4) OMB_CS(6) OMB_CS(8) OMB_CS(16) OMB_CS(32) OMB_CS(64)
+#undef OMB_CS
+    default:
+      return 0;
+  }
+  *err = hipGetLastError();
+  return KP;
+}
+
 hipError_t launch_mirror_lower(hipStream_t stream, double* S, int64_t N, int64_t lds) {
   const unsigned nt = (unsigned)((N + 31) / 32);
   hipLaunchKernelGGL(mirror_lower_kernel, dim3(nt, nt), dim3(256), 0, stream, S, N, lds);

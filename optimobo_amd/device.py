@@ -78,7 +78,7 @@ class AcqContext:
         code = {"spin_limit": _lib.DEBUG_SPIN_LIMIT, "cov_table": _lib.DEBUG_COV_TABLE,
                 "fused_chain": _lib.DEBUG_FUSED_CHAIN, "argmax_passes": _lib.DEBUG_ARGMAX_PASSES,
                 "chol_mode": _lib.DEBUG_CHOL_MODE, "timing_stride": _lib.DEBUG_TIMING_STRIDE,
-                "posterior_persist": _lib.DEBUG_POSTERIOR_PERSIST}[what]
+                "posterior_persist": _lib.DEBUG_POSTERIOR_PERSIST, "cov_fused": _lib.DEBUG_COV_FUSED}[what]
         self._check(self.lib.omb_debug_set(self._h, code, int(value)), "omb_debug_set")
 
     # ------------------------------------------------------------------ GP state

@@ -61,6 +61,33 @@ def test_posterior_cov_vs_oracle(ctx, n, d, N, kernel):
     np.testing.assert_allclose(mu, m2[0].cpu().numpy(), rtol=1e-12, atol=1e-12 * np.sqrt(var))
 
 
+@pytest.mark.parametrize("n,d,N,kernel", [(20, 2, 77, "matern52"), (300, 6, 700, "rbf"), (512, 30, 3000, "matern52"),
+                                          (129, 64, 130, "matern52")])
+def test_posterior_cov_fused_epilogue_bitwise(ctx, n, d, N, kernel):
+    """OMB_DEBUG_COV_FUSED: K(X*, X*) formed in the covariance SYRK's epilogue against the two-launch build
+    (cand_cov_kernel, then the VᵀV update): the same arithmetic in the same order, compiled into two kernels whose
+    FMA contraction of the Matern polynomial may differ by an ulp (K** ≈ σ_f² cancels to Σ ≪ σ_f², so the entries
+    agree to ~1e-16·σ_f² absolute); the diagonal and μ bitwise; the joint draws to rounding."""
+    X, y, ls, var, og = fit(ctx, n, d, seed=n + d + 7, kernel=kernel)
+    rng = np.random.default_rng(N + 1)
+    Xc = dev(np.clip(X[0] + 0.4 * (rng.uniform(0, 1, (N, d)) - 0.5), 0, 1))
+    Z = dev(rng.standard_normal((8, N)))
+    mu1, cov1 = ctx.posterior_cov(0, Xc)
+    Y1, j1 = ctx.posterior_samples(0, Xc, Z)
+    ctx.debug_set("cov_fused", 0)
+    try:
+        mu0, cov0 = ctx.posterior_cov(0, Xc)
+        Y0, j0 = ctx.posterior_samples(0, Xc, Z)
+    finally:
+        ctx.debug_set("cov_fused", 1)
+    assert torch.equal(mu1, mu0)
+    c1, c0 = cov1.cpu().numpy(), cov0.cpu().numpy()
+    np.testing.assert_allclose(c1, c0, rtol=0, atol=1e-14 * var)
+    assert np.array_equal(np.diag(c1), np.diag(c0))
+    assert j1 == j0
+    np.testing.assert_allclose(Y1.cpu().numpy(), Y0.cpu().numpy(), rtol=0, atol=1e-8 * np.sqrt(var))
+
+
 # ----------------------------------------------------------------------------- Cholesky
 def spd(N, seed):
     rng = np.random.default_rng(seed)

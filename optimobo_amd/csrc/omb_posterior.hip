@@ -606,6 +606,19 @@ __global__ __launch_bounds__(512) void kernel_block_persist_kernel(GPDev g, int 
 // bound of 0 on the counter-ring waits (the fault-word path).
 // NW = waves per workgroup (8 or 16): waves w, w+4, w+8, w+12 share a SIMD.
 // WPE: minimum waves per SIMD the register allocation must allow (launch bounds); default NW / 4 (one workgroup)
+// The packed L⁻¹'s k-step pair P of row tile r (lane l: 16 B at Lp + 128 r(r+1) + 128 min(P, 2r+1) + 2l), as a buffer
+// load whose wave-uniform part is the SGPR offset: the global-pointer form cost one 64-bit VALU address add per load
+// on the FP64 pipe's issue port — 8 per k-step pair at RT = 8 — and was 2-3% slower (interleaved, bitwise the same:
+// configs 3 / 4 / 5 10.12 / 0.621 / 10.35 → 9.92 / 0.601 / 10.02 ms, profiles/r05_t_ablate_posterior_bufA_c*.txt).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t lp_rsrc(const GPDev& g) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(g.Lp), (short)0, (int)(1024ll * g.R * (g.R + 1)),
+                                           0x00020000);
+}
+__device__ __forceinline__ d2 load_lpair(__amdgpu_buffer_rsrc_t rsrc, int lane, int r, int P) {
+  const int soff = 1024 * (r * (r + 1) + min(P, 2 * r + 1));
+  return __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rsrc, 16 * lane, soff, 0));
+}
+
 template <int RT, int CT, int DP, int KIND, int NW = 8, int ABL = 0, int WPE = NW / 4>
 __global__ __launch_bounds__(64 * NW, WPE) void posterior_kernel(GPArgs args, const double* __restrict__ Xc,
                                                                      int64_t N, double* __restrict__ mu_out,
@@ -736,6 +749,7 @@ __global__ __launch_bounds__(64 * NW, WPE) void posterior_kernel(GPArgs args, co
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) acc[j][ct] = d4{0.0, 0.0, 0.0, 0.0};
   double mu_part = 0.0;
+  const __amdgpu_buffer_rsrc_t rsrc_L = lp_rsrc(g);
 
   // one K* element: Matern (or RBF) of training row k and this thread's candidate
   auto element = [&](int k) -> double {
@@ -868,10 +882,13 @@ __global__ __launch_bounds__(64 * NW, WPE) void posterior_kernel(GPArgs args, co
     auto load_a = [&](int sp, d2* dst) {
 #pragma unroll
       for (int j = 0; j < RT; ++j) {
-        if constexpr (ABL & 4)
+        if constexpr (ABL & 4) {
           dst[j] = d2{1e-3 * lane + sp, 2e-3 * j};
-        else
+        } else if constexpr (!(ABL & 131072)) {
+          dst[j] = load_lpair(rsrc_L, lane, slot_r[j], P0 + sp);
+        } else {   // ABL 131072: round 4's global load (a 64-bit VALU address add per load)
           dst[j] = *reinterpret_cast<const d2*>(slot_A[j] + 128 * min(P0 + sp, 2 * slot_r[j] + 1));
+        }
       }
     };
 #pragma unroll
@@ -1187,7 +1204,7 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_persist_kernel(GPAr
   // ---- multiply state (the unit being multiplied)
   const int simd = wave & 3, h = wave >> 2;
   int slot_r[RT], slot_q[RT];
-  const double* slot_A[RT];
+  __amdgpu_buffer_rsrc_t rsrc_L = lp_rsrc(args.gp[0]);   // the objective's packed L⁻¹ (load_lpair)
   d4 acc[RT][CT];
   auto start_mul_unit = [&](int64_t i) {
     int obj;
@@ -1201,8 +1218,8 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_persist_kernel(GPAr
       const bool ok = r < g.R;
       slot_q[j] = ok ? q : -1;
       slot_r[j] = ok ? r : 0;
-      slot_A[j] = g.Lp + 128ll * slot_r[j] * (slot_r[j] + 1) + 2 * lane;
     }
+    rsrc_L = lp_rsrc(g);
 #pragma unroll
     for (int j = 0; j < RT; ++j)
 #pragma unroll
@@ -1221,7 +1238,7 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void posterior_persist_kernel(GPAr
     auto load_a = [&](int sp, d2* dst) {
 #pragma unroll
       for (int j = 0; j < RT; ++j)
-        dst[j] = *reinterpret_cast<const d2*>(slot_A[j] + 128 * min(P0 + sp, 2 * slot_r[j] + 1));
+        dst[j] = load_lpair(rsrc_L, lane, slot_r[j], P0 + sp);
     };
 #pragma unroll
     for (int p = 0; p < PD; ++p) load_a(p, a_ring[p]);

@@ -290,6 +290,9 @@ int main(int argc, char** argv) {
   b.var = var;
   const Variant wide[] = {
       {"default RT8 CT2 (MFMA gen)", run<8, 2, 8, 0, 32>},
+      {"global A loads, r04 (131072)", run<8, 2, 8, 131072, 32>},
+      {"default again", run<8, 2, 8, 0, 32>},
+      {"global A loads again", run<8, 2, 8, 131072, 32>},
       {"tab64 exp (16384)", run<8, 2, 8, 16384, 32>},
       {"tab256 + short sqrt (32768)", run<8, 2, 8, 32768, 32>},
       {"VALU gen (2048)", run<8, 2, 8, 2048, 32>},
@@ -304,6 +307,9 @@ int main(int argc, char** argv) {
   };
   const Variant narrow[] = {
       {"default (ring, MFMA gen)", run<4, 4, 8, 0>},
+      {"global A loads, r04 (131072)", run<4, 4, 8, 131072>},
+      {"default again", run<4, 4, 8, 0>},
+      {"global A loads again", run<4, 4, 8, 131072>},
       {"RT4 CT2 counter ring", run<4, 2, 8, 0>},
       {"tab64 exp (16384)", run<4, 4, 8, 16384>},
       {"tab256 + short sqrt (32768)", run<4, 4, 8, 32768>},
@@ -340,6 +346,9 @@ int main(int argc, char** argv) {
   };
   const Variant small256[] = {
       {"RT2 CT2 counter ring (library n<=256)", run<2, 2, 8, 0>},
+      {"RT2 CT2 ring, global A loads (131072)", run<2, 2, 8, 131072>},
+      {"RT2 CT2 counter ring again", run<2, 2, 8, 0>},
+      {"RT2 CT2 ring, global A loads again", run<2, 2, 8, 131072>},
       {"RT2 CT2 ring, 5 waves/SIMD bound", run<2, 2, 8, 0, 6, 5>},
       {"RT2 CT2 ring, 6 waves/SIMD bound", run<2, 2, 8, 0, 6, 6>},
       {"RT2 CT4 counter ring", run<2, 4, 8, 0>},

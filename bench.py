@@ -443,7 +443,7 @@ def main():
                     help="record the timing events on every s-th step of the timed loop only (each record adds "
                          "~2.5 us of GPU time to its step: config 2 82.8 us per step with events on every step, "
                          "77.3-77.8 on every 8th, gpurun_out/r04_ae).  Default: from the warm-up's step length, "
-                         "1 for steps >= 1 ms (configs 3-5: 2.5 us is < 0.05%), else 8")
+                         "1 for steps >= 1 ms (configs 3-5: 2.5 us is < 0.05%%), else 8")
     ap.add_argument("--one-launch", type=int, default=None, choices=[0, 1, 2],
                     help="omb_debug_set(FUSED_CHAIN): 0 EHVI-2D and the arg-max as separate launches, 1 as one "
                          "ticketed launch, 2 EHVI-2D reducing to per-workgroup pairs + the arg-max's second pass "

@@ -43,3 +43,11 @@ def test_bench_two_ranks_on_device():
     assert rec["distributed"]["backend"] == "gloo"
     assert rec["config"]["global_batch"] == 2 * 4096 and rec["value"] > 0
     assert rec["best"]["index"] >= 0
+
+
+def test_bench_help_renders():
+    """Every option's help text formats (argparse %-expands it: a stray '%' broke `bench.py --help`)."""
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--help"], capture_output=True, text=True,
+                       timeout=240, cwd=REPO)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert "--config" in p.stdout and "--timing-stride" in p.stdout

@@ -376,20 +376,19 @@ int main(int argc, char** argv) {
       {"tile RMAX8 CT4", run_tile<8, 4, 0>},
   };
   const Variant small256[] = {
-      {"RT2 CT2 counter ring (library n<=256)", run<2, 2, 8, 0>},
-      {"persistent ring RT2 CT2", run_persist<2, 2>},
-      {"RT2 CT2 ring, global A loads (131072)", run<2, 2, 8, 131072>},
-      {"RT2 CT2 counter ring again", run<2, 2, 8, 0>},
-      {"RT2 CT2 ring, global A loads again", run<2, 2, 8, 131072>},
-      {"RT2 CT2 ring, 5 waves/SIMD bound", run<2, 2, 8, 0, 6, 5>},
+      {"(warm-up) library", run<2, 2, 8, 0>},
       {"RT2 CT2 ring, 6 waves/SIMD bound", run<2, 2, 8, 0, 6, 6>},
-      {"RT2 CT4 counter ring", run<2, 4, 8, 0>},
-      {"RT1 CT2 16 waves ring", run<1, 2, 16, 0>},
-      {"RT1 CT4 16 waves ring", run<1, 4, 16, 0>},
-      {"RT2 CT2 16 waves ring", run<2, 2, 16, 0>},
-      {"tile RMAX16 CT2", run_tile<16, 2, 0>},
-      {"RT2 CT2 counter ring again", run<2, 2, 8, 0>},
+      {"RT2 CT2 ring, 5 waves/SIMD bound", run<2, 2, 8, 0, 6, 5>},
+      {"RT2 CT2 counter ring (library n<=256)", run<2, 2, 8, 0>},
+      {"RT2 CT2 ring, 6 waves/SIMD bound 2", run<2, 2, 8, 0, 6, 6>},
+      {"RT2 CT2 ring, 5 waves/SIMD bound 2", run<2, 2, 8, 0, 6, 5>},
+      {"RT2 CT2 counter ring (library) 2", run<2, 2, 8, 0>},
+      {"RT2 CT2 counter ring (library) 3", run<2, 2, 8, 0>},
+      {"RT2 CT2 ring, 5 waves/SIMD bound 3", run<2, 2, 8, 0, 6, 5>},
+      {"RT2 CT2 ring, 6 waves/SIMD bound 3", run<2, 2, 8, 0, 6, 6>},
   };
+
+
   const Variant small[] = {
       {"RT2 CT4 barrier (library n<=256)", run<2, 4, 8, 32>},
       {"RT2 CT4 counter ring", run<2, 4, 8, 0>},

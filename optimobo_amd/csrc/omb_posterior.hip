@@ -778,6 +778,18 @@ __global__ __launch_bounds__(64 * NW, WPE) void posterior_kernel(GPArgs args, co
   constexpr bool kPairs = !kCandLds && !(ABL & (1 | 16 | 512));
   const double pm_s = (ABL & 256) ? 1.0 : g.variance;
   const double pm[3] = {pm_s, kSqrt5 * pm_s, kFiveThirds * pm_s};
+  // n_var ≤ 8 (r² on MFMA): the generation's per-lane loads (training fragments, α) as buffer loads with the
+  // wave-uniform part of the address in SGPRs, as load_lpair; rows ≥ n of α read as 0 (α's padding is 0).  Alternated
+  // A/B (profiles/r05_zi_ablate_posterior_bufgen_c{3,5}.txt, r05_zj_…_c4.txt): config 3 9.94-9.98 → 9.87-9.89 ms; at d =
+  // 30 (‖x/ℓ‖² loaded per element as well) it was 1.9% slower (10.01-10.08 → 10.21 ms) and stays off.  ABL 262144
+  // flips the choice (tools/ablate).
+  constexpr bool kBufGen = kAug != ((ABL & 262144) != 0);
+  const __amdgpu_buffer_rsrc_t rsrc_X = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<double*>(g.Xf), (short)0, (int)(8ll * 4 * Q * KSDP * 128), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsrc_xsq =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(g.xsq), (short)0, 8 * g.n, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsrc_al =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(g.alpha), (short)0, 8 * g.n, 0x00020000);
   auto generate_mfma = [&](int kc, double* buf) {
     if constexpr (kMfmaGen) {
       if (NW > TPC && (wave / TPC) != kc % (NW / TPC)) return;   // other waves take this chunk
@@ -789,18 +801,30 @@ __global__ __launch_bounds__(64 * NW, WPE) void posterior_kernel(GPArgs args, co
         const d2* xa = reinterpret_cast<const d2*>(g.Xf + (int64_t)(4 * kc + t) * (KSDP * 128) + 2 * lane);
         d2 a[(KSD + 1) / 2];
 #pragma unroll
-        for (int p = 0; p < (KSD + 1) / 2; ++p) a[p] = xa[64 * p];
+        for (int p = 0; p < (KSD + 1) / 2; ++p) {
+          if constexpr (kBufGen)
+            a[p] = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rsrc_X, 16 * lane,
+                                                                                 8 * ((4 * kc + t) * (KSDP * 128) + 128 * p), 0));
+          else
+            a[p] = xa[64 * p];
+        }
         d4 cr = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int s = 0; s < KSD; ++s)
           cr = __builtin_amdgcn_mfma_f64_16x16x4f64((s & 1) ? a[s >> 1].y : a[s >> 1].x, bfr[s], cr, 0, 0, 0);
+        auto row_val = [&](__amdgpu_buffer_rsrc_t rs, const double* __restrict__ v, int k, int kofs) -> double {
+          if constexpr (kBufGen)
+            return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, 8 * (lane >> 4), 8 * kofs, 0));
+          else
+            return v[k];
+        };
 #pragma unroll
         for (int e = 0; e < 4; e += 2) {
           const int k0 = rowbase + 4 * e + (lane >> 4), k1 = k0 + 4;
           double v0, v1;
           const double sf2 = (ABL & 256) ? 1.0 : g.variance;
-          const double r2a = kAug ? cr[e] : fma(-2.0, cr[e], g.xsq[k0] + csq_m);
-          const double r2b = kAug ? cr[e + 1] : fma(-2.0, cr[e + 1], g.xsq[k1] + csq_m);
+          const double r2a = kAug ? cr[e] : fma(-2.0, cr[e], row_val(rsrc_xsq, g.xsq, k0, rowbase + 4 * e) + csq_m);
+          const double r2b = kAug ? cr[e + 1] : fma(-2.0, cr[e + 1], row_val(rsrc_xsq, g.xsq, k1, rowbase + 4 * e + 4) + csq_m);
           if constexpr (ABL & 8192)   // ablation: the 17-instruction polynomial exp, two sqrt corrections
             kernel_of_r2_k_x2<KIND>(r2a, r2b, sf2, args.ec, v0, v1);
           else if constexpr (kTab256)
@@ -811,8 +835,8 @@ __global__ __launch_bounds__(64 * NW, WPE) void posterior_kernel(GPArgs args, co
             v0 = (k0 < g.n) ? v0 : 0.0;
             v1 = (k1 < g.n) ? v1 : 0.0;
           }
-          mu_part = fma(g.alpha[k0], v0, mu_part);
-          mu_part = fma(g.alpha[k1], v1, mu_part);
+          mu_part = fma(row_val(rsrc_al, g.alpha, k0, rowbase + 4 * e), v0, mu_part);
+          mu_part = fma(row_val(rsrc_al, g.alpha, k1, rowbase + 4 * e + 4), v1, mu_part);
           buf[((4 * t + e) * CT + mg_ct) * 64 + lane] = v0;
           buf[((4 * t + e + 1) * CT + mg_ct) * 64 + lane] = v1;
         }

@@ -320,6 +320,9 @@ int main(int argc, char** argv) {
   b.var = var;
   const Variant wide[] = {
       {"default RT8 CT2 (MFMA gen)", run<8, 2, 8, 0, 32>},
+      {"buffer generation loads (262144)", run<8, 2, 8, 262144, 32>},
+      {"default again", run<8, 2, 8, 0, 32>},
+      {"buffer generation loads again", run<8, 2, 8, 262144, 32>},
       {"global A loads, r04 (131072)", run<8, 2, 8, 131072, 32>},
       {"default again", run<8, 2, 8, 0, 32>},
       {"global A loads again", run<8, 2, 8, 131072, 32>},
@@ -337,6 +340,9 @@ int main(int argc, char** argv) {
   };
   const Variant narrow[] = {
       {"default (ring, MFMA gen)", run<4, 4, 8, 0>},
+      {"global generation loads (262144)", run<4, 4, 8, 262144>},
+      {"default again", run<4, 4, 8, 0>},
+      {"global generation loads again", run<4, 4, 8, 262144>},
       {"persistent ring RT4 CT4", run_persist<4, 4>},
       {"default again", run<4, 4, 8, 0>},
       {"persistent ring again", run_persist<4, 4>},
@@ -377,16 +383,17 @@ int main(int argc, char** argv) {
   };
   const Variant small256[] = {
       {"(warm-up) library", run<2, 2, 8, 0>},
-      {"RT2 CT2 ring, 6 waves/SIMD bound", run<2, 2, 8, 0, 6, 6>},
-      {"RT2 CT2 ring, 5 waves/SIMD bound", run<2, 2, 8, 0, 6, 5>},
       {"RT2 CT2 counter ring (library n<=256)", run<2, 2, 8, 0>},
-      {"RT2 CT2 ring, 6 waves/SIMD bound 2", run<2, 2, 8, 0, 6, 6>},
-      {"RT2 CT2 ring, 5 waves/SIMD bound 2", run<2, 2, 8, 0, 6, 5>},
+      {"RT2 CT2 ring, global generation loads", run<2, 2, 8, 262144>},
       {"RT2 CT2 counter ring (library) 2", run<2, 2, 8, 0>},
+      {"RT2 CT2 ring, global generation loads 2", run<2, 2, 8, 262144>},
       {"RT2 CT2 counter ring (library) 3", run<2, 2, 8, 0>},
-      {"RT2 CT2 ring, 5 waves/SIMD bound 3", run<2, 2, 8, 0, 6, 5>},
-      {"RT2 CT2 ring, 6 waves/SIMD bound 3", run<2, 2, 8, 0, 6, 6>},
+      {"RT2 CT2 ring, global generation loads 3", run<2, 2, 8, 262144>},
+      {"RT2 CT2 ring, 5 waves/SIMD bound", run<2, 2, 8, 0, 6, 5>},
+      {"RT2 CT2 ring, 6 waves/SIMD bound", run<2, 2, 8, 0, 6, 6>},
+      {"persistent ring RT2 CT2", run_persist<2, 2>},
   };
+
 
 
   const Variant small[] = {

@@ -111,7 +111,9 @@ const char* omb_last_error(const omb_ctx* ctx);
  * omb_debug_set(ctx, OMB_DEBUG_POSTERIOR_PERSIST, p) picks the fused posterior kernel for n_train > 128: 1 the persistent
  * ring (resident workgroups, ring chunks numbered across candidate blocks), 0 one workgroup per candidate block.
  * omb_debug_set(ctx, OMB_DEBUG_COV_FUSED, 0) builds the posterior covariance as K(X*, X*) then the VᵀV update (two
- * launches) instead of one SYRK with K(X*, X*) in its epilogue (default 1; the same matrix to the ulp). */
+ * launches) instead of one SYRK with K(X*, X*) in its epilogue (default 1; the same matrix to the ulp).
+ * omb_debug_set(ctx, OMB_DEBUG_SELECT_SEQ, 1) makes omb_thompson_select walk the samples in order for B ≤ 64 too
+ * (default 0: the picks in parallel rounds to their fixed point; the same picks). */
 enum {
   OMB_DEBUG_SPIN_LIMIT = 1,
   OMB_DEBUG_COV_TABLE = 2,
@@ -120,7 +122,8 @@ enum {
   OMB_DEBUG_CHOL_MODE = 5,
   OMB_DEBUG_TIMING_STRIDE = 6,
   OMB_DEBUG_POSTERIOR_PERSIST = 7,
-  OMB_DEBUG_COV_FUSED = 8
+  OMB_DEBUG_COV_FUSED = 8,
+  OMB_DEBUG_SELECT_SEQ = 9
 };
 int omb_debug_set(omb_ctx* ctx, int what, int64_t value);
 

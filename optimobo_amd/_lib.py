@@ -26,6 +26,7 @@ DEBUG_CHOL_MODE = 5
 DEBUG_TIMING_STRIDE = 6
 DEBUG_POSTERIOR_PERSIST = 7
 DEBUG_COV_FUSED = 8
+DEBUG_SELECT_SEQ = 9
 MAX_OBJ, MAX_DIM, MAX_TRAIN, MAX_TRAIN_DENSE = 8, 256, 1024, 16384
 
 _p = ctypes.c_void_p

@@ -97,6 +97,7 @@ struct omb_ctx {
   int posterior_persist = 0;     // OMB_DEBUG_POSTERIOR_PERSIST
   int chol_mode = kCholAuto;     // OMB_DEBUG_CHOL_MODE (value & 3)
   int chol_acq_rel = 0;          // OMB_DEBUG_CHOL_MODE (value & 4): release / acquire hand-offs
+  bool select_seq = false;       // OMB_DEBUG_SELECT_SEQ: the sequential greedy walk for B ≤ 64 too
 };
 
 namespace {
@@ -550,6 +551,10 @@ int omb_debug_set(omb_ctx* ctx, int what, int64_t value) {
   }
   if (what == OMB_DEBUG_COV_FUSED) {
     ctx->cov_fused = value != 0;
+    return OMB_OK;
+  }
+  if (what == OMB_DEBUG_SELECT_SEQ) {
+    ctx->select_seq = value != 0;
     return OMB_OK;
   }
   if (what == OMB_DEBUG_POSTERIOR_PERSIST) {
@@ -1177,7 +1182,7 @@ int omb_thompson_select(omb_ctx* ctx, const double* Y_dev, int B, int64_t N, int
   if (B == 0) return OMB_OK;
   const size_t sw = (size_t)select_ws_bytes(B, N);
   if (sw && (rc = grow_dev(ctx, &ctx->sws, &ctx->sws_cap, sw, "selection workspace"))) return rc;
-  hipError_t e = launch_select(ctx->stream, Y_dev, B, N, idx_dev, ctx->sws);
+  hipError_t e = launch_select(ctx->stream, Y_dev, B, N, idx_dev, ctx->sws, ctx->select_seq);
   if (e != hipSuccess) return hip_fail(ctx, e, "thompson_select");
   return OMB_OK;
 }

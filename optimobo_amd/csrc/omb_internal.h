@@ -188,7 +188,7 @@ hipError_t launch_chol_samples(hipStream_t stream, const double* L, int64_t N, i
 // (the sorted heads of every sample when N ≤ kSelectSortN; 0 otherwise).
 constexpr int64_t kSelectSortN = 8192;
 int64_t select_ws_bytes(int B, int64_t N);
-hipError_t launch_select(hipStream_t stream, const double* Y, int B, int64_t N, int64_t* idx, void* ws);
+hipError_t launch_select(hipStream_t stream, const double* Y, int B, int64_t N, int64_t* idx, void* ws, bool seq = false);
 // C (M, Nc) = β C + α AᵀB, A (K, M), B (K, Nc).
 hipError_t launch_gemm_tn(hipStream_t s, int64_t M, int64_t Nc, int64_t K, double alpha, const double* A, int64_t lda,
                           const double* B, int64_t ldb, double beta, double* C, int64_t ldc);

@@ -2441,6 +2441,110 @@ __global__ __launch_bounds__(256) void select_greedy_kernel(const long long* __r
   }
 }
 
+// The same picks for B ≤ 64 in rounds (round 5), one lane per sample.  Sample b's pick depends only on the picks of
+// the samples below it, so the sequential picks are the unique fixed point of
+//     pick_b ← the first head entry of b that no sample below b holds (the +inf rule as above, min_taken = the lowest
+//              pick below b; every entry held: min_taken),
+// and each round applies it to every sample at once against the previous round's picks (owner[i] = the lowest sample
+// whose pick is i).  A prefix stays final: with all samples below F final, sample F's new pick is final, and so is
+// every sample up to the first one ≥ F whose pick changed in the round (c): F → c + 1; a round that changes no pick
+// ends it (F = B).  Samples rarely share their minima, so that takes two or three rounds (≈ 1 µs, against ≈ 22 µs for
+// 64 sequential steps).  After kGreedyRounds rounds (long conflict chains: a collapsed posterior whose samples order
+// the candidates alike) the samples from F on are picked by the sequential walk, against the final picks below F.
+constexpr int kGreedyHeadRegs = 4;      // head entries per sample kept in registers (later ones read from `heads`)
+constexpr int kGreedyRounds = 8;
+__global__ __launch_bounds__(64) void select_greedy_par_kernel(const long long* __restrict__ heads, int B, int64_t N,
+                                                               int K, int64_t* __restrict__ idx_out) {
+  __shared__ int owner[kSelectSortN];
+  __shared__ long long hl[kSelHeadLds];
+  const int lane = threadIdx.x;
+  const bool act = lane < B;
+  for (int i = lane; i < N; i += 64) owner[i] = 0x7fffffff;
+  long long h[kGreedyHeadRegs];
+#pragma unroll
+  for (int j = 0; j < kGreedyHeadRegs; ++j) h[j] = (act && j < K) ? heads[(int64_t)lane * K + j] : -1;
+  auto lds_order = [] {
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  lds_order();
+  long long pick = -1;
+  int F = 0;
+  for (int round = 0; round < kGreedyRounds && F < B; ++round) {
+    // the lowest pick below each sample (N: none), an exclusive prefix min over the lanes
+    long long m = (act && pick >= 0) ? pick : N;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const long long t = __shfl_up(m, o);
+      if (lane >= o) m = t < m ? t : m;
+    }
+    long long below = __shfl_up(m, 1);
+    if (lane == 0) below = N;
+    long long np = pick;
+    if (act && lane >= F) {
+      np = -1;
+      for (int j = 0; j < K; ++j) {
+        const long long e = j == 0 ? h[0] : j == 1 ? h[1] : j == 2 ? h[2] : j == 3 ? h[3] : heads[(int64_t)lane * K + j];
+        if (e < 0) break;
+        const long long i = e & (kSelInfFlag - 1);
+        if (owner[i] < lane) continue;                      // held by a lower sample
+        np = (e & kSelInfFlag) ? (i < below ? i : below) : i;
+        break;
+      }
+      if (np < 0) np = below;
+    }
+    const unsigned long long changed = __ballot(act && np != pick) & (~0ull << F);
+    const int c = changed ? __builtin_ctzll(changed) : B;
+    const int Fn = c >= B ? B : c + 1;
+    // owner ← the new picks: every old pick reset, then every new one min-ed in
+    if (act && pick >= 0) owner[pick] = 0x7fffffff;
+    lds_order();
+    if (act) atomicMin(&owner[np], lane);
+    lds_order();
+    pick = np;
+    F = Fn;
+  }
+  if (F < B) {
+    // the sequential walk from F (select_greedy_kernel's loop) against the final picks below F
+    if (act && lane >= F) owner[pick] = 0x7fffffff;
+    lds_order();
+    if (act && lane < F) atomicMin(&owner[pick], lane);
+    const int H = K < 64 ? K : 64;
+    for (int i = lane; i < (B - F) * H; i += 64) hl[i] = heads[(int64_t)(F + i / H) * K + i % H];
+    long long m = (act && lane < F) ? pick : N;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const long long t = __shfl_xor(m, o);
+      m = t < m ? t : m;
+    }
+    long long min_taken = m;
+    lds_order();
+    for (int b = F; b < B; ++b) {
+      long long p = -1;
+      for (int c0 = 0; c0 < K && p < 0; c0 += 64) {
+        long long e = -1;
+        if (c0 + lane < K) e = c0 == 0 ? hl[(b - F) * H + lane] : heads[(int64_t)b * K + c0 + lane];
+        const long long i = e >= 0 ? (e & (kSelInfFlag - 1)) : 0;
+        const bool free_ = e >= 0 && owner[i] == 0x7fffffff;
+        const unsigned long long msk = __ballot(free_);
+        if (msk) {
+          const int f = __builtin_ctzll(msk);
+          const long long ef = __shfl(e, f);
+          const long long fi = ef & (kSelInfFlag - 1);
+          p = (ef & kSelInfFlag) ? (fi < min_taken ? fi : min_taken) : fi;
+        }
+      }
+      if (p < 0) p = min_taken;
+      if (lane == 0) owner[p] = b;
+      if (lane == b) pick = p;
+      min_taken = p < min_taken ? p : min_taken;
+      lds_order();
+    }
+  }
+  if (act) idx_out[lane] = pick;
+}
+
 // ----------------------------------------------------------------------------- launchers
 int64_t cand_cov_ws_doubles(int64_t N, int DP) { return N * ((DP + 3) / 4 * 4) + N; }
 
@@ -2850,7 +2954,7 @@ int64_t select_ws_bytes(int B, int64_t N) {
   return (int64_t)B * K * (int64_t)sizeof(long long);
 }
 
-hipError_t launch_select(hipStream_t stream, const double* Y, int B, int64_t N, int64_t* idx, void* ws) {
+hipError_t launch_select(hipStream_t stream, const double* Y, int B, int64_t N, int64_t* idx, void* ws, bool seq) {
   if (B <= 0) return hipSuccess;
   if (select_sorted(B, N)) {
     int N2 = 2;
@@ -2863,7 +2967,10 @@ hipError_t launch_select(hipStream_t stream, const double* Y, int B, int64_t N, 
       hipLaunchKernelGGL(select_sort_kernel, dim3((unsigned)B), dim3(kSelThreads), 0, stream, Y, N, N2, K, heads);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(select_greedy_kernel, dim3(1), dim3(256), 0, stream, heads, B, N, K, idx);
+    if (B <= 64 && !seq)
+      hipLaunchKernelGGL(select_greedy_par_kernel, dim3(1), dim3(64), 0, stream, heads, B, N, K, idx);
+    else
+      hipLaunchKernelGGL(select_greedy_kernel, dim3(1), dim3(256), 0, stream, heads, B, N, K, idx);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(select_kernel, dim3(1), dim3(1024), 0, stream, Y, B, N, idx);

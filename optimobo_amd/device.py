@@ -74,11 +74,13 @@ class AcqContext:
         and the arg-max's second pass; ("argmax_passes", 1/2) runs the arg-max as one
         launch / as two; ("chol_mode", 0/1/2 [+ 4]) factors auto / by per-step launches / in one persistent launch
         [with release-acquire hand-offs];
-        ("timing_stride", s) records the timing events on every s-th chain only."""
+        ("timing_stride", s) records the timing events on every s-th chain only; ("select_seq", 0/1) picks the
+        Thompson selection's parallel rounds (default) / its sequential walk for B <= 64."""
         code = {"spin_limit": _lib.DEBUG_SPIN_LIMIT, "cov_table": _lib.DEBUG_COV_TABLE,
                 "fused_chain": _lib.DEBUG_FUSED_CHAIN, "argmax_passes": _lib.DEBUG_ARGMAX_PASSES,
                 "chol_mode": _lib.DEBUG_CHOL_MODE, "timing_stride": _lib.DEBUG_TIMING_STRIDE,
-                "posterior_persist": _lib.DEBUG_POSTERIOR_PERSIST, "cov_fused": _lib.DEBUG_COV_FUSED}[what]
+                "posterior_persist": _lib.DEBUG_POSTERIOR_PERSIST, "cov_fused": _lib.DEBUG_COV_FUSED,
+                "select_seq": _lib.DEBUG_SELECT_SEQ}[what]
         self._check(self.lib.omb_debug_set(self._h, code, int(value)), "omb_debug_set")
 
     # ------------------------------------------------------------------ GP state

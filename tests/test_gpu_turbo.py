@@ -276,6 +276,32 @@ def test_select_topk_heads_ties_nans(ctx):
         check_select(ctx, y)
 
 
+@pytest.mark.parametrize("seq", [0, 1], ids=["rounds", "sequential"])
+def test_select_rounds_conflict_chains(ctx, seq):
+    """B ≤ 64 picks in parallel rounds (select_greedy_par_kernel) unless select_seq: samples that share their minima —
+    64 identical samples (a 64-long conflict chain: the hand-off to the sequential walk), identical pairs, every 5th
+    sample sharing one arg-min, near-identical samples, +inf tails, NaNs, fewer candidates than samples."""
+    rng = np.random.default_rng(44)
+    base = rng.standard_normal((3000, 1, 1))
+    pairs = np.repeat(rng.standard_normal((3000, 1, 32)), 2, axis=2)
+    every5 = rng.standard_normal((3000, 1, 64))
+    every5[17, 0, ::5] = -10.0
+    every5[18, 0, 1::5] = -10.0
+    near = base + 1e-3 * rng.standard_normal((3000, 1, 64))
+    infs = np.full((500, 1, 48), np.inf)
+    infs[rng.integers(0, 500, 30), 0, rng.integers(0, 48, 30)] = rng.standard_normal(30)
+    nans = rng.standard_normal((700, 1, 40))
+    nans[[5, 9, 11], 0, :] = np.nan
+    cases = [np.repeat(base, 64, axis=2), pairs, every5, near, infs, nans, rng.standard_normal((20, 1, 40)),
+             np.zeros((33, 1, 64)), rng.standard_normal((8192, 1, 64)), rng.standard_normal((3000, 1, 1))]
+    ctx.debug_set("select_seq", seq)
+    try:
+        for y in cases:
+            check_select(ctx, y)
+    finally:
+        ctx.debug_set("select_seq", 0)
+
+
 def test_select_all_equal_and_exhausted(ctx):
     check_select(ctx, np.zeros((4, 1, 9)))           # more samples than candidates: picks repeat index 0
     check_select(ctx, np.full((6, 1, 3), np.inf))

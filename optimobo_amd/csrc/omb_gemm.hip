@@ -14,6 +14,10 @@
 // every slab (64 VALU instructions per 16 MFMAs; FP64 MFMA does not overlap VALU on gfx950).  The
 // Cholesky kernels in omb_linalg.hip keep the default form: their diagonal-block chain runs slower in
 // the VGPR form (N = 3000 factorisation 1.37 → 1.40 ms, profiles/r03_z2_chol_{agpr,vgpr}.txt).
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
 #include "omb_internal.h"
 
 namespace omb {
@@ -45,9 +49,16 @@ __global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t Nc, int64_
                                                    const double* __restrict__ B, int64_t ldb, double beta,
                                                    double* __restrict__ C, int64_t ldc,
                                                    const double* __restrict__ col_bias, int64_t kchunk,
-                                                   int64_t zstride, CovEpi ce) {
+                                                   int64_t zstride, CovEpi ce,
+                                                   const int* __restrict__ tmap = nullptr) {
   // ATRI: the last row tiles carry the most slabs, so they are dispatched first
-  const int64_t m0 = (int64_t)(ATRI ? gridDim.y - 1 - blockIdx.y : blockIdx.y) * kGT, n0 = (int64_t)blockIdx.x * kGT;
+  int64_t m0 = (int64_t)(ATRI ? gridDim.y - 1 - blockIdx.y : blockIdx.y) * kGT, n0 = (int64_t)blockIdx.x * kGT;
+  if (tmap) {   // 1-D grid, workgroup b → tile tmap[b] = (row tile << 16 | column tile), −1: none (syrk_tile_map)
+    const int code = tmap[blockIdx.x];
+    if (code < 0) return;
+    m0 = (int64_t)(code >> 16) * kGT;
+    n0 = (int64_t)(code & 0xffff) * kGT;
+  }
   if (LOWER && n0 > m0) return;   // tile strictly above the diagonal
   __shared__ double As[2][kGK][kGP];   // As[k][m] = op(A)(m0 + m, k0 + k)
   __shared__ double Bs[2][kGK][kGP];   // Bs[k][n] = op(B)(k0 + k, n0 + n)
@@ -316,13 +327,81 @@ hipError_t launch_chol_samples(hipStream_t stream, const double* L, int64_t N, i
   return hipGetLastError();
 }
 
+// XCD-grouped order of the lower 64 × 64 tiles of Σ = K** − VᵀV (round 5).  Tile (m, n) streams V's column panels m
+// and n (K × 64 doubles each, 256 KB at K = 512); with the 2-D grid every XCD ran tiles from the whole triangle, so its
+// 4-MB L2 cycled through all ⌈N/64⌉ panels (12 MB at N = 3000) and hit 54% (PMC, profiles/r05_zt_pmc_c6_gemm.txt).
+// Here the panels form 4 contiguous groups; the 10 group pairs (g_m ≥ g_n) go to the 8 XCDs largest first onto the
+// least-loaded XCD, so an XCD's tiles touch at most two groups (half the panels).  Workgroups reach the XCDs in turn
+// (b mod 8), so workgroup 8j + x runs the j-th tile of XCD x (−1 past its list).  Built once per (device, tiles).
+static const int* syrk_tile_map(int T, int* grid) {
+  struct Map {
+    int dev, T, grid;
+    int* d;
+  };
+  static std::mutex mu;
+  static std::vector<Map> maps;
+  int dev = 0;
+  if (T > 0xffff || hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  for (const Map& e : maps)
+    if (e.dev == dev && e.T == T) {
+      *grid = e.grid;
+      return e.d;
+    }
+  constexpr int G = 4, X = 8;
+  auto gstart = [&](int g) { return (int)((int64_t)T * g / G); };
+  std::vector<std::pair<int, int>> pairs;
+  for (int a = 0; a < G; ++a)
+    for (int b = 0; b <= a; ++b) pairs.push_back({a, b});
+  auto ntiles = [&](std::pair<int, int> p) {
+    const int ra = gstart(p.first + 1) - gstart(p.first), rb = gstart(p.second + 1) - gstart(p.second);
+    return p.first == p.second ? ra * (ra + 1) / 2 : ra * rb;
+  };
+  std::stable_sort(pairs.begin(), pairs.end(), [&](auto x, auto y) { return ntiles(x) > ntiles(y); });
+  std::vector<std::vector<int>> lists(X);
+  for (const auto& p : pairs) {
+    int x = 0;
+    for (int q = 1; q < X; ++q)
+      if (lists[q].size() < lists[x].size()) x = q;
+    for (int m = gstart(p.first); m < gstart(p.first + 1); ++m)
+      for (int n = gstart(p.second); n < gstart(p.second + 1) && (p.first != p.second || n <= m); ++n)
+        lists[x].push_back((m << 16) | n);
+  }
+  size_t len = 0;
+  for (const auto& l : lists) len = std::max(len, l.size());
+  std::vector<int> codes(X * len, -1);
+  for (int x = 0; x < X; ++x)
+    for (size_t j = 0; j < lists[x].size(); ++j) codes[X * j + x] = lists[x][j];
+  int* d = nullptr;
+  if (hipMalloc(&d, sizeof(int) * codes.size()) != hipSuccess) return nullptr;
+  if (hipMemcpy(d, codes.data(), sizeof(int) * codes.size(), hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(d);
+    return nullptr;
+  }
+  maps.push_back({dev, T, (int)codes.size(), d});
+  *grid = (int)codes.size();
+  return d;
+}
+
+#ifdef OMB_TOOLS_KNOBS
+static bool g_syrk_xcd_map = true;
+void set_syrk_xcd_map(bool on) { g_syrk_xcd_map = on; }
+#elif defined(OMB_SYRK_NOMAP)
+constexpr bool g_syrk_xcd_map = false;
+#else
+constexpr bool g_syrk_xcd_map = true;
+#endif
+
 hipError_t launch_cov_syrk(hipStream_t s, int64_t N, int64_t K, const double* V, int64_t ldv, double* S, int64_t lds,
                            const double* xs, const double* xsq, int kp, int kind, double variance, double diag_add) {
   if (N <= 0) return hipSuccess;
-  const dim3 grid((unsigned)((N + kGT - 1) / kGT), (unsigned)((N + kGT - 1) / kGT));
+  const int T = (int)((N + kGT - 1) / kGT);
+  int g1 = 0;
+  const int* tmap = g_syrk_xcd_map ? syrk_tile_map(T, &g1) : nullptr;
+  const dim3 grid = tmap ? dim3((unsigned)g1) : dim3((unsigned)T, (unsigned)T);
   hipLaunchKernelGGL((gemm_kernel<true, false, false, true, false, true>), grid, dim3(256), 0, s, N, N, K, -1.0, V, ldv,
                      V, ldv, 0.0, S, lds, (const double*)nullptr, (int64_t)0, (int64_t)0,
-                     CovEpi{xs, xsq, kp, kind, variance, diag_add});
+                     CovEpi{xs, xsq, kp, kind, variance, diag_add}, tmap);
   return hipGetLastError();
 }
 

@@ -276,6 +276,72 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const double* __rest
 
 
 // ----------------------------------------------------------------------------- launchers
+// Tile tables for 1-D launches in an XCD-aware order (round 5): workgroups reach the 8 XCDs in turn (b mod 8), so
+// workgroup 8j + x runs the j-th tile of XCD x's list (−1 past its end); codes are (row tile << 16 | column tile).
+// Built on the host once per (device, kind, shape) and kept (the first 64 shapes).
+//   kMapSyrk (T × T lower tiles of Σ = K** − VᵀV): tile (m, n) streams V's column panels m and n (K × 64 doubles,
+//     256 KB at K = 512); with the 2-D grid every XCD ran tiles from the whole triangle, cycling its 4-MB L2 through
+//     all ⌈N/64⌉ panels (12 MB at N = 3000): L2 hit rate 0.54 (PMC, profiles/r05_zt_pmc_c6_gemm.txt).  The panels form
+//     4 contiguous groups and the 10 group pairs (g_m ≥ g_n) go to the XCDs largest first onto the least-loaded one,
+//     so an XCD's tiles touch two groups (≈ 6 MB, the least for ≈ 141 tiles): hit rate 0.84.
+// (The same grouping by column tiles for V = L⁻¹K* raised its L2 hit rate from 0.45 to 0.74 and left it at 38 µs,
+// profiles/r05_zv_ltri_xcd_map_ab.txt: that launch is bound by its heaviest row tiles, not by their loads.)
+enum { kMapSyrk = 0 };
+static const int* xcd_tile_map(int kind, int T1, int T2, int* grid) {
+  struct Map {
+    int dev, kind, T1, T2, grid;
+    int* d;
+  };
+  static std::mutex mu;
+  static std::vector<Map> maps;
+  int dev = 0;
+  if (T1 > 0xffff || T2 > 0xffff || hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  for (const Map& e : maps)
+    if (e.dev == dev && e.kind == kind && e.T1 == T1 && e.T2 == T2) {
+      *grid = e.grid;
+      return e.d;
+    }
+  if (maps.size() >= 64) return nullptr;   // shapes past the first 64 launch on the 2-D grid (bounded host cache)
+  constexpr int X = 8;
+  std::vector<std::vector<int>> lists(X);
+  if (kind == kMapSyrk) {
+    constexpr int G = 4;
+    const int T = T1;
+    auto gstart = [&](int g) { return (int)((int64_t)T * g / G); };
+    std::vector<std::pair<int, int>> pairs;
+    for (int a = 0; a < G; ++a)
+      for (int b = 0; b <= a; ++b) pairs.push_back({a, b});
+    auto ntiles = [&](std::pair<int, int> p) {
+      const int ra = gstart(p.first + 1) - gstart(p.first), rb = gstart(p.second + 1) - gstart(p.second);
+      return p.first == p.second ? ra * (ra + 1) / 2 : ra * rb;
+    };
+    std::stable_sort(pairs.begin(), pairs.end(), [&](auto x, auto y) { return ntiles(x) > ntiles(y); });
+    for (const auto& p : pairs) {
+      int x = 0;
+      for (int q = 1; q < X; ++q)
+        if (lists[q].size() < lists[x].size()) x = q;
+      for (int m = gstart(p.first); m < gstart(p.first + 1); ++m)
+        for (int n = gstart(p.second); n < gstart(p.second + 1) && (p.first != p.second || n <= m); ++n)
+          lists[x].push_back((m << 16) | n);
+    }
+  }
+  size_t len = 0;
+  for (const auto& l : lists) len = std::max(len, l.size());
+  std::vector<int> codes(X * len, -1);
+  for (int x = 0; x < X; ++x)
+    for (size_t j = 0; j < lists[x].size(); ++j) codes[X * j + x] = lists[x][j];
+  int* d = nullptr;
+  if (hipMalloc(&d, sizeof(int) * codes.size()) != hipSuccess) return nullptr;
+  if (hipMemcpy(d, codes.data(), sizeof(int) * codes.size(), hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(d);
+    return nullptr;
+  }
+  maps.push_back({dev, kind, T1, T2, (int)codes.size(), d});
+  *grid = (int)codes.size();
+  return d;
+}
+
 hipError_t launch_gemm_ltri_nn(hipStream_t s, int64_t M, int64_t Nc, double alpha, const double* L, int64_t ldl,
                                const double* B, int64_t ldb, double beta, double* C, int64_t ldc) {
   return gemm<false, false, false, false, true>(s, M, Nc, M, alpha, L, ldl, B, ldb, beta, C, ldc, nullptr);
@@ -327,62 +393,6 @@ hipError_t launch_chol_samples(hipStream_t stream, const double* L, int64_t N, i
   return hipGetLastError();
 }
 
-// XCD-grouped order of the lower 64 × 64 tiles of Σ = K** − VᵀV (round 5).  Tile (m, n) streams V's column panels m
-// and n (K × 64 doubles each, 256 KB at K = 512); with the 2-D grid every XCD ran tiles from the whole triangle, so its
-// 4-MB L2 cycled through all ⌈N/64⌉ panels (12 MB at N = 3000) and hit 54% (PMC, profiles/r05_zt_pmc_c6_gemm.txt).
-// Here the panels form 4 contiguous groups; the 10 group pairs (g_m ≥ g_n) go to the 8 XCDs largest first onto the
-// least-loaded XCD, so an XCD's tiles touch at most two groups (half the panels).  Workgroups reach the XCDs in turn
-// (b mod 8), so workgroup 8j + x runs the j-th tile of XCD x (−1 past its list).  Built once per (device, tiles).
-static const int* syrk_tile_map(int T, int* grid) {
-  struct Map {
-    int dev, T, grid;
-    int* d;
-  };
-  static std::mutex mu;
-  static std::vector<Map> maps;
-  int dev = 0;
-  if (T > 0xffff || hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> lock(mu);
-  for (const Map& e : maps)
-    if (e.dev == dev && e.T == T) {
-      *grid = e.grid;
-      return e.d;
-    }
-  constexpr int G = 4, X = 8;
-  auto gstart = [&](int g) { return (int)((int64_t)T * g / G); };
-  std::vector<std::pair<int, int>> pairs;
-  for (int a = 0; a < G; ++a)
-    for (int b = 0; b <= a; ++b) pairs.push_back({a, b});
-  auto ntiles = [&](std::pair<int, int> p) {
-    const int ra = gstart(p.first + 1) - gstart(p.first), rb = gstart(p.second + 1) - gstart(p.second);
-    return p.first == p.second ? ra * (ra + 1) / 2 : ra * rb;
-  };
-  std::stable_sort(pairs.begin(), pairs.end(), [&](auto x, auto y) { return ntiles(x) > ntiles(y); });
-  std::vector<std::vector<int>> lists(X);
-  for (const auto& p : pairs) {
-    int x = 0;
-    for (int q = 1; q < X; ++q)
-      if (lists[q].size() < lists[x].size()) x = q;
-    for (int m = gstart(p.first); m < gstart(p.first + 1); ++m)
-      for (int n = gstart(p.second); n < gstart(p.second + 1) && (p.first != p.second || n <= m); ++n)
-        lists[x].push_back((m << 16) | n);
-  }
-  size_t len = 0;
-  for (const auto& l : lists) len = std::max(len, l.size());
-  std::vector<int> codes(X * len, -1);
-  for (int x = 0; x < X; ++x)
-    for (size_t j = 0; j < lists[x].size(); ++j) codes[X * j + x] = lists[x][j];
-  int* d = nullptr;
-  if (hipMalloc(&d, sizeof(int) * codes.size()) != hipSuccess) return nullptr;
-  if (hipMemcpy(d, codes.data(), sizeof(int) * codes.size(), hipMemcpyHostToDevice) != hipSuccess) {
-    (void)hipFree(d);
-    return nullptr;
-  }
-  maps.push_back({dev, T, (int)codes.size(), d});
-  *grid = (int)codes.size();
-  return d;
-}
-
 #ifdef OMB_TOOLS_KNOBS
 static bool g_syrk_xcd_map = true;
 void set_syrk_xcd_map(bool on) { g_syrk_xcd_map = on; }
@@ -397,7 +407,7 @@ hipError_t launch_cov_syrk(hipStream_t s, int64_t N, int64_t K, const double* V,
   if (N <= 0) return hipSuccess;
   const int T = (int)((N + kGT - 1) / kGT);
   int g1 = 0;
-  const int* tmap = g_syrk_xcd_map ? syrk_tile_map(T, &g1) : nullptr;
+  const int* tmap = g_syrk_xcd_map ? xcd_tile_map(kMapSyrk, T, T, &g1) : nullptr;
   const dim3 grid = tmap ? dim3((unsigned)g1) : dim3((unsigned)T, (unsigned)T);
   hipLaunchKernelGGL((gemm_kernel<true, false, false, true, false, true>), grid, dim3(256), 0, s, N, N, K, -1.0, V, ldv,
                      V, ldv, 0.0, S, lds, (const double*)nullptr, (int64_t)0, (int64_t)0,

@@ -270,7 +270,15 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const double* __rest
     Sc = a < S ? (int)a : S;
   }
   double v = 0.0;
-  for (int z = 0; z < Sc; ++z) v += P[z * zstride + i];
+  int z = 0;
+  for (; z + 8 <= Sc; z += 8) {   // 8 slices' loads in flight, added in slice order
+    double p[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) p[u] = P[(z + u) * zstride + i];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v += p[u];
+  }
+  for (; z < Sc; ++z) v += P[z * zstride + i];
   C[r * ldc + c] = v + (bias ? bias[c] : 0.0);
 }
 

@@ -782,9 +782,31 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(double* __restrict__ A, 
 // MFMAs each).  The k index is permuted as m(s, g) = 16(s >> 2) + 4g + (s & 3) so a lane's A operands
 // are 4 contiguous doubles per 16-column group; the barrier separates both waves' reads of the rows
 // from the in-place writes.
+// The persistent launch's sync words for t steps after k0 per-step launches (chol_persist_kernel's layout: wflag[t] |
+// pflag[t·t] | cnt[t·t] | ticket | abort), word x.
+__device__ __forceinline__ int chol_persist_init_word(int x, int t, int k0) {
+  if (k0 > 0 && x >= t && x < t + t * t) {
+    const int i = (x - t) / t, k = (x - t) % t;
+    return (k == k0 && i > k0) ? 4 : 0;
+  }
+  if (k0 > 0 && x >= t + t * t && x < t + 2 * t * t) {
+    const int i = (x - t - t * t) / t, j = (x - t - t * t) % t;
+    return (j > k0 && j <= i) ? k0 : 0;
+  }
+  return 0;
+}
+
+// pinit (round 5, the hybrid schedule): step 0's panel launch also writes the later persistent launch's sync words
+// (chol_persist_init_kernel's job; the per-step launches never touch them), one launch fewer on the chain.
 template <bool VEC>
 __global__ __launch_bounds__(128) void chol_panel_kernel(double* __restrict__ A, int64_t N, int64_t lda, int step,
-                                                         const double* __restrict__ Wf, const int* __restrict__ info) {
+                                                         const double* __restrict__ Wf, const int* __restrict__ info,
+                                                         int* __restrict__ pinit = nullptr, int pt = 0, int pk0 = 0) {
+  if (pinit) {
+    const int pn = pt + 2 * pt * pt + 2;
+    for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < pn; x += gridDim.x * blockDim.x)
+      pinit[x] = chol_persist_init_word(x, pt, pk0);
+  }
   if (*info != 0) return;
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1344,17 +1366,7 @@ __host__ __device__ __forceinline__ int chol_persist_step_tasks(int t, int k, in
 __global__ __launch_bounds__(256) void chol_persist_init_kernel(int* __restrict__ ints, int t, int k0,
                                                                 int* __restrict__ info) {
   const int n = t + 2 * t * t + 2;
-  for (int x = threadIdx.x; x < n; x += 256) {
-    int v = 0;
-    if (k0 > 0 && x >= t && x < t + t * t) {
-      const int i = (x - t) / t, k = (x - t) % t;
-      v = (k == k0 && i > k0) ? 4 : 0;
-    } else if (k0 > 0 && x >= t + t * t && x < t + 2 * t * t) {
-      const int i = (x - t - t * t) / t, j = (x - t - t * t) % t;
-      v = (j > k0 && j <= i) ? k0 : 0;
-    }
-    ints[x] = v;
-  }
+  for (int x = threadIdx.x; x < n; x += 256) ints[x] = chol_persist_init_word(x, t, k0);
   if (threadIdx.x == 0 && k0 == 0) *info = 0;
 }
 
@@ -2620,14 +2632,20 @@ int64_t chol_ws_doubles(int64_t N) {
   return launches > persist ? launches : persist;
 }
 
+struct CholPersistInit {
+  int* ints = nullptr;   // the persistent launch's sync words (nullptr: none to write)
+  int t = 0, k0 = 0;
+};
 static hipError_t chol_panel(hipStream_t stream, double* A, int64_t N, int64_t lda, int k, const double* ws,
-                             const int* info, bool vec) {
+                             const int* info, bool vec, CholPersistInit pi = {}) {
   const int64_t rest = N - (int64_t)(k + 1) * kNB;          // rows below the diagonal block
   const unsigned pblocks = (unsigned)((rest + 15) / 16);
   if (vec)
-    hipLaunchKernelGGL((chol_panel_kernel<true>), dim3(pblocks), dim3(128), 0, stream, A, N, lda, k, ws, info);
+    hipLaunchKernelGGL((chol_panel_kernel<true>), dim3(pblocks), dim3(128), 0, stream, A, N, lda, k, ws, info, pi.ints,
+                       pi.t, pi.k0);
   else
-    hipLaunchKernelGGL((chol_panel_kernel<false>), dim3(pblocks), dim3(128), 0, stream, A, N, lda, k, ws, info);
+    hipLaunchKernelGGL((chol_panel_kernel<false>), dim3(pblocks), dim3(128), 0, stream, A, N, lda, k, ws, info, pi.ints,
+                       pi.t, pi.k0);
   return hipGetLastError();
 }
 
@@ -2645,7 +2663,7 @@ constexpr int g_chol_update_delay = 0;
 
 // Round 4: the diagonal blocks by tiles of 16 (chol64_blocked), one launch per step with the next panel inside.
 static hipError_t launch_cholesky_blocked(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws,
-                                          int spin_limit, int acq_rel, int steps_limit) {
+                                          int spin_limit, int acq_rel, int steps_limit, CholPersistInit pi) {
   int steps = (int)((N + kNB - 1) / kNB);
   // steps_limit k0 ≥ 1: only the launches that factor blocks 0 .. k0 and form panel columns 0 .. k0
   if (steps_limit > 0 && steps_limit + 1 < steps) steps = steps_limit + 1;
@@ -2657,7 +2675,7 @@ static hipError_t launch_cholesky_blocked(hipStream_t stream, double* A, int64_t
     const int64_t rest = N - (int64_t)(k + 1) * kNB;
     const int t = (int)((rest + kGT - 1) / kGT);
     if (k == 0) {
-      e = chol_panel(stream, A, N, lda, k, ws, info, vec);
+      e = chol_panel(stream, A, N, lda, k, ws, info, vec, pi);
       if (e != hipSuccess) break;
     }
     hipLaunchKernelGGL((chol_update_kernel<true, true>), dim3((unsigned)(t * (t + 1) / 2)), dim3(256), g_chol_update_lds,
@@ -2704,7 +2722,7 @@ static bool chol_persist_fits(int64_t N, int64_t lda) {
 }
 
 static hipError_t launch_cholesky_blocked(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws,
-                                          int spin_limit, int acq_rel, int steps_limit = -1);
+                                          int spin_limit, int acq_rel, int steps_limit = -1, CholPersistInit pi = {});
 
 // Round 5: the persistent launch's task order.  Step-major tickets put step k's critical tasks (its panel tiles, the
 // next column's updates) behind every far-column update of step k − 1, and the diagonal walk waited for them.  Here
@@ -2777,18 +2795,20 @@ static hipError_t launch_cholesky_persist(hipStream_t stream, double* A, int64_t
   const int t = (int)((N + kNB - 1) / kNB);
   if (k0 > t - 2) k0 = 0;
   hipError_t e = hipSuccess;
-  if (k0 > 0) e = launch_cholesky_blocked(stream, A, N, lda, info, ws, spin_limit, acq_rel, k0);
+  double* Wf = ws;
+  int* ints = reinterpret_cast<int*>(ws + (int64_t)t * kCholWsDoubles);
+  if (k0 > 0) e = launch_cholesky_blocked(stream, A, N, lda, info, ws, spin_limit, acq_rel, k0, CholPersistInit{ints, t, k0});
   if (e != hipSuccess) return e;
   int total = 0;
   for (int k = k0; k < t; ++k) total += chol_persist_step_tasks(t, k, k0);
-  double* Wf = ws;
-  int* ints = reinterpret_cast<int*>(ws + (int64_t)t * kCholWsDoubles);
   const int L = g_chol_lookahead >= 0 ? g_chol_lookahead : kCholLookahead;
   // L = 0 (tools): the step-major arithmetic order of round 4
   const int* tab = L > 0 ? chol_task_table(t, k0, L, total) : nullptr;
   CholSync sync{ints, ints + t, ints + t + t * t, ints + t + 2 * t * t, ints + t + 2 * t * t + 1, tab};
-  hipLaunchKernelGGL(chol_persist_init_kernel, dim3(1), dim3(256), 0, stream, ints, t, k0, info);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if (k0 == 0) {   // with k0 > 0 step 0's panel launch wrote the sync words
+    hipLaunchKernelGGL(chol_persist_init_kernel, dim3(1), dim3(256), 0, stream, ints, t, k0, info);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
   const int slots = kPersistWgPerCu * device_cus() - 1;
   const int grid = 1 + (total < slots ? total : slots);
   if (acq_rel)
@@ -2905,33 +2925,55 @@ hipError_t launch_gp_grad(hipStream_t stream, int kind, int DP, const double* X,
 // × 16 row slices (coalesced 512-B row segments); the slices' partial sums are added in slice order.
 // One thread per candidate over all rows ran 12 workgroups at N = 3000 (142 µs,
 // profiles/r02_v23_c6_kernel_stats.csv).
+// μ = αᵀK*, σ² = σ_f² − ΣV² per candidate column: 16 row slices of ⌈n/16⌉ rows, each summed in row order by one thread,
+// the slices' partials met in slice order.  16 columns per workgroup (lane = slice-in-wave × 16 + column: 128-B row
+// segments), so N = 3000 candidates spread over 188 workgroups (round 5; 64 columns per 1,024-thread workgroup ran on
+// 47 CUs) and each thread keeps 8 rows' loads in flight (one row per load latency: 12.9 µs per config-6 step, and
+// 12.75 µs with the wider grid alone) — the same sums in the same order, bitwise.
 constexpr int kColSlices = 16;
-__global__ __launch_bounds__(64 * kColSlices) void post_colreduce_kernel(const double* __restrict__ Kst,
-                                                                          const double* __restrict__ V, int64_t n,
-                                                                          int64_t Nc, const double* __restrict__ alpha,
-                                                                          double variance, double* __restrict__ mu,
-                                                                          double* __restrict__ var) {
-  __shared__ double pm[kColSlices][64], ps[kColSlices][64];
-  const int lane = threadIdx.x & 63, sl = threadIdx.x >> 6;
-  const int64_t c = (int64_t)blockIdx.x * 64 + lane;
+constexpr int kColTile = 16;
+__global__ __launch_bounds__(kColSlices * kColTile) void post_colreduce_kernel(const double* __restrict__ Kst,
+                                                                                const double* __restrict__ V, int64_t n,
+                                                                                int64_t Nc, const double* __restrict__ alpha,
+                                                                                double variance, double* __restrict__ mu,
+                                                                                double* __restrict__ var) {
+  __shared__ double pm[kColSlices][kColTile], ps[kColSlices][kColTile];
+  const int col = threadIdx.x % kColTile, sl = threadIdx.x / kColTile;
+  const int64_t c = (int64_t)blockIdx.x * kColTile + col;
   const int64_t rs = (n + kColSlices - 1) / kColSlices;
   const int64_t k0 = sl * rs, k1 = (k0 + rs) < n ? (k0 + rs) : n;
   double m = 0.0, s = 0.0;
   if (c < Nc) {
-    for (int64_t k = k0; k < k1; ++k) {
+    // 8 rows' loads in flight before their fmas (the sums keep row order): one memory latency per 8 rows, not per row
+    constexpr int U = 8;
+    int64_t k = k0;
+    for (; k + U <= k1; k += U) {
+      double kv[U], vv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        kv[u] = Kst[(k + u) * Nc + c];
+        vv[u] = V[(k + u) * Nc + c];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        m = fma(alpha[k + u], kv[u], m);
+        s = fma(vv[u], vv[u], s);
+      }
+    }
+    for (; k < k1; ++k) {
       m = fma(alpha[k], Kst[k * Nc + c], m);
       const double v = V[k * Nc + c];
       s = fma(v, v, s);
     }
   }
-  pm[sl][lane] = m;
-  ps[sl][lane] = s;
+  pm[sl][col] = m;
+  ps[sl][col] = s;
   __syncthreads();
   if (sl == 0 && c < Nc) {
 #pragma unroll
     for (int j = 1; j < kColSlices; ++j) {
-      m += pm[j][lane];
-      s += ps[j][lane];
+      m += pm[j][col];
+      s += ps[j][col];
     }
     mu[c] = m;
     var[c] = variance - s;
@@ -2941,8 +2983,8 @@ __global__ __launch_bounds__(64 * kColSlices) void post_colreduce_kernel(const d
 hipError_t launch_post_colreduce(hipStream_t stream, const double* Kst, const double* V, int64_t n, int64_t Nc,
                                  const double* alpha, double variance, double* mu, double* var) {
   if (Nc <= 0) return hipSuccess;
-  hipLaunchKernelGGL(post_colreduce_kernel, dim3((unsigned)((Nc + 63) / 64)), dim3(64 * kColSlices), 0, stream, Kst, V,
-                     n, Nc, alpha, variance, mu, var);
+  hipLaunchKernelGGL(post_colreduce_kernel, dim3((unsigned)((Nc + kColTile - 1) / kColTile)), dim3(kColSlices * kColTile),
+                     0, stream, Kst, V, n, Nc, alpha, variance, mu, var);
   return hipGetLastError();
 }
 

@@ -2302,6 +2302,7 @@ __global__ __launch_bounds__(kSelThreads) void select_topk_kernel(const double* 
   __shared__ unsigned hist[256];
   __shared__ unsigned long long s_prefix;
   __shared__ unsigned s_rank, s_less;
+  __shared__ int s_done;
   __shared__ unsigned wsum[kSelThreads / 64];
   __shared__ unsigned s_slot;
   __shared__ unsigned long long sk[kSelTopK];
@@ -2319,8 +2320,12 @@ __global__ __launch_bounds__(kSelThreads) void select_topk_kernel(const double* 
     s_prefix = 0ull;
     s_rank = (unsigned)K;            // 1-based rank of T among the keys matching the prefix
     s_less = 0u;
+    s_done = -1;
   }
-  // ---- radix select of T = the K-th smallest key, most significant byte first
+  // ---- radix select of T = the K-th smallest key, most significant byte first.  Round 5: a pass whose chosen bin
+  // is needed whole (its count equals the rank still to take) ends the search — the K smallest keys are then the
+  // keys whose bits from `shift` up are ≤ the prefix's, with no tie at the boundary (equal keys share every bin), so
+  // the heads are the same; random draws get there in 2-3 of the 8 passes.
   for (int shift = 56; shift >= 0; shift -= 8) {
     for (int i = tid; i < 256; i += kSelThreads) hist[i] = 0u;
     __syncthreads();
@@ -2351,13 +2356,31 @@ __global__ __launch_bounds__(kSelThreads) void select_topk_kernel(const double* 
           s_prefix = prefix | ((unsigned long long)(4 * lane + q) << shift);
           s_rank = rank - run;
           s_less += run;
+          if (run + c[q] == rank) s_done = shift;
         }
         run += c[q];
       }
     }
     __syncthreads();
+    if (s_done >= 0) break;
   }
   const unsigned long long T = s_prefix;
+  if (s_done > 0) {
+    // the whole bin: every key whose bits from s_done up are ≤ T's (K of them, slot order arbitrary)
+    const int sd = s_done;
+    if (tid == 0) s_slot = 0u;
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < kE; ++e) {
+      const int64_t i = (int64_t)tid * E + e;
+      if (e < E && i < N && (key[e] >> sd) <= (T >> sd)) {
+        const unsigned slot = atomicAdd(&s_slot, 1u);
+        sk[slot] = key[e];
+        si[slot] = (unsigned short)i;
+      }
+    }
+    __syncthreads();
+  } else {
   const unsigned need_ties = (unsigned)K - s_less;         // ties at T to take, lowest indices first
   // ---- number the ties at T in index order (block scan of per-thread counts)
   unsigned nt = 0u;
@@ -2391,6 +2414,7 @@ __global__ __launch_bounds__(kSelThreads) void select_topk_kernel(const double* 
     }
   }
   __syncthreads();
+  }
   // ---- one wave sorts the K pairs by (key, index); slots past K hold +max sentinels
   if (wave == 0) {
     unsigned long long kk = lane < K ? sk[lane] : ~0ull;

@@ -1022,8 +1022,13 @@ static int check_cov_n(omb_ctx* ctx, int64_t N) {
 // K* (n, N) by the K block, V = L⁻¹K* (n, N) by GEMM, μ = K*ᵀα and σ² = σ_f² − Σ V² by the column
 // reduction over those two (the fused posterior kernel would recompute K* and V; at TuRBO's ≤ 5,000
 // candidates it also runs on a few dozen workgroups: 90 µs of a 3 ms step, profiles/r02_v21_c6_kernel_stats.csv).
+// scale_ws (omb_posterior_samples): the column reduction also writes launch_cand_scale's rows into it, for the first
+// cov_build (prescaled); the fused SYRK path only.
+static bool cov_fused_path(const omb_ctx* ctx, const ObjState& s) {
+  return !ctx->cov_table && ctx->cov_fused && s.DP <= kMaxFusedDP;
+}
 static hipError_t cov_prepare(omb_ctx* ctx, const ObjState& s, const double* Xc, int64_t N, double* Kst, double* V,
-                              double* mu, double* var) {
+                              double* mu, double* var, double* scale_ws = nullptr) {
   GPArgs args;
   init_args(ctx, &args);
   args.gp[0] = s.dev;
@@ -1031,18 +1036,20 @@ static hipError_t cov_prepare(omb_ctx* ctx, const ObjState& s, const double* Xc,
   args.DP = s.DP;
   hipError_t e = launch_kernel_block(ctx->stream, args, 0, Xc, N, Kst);
   if (e == hipSuccess) e = launch_gemm_ltri_nn(ctx->stream, s.n, N, 1.0, s.Ld, s.n, Kst, N, 0.0, V, N);
-  if (e == hipSuccess) e = launch_post_colreduce(ctx->stream, Kst, V, s.n, N, s.dev.alpha, s.dev.variance, mu, var);
+  if (e == hipSuccess)
+    e = launch_post_colreduce(ctx->stream, Kst, V, s.n, N, s.dev.alpha, s.dev.variance, mu, var,
+                              scale_ws ? &s.dev : nullptr, s.d, s.DP, Xc, scale_ws);
   return e;
 }
 
 // lower triangle of Σ = K(X*, X*) − VᵀV (GPy PosteriorExact._raw_predict, full_cov=True); cws:
 // cand_cov_ws_doubles(N, DP) doubles.
 static hipError_t cov_build(omb_ctx* ctx, const ObjState& s, const double* Xc, int64_t N, const double* V, double* S,
-                            int64_t lds, double* cws, double jitter = 0.0) {
-  if (!ctx->cov_table && ctx->cov_fused && s.DP <= kMaxFusedDP) {
+                            int64_t lds, double* cws, double jitter = 0.0, bool prescaled = false) {
+  if (cov_fused_path(ctx, s)) {
     // K(X*, X*) formed in the SYRK's epilogue (launch_cov_syrk): the two-launch result below to the ulp
     hipError_t e = hipSuccess;
-    const int kp = launch_cand_scale(ctx->stream, s.dev, s.d, s.DP, Xc, N, cws, &e);
+    const int kp = prescaled ? (s.DP + 3) / 4 * 4 : launch_cand_scale(ctx->stream, s.dev, s.d, s.DP, Xc, N, cws, &e);
     if (e == hipSuccess && kp > 0)
       return launch_cov_syrk(ctx->stream, N, s.n, V, N, S, lds, cws, cws + N * kp, kp, s.kind, s.variance, jitter);
     if (e != hipSuccess) return e;
@@ -1145,12 +1152,15 @@ int omb_posterior_samples(omb_ctx* ctx, int obj, const double* Xc_dev, int64_t N
   double* var = mu + N;
   double* S = var + N;
   double* cws = S + (size_t)N * N;
-  hipError_t e = cov_prepare(ctx, s, Xc_dev, N, Kst, V, mu, var);
+  // the first try's scaled candidates come from the column reduction's launch; later tries rescale (the draws'
+  // split-K partials share cws)
+  const bool prescale = cov_fused_path(ctx, s);
+  hipError_t e = cov_prepare(ctx, s, Xc_dev, N, Kst, V, mu, var, prescale ? cws : nullptr);
   if (e != hipSuccess) return hip_fail(ctx, e, "posterior_samples (posterior)");
   double jit = jitter_rel * s.variance;
   int info = -1, t = 0;
   for (; t < max_tries; ++t, jit *= 10.0) {
-    if ((e = cov_build(ctx, s, Xc_dev, N, V, S, N, cws, jit)) != hipSuccess)   // Σ + jit·I
+    if ((e = cov_build(ctx, s, Xc_dev, N, V, S, N, cws, jit, prescale && t == 0)) != hipSuccess)   // Σ + jit·I
       return hip_fail(ctx, e, "posterior_samples (cov)");
     if ((rc = chol_enqueue(ctx, S, N, N, 0.0))) return rc;
     // the draws are queued before the status is read (no idle GPU between the factor and them); a failed factor's

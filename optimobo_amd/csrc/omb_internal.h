@@ -211,7 +211,9 @@ hipError_t launch_gp_lml_small_batch(hipStream_t stream, int kind, int DP, const
                                      double base, double* const* out);
 // dense posterior path: μ, σ² of a candidate chunk from K* (n, Nc) and V = L⁻¹K* (n, Nc).
 hipError_t launch_post_colreduce(hipStream_t stream, const double* Kst, const double* V, int64_t n, int64_t Nc,
-                                 const double* alpha, double variance, double* mu, double* var);
+                                 const double* alpha, double variance, double* mu, double* var,
+                                 const GPDev* scale_g = nullptr, int d = 0, int DP = 0, const double* Xc = nullptr,
+                                 double* ws = nullptr);   // scale_g: also launch_cand_scale's rows into ws
 hipError_t launch_gp_grad(hipStream_t stream, int kind, int DP, const double* X, int d, int64_t n, const double* ls,
                           double variance, const double* alpha, const double* Kinv, int64_t ldk, double* partials,
                           const double* L, int64_t lda, const double* y, double* out);

@@ -2956,11 +2956,33 @@ hipError_t launch_gp_grad(hipStream_t stream, int kind, int DP, const double* X,
 // 12.75 µs with the wider grid alone) — the same sums in the same order, bitwise.
 constexpr int kColSlices = 16;
 constexpr int kColTile = 16;
+// sc (round 5, omb_posterior_samples): the launch also writes cand_scale_kernel's rows for its kColTile candidates —
+// Xs[i·KP + k] = X*[i][k] / ℓ_k and ‖Xs_i‖² by the same xor tree over the KP lanes of one wave — one launch fewer.
+struct ColScale {
+  const double* Xc = nullptr;   // nullptr: no scaling job
+  const double* ls = nullptr;
+  int d = 0, KP = 0;
+  double* Xs = nullptr;
+  double* xsq = nullptr;
+};
 __global__ __launch_bounds__(kColSlices * kColTile) void post_colreduce_kernel(const double* __restrict__ Kst,
                                                                                 const double* __restrict__ V, int64_t n,
                                                                                 int64_t Nc, const double* __restrict__ alpha,
                                                                                 double variance, double* __restrict__ mu,
-                                                                                double* __restrict__ var) {
+                                                                                double* __restrict__ var, ColScale sc) {
+  if (sc.Xc) {
+    const int KP = sc.KP;
+    for (int p = threadIdx.x; p < kColTile * KP; p += kColSlices * kColTile) {   // KP | 64: a candidate's lanes in one wave
+      const int64_t i = (int64_t)blockIdx.x * kColTile + p / KP;
+      const int k = p % KP;
+      double a = 0.0;
+      if (i < Nc && k < sc.d) a = sc.Xc[i * sc.d + k] / sc.ls[k];
+      if (i < Nc) sc.Xs[i * KP + k] = a;
+      double q = a * a;
+      for (int o = KP / 2; o > 0; o >>= 1) q += __shfl_xor(q, o);
+      if (i < Nc && k == 0) sc.xsq[i] = q;
+    }
+  }
   __shared__ double pm[kColSlices][kColTile], ps[kColSlices][kColTile];
   const int col = threadIdx.x % kColTile, sl = threadIdx.x / kColTile;
   const int64_t c = (int64_t)blockIdx.x * kColTile + col;
@@ -3005,10 +3027,20 @@ __global__ __launch_bounds__(kColSlices * kColTile) void post_colreduce_kernel(c
 }
 
 hipError_t launch_post_colreduce(hipStream_t stream, const double* Kst, const double* V, int64_t n, int64_t Nc,
-                                 const double* alpha, double variance, double* mu, double* var) {
+                                 const double* alpha, double variance, double* mu, double* var, const GPDev* scale_g,
+                                 int d, int DP, const double* Xc, double* ws) {
   if (Nc <= 0) return hipSuccess;
+  ColScale sc;
+  if (scale_g && DP <= kMaxFusedDP) {
+    sc.KP = (DP + 3) / 4 * 4;
+    sc.Xc = Xc;
+    sc.ls = scale_g->ls;
+    sc.d = d;
+    sc.Xs = ws;
+    sc.xsq = ws + Nc * sc.KP;
+  }
   hipLaunchKernelGGL(post_colreduce_kernel, dim3((unsigned)((Nc + kColTile - 1) / kColTile)), dim3(kColSlices * kColTile),
-                     0, stream, Kst, V, n, Nc, alpha, variance, mu, var);
+                     0, stream, Kst, V, n, Nc, alpha, variance, mu, var, sc);
   return hipGetLastError();
 }
 

@@ -456,9 +456,6 @@ def main():
     ap.add_argument("--cov-fused", type=int, default=None, choices=[0, 1],
                     help="omb_debug_set(COV_FUSED): K(X*, X*) in the covariance SYRK's epilogue (config 6; default: "
                          "the library's, 1)")
-    ap.add_argument("--posterior-persist", type=int, default=None, choices=[0, 1],
-                    help="omb_debug_set(POSTERIOR_PERSIST): the persistent-ring posterior kernel for n_train > 128 "
-                         "(default: the library's)")
     ap.add_argument("--uniform-train", action="store_true",
                     help="train on X uniform in [0, 1]^d (SURVEY 8d) instead of the config's mid-run BO box "
                          "(configs 2-5); the step's work is the same, the arg-max lands on the unexplored corner")
@@ -529,8 +526,6 @@ def main():
         ctx.debug_set("argmax_passes", args.argmax_passes)
     if args.chol_mode is not None:
         ctx.debug_set("chol_mode", args.chol_mode)
-    if args.posterior_persist is not None:
-        ctx.debug_set("posterior_persist", args.posterior_persist)
     if acq_kind == "ei_tch":
         # ParEGO-style mono surrogate: Tchebicheff-aggregate the objectives (parego.py:212-219)
         tch = sc.Tchebicheff(Y.min(axis=0), Y.max(axis=0))

@@ -108,8 +108,8 @@ const char* omb_last_error(const omb_ctx* ctx);
  * wait and relaxed flags — is measured valid on gfx950), bitwise the same factor as schedule m.
  * omb_debug_set(ctx, OMB_DEBUG_TIMING_STRIDE, s) records omb_timing's events on every s-th chain only (default 1;
  * omb_timing_read then averages over the recorded chains), so that a timed loop carries fewer event records. *
- * omb_debug_set(ctx, OMB_DEBUG_POSTERIOR_PERSIST, p) picks the fused posterior kernel for n_train > 128: 1 the persistent
- * ring (resident workgroups, ring chunks numbered across candidate blocks), 0 one workgroup per candidate block.
+ * Value 7 (round 5's OMB_DEBUG_POSTERIOR_PERSIST, a persistent-ring posterior kernel measured 2-5% slower at every
+ * configuration) is retired: the library has one posterior kernel per shape, and omb_debug_set(ctx, 7, ·) fails.
  * omb_debug_set(ctx, OMB_DEBUG_COV_FUSED, 0) builds the posterior covariance as K(X*, X*) then the VᵀV update (two
  * launches) instead of one SYRK with K(X*, X*) in its epilogue (default 1; the same matrix to the ulp).
  * omb_debug_set(ctx, OMB_DEBUG_SELECT_SEQ, 1) makes omb_thompson_select walk the samples in order for B ≤ 64 too
@@ -121,7 +121,6 @@ enum {
   OMB_DEBUG_ARGMAX_PASSES = 4,
   OMB_DEBUG_CHOL_MODE = 5,
   OMB_DEBUG_TIMING_STRIDE = 6,
-  OMB_DEBUG_POSTERIOR_PERSIST = 7,
   OMB_DEBUG_COV_FUSED = 8,
   OMB_DEBUG_SELECT_SEQ = 9
 };
@@ -167,6 +166,14 @@ int omb_ehvi2d(omb_ctx* ctx, const double* mu_dev, const double* var_dev, int64_
 int omb_ehvi3d_mc(omb_ctx* ctx, const double* mu_dev, const double* var_dev, int64_t ld, int64_t N,
                   const double* cache_dev, int M, const double* r_host, double hv_pf, double* out_dev,
                   int32_t* raised_dev);
+/* The same Monte-Carlo EHVI for any 2 ≤ k ≤ OMB_MAX_OBJ objectives (omb_ehvi3d_mc is k = 3): the
+ * reference calls EHVI_3D for every n_obj != 2 (optimisers.py:245-248), and EHVI_3D's per-sample volume
+ * is pygmo's k-D hypervolume([s]).compute(r) = Π_{j<k}(r_j − s_j) (util_functions.py:205-206; the 3-term
+ * product of :204 is overwritten).  cache_dev (M, k) row-major, r_host (k), hv_pf = HV(PF, r) in k-D;
+ * k·M ≤ 8192 (the cache is staged in LDS). */
+int omb_ehvi_mc(omb_ctx* ctx, int k, const double* mu_dev, const double* var_dev, int64_t ld, int64_t N,
+                const double* cache_dev, int M, const double* r_host, double hv_pf, double* out_dev,
+                int32_t* raised_dev);
 
 /* Exact ("textbook") EHVI for k = 2 or 3 objectives — the exact value the Monte-Carlo
  * EHVI_3D (util_functions.py:170-214) estimates — from a disjoint box decomposition of the
@@ -228,6 +235,8 @@ int omb_plan_ehvi2d(omb_ctx* ctx, const double* pf_sorted_host, int P, const dou
                     double s01, int mode);
 /* util_functions.EHVI_3D reference Monte-Carlo form (k = 3): as omb_ehvi3d_mc, cache_host (M, 3). */
 int omb_plan_ehvi3d_mc(omb_ctx* ctx, const double* cache_host, int M, const double* r_host, double hv_pf);
+/* EHVI_3D's Monte-Carlo form for k objectives (2 ≤ k ≤ OMB_MAX_OBJ): as omb_ehvi_mc, cache_host (M, k). */
+int omb_plan_ehvi_mc(omb_ctx* ctx, int k, const double* cache_host, int M, const double* r_host, double hv_pf);
 /* Exact EHVI (k = 2, 3): as omb_ehvi_boxes, coords_host (k, C), boxes_host (B, 2k). */
 int omb_plan_ehvi_boxes(omb_ctx* ctx, int k, const double* coords_host, int C, const uint16_t* boxes_host, int B);
 /* EMO hypervolume-based PoI (k = 2): as omb_hvpoi, cells_host (C, 2, 2). */

@@ -24,7 +24,6 @@ DEBUG_FUSED_CHAIN = 3
 DEBUG_ARGMAX_PASSES = 4
 DEBUG_CHOL_MODE = 5
 DEBUG_TIMING_STRIDE = 6
-DEBUG_POSTERIOR_PERSIST = 7
 DEBUG_COV_FUSED = 8
 DEBUG_SELECT_SEQ = 9
 MAX_OBJ, MAX_DIM, MAX_TRAIN, MAX_TRAIN_DENSE = 8, 256, 1024, 16384
@@ -50,6 +49,7 @@ SIGNATURES = {
     "omb_posterior": (_i, [_p, _i, _p, _i64, _p, _p]),
     "omb_ehvi2d": (_i, [_p, _p, _p, _i64, _i64, _p, _i, _dp, _d, _d, _i, _p]),
     "omb_ehvi3d_mc": (_i, [_p, _p, _p, _i64, _i64, _p, _i, _dp, _d, _p, _p]),
+    "omb_ehvi_mc": (_i, [_p, _i, _p, _p, _i64, _i64, _p, _i, _dp, _d, _p, _p]),
     "omb_ehvi_boxes": (_i, [_p, _i, _p, _p, _i64, _i64, _p, _i, _p, _i, _p]),
     "omb_hvpoi": (_i, [_p, _p, _p, _i64, _i64, _p, _i, _p]),
     "omb_expdec": (_i, [_p, _i, _p, _p, _i64, _i64, _p, _i, _i, _dp, _dp, _dp, _dp, _d, _p]),
@@ -60,6 +60,7 @@ SIGNATURES = {
     # fused chain (host pointers for plan geometry)
     "omb_plan_ehvi2d": (_i, [_p, _p, _i, _dp, _d, _d, _i]),
     "omb_plan_ehvi3d_mc": (_i, [_p, _p, _i, _dp, _d]),
+    "omb_plan_ehvi_mc": (_i, [_p, _i, _p, _i, _dp, _d]),
     "omb_plan_ehvi_boxes": (_i, [_p, _i, _p, _i, _p, _i]),
     "omb_plan_hvpoi": (_i, [_p, _p, _i]),
     "omb_plan_expdec": (_i, [_p, _i, _p, _i, _i, _dp, _dp, _dp, _dp, _d]),

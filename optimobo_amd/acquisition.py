@@ -74,9 +74,11 @@ class AcquisitionEngine:
         return self.ctx.ehvi_boxes(mu, var, coords, boxes)
 
     def ehvi3d(self, Xc, max_point, PF, cache):
+        """util_functions.EHVI_3D (Monte-Carlo form) on every row of Xc, for k = n_obj ≥ 3 objectives (the
+        reference calls it for every n_obj != 2): (values (N,), raised (N,) int32)."""
         mu, var = self.posterior(Xc)
         hv = pareto.hypervolume(PF, max_point)
-        return self.ctx.ehvi3d_mc(mu, var, np.asarray(cache, np.float64), np.asarray(max_point, np.float64), hv)
+        return self.ctx.ehvi_mc(mu, var, np.asarray(cache, np.float64), np.asarray(max_point, np.float64), hv)
 
     def expected_decomposition(self, Xc, weights, agg_func, agg_min, cache):
         mu, var = self.posterior(Xc)
@@ -115,8 +117,8 @@ class AcquisitionEngine:
         self.ctx.plan_ehvi_boxes(coords, boxes)
 
     def plan_ehvi3d(self, max_point, PF, cache):
-        self.ctx.plan_ehvi3d_mc(np.asarray(cache, np.float64), np.asarray(max_point, np.float64),
-                                pareto.hypervolume(PF, max_point))
+        self.ctx.plan_ehvi_mc(np.asarray(cache, np.float64), np.asarray(max_point, np.float64),
+                              pareto.hypervolume(PF, max_point))
 
     def plan_expected_decomposition(self, weights, agg_func, agg_min, cache):
         sid, params = agg_func.device_spec()

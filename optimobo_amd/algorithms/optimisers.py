@@ -25,10 +25,11 @@ class MultiSurrogateOptimiser(BODriver):
         """optimisers.py:91-119 on the device: returns (x, −EHVI(x))."""
         from ..acquisition import engine_for
         eng = engine_for(models, self.device)
-        if (function == "EHVI_3D" or self.n_obj == 3) and self.mode == "textbook":
-            eng.plan_ehvi_exact(max_point, pf)          # exact EHVI in place of the MC estimate
-        elif function == "EHVI_3D" or self.n_obj == 3:
-            eng.plan_ehvi3d(max_point, pf, cache)
+        mc = function == "EHVI_3D" or self.n_obj >= 3          # optimisers.py:245-248: EHVI_3D for n_obj != 2
+        if mc and self.mode == "textbook" and self.n_obj <= 3:
+            eng.plan_ehvi_exact(max_point, pf)          # exact EHVI in place of the MC estimate (k = 2, 3)
+        elif mc:
+            eng.plan_ehvi3d(max_point, pf, cache)       # the reference's Monte-Carlo form, any k ≥ 3
         else:
             eng.plan_ehvi(max_point, pf, cache, mode=self.mode)
         x, v = self._maximise(models, None)

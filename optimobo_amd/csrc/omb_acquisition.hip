@@ -177,27 +177,47 @@ hipError_t launch_ehvi2d_argmax(hipStream_t stream, const double* mu, const doub
   return launch_argmax_reduce(stream, am.partials, (int)nb, am.offset, am.result);
 }
 
-// ------------------------------------------------------------------------------ EHVI 3-D
-// util_functions.py:170-214: samples s = cache·sqrt(σ²0) + μ (change, :217-237), then
-// mean_s max(0, Π_j(r_j − s_j) − HV(PF)).  pygmo raises ValueError when a sample is not inside
-// the reference box (some s_j > r_j, or s == r): flagged per candidate, value NaN.
-__global__ __launch_bounds__(kAcqThreads) void ehvi3d_kernel(const double* __restrict__ mu,
-                                                             const double* __restrict__ var, int64_t ld, int64_t N,
-                                                             const double* __restrict__ cache, int M, double r0,
-                                                             double r1, double r2, double hv_pf,
-                                                             double* __restrict__ out, int32_t* __restrict__ raised) {
+// ------------------------------------------------------------------------------ EHVI, Monte-Carlo (k objectives)
+// util_functions.py:170-214 (EHVI_3D, which the reference calls for every n_obj != 2, optimisers.py:245-248):
+// samples s = cache·sqrt(σ²0) + μ (change, :217-237), then mean_s max(0, HV({s}) − HV(PF)) with HV({s}) =
+// pygmo's hypervolume([s]).compute(r) = Π_{j<K}(r_j − s_j), multiplied left to right (:205-206; the 3-term
+// product of :204 is dead code).  pygmo raises ValueError when a sample is not inside the reference box (some
+// s_j > r_j, or s == r): flagged per candidate, value NaN.  One thread per candidate, the (M, K) cache in LDS
+// read as a broadcast; μ_j and r_j in registers (K is a template parameter, so nothing spills to scratch).
+struct RefPoint {
+  double r[OMB_MAX_OBJ];
+};
+
+template <int K>
+__global__ __launch_bounds__(kAcqThreads) void ehvi_mc_kernel(const double* __restrict__ mu,
+                                                              const double* __restrict__ var, int64_t ld, int64_t N,
+                                                              const double* __restrict__ cache, int M, RefPoint rp,
+                                                              double hv_pf, double* __restrict__ out,
+                                                              int32_t* __restrict__ raised) {
   extern __shared__ double sm[];
-  for (int i = threadIdx.x; i < 3 * M; i += blockDim.x) sm[i] = cache[i];
+  for (int i = threadIdx.x; i < K * M; i += blockDim.x) sm[i] = cache[i];
   __syncthreads();
   for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < N; c += (int64_t)gridDim.x * blockDim.x) {
-    const double m0 = mu[c], m1 = mu[ld + c], m2 = mu[2 * ld + c];
+    double m[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) m[j] = mu[j * ld + c];
     const double sd = sqrt(var[c]);   // σ²0 for every objective (quirk 1)
     double answer = 0.0;
     bool bad = !(sd == sd);
     for (int s = 0; s < M; ++s) {
-      const double x0 = sm[3 * s] * sd + m0, x1 = sm[3 * s + 1] * sd + m1, x2 = sm[3 * s + 2] * sd + m2;
-      bad |= (x0 > r0) || (x1 > r1) || (x2 > r2) || ((x0 == r0) && (x1 == r1) && (x2 == r2));
-      double h = (r0 - x0) * (r1 - x1) * (r2 - x2) - hv_pf;
+      double x[K];
+#pragma unroll
+      for (int j = 0; j < K; ++j) x[j] = sm[K * s + j] * sd + m[j];
+      bool out_of_box = false, at_r = true;
+      double vol = rp.r[0] - x[0];
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        out_of_box |= x[j] > rp.r[j];
+        at_r = at_r && (x[j] == rp.r[j]);
+        if (j > 0) vol *= rp.r[j] - x[j];
+      }
+      bad |= out_of_box || at_r;
+      const double h = vol - hv_pf;
       if (h > 0.0) answer += h;
     }
     out[c] = bad ? __builtin_nan("") : answer / M;
@@ -205,12 +225,19 @@ __global__ __launch_bounds__(kAcqThreads) void ehvi3d_kernel(const double* __res
   }
 }
 
-hipError_t launch_ehvi3d_mc(hipStream_t stream, const double* mu, const double* var, int64_t ld, int64_t N,
-                            const double* cache, int M, const double* r, double hv_pf, double* out,
-                            int32_t* raised) {
-  size_t shm = sizeof(double) * 3 * M;
-  hipLaunchKernelGGL(ehvi3d_kernel, dim3(acq_grid(N)), dim3(kAcqThreads), shm, stream, mu, var, ld, N, cache, M,
-                     r[0], r[1], r[2], hv_pf, out, raised);
+hipError_t launch_ehvi_mc(hipStream_t stream, int k, const double* mu, const double* var, int64_t ld, int64_t N,
+                          const double* cache, int M, const double* r, double hv_pf, double* out, int32_t* raised) {
+  const size_t shm = sizeof(double) * (size_t)k * M;
+  RefPoint rp{};
+  for (int j = 0; j < k; ++j) rp.r[j] = r[j];
+  const dim3 g(acq_grid(N)), b(kAcqThreads);
+  switch (k) {
+#define OMB_MC(KV) \
+  case KV: hipLaunchKernelGGL(ehvi_mc_kernel<KV>, g, b, shm, stream, mu, var, ld, N, cache, M, rp, hv_pf, out, raised); break;
+    OMB_MC(2) OMB_MC(3) OMB_MC(4) OMB_MC(5) OMB_MC(6) OMB_MC(7) OMB_MC(8)
+#undef OMB_MC
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

@@ -24,7 +24,7 @@ struct ObjState {
 };
 
 // Acquisition of the fused chain (omb_plan_*), with its geometry resident in ctx->geo.
-enum PlanKind { PLAN_NONE = 0, PLAN_EHVI2D, PLAN_EHVI3D_MC, PLAN_EHVI_BOXES, PLAN_HVPOI, PLAN_EXPDEC, PLAN_EI };
+enum PlanKind { PLAN_NONE = 0, PLAN_EHVI2D, PLAN_EHVI_MC, PLAN_EHVI_BOXES, PLAN_HVPOI, PLAN_EXPDEC, PLAN_EI };
 
 struct Plan {
   int kind = PLAN_NONE;
@@ -94,7 +94,6 @@ struct omb_ctx {
   int fused_chain = 0;  // OMB_DEBUG_FUSED_CHAIN: 0 EHVI-2D then the arg-max's passes, 1 one ticketed launch, 2 EHVI
                         // with the per-workgroup pairs, then the arg-max's second pass
   bool argmax_one_pass = false;  // OMB_DEBUG_ARGMAX_PASSES: 1 (one launch) or 2 (default: measured level)
-  int posterior_persist = 0;     // OMB_DEBUG_POSTERIOR_PERSIST
   int chol_mode = kCholAuto;     // OMB_DEBUG_CHOL_MODE (value & 3)
   int chol_acq_rel = 0;          // OMB_DEBUG_CHOL_MODE (value & 4): release / acquire hand-offs
   bool select_seq = false;       // OMB_DEBUG_SELECT_SEQ: the sequential greedy walk for B ≤ 64 too
@@ -156,7 +155,6 @@ void init_args(omb_ctx* ctx, GPArgs* args) {
   memset(args, 0, sizeof(*args));
   args->fault = ctx->fault_dev;
   args->spin_limit = ctx->spin_limit;
-  args->persist = ctx->posterior_persist;
 }
 
 // GP state of objectives 0..n_obj-1, all set, sharing d.
@@ -194,8 +192,12 @@ int check_ehvi2d(omb_ctx* ctx, int P, const double* r, int mode) {
   return OMB_OK;
 }
 
-int check_ehvi3d(omb_ctx* ctx, int M, const double* r) {
-  if (M < 1 || 3 * M > kMaxLdsDoubles) return fail(ctx, OMB_EUNSUP, "cache size M=%d outside [1, %d]", M, kMaxLdsDoubles / 3);
+int check_ehvi_mc(omb_ctx* ctx, int k, int M, const double* r) {
+  if (k < 2 || k > OMB_MAX_OBJ) return fail(ctx, OMB_EINVAL, "Monte-Carlo EHVI needs 2 <= k <= %d objectives (k=%d)",
+                                           OMB_MAX_OBJ, k);
+  // the (M, k) cache is staged in <= 64 KiB of dynamic LDS
+  if (M < 1 || (int64_t)k * M > kMaxLdsDoubles)
+    return fail(ctx, OMB_EUNSUP, "cache size M=%d outside [1, %d] for k=%d", M, kMaxLdsDoubles / k, k);
   if (!r) return fail(ctx, OMB_EINVAL, "null reference point");
   return OMB_OK;
 }
@@ -413,8 +415,8 @@ int run_chain(omb_ctx* ctx, const double* Xc, bool sobol, int64_t start, int64_t
           e = launch_ehvi2d(ctx->stream, mu, var, N, N, pl.geo, pl.P, pl.r[0], pl.r[1], pl.s00, pl.s01, pl.mode, vals);
         }
         break;
-      case PLAN_EHVI3D_MC:
-        e = launch_ehvi3d_mc(ctx->stream, mu, var, N, N, pl.geo, pl.M, pl.r, pl.hv, vals, raised);
+      case PLAN_EHVI_MC:
+        e = launch_ehvi_mc(ctx->stream, k, mu, var, N, N, pl.geo, pl.M, pl.r, pl.hv, vals, raised);
         break;
       case PLAN_EHVI_BOXES:
         e = launch_ehvi_boxes(ctx->stream, k, mu, var, N, N, pl.geo, pl.C, pl.boxes, pl.B, vals);
@@ -557,11 +559,6 @@ int omb_debug_set(omb_ctx* ctx, int what, int64_t value) {
     ctx->select_seq = value != 0;
     return OMB_OK;
   }
-  if (what == OMB_DEBUG_POSTERIOR_PERSIST) {
-    if (value != 0 && value != 1) return fail(ctx, OMB_EINVAL, "posterior persist %lld (0 or 1)", (long long)value);
-    ctx->posterior_persist = (int)value;
-    return OMB_OK;
-  }
   if (what == OMB_DEBUG_CHOL_MODE) {
     if ((value & 3) == 3 || value < 0 || value > 6)
       return fail(ctx, OMB_EINVAL, "Cholesky mode %lld (0 auto, 1 per-step launches, 2 one persistent launch; + 4: "
@@ -689,18 +686,25 @@ int omb_ehvi2d(omb_ctx* ctx, const double* mu_dev, const double* var_dev, int64_
   return OMB_OK;
 }
 
+int omb_ehvi_mc(omb_ctx* ctx, int k, const double* mu_dev, const double* var_dev, int64_t ld, int64_t N,
+                const double* cache_dev, int M, const double* r_host, double hv_pf, double* out_dev,
+                int32_t* raised_dev) {
+  int rc = enter(ctx);
+  if (rc) return rc;
+  if ((rc = check_ehvi_mc(ctx, k, M, r_host))) return rc;
+  if ((rc = check_moments(ctx, mu_dev, var_dev, ld, N, k, out_dev))) return rc;
+  if (!cache_dev) return fail(ctx, OMB_EINVAL, "null cache");
+  if (N == 0) return OMB_OK;
+  hipError_t e = launch_ehvi_mc(ctx->stream, k, mu_dev, var_dev, ld, N, cache_dev, M, r_host, hv_pf, out_dev,
+                                raised_dev);
+  if (e != hipSuccess) return hip_fail(ctx, e, "ehvi_mc");
+  return OMB_OK;
+}
+
 int omb_ehvi3d_mc(omb_ctx* ctx, const double* mu_dev, const double* var_dev, int64_t ld, int64_t N,
                   const double* cache_dev, int M, const double* r_host, double hv_pf, double* out_dev,
                   int32_t* raised_dev) {
-  int rc = enter(ctx);
-  if (rc) return rc;
-  if ((rc = check_moments(ctx, mu_dev, var_dev, ld, N, 3, out_dev))) return rc;
-  if (!cache_dev) return fail(ctx, OMB_EINVAL, "null cache");
-  if ((rc = check_ehvi3d(ctx, M, r_host))) return rc;
-  if (N == 0) return OMB_OK;
-  hipError_t e = launch_ehvi3d_mc(ctx->stream, mu_dev, var_dev, ld, N, cache_dev, M, r_host, hv_pf, out_dev, raised_dev);
-  if (e != hipSuccess) return hip_fail(ctx, e, "ehvi3d_mc");
-  return OMB_OK;
+  return omb_ehvi_mc(ctx, 3, mu_dev, var_dev, ld, N, cache_dev, M, r_host, hv_pf, out_dev, raised_dev);
 }
 
 int omb_ehvi_boxes(omb_ctx* ctx, int k, const double* mu_dev, const double* var_dev, int64_t ld, int64_t N,
@@ -809,26 +813,30 @@ int omb_plan_ehvi2d(omb_ctx* ctx, const double* pf_sorted_host, int P, const dou
   return OMB_OK;
 }
 
-int omb_plan_ehvi3d_mc(omb_ctx* ctx, const double* cache_host, int M, const double* r_host, double hv_pf) {
+int omb_plan_ehvi_mc(omb_ctx* ctx, int k, const double* cache_host, int M, const double* r_host, double hv_pf) {
   void* h = nullptr;
   int rc = enter(ctx);
   if (rc) return rc;
   ctx->plan = Plan();
-  if ((rc = check_ehvi3d(ctx, M, r_host))) return rc;
+  if ((rc = check_ehvi_mc(ctx, k, M, r_host))) return rc;
   if (!cache_host) return fail(ctx, OMB_EINVAL, "null cache");
-  const size_t bytes = sizeof(double) * 3 * (size_t)M;
+  const size_t bytes = sizeof(double) * (size_t)k * M;
   if ((rc = plan_begin(ctx, bytes, &h))) return rc;
   memcpy(h, cache_host, bytes);
   if ((rc = stage_to_geo(ctx, bytes))) return rc;
   Plan pl;
-  pl.kind = PLAN_EHVI3D_MC;
-  pl.k = 3;
+  pl.kind = PLAN_EHVI_MC;
+  pl.k = k;
   pl.M = M;
-  for (int j = 0; j < 3; ++j) pl.r[j] = r_host[j];
+  for (int j = 0; j < k; ++j) pl.r[j] = r_host[j];
   pl.hv = hv_pf;
   pl.geo = static_cast<const double*>(ctx->geo);
   ctx->plan = pl;
   return OMB_OK;
+}
+
+int omb_plan_ehvi3d_mc(omb_ctx* ctx, const double* cache_host, int M, const double* r_host, double hv_pf) {
+  return omb_plan_ehvi_mc(ctx, 3, cache_host, M, r_host, hv_pf);
 }
 
 int omb_plan_ehvi_boxes(omb_ctx* ctx, int k, const double* coords_host, int C, const uint16_t* boxes_host, int B) {

@@ -37,7 +37,6 @@ struct GPArgs {
   ExpCoef ec;      // exp_nonpos coefficients as kernel arguments (set by launch_posterior)
   int* fault;      // context fault word (pinned host memory): bit 0 = an LDS-counter wait ran out
   int spin_limit;  // polls per LDS-counter wait before the fault word is marked
-  int persist;     // OMB_DEBUG_POSTERIOR_PERSIST: 1 = the persistent ring (posterior_persist_kernel) where it applies
 };
 
 constexpr int kFaultSpin = 1;          // fault word bit: posterior counter-ring wait exhausted
@@ -77,9 +76,8 @@ hipError_t launch_ehvi2d(hipStream_t stream, const double* mu, const double* var
                          const double* pf, int P, double r0, double r1, double s00, double s01, int mode,
                          double* out);
 
-hipError_t launch_ehvi3d_mc(hipStream_t stream, const double* mu, const double* var, int64_t ld, int64_t N,
-                            const double* cache, int M, const double* r, double hv_pf, double* out,
-                            int32_t* raised);
+hipError_t launch_ehvi_mc(hipStream_t stream, int k, const double* mu, const double* var, int64_t ld, int64_t N,
+                          const double* cache, int M, const double* r, double hv_pf, double* out, int32_t* raised);
 
 hipError_t launch_ehvi_boxes(hipStream_t stream, int k, const double* mu, const double* var, int64_t ld, int64_t N,
                              const double* coords, int C, const uint16_t* boxes, int B, double* out);

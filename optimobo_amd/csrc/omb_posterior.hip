@@ -1054,321 +1054,6 @@ __global__ __launch_bounds__(64 * NW, WPE) void posterior_kernel(GPArgs args, co
   OMB_POST_TRACE(4);
 }
 
-// ----------------------------------------------------------------------------- posterior, persistent ring
-// posterior_kernel's counter ring without workgroup boundaries.  Each workgroup stays resident
-// and takes units u = blockIdx.x, + gridDim.x, … of the n_obj × ⌈N/BN⌉ (objective-major) candidate blocks; the
-// ring's chunks are numbered across units, so a wave generates the next unit's first chunks while the current
-// unit's last chunks are multiplied, and no workgroup pays a prologue (exp table, candidate coordinates, counter
-// init), a pipeline fill and drain, or a final barrier per block.
-//   * Ring: slot c mod 3 holds chunk c; ready[s] / done[s] count wave arrivals monotonically, so chunk c is ready
-//     when ready[c mod 3] ≥ NW·(⌊c/3⌋ + 1) (no resets).  Every wait is bounded as in posterior_kernel.
-//   * Generation state per wave (the unit being generated): the B fragments of its candidate tile, loaded straight
-//     from X* (each lane the ⌈(d+2)/4⌉ dimensions its fragment slots need, divided by ℓ as GPy does; ‖x*/ℓ‖² by two
-//     xor-shuffles), the next unit's coordinates loaded during the current unit's last chunk; μ accumulates as
-//     before and the wave's partial goes to red_mu[unit & 1] at the unit's last chunk.
-//   * Multiply state per wave (the unit being multiplied): the row-tile slots of its objective, the accumulators.
-//     At the unit's last chunk the wave's σ² partials go to red_s[unit & 1] and it takes an LDS ticket; the last
-//     of the NW waves sums the partials in wave order (the fixed order of posterior_kernel's epilogue: bitwise the
-//     same μ, σ² for d ≤ 8 — at d > 8 ‖x*/ℓ‖² sums per lane group) and stores μ, σ².  A unit's reduction buffers
-//     are reused two units later; the ring keeps every wave within two chunks of the slowest, so with Q ≥ 2
-//     chunks per unit the reuse never overtakes a pending reduction.
-// Requires every objective to have the same number of row tiles (R) and Q = ⌈R/4⌉ ≥ 2 (n > 64).
-template <int RT, int CT, int DP, int KIND, int NW = 8>
-__global__ __launch_bounds__(64 * NW, NW / 4) void posterior_persist_kernel(GPArgs args, const double* __restrict__ Xc,
-                                                                            int64_t N, int n_obj, int64_t nblk,
-                                                                            double* __restrict__ mu_out,
-                                                                            double* __restrict__ var_out) {
-  constexpr int NT = 64 * NW;
-  constexpr int G = NW / 4;
-  constexpr int BN = 16 * CT;
-  constexpr int KS = kChunkRows / 4;
-  constexpr int CHUNK = kChunkRows * BN;
-  constexpr bool kAug = DP <= 8;
-  constexpr int KSD = kAug ? (DP + 5) / 4 : (DP + 3) / 4;
-  constexpr int KSDP = ((DP + 5) / 4 + 1) / 2;
-  constexpr int TPC = 4 * CT;
-  constexpr int TPW = TPC >= NW ? TPC / NW : 1;
-  static_assert(NW % CT == 0 && (TPC % NW == 0 || NW % TPC == 0), "tile deal");
-  constexpr bool kTab256 = KIND == OMB_KERNEL_MATERN52;
-  constexpr int kTabN = kTab256 ? 256 : 64;
-  __shared__ double ring[3 * CHUNK];
-  __shared__ double etab[kTabN];
-  __shared__ double red_s[2][NW * BN];
-  __shared__ double red_mu[2][NW * 16];
-  __shared__ int ctr[8];                      // ready[3], done[3], tickets[2]
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t U = (int64_t)n_obj * nblk;
-  const int64_t G_wg = gridDim.x;
-  const int64_t nu = ((int64_t)blockIdx.x < U) ? (U - blockIdx.x + G_wg - 1) / G_wg : 0;
-  const int R = args.gp[0].R;
-  const int Q = (R + 3) >> 2;
-  const int64_t C = nu * Q;
-  for (int i = tid; i < kTabN; i += NT) etab[i] = kTab256 ? kExp2Tab256[i] : kExp2Tab64[i];
-  if (tid < 8) ctr[tid] = 0;
-  __syncthreads();
-  if (C == 0) return;
-  int* ready = ctr;
-  int* done = ctr + 3;
-  int* ticket = ctr + 6;
-
-  // ---- ring hand-offs (posterior_kernel's, with monotonic counters)
-  auto signal = [&](int* c) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (lane == 0) __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  };
-  const int spin_limit = args.spin_limit;
-  auto wait_ge = [&](int* c, int target) {
-    if (lane == 0) {
-      for (int spin = 0;; ++spin) {
-        if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
-        if (spin >= spin_limit) {
-          if (args.fault) __hip_atomic_store(args.fault, kFaultSpin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  };
-
-  // ---- generation state (the unit being generated)
-  const int mg_ct = wave % CT;
-  double bfr[KSD], raw[KSD];
-  double csq_m = 0.0, mu_part = 0.0;
-  int gen_obj = 0;
-  auto unit_of = [&](int64_t i, int& obj, int64_t& c0) {
-    const int64_t u = blockIdx.x + i * G_wg;
-    obj = (int)(u / nblk);
-    c0 = (u - (int64_t)obj * nblk) * BN;
-  };
-  auto load_raw = [&](int64_t i) {
-    int obj;
-    int64_t c0;
-    unit_of(i, obj, c0);
-    const int64_t ci = min(c0 + 16 * mg_ct + (lane & 15), N - 1);
-#pragma unroll
-    for (int s = 0; s < KSD; ++s) {
-      const int j = 4 * s + (lane >> 4);
-      raw[s] = (j < args.d) ? Xc[ci * args.d + j] : 0.0;
-    }
-  };
-  auto start_gen_unit = [&](int64_t i) {
-    int64_t c0;
-    unit_of(i, gen_obj, c0);
-    const double* ls = args.gp[gen_obj].ls;
-    double xs[KSD], s2 = 0.0;
-#pragma unroll
-    for (int s = 0; s < KSD; ++s) {
-      const int j = 4 * s + (lane >> 4);
-      xs[s] = (j < args.d) ? raw[s] / ls[j] : 0.0;      // GPy divides by ℓ
-      s2 = fma(xs[s], xs[s], s2);
-    }
-    s2 += __shfl_xor(s2, 16);
-    s2 += __shfl_xor(s2, 32);
-    csq_m = s2;
-#pragma unroll
-    for (int s = 0; s < KSD; ++s) {
-      const int j = 4 * s + (lane >> 4);
-      bfr[s] = kAug ? ((j < args.d) ? -2.0 * xs[s] : (j == args.d ? 1.0 : (j == args.d + 1 ? s2 : 0.0))) : xs[s];
-    }
-    mu_part = 0.0;
-  };
-  // chunk (unit i, kc) into ring slot `slot` (cursors are advanced by the caller: no 64-bit divisions per chunk)
-  auto gen_chunk = [&](int64_t i, int kc, int slot) {
-    if (kc == 0) start_gen_unit(i);
-    if (kc == Q - 1 && i + 1 < nu) load_raw(i + 1);     // the next unit's coordinates, in flight from here
-    const GPDev& g = args.gp[gen_obj];
-    double* buf = ring + slot * CHUNK;
-    const double pm[3] = {g.variance, kSqrt5 * g.variance, kFiveThirds * g.variance};
-    if (!(NW > TPC && (wave / TPC) != kc % (NW / TPC))) {
-#pragma unroll
-      for (int ti = 0; ti < TPW; ++ti) {
-        const int u = (NW > TPC) ? wave % TPC : wave + NW * ti;
-        const int t = u / CT;
-        const int rowbase = kc * kChunkRows + 16 * t;
-        const d2* xa = reinterpret_cast<const d2*>(g.Xf + (int64_t)(4 * kc + t) * (KSDP * 128) + 2 * lane);
-        d2 a[(KSD + 1) / 2];
-#pragma unroll
-        for (int p = 0; p < (KSD + 1) / 2; ++p) a[p] = xa[64 * p];
-        d4 cr = d4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int s = 0; s < KSD; ++s)
-          cr = __builtin_amdgcn_mfma_f64_16x16x4f64((s & 1) ? a[s >> 1].y : a[s >> 1].x, bfr[s], cr, 0, 0, 0);
-#pragma unroll
-        for (int e = 0; e < 4; e += 2) {
-          const int k0 = rowbase + 4 * e + (lane >> 4), k1 = k0 + 4;
-          double v0, v1;
-          const double r2a = kAug ? cr[e] : fma(-2.0, cr[e], g.xsq[k0] + csq_m);
-          const double r2b = kAug ? cr[e + 1] : fma(-2.0, cr[e + 1], g.xsq[k1] + csq_m);
-          if constexpr (kTab256)
-            matern_r2_tab256_x2(r2a, r2b, pm, args.ec, etab, v0, v1);
-          else
-            kernel_of_r2_tab_x2<KIND>(r2a, r2b, pm, args.ec, etab, v0, v1);
-          if constexpr (!kAug) {
-            v0 = (k0 < g.n) ? v0 : 0.0;
-            v1 = (k1 < g.n) ? v1 : 0.0;
-          }
-          mu_part = fma(g.alpha[k0], v0, mu_part);
-          mu_part = fma(g.alpha[k1], v1, mu_part);
-          buf[((4 * t + e) * CT + mg_ct) * 64 + lane] = v0;
-          buf[((4 * t + e + 1) * CT + mg_ct) * 64 + lane] = v1;
-        }
-      }
-    }
-    if (kc == Q - 1) {
-      // this wave's μ partial of unit i (lanes l, l^16, l^32, l^48 hold the same candidate)
-      double s = mu_part;
-      s += __shfl_xor(s, 16);
-      s += __shfl_xor(s, 32);
-      if (lane < 16) red_mu[i & 1][wave * 16 + lane] = s;
-    }
-  };
-
-  // ---- multiply state (the unit being multiplied)
-  const int simd = wave & 3, h = wave >> 2;
-  int slot_r[RT], slot_q[RT];
-  __amdgpu_buffer_rsrc_t rsrc_L = lp_rsrc(args.gp[0]);   // the objective's packed L⁻¹ (load_lpair)
-  d4 acc[RT][CT];
-  auto start_mul_unit = [&](int64_t i) {
-    int obj;
-    int64_t c0;
-    unit_of(i, obj, c0);
-    const GPDev& g = args.gp[obj];
-#pragma unroll
-    for (int j = 0; j < RT; ++j) {
-      const int q = 2 * G * (j >> 1) + ((j & 1) ? (2 * G - 1 - h) : h);
-      const int r = 4 * q + ((simd + q) & 3);
-      const bool ok = r < g.R;
-      slot_q[j] = ok ? q : -1;
-      slot_r[j] = ok ? r : 0;
-    }
-    rsrc_L = lp_rsrc(g);
-#pragma unroll
-    for (int j = 0; j < RT; ++j)
-#pragma unroll
-      for (int ct = 0; ct < CT; ++ct) acc[j][ct] = d4{0.0, 0.0, 0.0, 0.0};
-  };
-  auto mul_chunk = [&](int64_t i, int kc, int slot) {
-    if (kc == 0) start_mul_unit(i);
-    const double* buf = ring + slot * CHUNK;
-    int nS[RT];
-#pragma unroll
-    for (int j = 0; j < RT; ++j)
-      nS[j] = (slot_q[j] > kc) ? KS : (slot_q[j] == kc ? 4 * ((slot_r[j] & 3) + 1) : 0);
-    const int P0 = kc * (KS / 2);
-    constexpr int PD = (NW == 8) ? 1 : 0;
-    d2 a_ring[PD + 1][RT];
-    auto load_a = [&](int sp, d2* dst) {
-#pragma unroll
-      for (int j = 0; j < RT; ++j)
-        dst[j] = load_lpair(rsrc_L, lane, slot_r[j], P0 + sp);
-    };
-#pragma unroll
-    for (int p = 0; p < PD; ++p) load_a(p, a_ring[p]);
-#pragma unroll
-    for (int sp = 0; sp < KS / 2; ++sp) {
-      if (sp + PD < KS / 2) load_a(sp + PD, a_ring[(sp + PD) % (PD + 1)]);
-      const d2* a_cur = a_ring[sp % (PD + 1)];
-      double b0[CT], b1[CT];
-#pragma unroll
-      for (int ct = 0; ct < CT; ++ct) {
-        b0[ct] = buf[((2 * sp) * CT + ct) * 64 + lane];
-        b1[ct] = buf[((2 * sp + 1) * CT + ct) * 64 + lane];
-      }
-#pragma unroll
-      for (int j = 0; j < RT; ++j) {
-        if (2 * sp < nS[j]) {
-#pragma unroll
-          for (int ct = 0; ct < CT; ++ct) {
-            acc[j][ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(a_cur[j].x, b0[ct], acc[j][ct], 0, 0, 0);
-            acc[j][ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(a_cur[j].y, b1[ct], acc[j][ct], 0, 0, 0);
-          }
-        }
-      }
-    }
-    if (kc == Q - 1) {
-      // unit i done for this wave: σ² partials, then the last of the NW waves reduces and stores
-      const int p = (int)(i & 1);
-#pragma unroll
-      for (int ct = 0; ct < CT; ++ct) {
-        double s = 0.0;
-#pragma unroll
-        for (int j = 0; j < RT; ++j)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) s = fma(acc[j][ct][e], acc[j][ct][e], s);
-        s += __shfl_xor(s, 16);
-        s += __shfl_xor(s, 32);
-        if (lane < 16) red_s[p][wave * BN + ct * 16 + lane] = s;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      int old = 0;
-      if (lane == 0) old = __hip_atomic_fetch_add(&ticket[p], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      old = __builtin_amdgcn_readfirstlane(old);
-      if (old == NW - 1) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        int obj;
-        int64_t c0;
-        unit_of(i, obj, c0);
-        const double variance = args.gp[obj].variance;
-        for (int cl = lane; cl < BN; cl += 64) {
-          double s = 0.0;
-#pragma unroll
-          for (int w = 0; w < NW; ++w) s += red_s[p][w * BN + cl];
-          double m = 0.0;
-          for (int w = cl >> 4; w < NW; w += CT) m += red_mu[p][w * 16 + (cl & 15)];
-          const int64_t cc = c0 + cl;
-          if (cc < N) {
-            mu_out[(int64_t)obj * N + cc] = m;
-            var_out[(int64_t)obj * N + cc] = variance - s;
-          }
-        }
-        if (lane == 0) __hip_atomic_store(&ticket[p], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-    }
-  };
-
-  // ---- the ring over the workgroup's chunks.  Cursors: the multiplied chunk c (unit mi, chunk mk, slot ms, round mr:
-  // ready[ms] reaches NW·(mr + 1) when every wave has generated it), chunk c − 1 (slot ps, round pr) and the
-  // generated chunk c + 2 (unit gi, chunk gk) — all advanced incrementally.
-  int64_t gi = 0, mi = 0;
-  int gk = 0, mk = 0;
-  auto adv = [&](int64_t& ui, int& kk) {
-    if (++kk == Q) {
-      kk = 0;
-      ++ui;
-    }
-  };
-  load_raw(0);
-  gen_chunk(gi, gk, 0);
-  adv(gi, gk);
-  signal(&ready[0]);
-  if (C > 1) {
-    gen_chunk(gi, gk, 1);
-    adv(gi, gk);
-    signal(&ready[1]);
-  }
-  int ms = 0, mr = 0, ps = 2, pr = -1;
-  for (int64_t c = 0; c < C; ++c) {
-    wait_ge(&ready[ms], NW * (mr + 1));
-    mul_chunk(mi, mk, ms);
-    adv(mi, mk);
-    signal(&done[ms]);
-    if (c + 2 < C) {
-      if (c >= 1) wait_ge(&done[ps], NW * (pr + 1));   // slot ps held chunk c − 1; chunk c + 2 goes there
-      gen_chunk(gi, gk, ps);
-      adv(gi, gk);
-      signal(&ready[ps]);
-    }
-    ps = ms;
-    pr = mr;
-    if (++ms == 3) {
-      ms = 0;
-      ++mr;
-    }
-  }
-}
-
 // ----------------------------------------------------------------------------- posterior, n ≤ 256
 // Whole-tile variant for small training sets (BASELINE configs 2 and 4): the complete K* tile of the
 // workgroup (16·RMAX rows × BN = 16·CT candidates, 64 KiB) is generated into LDS in one pass, one
@@ -1816,13 +1501,6 @@ static dim3 reg_grid(int64_t N, int n_obj, int NW = 8, int per_cu = 2) {
 }
 
 // ----------------------------------------------------------------------------- dispatch
-// posterior_persist_kernel numbers its ring's chunks with one Q for every objective
-static bool same_R(const GPArgs& args, int n_obj) {
-  for (int o = 1; o < n_obj; ++o)
-    if (args.gp[o].R != args.gp[0].R) return false;
-  return true;
-}
-
 template <int DP, int KIND>
 static hipError_t launch_posterior_dp(hipStream_t stream, const GPArgs& args, int n_obj, int max_R,
                                       const double* Xc, int64_t N, double* mu, double* var) {
@@ -1848,26 +1526,6 @@ static hipError_t launch_posterior_dp(hipStream_t stream, const GPArgs& args, in
     // profiles/r02_v11_ablate_c2.txt)
     dim3 grid((unsigned)((N + 63) / 64), n_obj);
     hipLaunchKernelGGL((posterior_tile_kernel<8, 4, DP, KIND>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var);
-  } else if (args.persist && RTneed <= 4 && DP <= 32 && same_R(args, n_obj)) {
-    // the persistent ring (posterior_persist_kernel): resident workgroups, chunks numbered across candidate blocks.
-    // Its B fragments stay in registers, so the shapes that stage candidates in LDS in posterior_kernel (RT 8, and
-    // DP 64 at RT 4) would spill here: those keep posterior_kernel.
-    const int64_t BNp = RTneed <= 2 ? 32 : 64;
-    const int64_t nblk = (N + BNp - 1) / BNp;
-    auto go = [&](auto kern) {
-      int occ = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, kBlockThreads, 0) != hipSuccess || occ < 1) occ = 1;
-      const int64_t want = (int64_t)occ * device_cu_count();
-      const int64_t units = nblk * n_obj;
-      hipLaunchKernelGGL(kern, dim3((unsigned)std::min(want, units)), dim3(kBlockThreads), 0, stream, args, Xc, N, n_obj,
-                         nblk, mu, var);
-    };
-    if constexpr (DP <= 32) {
-      if (RTneed <= 2)
-        go(posterior_persist_kernel<2, 2, DP, KIND>);
-      else
-        go(posterior_persist_kernel<4, 4, DP, KIND>);
-    }
   } else if (RTneed <= 2) {
     // 128 < n ≤ 256: 32-candidate blocks on the counter ring (48 KiB, several workgroups per CU);
     // tools/ablate at n = 256, 3 objectives, 2^17 candidates: 0.709 ms (CT 4, barrier) → 0.641 ms;

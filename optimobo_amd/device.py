@@ -79,7 +79,7 @@ class AcqContext:
         code = {"spin_limit": _lib.DEBUG_SPIN_LIMIT, "cov_table": _lib.DEBUG_COV_TABLE,
                 "fused_chain": _lib.DEBUG_FUSED_CHAIN, "argmax_passes": _lib.DEBUG_ARGMAX_PASSES,
                 "chol_mode": _lib.DEBUG_CHOL_MODE, "timing_stride": _lib.DEBUG_TIMING_STRIDE,
-                "posterior_persist": _lib.DEBUG_POSTERIOR_PERSIST, "cov_fused": _lib.DEBUG_COV_FUSED,
+                "cov_fused": _lib.DEBUG_COV_FUSED,
                 "select_seq": _lib.DEBUG_SELECT_SEQ}[what]
         self._check(self.lib.omb_debug_set(self._h, code, int(value)), "omb_debug_set")
 
@@ -151,6 +151,21 @@ class AcqContext:
         self._check(self.lib.omb_ehvi2d(self._h, _ptr(mu), _ptr(var), mu.stride(0), N, _ptr(pf), pf.shape[0],
                                         _lib.darr(r), float(s00), float(s01), m, _ptr(out)), "omb_ehvi2d")
         return out
+
+    def ehvi_mc(self, mu, var, cache, r, hv_pf, out=None, raised=None):
+        """EHVI_3D's Monte-Carlo form over k = cache.shape[1] objectives (rows 0..k-1 of mu/var):
+        (values (N,), raised (N,) int32); NaN and raised = 1 where pygmo would raise."""
+        N = mu.shape[1]
+        cache = _dev_f64(cache, self.device)
+        if cache.dim() != 2 or not 2 <= cache.shape[1] <= mu.shape[0] or len(r) != cache.shape[1]:
+            raise ValueError(f"ehvi_mc: cache {tuple(cache.shape)}, r of {len(r)}, mu {tuple(mu.shape)} disagree on k")
+        out = out if out is not None else torch.empty(N, dtype=torch.float64, device=self.device)
+        raised = raised if raised is not None else torch.empty(N, dtype=torch.int32, device=self.device)
+        self._stream()
+        self._check(self.lib.omb_ehvi_mc(self._h, cache.shape[1], _ptr(mu), _ptr(var), mu.stride(0), N, _ptr(cache),
+                                         cache.shape[0], _lib.darr(r), float(hv_pf), _ptr(out), _ptr(raised)),
+                    "omb_ehvi_mc")
+        return out, raised
 
     def ehvi3d_mc(self, mu, var, cache, r, hv_pf, out=None, raised=None):
         N = mu.shape[1]
@@ -238,6 +253,13 @@ class AcqContext:
         pf = np.ascontiguousarray(pf_sorted, dtype=np.float64).reshape(-1, 2)
         m = {"reference": _lib.EHVI_REFERENCE, "textbook": _lib.EHVI_TEXTBOOK, "sigma": _lib.EHVI_SIGMA}[mode]
         self._plan("omb_plan_ehvi2d", _lib.host_ptr(pf), pf.shape[0], _lib.darr(r), float(s00), float(s01), m)
+
+    def plan_ehvi_mc(self, cache, r, hv_pf):
+        """EHVI_3D's Monte-Carlo form for k = cache.shape[1] objectives (cache (M, k), r (k,))."""
+        c = np.ascontiguousarray(cache, dtype=np.float64)
+        if c.ndim != 2 or len(r) != c.shape[1]:
+            raise ValueError(f"plan_ehvi_mc: cache {c.shape} and r of {len(r)} disagree on k")
+        self._plan("omb_plan_ehvi_mc", c.shape[1], _lib.host_ptr(c), c.shape[0], _lib.darr(r), float(hv_pf))
 
     def plan_ehvi3d_mc(self, cache, r, hv_pf):
         c = np.ascontiguousarray(cache, dtype=np.float64).reshape(-1, 3)

@@ -100,8 +100,10 @@ def EHVI(X, models, max_point, PF, cache, mode="reference"):
 def EHVI_3D(X, models, max_point, PF, cache, mode="reference"):
     """util_functions.py:170-214.  One x: float, ValueError where pygmo raises.
 
+    Any number of objectives k = len(models) ≥ 3, as the reference (which calls it for every n_obj != 2,
+    optimisers.py:245-248): the per-sample volume is pygmo's k-D single-point hypervolume.
     mode "reference": the reference's Monte-Carlo form; batch → (values (N,), raised (N,) bool),
-    NaN where the reference would raise.  mode "textbook": the exact EHVI over a box
+    NaN where the reference would raise.  mode "textbook" (k = 3): the exact EHVI over a box
     decomposition (no MC error, never raises); batch → (N,).
     """
     Xb, single = _batch(X)

@@ -9,7 +9,11 @@ TEST INFRASTRUCTURE ONLY — see oracle/__init__.py.
   (≡ util_functions.py:414-517) in closed form; pinned against the
   reference implementation's own output (tests/golden/cells.npz).
 * ``hypervolume`` is the exact dominated volume that ``pygmo.hypervolume(PF).compute(r)``
-  (util_functions.py:198-206) and pymoo's ``HV`` (optimisers.py:216-220) return.
+  (util_functions.py:198-206) and pymoo's ``HV`` (optimisers.py:216-220) return.  k = 2, 3: sweeps;
+  k ≥ 4 (EHVI_3D runs for every n_obj != 2, optimisers.py:245-248): one point is the product
+  Π_j (r_j − p_j) taken left to right (pagmo's single-point volume), a few points inclusion–exclusion
+  over their subsets, more points slices along objective 0 — an algorithm independent of the build's
+  last-objective sweep (optimobo_amd/pareto.py).
 """
 import numpy as np
 
@@ -78,7 +82,36 @@ def hypervolume(pts, r):
             z_next = zs[i + 1] if i + 1 < len(zs) else r[2]
             total += _hv2d(pts[pts[:, 2] <= z][:, :2], r[:2]) * (z_next - z)
         return total
-    raise NotImplementedError("hypervolume: k must be 2 or 3")
+    return _hv_kd(pts, r)
+
+
+def _box(p, r):
+    v = 1.0
+    for j in range(len(r)):
+        v *= r[j] - p[j]
+    return v
+
+
+def _hv_kd(pts, r):
+    """Exact HV for k ≥ 4 of points strictly inside the box."""
+    if len(pts) == 1:
+        return _box(pts[0], r)
+    if len(pts) <= 10:
+        total = 0.0
+        n = len(pts)
+        for mask in range(1, 1 << n):
+            idx = [i for i in range(n) if mask >> i & 1]
+            corner = np.max(pts[idx], axis=0)            # the intersection of the boxes [p_i, r]
+            total += (1.0 if len(idx) % 2 else -1.0) * _box(corner, r)
+        return total
+    # slice along objective 0: between consecutive levels, the (k-1)-D HV of the points at or below
+    xs = np.unique(pts[:, 0])
+    total = 0.0
+    for i, x in enumerate(xs):
+        x_next = xs[i + 1] if i + 1 < len(xs) else r[0]
+        sub = pts[pts[:, 0] <= x][:, 1:]
+        total += (x_next - x) * (hypervolume(sub, r[1:]) if sub.shape[1] >= 2 else r[1] - sub[:, 0].min())
+    return total
 
 
 def _hv2d(pts, r):

@@ -20,7 +20,7 @@ util_functions.py:410, emo.py:220); it is aliased to ``np.prod``.
 GP posterior fixtures come from scikit-learn's GaussianProcessRegressor (independent of
 both GPy and this build) with the reference's kernel (Matern-5/2 ARD, noise 0 + 1e-8).
 
-Usage:  python tests/golden/make_golden.py [ei_ext] [turbo] [cparego]
+Usage:  python tests/golden/make_golden.py [ei_ext] [turbo] [cparego] [ehvi_kd] ...
 """
 import os
 import sys
@@ -216,6 +216,64 @@ def make_ehvi3d_pos(rng, uf, seed=1):
     np.savez_compressed(os.path.join(HERE, "ehvi3d_pos.npz"), pf=pf, r=r, cache=cache, mu=mu, var=var,
                         hv_pf=opareto.hypervolume(pf, r), ehvi_reference=ref, raises=raises,
                         cache_seed=np.int64(seed))
+
+
+def make_ehvi_mc_kd(rng, uf, k, seed=1):
+    """EHVI_3D (util_functions.py:170-214) at k ≥ 4 objectives — the reference calls it for every n_obj != 2
+    (optimisers.py:245-248) and its per-sample volume is the k-D ``hypervolume([s]).compute(r)`` (:205-206;
+    the 3-term product of :204 is overwritten).  The double's k-D HV is oracle.pareto.hypervolume (single
+    point: Π_j (r_j − s_j) left to right; a front: inclusion–exclusion / slicing).  Means pulled towards the
+    ideal corner so most values are positive; the first 4 candidates beyond r (every sample raises), 4 more
+    with a wide σ²₀ (some samples leave the box)."""
+    cache = cached_samples(k, 5, seed=seed)
+    pf = random_pf(rng, 9, k=k)
+    r = pf.max(axis=0) + 0.3
+    N = 64
+    lam = rng.uniform(0.2, 1.0, N)
+    mu = (pf[rng.integers(0, len(pf), N)].T * lam) + rng.normal(0, 0.02, (k, N))
+    var = np.vstack([10 ** rng.uniform(-5, -2.2, N) for _ in range(k)])
+    mu[:, :4] = r[:, None] + 0.05
+    var[0, 4:8] = 0.5
+    ref = np.full(N, np.nan)
+    raises = np.zeros(N, bool)
+    for i in range(N):
+        models = [ConstModel(mu[j, i], var[j, i]) for j in range(k)]
+        try:
+            ref[i] = uf.EHVI_3D(np.zeros(3), models, r, pf, cache)
+        except ValueError:
+            raises[i] = True
+    print(f"  ehvi_mc_k{k}: P={len(pf)} positive {np.mean(ref > 0):.3f} raises {raises.mean():.3f}")
+    np.savez_compressed(os.path.join(HERE, f"ehvi_mc_k{k}.npz"), pf=pf, r=r, cache=cache, mu=mu, var=var,
+                        hv_pf=opareto.hypervolume(pf, r), ehvi_reference=ref, raises=raises,
+                        cache_seed=np.int64(seed))
+
+
+def make_expdec_k4(rng, uf, sc, k=4):
+    """expected_decomposition (util_functions.py:285-327) with all 12 scalarisations at k = 4 objectives
+    (the reference's scalarisations take any k, scalarisations.py:17-27)."""
+    names = ["WeightedSum", "Tchebicheff", "AugmentedTchebicheff", "ModifiedTchebicheff",
+             "ExponentialWeightedCriterion", "WeightedNorm", "WeightedPower", "WeightedProduct",
+             "PBI", "IPBI", "QPBI", "APD"]
+    cache = cached_samples(k, 5, seed=0)
+    ideal = np.zeros(k)
+    mx = np.array([700.0, 12.0, 5.0, 40.0])
+    w = np.array([0.1, 0.4, 0.3, 0.2])
+    N = 48
+    mu = np.vstack([rng.uniform(0, 1.0, N) * mx[j] for j in range(k)])
+    var = np.vstack([10 ** rng.uniform(-4, 0.5, N) * mx[j] for j in range(k)])
+    out = {"cache": cache, "ideal": ideal, "max": mx, "mu": mu, "var": var, "w": w}
+    for name in names:
+        s = getattr(sc, name)(ideal, mx)
+        ys = np.column_stack([rng.uniform(0, 1, 16) * mx[j] for j in range(k)])
+        agg_min = np.min([s(y, w) for y in ys])
+        vals = np.empty(N)
+        with np.errstate(all="ignore"):
+            for i in range(N):
+                models = [ConstModel(mu[j, i], var[j, i]) for j in range(k)]
+                vals[i] = uf.expected_decomposition(np.zeros(2), models, w, s, agg_min, cache)
+        out[f"{name}_min"] = np.float64(agg_min)
+        out[name] = vals
+    np.savez_compressed(os.path.join(HERE, f"expdec_k{k}.npz"), **out)
 
 
 def make_ehvi3d_c4(uf, n_pick=512):
@@ -848,6 +906,10 @@ def main():
     if not only or "ehvi_pos" in only:
         make_ehvi2d_pos(np.random.default_rng(20261019), uf)
         make_ehvi3d_pos(np.random.default_rng(20261020), uf)
+    if not only or "ehvi_kd" in only:
+        for k in (4, 5, 8):
+            make_ehvi_mc_kd(np.random.default_rng(20261021 + k), uf, k)
+        make_expdec_k4(np.random.default_rng(20261030), uf, sc)
     print("golden fixtures written to", HERE)
 
 

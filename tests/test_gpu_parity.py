@@ -133,10 +133,11 @@ def test_posterior_small_n_persistent(ctx, n, d, N, n_obj, kernel):
     (130, 6, 5000, 2, "matern52"), (200, 3, 777, 3, "rbf"), (256, 6, 131072, 3, "matern52"),   # RT 2 (config 4)
     (257, 6, 65, 1, "matern52"), (400, 17, 3001, 2, "matern52"), (512, 6, 70001, 2, "matern52"),   # RT 4 (config 3)
     (300, 32, 1000, 1, "rbf"), (256, 30, 33, 2, "matern52")])
-def test_posterior_persistent_ring(ctx, n, d, N, n_obj, kernel):
-    """posterior_persist_kernel (omb_debug_set POSTERIOR_PERSIST): resident workgroups whose LDS ring runs across
-    candidate blocks.  Against the oracle on a sample (whole batch finite) and against posterior_kernel on the same
-    inputs (to rounding: only ‖x*/ℓ‖²'s summation order differs)."""
+def test_posterior_counter_ring_shapes(ctx, n, d, N, n_obj, kernel):
+    """n > 128: posterior_kernel's counter ring at RT 2 (config 4's shape) and RT 4 (config 3's), ragged batches and
+    n_var up to 32; against the oracle on a sample, the whole batch finite, and deterministic call to call.  (Round 5's
+    persistent-ring variant of this kernel, 2-5% slower at every configuration, is retired: debug knob 7 now fails.)"""
+    from optimobo_amd import _lib
     rng = np.random.default_rng(n + d + N)
     X = rng.uniform(0, 1, (n, d))
     Y = np.column_stack([np.sin(3 * X).sum(1), np.cos(2 * X).prod(1), (X ** 2).sum(1)])[:, :n_obj]
@@ -146,25 +147,16 @@ def test_posterior_persistent_ring(ctx, n, d, N, n_obj, kernel):
     Xc = rng.uniform(0, 1, (N, d))
     Xc[: min(3, N)] = X[: min(3, N)]
     Xd = dev(Xc)
-    mu0, var0 = ctx.posterior(Xd, n_obj=n_obj)
-    ctx.debug_set("posterior_persist", 1)
-    try:
-        mu, var = ctx.posterior(Xd, n_obj=n_obj)
-        mu2, var2 = ctx.posterior(Xd, n_obj=n_obj)
-    finally:
-        ctx.debug_set("posterior_persist", 0)
-    mu, var, mu0, var0 = (t.cpu().numpy() for t in (mu, var, mu0, var0))
-    assert np.array_equal(mu, mu2.cpu().numpy()) and np.array_equal(var, var2.cpu().numpy())   # deterministic
+    mu, var = ctx.posterior(Xd, n_obj=n_obj)
+    mu2, var2 = ctx.posterior(Xd, n_obj=n_obj)
+    assert torch.equal(mu, mu2) and torch.equal(var, var2)
+    mu, var = mu.cpu().numpy(), var.cpu().numpy()
     assert np.isfinite(mu).all() and np.isfinite(var).all()
-    # ‖x*/ℓ‖² is summed per lane group here (sequentially over the dimensions in posterior_kernel): r² differs by an
-    # ulp, and μ = Σ α_k K*_k (|α| up to ~1e3 on these surrogates) by up to ~1e-12 absolute
-    for o in range(n_obj):
-        np.testing.assert_allclose(mu[o], mu0[o], rtol=1e-9, atol=1e-10 * np.sqrt(variances[o]))
-        np.testing.assert_allclose(var[o], var0[o], rtol=1e-9, atol=1e-12 * variances[o])
     idx = np.unique(np.concatenate([np.arange(min(N, 40)), np.arange(max(0, N - 40), N),
                                     rng.choice(N, min(N, 1500), replace=False)]))
     mu_o, var_o = oracle_posterior(X, Y, ls, variances, Xc[idx], kernel=kernel)
     assert_posterior(mu[:, idx], var[:, idx], mu_o, var_o, variances)
+    assert ctx.lib.omb_debug_set(ctx._h, 7, 1) == _lib.OMB_EINVAL
 
 
 @pytest.mark.parametrize("n", [96, 200, 400, 900])   # every posterior dispatch shape (RT 1/2/4/8)

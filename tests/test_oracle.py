@@ -100,6 +100,22 @@ def test_ehvi3d_reference_positive(golden_dir):
     np.testing.assert_allclose(val[ok], z["ehvi_reference"][ok], rtol=1e-10, atol=1e-15)
 
 
+@pytest.mark.parametrize("k", [4, 5, 8])
+def test_ehvi_mc_reference_k_objectives(golden_dir, k):
+    """The reference's EHVI_3D at k = 4, 5, 8 objectives (make_golden.py make_ehvi_mc_kd): the oracle reproduces
+    it, including the raise flags, and the build's k-D front hypervolume (optimobo_amd.pareto, last-objective
+    sweep) agrees with the oracle's (inclusion–exclusion) that the fixture's Sminus came from."""
+    from optimobo_amd import pareto as bpareto
+    z = load(golden_dir, f"ehvi_mc_k{k}.npz")
+    assert z["cache"].shape[1] == k and z["mu"].shape[0] == k
+    val, raises = acq.ehvi3d_reference(z["mu"], z["var"], float(z["hv_pf"]), z["r"], z["cache"])
+    assert np.array_equal(raises, z["raises"])
+    ok = ~z["raises"]
+    assert (z["ehvi_reference"][ok] > 0).sum() >= 20 and z["raises"].sum() >= 4
+    np.testing.assert_allclose(val[ok], z["ehvi_reference"][ok], rtol=1e-10, atol=1e-15)
+    assert abs(bpareto.hypervolume(z["pf"], z["r"]) - float(z["hv_pf"])) <= 1e-12 * float(z["hv_pf"])
+
+
 def test_ehvi3d_reference_config4_workload(golden_dir):
     """The reference's EHVI_3D on BASELINE config 4's bench workload (make_golden.py make_ehvi3d_c4): the
     oracle reproduces it, at least 5% of the values are positive, and bench.setup_problem still builds the
@@ -149,6 +165,15 @@ def test_expected_decomposition(golden_dir, k, cls):
                                          float(z[f"k{k}_{cls.__name__}_min"]))
     ref = z[f"k{k}_{cls.__name__}"]
     np.testing.assert_allclose(got, ref, rtol=1e-10, atol=1e-12)
+
+
+@pytest.mark.parametrize("cls", osc.ALL, ids=lambda c: c.__name__)
+def test_expected_decomposition_k4(golden_dir, cls):
+    z = load(golden_dir, "expdec_k4.npz")
+    s = cls(z["ideal"], z["max"])
+    with np.errstate(all="ignore"):
+        got = acq.expected_decomposition(z["mu"], z["var"], z["cache"], s, z["w"], float(z[f"{cls.__name__}_min"]))
+    np.testing.assert_allclose(got, z[cls.__name__], rtol=1e-10, atol=1e-12)
 
 
 def test_ei(golden_dir):

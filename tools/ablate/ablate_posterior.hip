@@ -64,35 +64,6 @@ float run(const Bench& b, int reps) {
   return ms / reps;
 }
 
-// the persistent ring (posterior_persist_kernel), launched as the library does: occupancy × CUs resident workgroups
-template <int RT, int CT, int DP = 6>
-float run_persist(const Bench& b, int reps) {
-  constexpr int BN = 16 * CT;
-  const int64_t nblk = (b.N + BN - 1) / BN;
-  int occ = 0, dev = 0, cus = 0;
-  CK(hipGetDevice(&dev));
-  CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, posterior_persist_kernel<RT, CT, DP, 0>, 512, 0));
-  if (occ < 1) occ = 1;
-  const int64_t units = nblk * b.n_obj;
-  const dim3 grid((unsigned)std::min<int64_t>((int64_t)occ * cus, units));
-  hipEvent_t e0, e1;
-  CK(hipEventCreate(&e0));
-  CK(hipEventCreate(&e1));
-  hipLaunchKernelGGL((posterior_persist_kernel<RT, CT, DP, 0>), grid, dim3(512), 0, 0, b.a, b.Xc, b.N, b.n_obj,
-                     nblk, b.mu, b.var);
-  CK(hipEventRecord(e0));
-  for (int i = 0; i < reps; ++i)
-    hipLaunchKernelGGL((posterior_persist_kernel<RT, CT, DP, 0>), grid, dim3(512), 0, 0, b.a, b.Xc, b.N,
-                       b.n_obj, nblk, b.mu, b.var);
-  CK(hipEventRecord(e1));
-  CK(hipEventSynchronize(e1));
-  float ms;
-  CK(hipEventElapsedTime(&ms, e0, e1));
-  CK(hipEventDestroy(e0));
-  CK(hipEventDestroy(e1));
-  return ms / reps;
-}
 
 template <int RMAX, int CT, int ABL, int DP = 6>
 float run_tile(const Bench& b, int reps) {
@@ -343,9 +314,7 @@ int main(int argc, char** argv) {
       {"global generation loads (262144)", run<4, 4, 8, 262144>},
       {"default again", run<4, 4, 8, 0>},
       {"global generation loads again", run<4, 4, 8, 262144>},
-      {"persistent ring RT4 CT4", run_persist<4, 4>},
       {"default again", run<4, 4, 8, 0>},
-      {"persistent ring again", run_persist<4, 4>},
       {"global A loads, r04 (131072)", run<4, 4, 8, 131072>},
       {"RT4 CT2 counter ring", run<4, 2, 8, 0>},
       {"tab64 exp (16384)", run<4, 4, 8, 16384>},
@@ -391,7 +360,6 @@ int main(int argc, char** argv) {
       {"RT2 CT2 ring, global generation loads 3", run<2, 2, 8, 262144>},
       {"RT2 CT2 ring, 5 waves/SIMD bound", run<2, 2, 8, 0, 6, 5>},
       {"RT2 CT2 ring, 6 waves/SIMD bound", run<2, 2, 8, 0, 6, 6>},
-      {"persistent ring RT2 CT2", run_persist<2, 2>},
   };
 
 

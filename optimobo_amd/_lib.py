@@ -9,7 +9,9 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liboptimobo_hip.so")
+# OMB_LIB_PATH: another build of the same library (tests/test_asan_host.py loads the host-sanitized build of
+# `make -C optimobo_amd/csrc asan` through it); the in-tree build otherwise
+LIB_PATH = os.environ.get("OMB_LIB_PATH") or os.path.join(HERE, "liboptimobo_hip.so")
 
 OMB_OK, OMB_EINVAL, OMB_EHIP, OMB_ENOMEM, OMB_ESTATE, OMB_EUNSUP, OMB_ENOTPD = 0, -1, -2, -3, -4, -5, -6
 ERROR_NAMES = {OMB_EINVAL: "OMB_EINVAL", OMB_EHIP: "OMB_EHIP", OMB_ENOMEM: "OMB_ENOMEM",

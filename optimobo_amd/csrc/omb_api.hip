@@ -123,17 +123,6 @@ int hip_fail(omb_ctx* ctx, hipError_t e, const char* where) {
     if (e_ != hipSuccess) return hip_fail(ctx, e_, #call);   \
   } while (0)
 
-// Acquisition kernels stage their per-iteration geometry in ≤ 64 KiB of dynamic LDS.
-constexpr int kMaxLdsDoubles = 8192;
-constexpr int kMaxStripes = (kMaxLdsDoubles - 1) / 2;
-
-int pad_dim(int d) {
-  const int opts[] = {2, 4, 6, 8, 16, 32, 64, 128, 256};   // > 64: the wide path (omb_wide.hip)
-  for (int o : opts)
-    if (d <= o) return o;
-  return -1;
-}
-
 // Reports (once) a fault a kernel marked since the last report.
 int check_fault(omb_ctx* ctx) {
   const int f = __atomic_exchange_n(ctx->fault_host, 0, __ATOMIC_ACQ_REL);
@@ -175,92 +164,8 @@ int gather_gp(omb_ctx* ctx, int n_obj, GPArgs* args, int* max_R) {
   return OMB_OK;
 }
 
-int check_moments(omb_ctx* ctx, const double* mu, const double* var, int64_t ld, int64_t N, int k, const double* out) {
-  if (N < 0) return fail(ctx, OMB_EINVAL, "N=%lld < 0", (long long)N);
-  if (N > 0 && (!mu || !var || !out)) return fail(ctx, OMB_EINVAL, "null device pointer");
-  if (k > 1 && ld < N) return fail(ctx, OMB_EINVAL, "ld=%lld < N=%lld", (long long)ld, (long long)N);
-  return OMB_OK;
-}
-
-// ---- geometry validation shared by the per-kernel entry points and the plans
-int check_ehvi2d(omb_ctx* ctx, int P, const double* r, int mode) {
-  // stripes y1[0..P], y2[1..P] are staged in ≤ 64 KiB of LDS
-  if (P < 1 || P > kMaxStripes) return fail(ctx, OMB_EUNSUP, "Pareto front size P=%d outside [1, %d]", P, kMaxStripes);
-  if (!r) return fail(ctx, OMB_EINVAL, "null reference point");
-  if (mode != OMB_EHVI_REFERENCE && mode != OMB_EHVI_TEXTBOOK && mode != OMB_EHVI_SIGMA)
-    return fail(ctx, OMB_EINVAL, "unknown EHVI mode %d", mode);
-  return OMB_OK;
-}
-
-int check_ehvi_mc(omb_ctx* ctx, int k, int M, const double* r) {
-  if (k < 2 || k > OMB_MAX_OBJ) return fail(ctx, OMB_EINVAL, "Monte-Carlo EHVI needs 2 <= k <= %d objectives (k=%d)",
-                                           OMB_MAX_OBJ, k);
-  // the (M, k) cache is staged in <= 64 KiB of dynamic LDS
-  if (M < 1 || (int64_t)k * M > kMaxLdsDoubles)
-    return fail(ctx, OMB_EUNSUP, "cache size M=%d outside [1, %d] for k=%d", M, kMaxLdsDoubles / k, k);
-  if (!r) return fail(ctx, OMB_EINVAL, "null reference point");
-  return OMB_OK;
-}
-
-int check_boxes(omb_ctx* ctx, int k, int C, int B) {
-  if (k != 2 && k != 3) return fail(ctx, OMB_EUNSUP, "exact EHVI needs k = 2 or 3 objectives (k=%d)", k);
-  // grid + 4 per-wave Φ/φ tables must fit the 64 KiB of dynamic LDS
-  if (C < 2 || (size_t)k * C * 9 > (size_t)kMaxLdsDoubles)
-    return fail(ctx, OMB_EUNSUP, "grid size C=%d outside [2, %d] for k=%d", C, kMaxLdsDoubles / (9 * k), k);
-  if (B < 1) return fail(ctx, OMB_EINVAL, "empty box list");
-  return OMB_OK;
-}
-
-int check_ei(omb_ctx* ctx, int kind, int k, double var_eps, double pof_eps) {
-  const bool ok = (kind == OMB_EI_PLAIN && k == 1) || (kind == OMB_EI_PARETO && k == 2) ||
-                  (kind == OMB_EI_CONSTRAINED && k >= 2 && k <= OMB_MAX_OBJ);
-  if (!ok) return fail(ctx, OMB_EINVAL, "EI kind %d does not take k=%d posterior rows", kind, k);
-  if (!(var_eps >= 0.0) || !(pof_eps >= 0.0)) return fail(ctx, OMB_EINVAL, "var_eps/pof_eps must be >= 0");
-  return OMB_OK;
-}
-
-int check_hvpoi(omb_ctx* ctx, int C) {
-  if (C < 1 || 4 * C > kMaxLdsDoubles) return fail(ctx, OMB_EUNSUP, "cell count C=%d outside [1, %d]", C, kMaxLdsDoubles / 4);
-  return OMB_OK;
-}
-
-// Validates an expected_decomposition request and fills its ScalParams.
-int build_scal(omb_ctx* ctx, int k, int M, int scal_id, const double* params_host, const double* weights_host,
-               const double* ideal_host, const double* max_host, double agg_min, ScalParams* out) {
-  if (k < 1 || k > OMB_MAX_OBJ) return fail(ctx, OMB_EINVAL, "k=%d outside [1, %d]", k, OMB_MAX_OBJ);
-  if (M < 1 || k * M > kMaxLdsDoubles)
-    return fail(ctx, OMB_EUNSUP, "cache size M=%d x k=%d exceeds %d doubles of LDS", M, k, kMaxLdsDoubles);
-  if (scal_id < OMB_SCAL_WS || scal_id > OMB_SCAL_APD) return fail(ctx, OMB_EINVAL, "unknown scalarisation %d", scal_id);
-  if (!weights_host || !ideal_host || !max_host) return fail(ctx, OMB_EINVAL, "null weights/ideal/max");
-  ScalParams& sp = *out;
-  memset(&sp, 0, sizeof(sp));
-  sp.id = scal_id;
-  sp.k = k;
-  sp.agg_min = agg_min;
-  double wq = 0.0, rsum = 0.0;
-  for (int i = 0; i < k; ++i) {
-    sp.w[i] = weights_host[i];
-    sp.ideal[i] = ideal_host[i];
-    sp.range[i] = max_host[i] - ideal_host[i];
-    wq += sp.w[i] * sp.w[i];
-    rsum += sp.range[i];
-  }
-  sp.wnorm = sqrt(wq);
-  const int np = (scal_id == OMB_SCAL_QPBI || scal_id == OMB_SCAL_APD) ? 3
-                 : (scal_id == OMB_SCAL_WS || scal_id == OMB_SCAL_TCH || scal_id == OMB_SCAL_WPR) ? 0 : 1;
-  if (np > 0 && !params_host) return fail(ctx, OMB_EINVAL, "scalarisation %d needs %d parameter(s)", scal_id, np);
-  for (int i = 0; i < np; ++i) sp.p[i] = params_host[i];
-  if (scal_id == OMB_SCAL_APD && sp.wnorm == 0.0) {
-    // scalarisations.py:392-393 substitutes 1e-5 weights (the reference then fails for k > 1).
-    for (int i = 0; i < k; ++i) sp.w[i] = 1e-5;
-    sp.wnorm = sqrt(k * 1e-10);
-  }
-  if (scal_id == OMB_SCAL_QPBI) {
-    // scalarisations.py:347: alpha * (1/H * 1/k * Σ(max − ideal))
-    sp.d_star = sp.p[1] * ((1.0 / sp.p[2]) * (1.0 / (double)k) * rsum);
-  }
-  return OMB_OK;
-}
+// The context's error sink for the host-only checks (omb_host.cpp).
+std::string* E(omb_ctx* ctx) { return ctx ? &ctx->err : nullptr; }
 
 // ---- ctx-owned buffers
 int grow_dev(omb_ctx* ctx, void** buf, size_t* cap, size_t bytes, const char* what) {
@@ -577,15 +482,8 @@ int omb_set_gp(omb_ctx* ctx, int obj, int kernel, int n, int d, const double* X_
                double variance, const double* alpha_dev, const double* Linv_dev) {
   int rc = enter(ctx);
   if (rc) return rc;
-  if (obj < 0 || obj >= OMB_MAX_OBJ) return fail(ctx, OMB_EINVAL, "obj=%d outside [0, %d)", obj, OMB_MAX_OBJ);
-  if (kernel != OMB_KERNEL_MATERN52 && kernel != OMB_KERNEL_RBF) return fail(ctx, OMB_EINVAL, "unknown kernel %d", kernel);
-  if (n < 1 || n > OMB_MAX_TRAIN_DENSE)
-    return fail(ctx, OMB_EUNSUP, "n_train=%d outside [1, %d]", n, OMB_MAX_TRAIN_DENSE);
-  if (d < 1 || d > OMB_MAX_DIM) return fail(ctx, OMB_EUNSUP, "n_var=%d outside [1, %d]", d, OMB_MAX_DIM);
-  if (!X_dev || !lengthscale_host || !alpha_dev || !Linv_dev) return fail(ctx, OMB_EINVAL, "null pointer");
-  for (int j = 0; j < d; ++j)
-    if (!(lengthscale_host[j] > 0.0)) return fail(ctx, OMB_EINVAL, "lengthscale[%d]=%g must be > 0", j, lengthscale_host[j]);
-  if (!(variance >= 0.0)) return fail(ctx, OMB_EINVAL, "variance=%g must be >= 0", variance);
+  if ((rc = check_gp_args(E(ctx), obj, kernel, n, d, X_dev, lengthscale_host, variance, alpha_dev, Linv_dev)))
+    return rc;
 
   ObjState& s = ctx->obj[obj];
   // The previous state may still be read by queued kernels.
@@ -676,9 +574,9 @@ int omb_ehvi2d(omb_ctx* ctx, const double* mu_dev, const double* var_dev, int64_
                double* out_dev) {
   int rc = enter(ctx);
   if (rc) return rc;
-  if ((rc = check_moments(ctx, mu_dev, var_dev, ld, N, 2, out_dev))) return rc;
+  if ((rc = check_moments(E(ctx), mu_dev, var_dev, ld, N, 2, out_dev))) return rc;
   if (!pf_sorted_dev) return fail(ctx, OMB_EINVAL, "null Pareto front");
-  if ((rc = check_ehvi2d(ctx, P, r_host, mode))) return rc;
+  if ((rc = check_ehvi2d(E(ctx), P, r_host, mode))) return rc;
   if (N == 0) return OMB_OK;
   hipError_t e = launch_ehvi2d(ctx->stream, mu_dev, var_dev, ld, N, pf_sorted_dev, P, r_host[0], r_host[1], s00, s01,
                                mode, out_dev);
@@ -691,8 +589,8 @@ int omb_ehvi_mc(omb_ctx* ctx, int k, const double* mu_dev, const double* var_dev
                 int32_t* raised_dev) {
   int rc = enter(ctx);
   if (rc) return rc;
-  if ((rc = check_ehvi_mc(ctx, k, M, r_host))) return rc;
-  if ((rc = check_moments(ctx, mu_dev, var_dev, ld, N, k, out_dev))) return rc;
+  if ((rc = check_ehvi_mc(E(ctx), k, M, r_host))) return rc;
+  if ((rc = check_moments(E(ctx), mu_dev, var_dev, ld, N, k, out_dev))) return rc;
   if (!cache_dev) return fail(ctx, OMB_EINVAL, "null cache");
   if (N == 0) return OMB_OK;
   hipError_t e = launch_ehvi_mc(ctx->stream, k, mu_dev, var_dev, ld, N, cache_dev, M, r_host, hv_pf, out_dev,
@@ -711,8 +609,8 @@ int omb_ehvi_boxes(omb_ctx* ctx, int k, const double* mu_dev, const double* var_
                    const double* coords_dev, int C, const uint16_t* boxes_dev, int B, double* out_dev) {
   int rc = enter(ctx);
   if (rc) return rc;
-  if ((rc = check_boxes(ctx, k, C, B))) return rc;
-  if ((rc = check_moments(ctx, mu_dev, var_dev, ld, N, k, out_dev))) return rc;
+  if ((rc = check_boxes(E(ctx), k, C, B))) return rc;
+  if ((rc = check_moments(E(ctx), mu_dev, var_dev, ld, N, k, out_dev))) return rc;
   if (!coords_dev || !boxes_dev) return fail(ctx, OMB_EINVAL, "null grid/box list");
   if (N == 0) return OMB_OK;
   hipError_t e = launch_ehvi_boxes(ctx->stream, k, mu_dev, var_dev, ld, N, coords_dev, C, boxes_dev, B, out_dev);
@@ -724,9 +622,9 @@ int omb_hvpoi(omb_ctx* ctx, const double* mu_dev, const double* var_dev, int64_t
               const double* cells_dev, int C, double* out_dev) {
   int rc = enter(ctx);
   if (rc) return rc;
-  if ((rc = check_moments(ctx, mu_dev, var_dev, ld, N, 2, out_dev))) return rc;
+  if ((rc = check_moments(E(ctx), mu_dev, var_dev, ld, N, 2, out_dev))) return rc;
   if (!cells_dev) return fail(ctx, OMB_EINVAL, "null cells");
-  if ((rc = check_hvpoi(ctx, C))) return rc;
+  if ((rc = check_hvpoi(E(ctx), C))) return rc;
   if (N == 0) return OMB_OK;
   hipError_t e = launch_hvpoi(ctx->stream, mu_dev, var_dev, ld, N, cells_dev, C, out_dev);
   if (e != hipSuccess) return hip_fail(ctx, e, "hvpoi");
@@ -739,8 +637,8 @@ int omb_expdec(omb_ctx* ctx, int k, const double* mu_dev, const double* var_dev,
   int rc = enter(ctx);
   if (rc) return rc;
   ScalParams sp;
-  if ((rc = build_scal(ctx, k, M, scal_id, params_host, weights_host, ideal_host, max_host, agg_min, &sp))) return rc;
-  if ((rc = check_moments(ctx, mu_dev, var_dev, ld, N, k, out_dev))) return rc;
+  if ((rc = build_scal(E(ctx), k, M, scal_id, params_host, weights_host, ideal_host, max_host, agg_min, &sp))) return rc;
+  if ((rc = check_moments(E(ctx), mu_dev, var_dev, ld, N, k, out_dev))) return rc;
   if (!cache_dev) return fail(ctx, OMB_EINVAL, "null cache");
   if (N == 0) return OMB_OK;
   hipError_t e = launch_expdec(ctx->stream, sp, mu_dev, var_dev, ld, N, cache_dev, M, out_dev);
@@ -757,8 +655,8 @@ int omb_ei_ext(omb_ctx* ctx, int kind, int k, const double* mu_dev, const double
                double best, double var_eps, double pof_eps, double* out_dev) {
   int rc = enter(ctx);
   if (rc) return rc;
-  if ((rc = check_ei(ctx, kind, k, var_eps, pof_eps))) return rc;
-  if ((rc = check_moments(ctx, mu_dev, var_dev, ld, N, k, out_dev))) return rc;
+  if ((rc = check_ei(E(ctx), kind, k, var_eps, pof_eps))) return rc;
+  if ((rc = check_moments(E(ctx), mu_dev, var_dev, ld, N, k, out_dev))) return rc;
   if (N == 0) return OMB_OK;
   hipError_t e = launch_ei(ctx->stream, kind, k, mu_dev, var_dev, ld, N, best, var_eps, pof_eps, out_dev);
   if (e != hipSuccess) return hip_fail(ctx, e, "ei");
@@ -793,7 +691,7 @@ int omb_plan_ehvi2d(omb_ctx* ctx, const double* pf_sorted_host, int P, const dou
   int rc = enter(ctx);
   if (rc) return rc;
   ctx->plan = Plan();
-  if ((rc = check_ehvi2d(ctx, P, r_host, mode))) return rc;
+  if ((rc = check_ehvi2d(E(ctx), P, r_host, mode))) return rc;
   if (!pf_sorted_host) return fail(ctx, OMB_EINVAL, "null Pareto front");
   const size_t bytes = sizeof(double) * 2 * (size_t)P;
   if ((rc = plan_begin(ctx, bytes, &h))) return rc;
@@ -818,7 +716,7 @@ int omb_plan_ehvi_mc(omb_ctx* ctx, int k, const double* cache_host, int M, const
   int rc = enter(ctx);
   if (rc) return rc;
   ctx->plan = Plan();
-  if ((rc = check_ehvi_mc(ctx, k, M, r_host))) return rc;
+  if ((rc = check_ehvi_mc(E(ctx), k, M, r_host))) return rc;
   if (!cache_host) return fail(ctx, OMB_EINVAL, "null cache");
   const size_t bytes = sizeof(double) * (size_t)k * M;
   if ((rc = plan_begin(ctx, bytes, &h))) return rc;
@@ -844,7 +742,7 @@ int omb_plan_ehvi_boxes(omb_ctx* ctx, int k, const double* coords_host, int C, c
   int rc = enter(ctx);
   if (rc) return rc;
   ctx->plan = Plan();
-  if ((rc = check_boxes(ctx, k, C, B))) return rc;
+  if ((rc = check_boxes(E(ctx), k, C, B))) return rc;
   if (!coords_host || !boxes_host) return fail(ctx, OMB_EINVAL, "null grid/box list");
   const size_t cbytes = sizeof(double) * (size_t)k * C;
   const size_t bbytes = sizeof(uint16_t) * 2 * (size_t)k * B;
@@ -868,7 +766,7 @@ int omb_plan_hvpoi(omb_ctx* ctx, const double* cells_host, int C) {
   int rc = enter(ctx);
   if (rc) return rc;
   ctx->plan = Plan();
-  if ((rc = check_hvpoi(ctx, C))) return rc;
+  if ((rc = check_hvpoi(E(ctx), C))) return rc;
   if (!cells_host) return fail(ctx, OMB_EINVAL, "null cells");
   const size_t bytes = sizeof(double) * 4 * (size_t)C;
   if ((rc = plan_begin(ctx, bytes, &h))) return rc;
@@ -890,7 +788,7 @@ int omb_plan_expdec(omb_ctx* ctx, int k, const double* cache_host, int M, int sc
   if (rc) return rc;
   ctx->plan = Plan();
   ScalParams sp;
-  if ((rc = build_scal(ctx, k, M, scal_id, params_host, weights_host, ideal_host, max_host, agg_min, &sp))) return rc;
+  if ((rc = build_scal(E(ctx), k, M, scal_id, params_host, weights_host, ideal_host, max_host, agg_min, &sp))) return rc;
   if (!cache_host) return fail(ctx, OMB_EINVAL, "null cache");
   const size_t bytes = sizeof(double) * (size_t)k * M;
   if ((rc = plan_begin(ctx, bytes, &h))) return rc;
@@ -914,7 +812,7 @@ int omb_plan_ei_ext(omb_ctx* ctx, int kind, int k, double best, double var_eps, 
   int rc = enter(ctx);
   if (rc) return rc;
   ctx->plan = Plan();
-  if ((rc = check_ei(ctx, kind, k, var_eps, pof_eps))) return rc;
+  if ((rc = check_ei(E(ctx), kind, k, var_eps, pof_eps))) return rc;
   Plan pl;
   pl.kind = PLAN_EI;
   pl.ei_kind = kind;
@@ -931,11 +829,7 @@ int omb_set_sobol(omb_ctx* ctx, int d, int bits, const uint32_t* sv_host, const 
   int rc = enter(ctx);
   if (rc) return rc;
   ctx->sob_d = 0;
-  if (d < 1 || d > OMB_MAX_DIM) return fail(ctx, OMB_EUNSUP, "Sobol dimension %d outside [1, %d]", d, OMB_MAX_DIM);
-  if (bits < 1 || bits > 32) return fail(ctx, OMB_EUNSUP, "Sobol bits=%d outside [1, 32]", bits);
-  if (!sv_host || !shift_host || !lo_host || !hi_host) return fail(ctx, OMB_EINVAL, "null Sobol state");
-  for (int j = 0; j < d; ++j)
-    if (!(hi_host[j] >= lo_host[j])) return fail(ctx, OMB_EINVAL, "box [%g, %g] of dimension %d is empty", lo_host[j], hi_host[j], j);
+  if ((rc = check_sobol_args(E(ctx), d, bits, sv_host, shift_host, lo_host, hi_host))) return rc;
   const size_t bytes = sobol_state_bytes(d, bits);
   void* h = nullptr;
   if ((rc = stage_begin(ctx, bytes, &h))) return rc;

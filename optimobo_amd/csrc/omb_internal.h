@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "../../include/optimobo_hip.h"
+#include "omb_host.h"
 #include "omb_math.h"
 
 namespace omb {
@@ -85,17 +86,6 @@ hipError_t launch_ehvi_boxes(hipStream_t stream, int k, const double* mu, const 
 hipError_t launch_hvpoi(hipStream_t stream, const double* mu, const double* var, int64_t ld, int64_t N,
                         const double* cells, int C, double* out);
 
-struct ScalParams {
-  int id;
-  int k;
-  double w[OMB_MAX_OBJ];
-  double ideal[OMB_MAX_OBJ];
-  double range[OMB_MAX_OBJ];   // max − ideal
-  double p[4];
-  double wnorm;                // ‖w‖ (PBI family)
-  double d_star;               // QPBI
-  double agg_min;
-};
 
 hipError_t launch_expdec(hipStream_t stream, const ScalParams& sp, const double* mu, const double* var,
                          int64_t ld, int64_t N, const double* cache, int M, double* out);
@@ -112,11 +102,8 @@ hipError_t launch_argmax(hipStream_t stream, const double* vals, int64_t N, int6
 hipError_t launch_argmax_reduce(hipStream_t stream, const double* partials, int nb, int64_t offset, double* result);
 
 // Scrambled Sobol' generation (omb_sobol.hip).  The packed state holds the direction
-// numbers, shift and box of one engine; sobol_pack_state fills a host buffer of
+// numbers, shift and box of one engine; sobol_pack_state (omb_host.cpp) fills a host buffer of
 // sobol_state_bytes(d, bits) that is then copied to the device.
-size_t sobol_state_bytes(int d, int bits);
-void sobol_pack_state(int d, int bits, const uint32_t* sv, const uint32_t* shift, const double* lo,
-                      const double* hi, void* dst);
 hipError_t launch_sobol(hipStream_t stream, const void* state_dev, int d, int bits, int64_t start, int64_t N,
                         double* X);
 

@@ -61,25 +61,6 @@ __global__ __launch_bounds__(kSobolThreads) void sobol_kernel(const uint32_t* __
 
 }  // namespace
 
-size_t sobol_state_bytes(int d, int bits) {
-  const int words = d * bits + d;
-  return (size_t)((words + 1) & ~1) * 4 + (size_t)2 * d * sizeof(double);
-}
-
-void sobol_pack_state(int d, int bits, const uint32_t* sv, const uint32_t* shift, const double* lo,
-                      const double* hi, void* dst) {
-  uint32_t* w = static_cast<uint32_t*>(dst);
-  const int words = d * bits + d;
-  for (int t = 0; t < d * bits; ++t) w[t] = sv[t];
-  for (int t = 0; t < d; ++t) w[d * bits + t] = shift[t];
-  if (words & 1) w[words] = 0;
-  double* f = reinterpret_cast<double*>(w + ((words + 1) & ~1));
-  for (int t = 0; t < d; ++t) {
-    f[t] = lo[t];
-    f[d + t] = hi[t] - lo[t];   // numpy's (hi - lo), rounded once
-  }
-}
-
 hipError_t launch_sobol(hipStream_t stream, const void* state_dev, int d, int bits, int64_t start, int64_t N,
                         double* X) {
   const int64_t total = N * d;

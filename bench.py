@@ -450,7 +450,7 @@ def main():
                          "(default: the library's)")
     ap.add_argument("--argmax-passes", type=int, default=None, choices=[1, 2],
                     help="omb_debug_set(ARGMAX_PASSES): the arg-max as one launch or two (default: the library's, 2)")
-    ap.add_argument("--chol-mode", type=int, default=None, choices=[0, 1, 2, 4, 5, 6],
+    ap.add_argument("--chol-mode", type=int, default=None, choices=[0, 1, 2, 4, 5, 6, 8, 10, 12, 14],
                     help="omb_debug_set(CHOL_MODE): Cholesky auto / per-step launches / one persistent launch; + 4: "
                          "with release-acquire hand-offs")
     ap.add_argument("--cov-fused", type=int, default=None, choices=[0, 1],

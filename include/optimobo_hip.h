@@ -105,7 +105,9 @@ const char* omb_last_error(const omb_ctx* ctx);
  * all but the last min(steps, 32) 64-column steps and one persistent launch for those; else 1), 1 one launch per
  * step, 2 the whole factorisation in one persistent launch; m + 4 runs schedule m with every cross-workgroup hand-off
  * an agent-scope release / acquire pair (the HIP memory model's guarantee; the default form — sc1 payloads, a vmcnt
- * wait and relaxed flags — is measured valid on gfx950), bitwise the same factor as schedule m.
+ * wait and relaxed flags — is measured valid on gfx950), bitwise the same factor as schedule m; m + 8 has the persistent
+ * launch's workers apply every trailing update as its own task instead of batching the far tiles' updates (round 5's
+ * schedule), again bitwise the same factor.
  * omb_debug_set(ctx, OMB_DEBUG_TIMING_STRIDE, s) records omb_timing's events on every s-th chain only (default 1;
  * omb_timing_read then averages over the recorded chains), so that a timed loop carries fewer event records. *
  * Value 7 (round 5's OMB_DEBUG_POSTERIOR_PERSIST, a persistent-ring posterior kernel measured 2-5% slower at every

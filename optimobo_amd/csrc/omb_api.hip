@@ -96,6 +96,7 @@ struct omb_ctx {
   bool argmax_one_pass = false;  // OMB_DEBUG_ARGMAX_PASSES: 1 (one launch) or 2 (default: measured level)
   int chol_mode = kCholAuto;     // OMB_DEBUG_CHOL_MODE (value & 3)
   int chol_acq_rel = 0;          // OMB_DEBUG_CHOL_MODE (value & 4): release / acquire hand-offs
+  int chol_single = 0;           // OMB_DEBUG_CHOL_MODE (value & 8): every trailing update its own task
   bool select_seq = false;       // OMB_DEBUG_SELECT_SEQ: the sequential greedy walk for B ≤ 64 too
 };
 
@@ -465,12 +466,14 @@ int omb_debug_set(omb_ctx* ctx, int what, int64_t value) {
     return OMB_OK;
   }
   if (what == OMB_DEBUG_CHOL_MODE) {
-    if ((value & 3) == 3 || value < 0 || value > 6)
+    if ((value & 3) == 3 || value < 0 || value > 14)
       return fail(ctx, OMB_EINVAL, "Cholesky mode %lld (0 auto, 1 per-step launches, 2 one persistent launch; + 4: "
-                  "release / acquire hand-offs)", (long long)value);
+                  "release / acquire hand-offs; + 8: the persistent launch's trailing updates one task per step)",
+                  (long long)value);
     const int modes[3] = {kCholAuto, kCholBlocked, kCholPersistOnly};
     ctx->chol_mode = modes[value & 3];
     ctx->chol_acq_rel = (value & 4) ? 1 : 0;
+    ctx->chol_single = (value & 8) ? 1 : 0;
     return OMB_OK;
   }
   return fail(ctx, OMB_EINVAL, "unknown debug setting %d", what);
@@ -973,7 +976,7 @@ static int chol_enqueue(omb_ctx* ctx, double* A, int64_t N, int64_t lda, double 
   double* ws = reinterpret_cast<double*>(static_cast<char*>(ctx->ichol) + 16);
   OMB_HIP(ctx, launch_add_diag(ctx->stream, A, N, lda, jitter));
   OMB_HIP(ctx, launch_cholesky_mode(ctx->stream, A, N, lda, dinfo, ws, ctx->chol_mode, ctx->spin_limit,
-                                    ctx->chol_acq_rel));
+                                    ctx->chol_acq_rel, ctx->chol_single));
   OMB_HIP(ctx, hipMemcpyAsync(ctx->info_host, dinfo, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   return OMB_OK;
 }

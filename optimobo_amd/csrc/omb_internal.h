@@ -161,9 +161,11 @@ int64_t chol_ws_doubles(int64_t N);
 hipError_t launch_cholesky(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws,
                            int spin_limit = kDefaultSpinLimit);
 // acq_rel = 1: every cross-workgroup hand-off of the schedule as an agent-scope release / acquire pair (the HIP memory
-// model's form; the default relaxed / sc1 form is measured valid on gfx950 and checked bitwise against this one)
+// model's form; the default relaxed / sc1 form is measured valid on gfx950 and checked bitwise against this one).
+// single_steps = 1: the persistent launch's workers take every trailing update as its own task (round 5's table; the
+// default batches far tiles' updates, bitwise the same factor — checked against this one)
 hipError_t launch_cholesky_mode(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws, int mode,
-                                int spin_limit = kDefaultSpinLimit, int acq_rel = 0);
+                                int spin_limit = kDefaultSpinLimit, int acq_rel = 0, int single_steps = 0);
 // Y (B, N) = μ + Zt Lᵀ (L lower, N×N): row b of Y is the sample μ + L z_b.
 // ws: chol_samples_ws_doubles(N, B) device doubles (split-K partial products; 0 when unsplit).
 int64_t chol_samples_ws_doubles(int64_t N, int B);

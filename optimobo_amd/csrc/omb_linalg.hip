@@ -1225,7 +1225,8 @@ struct CholSync {
   int* cnt;     // [t·t]    updates applied to tile (i, j)
   int* ticket;  // task counter of the worker workgroups
   int* abort;   // set by the first wait that runs out
-  const int* tab;   // the workers' task order (chol_task_table), or null for the step-major arithmetic order
+  const int* tab;   // the workers' tasks in order, (code, steps) pairs (chol_task_table), or null for the
+                    // step-major arithmetic order
 };
 
 // Wave 0 waits (every lane of it, on wave-uniform values) until *p ≥ v: relaxed polls; false after an abort or
@@ -1245,6 +1246,33 @@ __device__ __forceinline__ bool chol_poll_ge(const int* p, int v, const CholSync
                        : 0;
     if (ab != 0 || ++polls > spin_limit) {
       atomicCAS(s.abort, 0, (int)(p - s.wflag) + 1);
+      atomicCAS(info, 0, kCholSpinFault);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  if constexpr (AR) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return true;
+}
+
+// Wave 0 waits until the panel flags of rows i and j are ≥ 4 for every step of [k, k + B) (B ≤ 32): lane 2b + r
+// polls row r's flag of step k + b, one round trip per poll for the whole set (a batch's flags are mostly set long
+// before its task is drawn); the same bound, abort word and AR fence as chol_poll_ge.
+template <bool AR = false>
+__device__ __forceinline__ bool chol_poll_panels(const int* pflag, int t, int i, int j, int k, int B, const CholSync& s,
+                                                 int spin_limit, int* info) {
+  const int lane = threadIdx.x & 63;
+  const bool mine = lane < 2 * B;
+  const int* p = pflag + ((lane & 1) ? j : i) * t + k + (lane >> 1);
+  int polls = 0;
+  for (;;) {
+    const int v = mine ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 4;
+    if (__builtin_amdgcn_ballot_w64(v < 4) == 0) break;
+    const int ab = (polls & 63) == 0
+                       ? __builtin_amdgcn_readfirstlane(__hip_atomic_load(s.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                       : 0;
+    if (ab != 0 || ++polls > spin_limit) {
+      atomicCAS(s.abort, 0, (int)(pflag + i * t + k - s.wflag) + 1);
       atomicCAS(info, 0, kCholSpinFault);
       return false;
     }
@@ -1345,6 +1373,80 @@ __device__ __forceinline__ void chol_persist_update(__amdgpu_buffer_rsrc_t ra, d
       for (int e = 0; e < 4; ++e) {
         const int64_t row = ri + 16 * rb + 4 * e + g, col = rj + 16 * cb + c;
         if (row < N && col < N && (i != j || col <= row)) st_sc1(A + row * lda + col, av[rb][cb][e] - acc[rb][cb][e]);
+      }
+}
+
+// U(i, j, k .. k+B−1) (round 6): the updates of B consecutive steps to one tile in one task, A_ij loaded once,
+// A_ij −= L_is L_jsᵀ for s = k, k+1, … in order and stored once — every step's product summed from zero and
+// subtracted as U(i, j, s) does, so the tile is bitwise what B single tasks leave.  The next step's panel rows load
+// while the current step's MFMAs run (two register sets, the loop unrolled by two).  A far tile (its deadline more
+// than the near window ahead) takes its updates in batches: one A-tile round trip, one hand-off and one poll chain
+// per B steps instead of per step, and B·64 MFMAs per wave behind one set of load latencies.
+__device__ __forceinline__ void chol_persist_update_batch(__amdgpu_buffer_rsrc_t ra, double* __restrict__ A, int64_t N,
+                                                          int64_t lda, int i, int j, int k, int B) {
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  if (i == j && wm < wn) return;
+  const int64_t ri = (int64_t)i * kNB + 32 * wm, rj = (int64_t)j * kNB + 32 * wn;
+  double av[2][2][4];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t row = ri + 16 * rb + 4 * e + g, col = rj + 16 * cb + c;
+        av[rb][cb][e] = (row < N && col < N) ? ld_sc1(A + row * lda + col) : 0.0;
+      }
+  struct Rows {
+    double a0[16], a1[16], b0[16], b1[16];
+  };
+  auto load = [&](int s, Rows& p) {
+    const int64_t ck = (int64_t)s * kNB + 4 * g;
+    load_row16_sc1(ra, (ri + c) * lda + ck, p.a0);
+    load_row16_sc1(ra, (ri + 16 + c) * lda + ck, p.a1);
+    load_row16_sc1(ra, (rj + c) * lda + ck, p.b0);
+    load_row16_sc1(ra, (rj + 16 + c) * lda + ck, p.b1);
+  };
+  auto apply = [&](const Rows& p) {
+    d4 acc[2][2];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) acc[rb][cb] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(p.a0[s], p.b0[s], acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(p.a0[s], p.b1[s], acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(p.a1[s], p.b0[s], acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(p.a1[s], p.b1[s], acc[1][1], 0, 0, 0);
+    }
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) av[rb][cb][e] = av[rb][cb][e] - acc[rb][cb][e];
+  };
+  Rows p0, p1;
+  load(k, p0);
+  for (int s = 0; s < B; s += 2) {
+    if (s + 1 < B) load(k + s + 1, p1);
+    apply(p0);
+    if (s + 1 < B) {
+      if (s + 2 < B) load(k + s + 2, p0);
+      apply(p1);
+    }
+  }
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t row = ri + 16 * rb + 4 * e + g, col = rj + 16 * cb + c;
+        if (row < N && col < N && (i != j || col <= row)) st_sc1(A + row * lda + col, av[rb][cb][e]);
       }
 }
 
@@ -1505,10 +1607,11 @@ __global__ __launch_bounds__(256, kPersistWgPerCu) void chol_persist_kernel(doub
       return;
     }
     // the task: from the table (round 5, lookahead order) or the step-major arithmetic order
-    int k = k0, i = 0, j = 0;
+    int k = k0, i = 0, j = 0, nb = 1;
     bool panel;
     if (sync.tab) {
-      const int e = __builtin_amdgcn_readfirstlane(sync.tab[q]);
+      const int e = __builtin_amdgcn_readfirstlane(sync.tab[2 * q]);
+      nb = __builtin_amdgcn_readfirstlane(sync.tab[2 * q + 1]);
       panel = (e >> 30) == 0;
       k = (e >> 20) & 1023;
       i = (e >> 10) & 1023;
@@ -1544,7 +1647,7 @@ __global__ __launch_bounds__(256, kPersistWgPerCu) void chol_persist_kernel(doub
       chol_signal<AR>(sync.pflag + i * t + k, 4);
       OMB_PDBG(8 * blockIdx.x + 1, 3);
       OMB_PTIME(8 * t + 4 * s_task[0] + 2);
-    } else {
+    } else if (nb == 1) {
       if (w == 0 && chol_poll_ge<AR>(sync.pflag + i * t + k, 4, sync, spin_limit, info) &&
           chol_poll_ge<AR>(sync.pflag + j * t + k, 4, sync, spin_limit, info))
         chol_poll_ge<AR>(sync.cnt + i * t + j, k, sync, spin_limit, info);
@@ -1554,6 +1657,20 @@ __global__ __launch_bounds__(256, kPersistWgPerCu) void chol_persist_kernel(doub
       chol_persist_update(ra, A, N, lda, i, j, k);
       OMB_PDBG(8 * blockIdx.x + 2 + w, 12);
       chol_signal<AR>(sync.cnt + i * t + j, k + 1);
+      OMB_PDBG(8 * blockIdx.x + 1, 13);
+      OMB_PTIME(8 * t + 4 * s_task[0] + 2);
+    } else {
+      // U(i, j, k .. k + nb − 1): the last step's panels first (the latest to appear), then all of them at once
+      if (w == 0 && chol_poll_ge<AR>(sync.pflag + i * t + k + nb - 1, 4, sync, spin_limit, info) &&
+          chol_poll_ge<AR>(sync.pflag + j * t + k + nb - 1, 4, sync, spin_limit, info) &&
+          chol_poll_panels<AR>(sync.pflag, t, i, j, k, nb, sync, spin_limit, info))
+        chol_poll_ge<AR>(sync.cnt + i * t + j, k, sync, spin_limit, info);
+      __syncthreads();
+      OMB_PDBG(8 * blockIdx.x + 1, 21);
+      OMB_PTIME(8 * t + 4 * s_task[0] + 1);
+      chol_persist_update_batch(ra, A, N, lda, i, j, k, nb);
+      OMB_PDBG(8 * blockIdx.x + 2 + w, 22);
+      chol_signal<AR>(sync.cnt + i * t + j, k + nb);
       OMB_PDBG(8 * blockIdx.x + 1, 13);
       OMB_PTIME(8 * t + 4 * s_task[0] + 2);
     }
@@ -2755,8 +2872,9 @@ static hipError_t launch_cholesky_blocked(hipStream_t stream, double* A, int64_t
 // — step k's update of column j no later than "step" k + L, the near columns by their deadline j (the step whose
 // panel needs them).  Every task's inputs (U(i, j, k − 1), P(i, k), P(j, k); P(i, k)'s U(i, k, k − 1)) sort before
 // it, and everything the walk waits for at step k (tiles (k + 1, k), (k + 1, k + 1) through step k − 1) sorts before
-// every task that needs W_k, so the order stays topological and the grid needs no co-residency.  The table (one int
-// per task: panel flag, k, i, j in 10-bit fields) is built once per (device, t, k0, L) and kept.
+// every task that needs W_k, so the order stays topological and the grid needs no co-residency.  The table (per task
+// the code — panel flag, k, i, j in 10-bit fields — and its number of steps) is built once per (device, t, k0, L,
+// batch, window) and kept.
 #ifdef OMB_TOOLS_KNOBS
 static int g_chol_lookahead = -1;
 void set_chol_lookahead(int L) { g_chol_lookahead = L; }
@@ -2765,34 +2883,64 @@ constexpr int g_chol_lookahead = -1;
 #endif
 constexpr int kCholLookahead = 3;
 
+// Round 6: far tiles take their updates in batches (chol_persist_update_batch).  Tile (i, j)'s worker steps are
+// [k0, e) — e = j below the diagonal, i − 1 on it (the walker applies step i − 1 to its own D); the last `window`
+// steps before e (the ones the walk is about to need) stay single tasks, the earlier ones go in batches of up to
+// `batch` steps aligned to multiples of `batch`.  A batch [ka, kb) sorts as its last step's update would,
+// (min(j, kb − 1 + L), kb − 1, 1, j, i): its inputs — the panels of its steps, the tile's previous batch — still sort
+// before it, and a tile the walk waits for at step k (its last worker step k − 1, inside the window) is a single
+// task sorting before every task that needs W_k, so the order stays topological.  The entries are pairs (code,
+// steps); batch 1 is round 5's table.
+#ifdef OMB_TOOLS_KNOBS
+static int g_chol_batch = -1, g_chol_window = -1;
+void set_chol_batch(int batch, int window) {
+  g_chol_batch = batch;
+  g_chol_window = window;
+}
+#else
+constexpr int g_chol_batch = -1, g_chol_window = -1;
+#endif
+constexpr int kCholBatch = 4;
+constexpr int kCholWindow = 4;
+
 struct CholTaskTab {
-  int dev, t, k0, L;
+  int dev, t, k0, L, batch, window, total;
   int* d;
 };
 
-static const int* chol_task_table(int t, int k0, int L, int total) {
+static const int* chol_task_table(int t, int k0, int L, int batch, int window, int* total_out) {
   static std::mutex mu;
   static std::vector<CholTaskTab> tabs;
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  if (hipGetDevice(&dev) != hipSuccess || t > 1024 || batch < 1 || batch > 32) return nullptr;
   std::lock_guard<std::mutex> lock(mu);
   for (const CholTaskTab& e : tabs)
-    if (e.dev == dev && e.t == t && e.k0 == k0 && e.L == L) return e.d;
+    if (e.dev == dev && e.t == t && e.k0 == k0 && e.L == L && e.batch == batch && e.window == window) {
+      *total_out = e.total;
+      return e.d;
+    }
   struct Key {
-    int a, b, c, d, e, code;
+    int a, b, c, d, e, code, steps;
   };
   std::vector<Key> keys;
-  keys.reserve(total);
-  for (int k = k0; k < t; ++k) {
+  for (int k = k0; k < t; ++k)
     if (!(k0 > 0 && k == k0))
-      for (int i = k + 2; i < t; ++i) keys.push_back({k + 1, k, 0, 0, i, (k << 20) | (i << 10)});
-    for (int j = k + 1; j < t; ++j)
-      for (int i = j; i < t; ++i) {
-        if (i == k + 1 && j == k + 1) continue;                 // the walker's own D product
-        keys.push_back({std::min(j, k + L), k, 1, j, i, (1 << 30) | (k << 20) | (i << 10) | j});
+      for (int i = k + 2; i < t; ++i) keys.push_back({k + 1, k, 0, 0, i, (k << 20) | (i << 10), 1});
+  auto add_update = [&](int i, int j, int ka, int kb) {   // steps [ka, kb) of tile (i, j)
+    const int kl = kb - 1;
+    keys.push_back({std::min(j, kl + L), kl, 1, j, i, (1 << 30) | (ka << 20) | (i << 10) | j, kb - ka});
+  };
+  for (int j = k0 + 1; j < t; ++j)
+    for (int i = j; i < t; ++i) {
+      const int e = (i == j) ? i - 1 : j;                     // worker steps [k0, e)
+      const int near = std::max(k0, e - window);
+      for (int ka = k0; ka < near;) {                         // batches, aligned to multiples of `batch`
+        const int kb = std::min(near, (ka / batch + 1) * batch);
+        add_update(i, j, ka, kb);
+        ka = kb;
       }
-  }
-  if ((int)keys.size() != total || t > 1024) return nullptr;
+      for (int k = near; k < e; ++k) add_update(i, j, k, k + 1);
+    }
   std::sort(keys.begin(), keys.end(), [](const Key& x, const Key& y) {
     if (x.a != y.a) return x.a < y.a;
     if (x.b != y.b) return x.b < y.b;
@@ -2800,22 +2948,27 @@ static const int* chol_task_table(int t, int k0, int L, int total) {
     if (x.d != y.d) return x.d < y.d;
     return x.e < y.e;
   });
-  std::vector<int> codes(total);
-  for (int q = 0; q < total; ++q) codes[q] = keys[q].code;
+  const int total = (int)keys.size();
+  std::vector<int> codes(2 * (size_t)total);
+  for (int q = 0; q < total; ++q) {
+    codes[2 * q] = keys[q].code;
+    codes[2 * q + 1] = keys[q].steps;
+  }
   int* d = nullptr;
-  if (hipMalloc(&d, sizeof(int) * (size_t)std::max(total, 1)) != hipSuccess) return nullptr;
-  if (hipMemcpy(d, codes.data(), sizeof(int) * (size_t)total, hipMemcpyHostToDevice) != hipSuccess) {
+  if (hipMalloc(&d, sizeof(int) * (size_t)std::max(2 * total, 1)) != hipSuccess) return nullptr;
+  if (hipMemcpy(d, codes.data(), sizeof(int) * 2 * (size_t)total, hipMemcpyHostToDevice) != hipSuccess) {
     (void)hipFree(d);
     return nullptr;
   }
-  tabs.push_back({dev, t, k0, L, d});
+  tabs.push_back({dev, t, k0, L, batch, window, total, d});
+  *total_out = total;
   return d;
 }
 
 // k0 > 0: steps 0 .. k0 − 1 as per-step launches (their bulk trailing updates run at three workgroups per CU), the
 // rest in one persistent launch (the diagonal walk without kernel boundaries once the trailing matrix is small).
 static hipError_t launch_cholesky_persist(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws,
-                                          int spin_limit, int k0 = 0, int acq_rel = 0) {
+                                          int spin_limit, int k0 = 0, int acq_rel = 0, int single_steps = 0) {
   const int t = (int)((N + kNB - 1) / kNB);
   if (k0 > t - 2) k0 = 0;
   hipError_t e = hipSuccess;
@@ -2826,8 +2979,12 @@ static hipError_t launch_cholesky_persist(hipStream_t stream, double* A, int64_t
   int total = 0;
   for (int k = k0; k < t; ++k) total += chol_persist_step_tasks(t, k, k0);
   const int L = g_chol_lookahead >= 0 ? g_chol_lookahead : kCholLookahead;
-  // L = 0 (tools): the step-major arithmetic order of round 4
-  const int* tab = L > 0 ? chol_task_table(t, k0, L, total) : nullptr;
+  const int batch = single_steps ? 1 : (g_chol_batch >= 1 ? g_chol_batch : kCholBatch);
+  const int window = g_chol_window >= 0 ? g_chol_window : kCholWindow;
+  // L = 0 (tools): the step-major arithmetic order of round 4 (single-step tasks)
+  int tab_total = 0;
+  const int* tab = L > 0 ? chol_task_table(t, k0, L, batch, window, &tab_total) : nullptr;
+  if (tab) total = tab_total;
   CholSync sync{ints, ints + t, ints + t + t * t, ints + t + 2 * t * t, ints + t + 2 * t * t + 1, tab};
   if (k0 == 0) {   // with k0 > 0 step 0's panel launch wrote the sync words
     hipLaunchKernelGGL(chol_persist_init_kernel, dim3(1), dim3(256), 0, stream, ints, t, k0, info);
@@ -2845,17 +3002,18 @@ static hipError_t launch_cholesky_persist(hipStream_t stream, double* A, int64_t
 }
 
 hipError_t launch_cholesky_mode(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws, int mode,
-                                int spin_limit, int acq_rel) {
+                                int spin_limit, int acq_rel, int single_steps) {
   if (N <= 0) return hipSuccess;
   if (mode == kCholAuto) mode = kCholPersistent;
   if (mode == kCholPersistOnly) {
-    if (chol_persist_fits(N, lda)) return launch_cholesky_persist(stream, A, N, lda, info, ws, spin_limit, 0, acq_rel);
+    if (chol_persist_fits(N, lda))
+      return launch_cholesky_persist(stream, A, N, lda, info, ws, spin_limit, 0, acq_rel, single_steps);
     mode = kCholBlocked;
   }
   if (mode == kCholPersistent) {
     if (chol_persist_fits(N, lda))
       return launch_cholesky_persist(stream, A, N, lda, info, ws, spin_limit, chol_hybrid_k0((int)((N + kNB - 1) / kNB)),
-                                     acq_rel);
+                                     acq_rel, single_steps);
     mode = kCholBlocked;
   }
   if (acq_rel && mode == kCholBlocked) mode = kCholBlockedAcqRel;

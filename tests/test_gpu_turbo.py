@@ -173,6 +173,28 @@ def test_cholesky_randomized_stress(ctx, chol_mode):
         assert np.array_equal(got, first)
 
 
+@pytest.mark.parametrize("mode", [0, 2], ids=["auto", "persistent"])
+def test_cholesky_batched_updates_bitwise_single_steps(ctx, mode):
+    """Round 6: the persistent launch's workers take a far tile's trailing updates in batches of steps (one A-tile
+    round trip per batch); each step's product is still summed from zero and subtracted in step order, so the factor
+    is bitwise the one-task-per-step schedule's (OMB_DEBUG_CHOL_MODE + 8) — at sizes with 3 … 65 block columns, under
+    the default hybrid (per-step launches first) and the pure persistent launch."""
+    for N in [130, 333, 700, 1500, 2113, 3000, 4097]:
+        A = spd(N, 77 + N)
+        ctx.debug_set("chol_mode", mode)
+        At = dev(A)
+        try:
+            assert ctx.cholesky(At, jitter=0.0) == 0, N
+            ctx.debug_set("chol_mode", mode | 8)
+            As = dev(A)
+            assert ctx.cholesky(As, jitter=0.0) == 0, N
+        finally:
+            ctx.debug_set("chol_mode", 0)
+        got = np.tril(At.cpu().numpy())
+        assert np.array_equal(got, np.tril(As.cpu().numpy())), N
+        np.testing.assert_allclose(got, np.linalg.cholesky(A), rtol=1e-10, atol=1e-12)
+
+
 def test_cholesky_step_wait_timeout_is_reported(ctx, chol_mode):
     """The fused Cholesky step (the next panel formed in the update launch) waits for the diagonal
     workgroup's flag with a bounded poll; omb_debug_set(SPIN_LIMIT, 0) makes the first unset poll run

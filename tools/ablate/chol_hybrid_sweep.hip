@@ -2,7 +2,8 @@
 // factor against the per-step launches alone, for a list of k0 (tools only).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/ablate/chol_hybrid_sweep tools/ablate/chol_hybrid_sweep.hip
 // Run:   ./tools/ablate/chol_hybrid_sweep N [N ...]   (k0 list from CHOL_K0S, default 0,4,8,12,16,24,32; the
-//        persistent launch's lookahead L list from CHOL_LS, default 3 — 0 = round 4's step-major task order)
+//        persistent launch's lookahead L list from CHOL_LS, default 3 — 0 = round 4's step-major task order; the
+//        far tiles' update batching from CHOL_BW, "batch:window" pairs, default the library's — 1:0 = round 5's table)
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -53,6 +54,20 @@ int main(int argc, char** argv) {
       p = q + 1;
     }
   }
+  std::vector<std::pair<int, int>> bws = {{-1, -1}};
+  if (const char* e = getenv("CHOL_BW")) {
+    bws.clear();
+    std::string s(e);
+    size_t p = 0;
+    while (p < s.size()) {
+      size_t q = s.find(',', p);
+      if (q == std::string::npos) q = s.size();
+      const std::string item = s.substr(p, q - p);
+      const size_t c = item.find(':');
+      bws.push_back({atoi(item.substr(0, c).c_str()), c == std::string::npos ? 0 : atoi(item.substr(c + 1).c_str())});
+      p = q + 1;
+    }
+  }
   std::vector<int64_t> sizes;
   for (int i = 1; i < argc; ++i) sizes.push_back(atoll(argv[i]));
   if (sizes.empty()) sizes = {3000};
@@ -94,18 +109,30 @@ int main(int argc, char** argv) {
     int ib = run(kCholBlocked, -1, tb);
     CK(hipMemcpy(R.data(), A, N * N * 8, hipMemcpyDeviceToHost));
     printf("N=%lld per-step launches %.3f ms info %d\n", (long long)N, tb, ib);
+    std::vector<double> L1(N * N);
     for (int la : Ls)
     for (int k0 : k0s) {
-      set_chol_lookahead(la);
-      float tp;
-      const int ip = run(kCholPersistent, k0, tp);
-      CK(hipMemcpy(L.data(), A, N * N * 8, hipMemcpyDeviceToHost));
-      double md = 0.0;
-      for (int64_t i = 0; i < N; ++i)
-        for (int64_t j = 0; j <= i; ++j) md = std::max(md, std::abs(L[i * N + j] - R[i * N + j]) / std::sqrt(h[i * N + i]));
-      printf("N=%lld L=%d k0=%d: %.3f ms info %d max |L - L_steps|/sqrt(A_ii) %.2e\n", (long long)N, la, k0, tp, ip, md);
+      for (size_t v = 0; v < bws.size(); ++v) {
+        set_chol_lookahead(la);
+        set_chol_batch(bws[v].first, bws[v].second);
+        float tp;
+        const int ip = run(kCholPersistent, k0, tp);
+        CK(hipMemcpy(L.data(), A, N * N * 8, hipMemcpyDeviceToHost));
+        double md = 0.0;
+        for (int64_t i = 0; i < N; ++i)
+          for (int64_t j = 0; j <= i; ++j) md = std::max(md, std::abs(L[i * N + j] - R[i * N + j]) / std::sqrt(h[i * N + i]));
+        // batches are bitwise the single-step tasks: every variant against the first of this (L, k0)
+        long long ndiff = 0;
+        if (v == 0) L1 = L;
+        else
+          for (int64_t i = 0; i < N; ++i)
+            for (int64_t j = 0; j <= i; ++j) ndiff += L[i * N + j] != L1[i * N + j];
+        printf("N=%lld L=%d k0=%d batch=%d window=%d: %.3f ms info %d max |L - L_steps|/sqrt(A_ii) %.2e  bits != first %lld\n",
+               (long long)N, la, k0, bws[v].first, bws[v].second, tp, ip, md, ndiff);
+      }
     }
     set_chol_lookahead(-1);
+    set_chol_batch(-1, -1);
     set_chol_hybrid_k0(-1);
     CK(hipFree(A0)); CK(hipFree(A)); CK(hipFree(ws)); CK(hipFree(info));
   }

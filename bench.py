@@ -244,6 +244,8 @@ def run_thompson(args, cfg, world_size, rank, device, backend):
         ctx.debug_set("chol_mode", args.chol_mode)
     if args.cov_fused is not None:
         ctx.debug_set("cov_fused", args.cov_fused)
+    if args.syrk_glds is not None:
+        ctx.debug_set("syrk_glds", args.syrk_glds)
     ctx.set_gp_state(0, GPState(X, yagg, ls, var))
     rng = np.random.default_rng(100 + rank)
     # a trust region of side 0.2 around a training point (turbo.py:82-111), one per rank
@@ -453,6 +455,9 @@ def main():
     ap.add_argument("--chol-mode", type=int, default=None, choices=[0, 1, 2, 4, 5, 6, 8, 10, 12, 14],
                     help="omb_debug_set(CHOL_MODE): Cholesky auto / per-step launches / one persistent launch; + 4: "
                          "with release-acquire hand-offs")
+    ap.add_argument("--syrk-glds", type=int, default=None, choices=[0, 1],
+                    help="omb_debug_set(SYRK_GLDS): the covariance SYRK's three-stage direct-to-LDS operand pipeline "
+                         "(config 6; default: the library's, 1)")
     ap.add_argument("--cov-fused", type=int, default=None, choices=[0, 1],
                     help="omb_debug_set(COV_FUSED): K(X*, X*) in the covariance SYRK's epilogue (config 6; default: "
                          "the library's, 1)")

@@ -101,9 +101,9 @@ const char* omb_last_error(const omb_ctx* ctx);
  * reduces the per-workgroup pairs) instead of two (default 2: config 2 measured 719.6 vs 719.5 M candidates/s,
  * gpurun_out/r04_l; bit-identical pair).
  * omb_debug_set(ctx, OMB_DEBUG_CHOL_MODE, m) picks the Cholesky schedule of omb_cholesky / omb_posterior_samples /
- * omb_gp_fit_state: 0 auto (default: where A fits the persistent launch's 32-bit buffer offsets, per-step launches for
- * all but the last min(steps, 32) 64-column steps and one persistent launch for those; else 1), 1 one launch per
- * step, 2 the whole factorisation in one persistent launch; m + 4 runs schedule m with every cross-workgroup hand-off
+ * omb_gp_fit_state: 0 auto (default: where A fits the persistent launch's 32-bit buffer offsets, the whole
+ * factorisation in one persistent launch — round 5 ran per-step launches for all but the last 32 steps first; else 1),
+ * 1 one launch per step, 2 the persistent launch whatever the size; m + 4 runs schedule m with every cross-workgroup hand-off
  * an agent-scope release / acquire pair (the HIP memory model's guarantee; the default form — sc1 payloads, a vmcnt
  * wait and relaxed flags — is measured valid on gfx950), bitwise the same factor as schedule m; m + 8 has the persistent
  * launch's workers apply every trailing update as its own task instead of batching the far tiles' updates (round 5's
@@ -115,7 +115,10 @@ const char* omb_last_error(const omb_ctx* ctx);
  * omb_debug_set(ctx, OMB_DEBUG_COV_FUSED, 0) builds the posterior covariance as K(X*, X*) then the VᵀV update (two
  * launches) instead of one SYRK with K(X*, X*) in its epilogue (default 1; the same matrix to the ulp).
  * omb_debug_set(ctx, OMB_DEBUG_SELECT_SEQ, 1) makes omb_thompson_select walk the samples in order for B ≤ 64 too
- * (default 0: the picks in parallel rounds to their fixed point; the same picks). */
+ * (default 0: the picks in parallel rounds to their fixed point; the same picks).
+ * omb_debug_set(ctx, OMB_DEBUG_SYRK_GLDS, 0) builds the posterior covariance's SYRK with the register-staged two-slab
+ * pipeline instead of the three-stage direct-to-LDS one (default 1 where n_train % 16 = 0 and N is even; the same
+ * matrix bit for bit). */
 enum {
   OMB_DEBUG_SPIN_LIMIT = 1,
   OMB_DEBUG_COV_TABLE = 2,
@@ -124,7 +127,8 @@ enum {
   OMB_DEBUG_CHOL_MODE = 5,
   OMB_DEBUG_TIMING_STRIDE = 6,
   OMB_DEBUG_COV_FUSED = 8,
-  OMB_DEBUG_SELECT_SEQ = 9
+  OMB_DEBUG_SELECT_SEQ = 9,
+  OMB_DEBUG_SYRK_GLDS = 10
 };
 int omb_debug_set(omb_ctx* ctx, int what, int64_t value);
 

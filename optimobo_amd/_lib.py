@@ -28,6 +28,7 @@ DEBUG_CHOL_MODE = 5
 DEBUG_TIMING_STRIDE = 6
 DEBUG_COV_FUSED = 8
 DEBUG_SELECT_SEQ = 9
+DEBUG_SYRK_GLDS = 10
 MAX_OBJ, MAX_DIM, MAX_TRAIN, MAX_TRAIN_DENSE = 8, 256, 1024, 16384
 
 _p = ctypes.c_void_p

@@ -91,6 +91,7 @@ struct omb_ctx {
   int spin_limit = kDefaultSpinLimit;
   bool cov_table = false;   // OMB_DEBUG_COV_TABLE
   bool cov_fused = true;    // OMB_DEBUG_COV_FUSED: K(X*, X*) in the covariance SYRK's epilogue
+  bool syrk_glds = true;    // OMB_DEBUG_SYRK_GLDS: the covariance SYRK's direct-to-LDS operand pipeline
   int fused_chain = 0;  // OMB_DEBUG_FUSED_CHAIN: 0 EHVI-2D then the arg-max's passes, 1 one ticketed launch, 2 EHVI
                         // with the per-workgroup pairs, then the arg-max's second pass
   bool argmax_one_pass = false;  // OMB_DEBUG_ARGMAX_PASSES: 1 (one launch) or 2 (default: measured level)
@@ -459,6 +460,10 @@ int omb_debug_set(omb_ctx* ctx, int what, int64_t value) {
   }
   if (what == OMB_DEBUG_COV_FUSED) {
     ctx->cov_fused = value != 0;
+    return OMB_OK;
+  }
+  if (what == OMB_DEBUG_SYRK_GLDS) {
+    ctx->syrk_glds = value != 0;
     return OMB_OK;
   }
   if (what == OMB_DEBUG_SELECT_SEQ) {
@@ -956,7 +961,8 @@ static hipError_t cov_build(omb_ctx* ctx, const ObjState& s, const double* Xc, i
     hipError_t e = hipSuccess;
     const int kp = prescaled ? (s.DP + 3) / 4 * 4 : launch_cand_scale(ctx->stream, s.dev, s.d, s.DP, Xc, N, cws, &e);
     if (e == hipSuccess && kp > 0)
-      return launch_cov_syrk(ctx->stream, N, s.n, V, N, S, lds, cws, cws + N * kp, kp, s.kind, s.variance, jitter);
+      return launch_cov_syrk(ctx->stream, N, s.n, V, N, S, lds, cws, cws + N * kp, kp, s.kind, s.variance, jitter,
+                             ctx->syrk_glds);
     if (e != hipSuccess) return e;
   }
   hipError_t e = launch_cand_cov(ctx->stream, s.dev, s.d, s.DP, Xc, N, S, lds, cws, jitter, ctx->cov_table);

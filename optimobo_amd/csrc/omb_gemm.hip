@@ -43,6 +43,62 @@ struct CovEpi {
   double diag_add;
 };
 
+// KSS epilogue (gemm_kernel, syrk_glds_kernel): C = K(X*, X*) + α·acc on the tile's lower triangle, the kernel block's
+// cross term over kp dimensions in slabs of 16 staged through the LDS scratch As / Bs ([16][pitch] doubles each).
+__device__ __forceinline__ void cov_epilogue(int64_t m0, int64_t n0, int64_t M, int64_t Nc, const d4 (&acc)[2][2],
+                                             double alpha, const CovEpi& ce, double* __restrict__ C, int64_t ldc,
+                                             double* As, double* Bs, int pitch) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  d4 cr[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) cr[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+  for (int k0 = 0; k0 < ce.kp; k0 += kGK) {
+    __syncthreads();                                       // the product's last slab is read by every wave
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int idx = tid + 256 * e, r = idx >> 4, k = idx & 15;
+      const int64_t ra = m0 + r < M ? m0 + r : M - 1, rb = n0 + r < Nc ? n0 + r : Nc - 1;
+      As[k * pitch + r] = k0 + k < ce.kp ? ce.xs[ra * ce.kp + k0 + k] : 0.0;
+      Bs[k * pitch + r] = k0 + k < ce.kp ? ce.xs[rb * ce.kp + k0 + k] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < kGK / 4; ++ks) {
+      const int kk = 4 * ks + (lane >> 4);
+      const double a0 = As[kk * pitch + 32 * wm + (lane & 15)];
+      const double a1 = As[kk * pitch + 32 * wm + 16 + (lane & 15)];
+      const double b0 = Bs[kk * pitch + 32 * wn + (lane & 15)];
+      const double b1 = Bs[kk * pitch + 32 * wn + 16 + (lane & 15)];
+      cr[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, cr[0][0], 0, 0, 0);
+      cr[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, cr[0][1], 0, 0, 0);
+      cr[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, cr[1][0], 0, 0, 0);
+      cr[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, cr[1][1], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb) {
+    const int64_t col = n0 + 32 * wn + 16 * cb + (lane & 15);
+    const double bsq = col < Nc ? ce.xsq[col] : 0.0;
+#pragma unroll
+    for (int rb2 = 0; rb2 < 2; ++rb2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t row = m0 + 32 * wm + 16 * rb2 + (lane >> 4) + 4 * i;
+        if (row < M && col < Nc && col <= row) {
+          const double r2 = (row == col) ? 0.0 : fma(-2.0, cr[rb2][cb][i], ce.xsq[row] + bsq);
+          double kv = ce.kind == OMB_KERNEL_RBF ? kernel_of_r2<OMB_KERNEL_RBF>(r2, ce.variance)
+                                                : kernel_of_r2<OMB_KERNEL_MATERN52>(r2, ce.variance);
+          if (row == col) kv = kv + ce.diag_add;
+          C[row * ldc + col] = fma(1.0, kv, alpha * acc[rb2][cb][i]);
+        }
+      }
+  }
+}
+
 template <bool TA, bool TB, bool BTRI, bool LOWER, bool ATRI = false, bool KSS = false>
 __global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t Nc, int64_t K, double alpha,
                                                    const double* __restrict__ A, int64_t lda,
@@ -174,53 +230,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t Nc, int64_
   }
 
   if constexpr (KSS) {
-    // the tile of K(X*, X*): cross term over kp dimensions in slabs of 16 through As[0] / Bs[0]
-    d4 cr[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) cr[i][j] = d4{0.0, 0.0, 0.0, 0.0};
-    for (int k0 = 0; k0 < ce.kp; k0 += kGK) {
-      __syncthreads();                                       // the product's last slab is read by every wave
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int idx = tid + 256 * e, r = idx >> 4, k = idx & 15;
-        const int64_t ra = m0 + r < M ? m0 + r : M - 1, rb = n0 + r < Nc ? n0 + r : Nc - 1;
-        As[0][k][r] = k0 + k < ce.kp ? ce.xs[ra * ce.kp + k0 + k] : 0.0;
-        Bs[0][k][r] = k0 + k < ce.kp ? ce.xs[rb * ce.kp + k0 + k] : 0.0;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int ks = 0; ks < kGK / 4; ++ks) {
-        const int kk = 4 * ks + (lane >> 4);
-        const double a0 = As[0][kk][32 * wm + (lane & 15)];
-        const double a1 = As[0][kk][32 * wm + 16 + (lane & 15)];
-        const double b0 = Bs[0][kk][32 * wn + (lane & 15)];
-        const double b1 = Bs[0][kk][32 * wn + 16 + (lane & 15)];
-        cr[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, cr[0][0], 0, 0, 0);
-        cr[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, cr[0][1], 0, 0, 0);
-        cr[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, cr[1][0], 0, 0, 0);
-        cr[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, cr[1][1], 0, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-      const int64_t col = n0 + 32 * wn + 16 * cb + (lane & 15);
-      const double bsq = col < Nc ? ce.xsq[col] : 0.0;
-#pragma unroll
-      for (int rb2 = 0; rb2 < 2; ++rb2)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int64_t row = m0 + 32 * wm + 16 * rb2 + (lane >> 4) + 4 * i;
-          if (row < M && col < Nc && col <= row) {
-            const double r2 = (row == col) ? 0.0 : fma(-2.0, cr[rb2][cb][i], ce.xsq[row] + bsq);
-            double kv = ce.kind == OMB_KERNEL_RBF ? kernel_of_r2<OMB_KERNEL_RBF>(r2, ce.variance)
-                                                  : kernel_of_r2<OMB_KERNEL_MATERN52>(r2, ce.variance);
-            if (row == col) kv = kv + ce.diag_add;
-            C[row * ldc + col] = fma(1.0, kv, alpha * acc[rb2][cb][i]);
-          }
-        }
-    }
+    cov_epilogue(m0, n0, M, Nc, acc, alpha, ce, C, ldc, &As[0][0][0], &Bs[0][0][0], kGP);
     return;
   }
 
@@ -240,6 +250,98 @@ __global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t Nc, int64_
           C[row * ldc + col] = v;
         }
       }
+}
+
+// Round 6: the covariance SYRK (Σ = K(X*, X*) − VᵀV, lower triangle, V (K, N) row-major) with a three-stage operand
+// pipeline filled by direct-to-LDS loads (gemm_kernel's waves waited on their slab loads 66% of
+// their cycles, and a second register slab spilled).  Stage s holds slab k's A and B tiles — 16 rows of
+// V × 64 columns each, XOR-swizzled in pairs of columns so the four 16-lane row groups of an MFMA operand read hit
+// both halves of the bank row — written by global_load_lds_dwordx4: one wave-instruction is 1 KiB, two rows, lane l
+// the 16 B at row 2p + (l >> 5), column pair (l & 31) ^ 8·(row & 1) of the source (linear LDS, swizzle on the source
+// and on the read).  Slab k + 2 is issued after the barrier that retires slab k, so two slabs stay in flight while
+// one multiplies; the wait is a counted vmcnt and the barrier a raw s_barrier (a __syncthreads would drain the DMA).
+// Every LDS byte lives in the one __shared__ array (a second __shared__ object can make hipcc wait vmcnt(0) before
+// each ds_read).  Requires K a multiple of 16 and N even with V 16-B aligned (launch_cov_syrk checks); the products
+// are summed in gemm_kernel's k order, so C is bitwise gemm_kernel<…, KSS>'s.
+constexpr int kSyrkStages = 3;
+__device__ __forceinline__ int syrk_swz(int row, int col) { return ((((col >> 1) ^ ((row & 1) << 3)) << 1) | (col & 1)); }
+
+__global__ __launch_bounds__(256) void syrk_glds_kernel(int64_t N, int64_t K, double alpha, const double* __restrict__ V,
+                                                        int64_t ldv, double* __restrict__ C, int64_t ldc, CovEpi ce,
+                                                        const int* __restrict__ tmap) {
+  int64_t m0 = (int64_t)blockIdx.y * kGT, n0 = (int64_t)blockIdx.x * kGT;
+  if (tmap) {
+    const int code = tmap[blockIdx.x];
+    if (code < 0) return;
+    m0 = (int64_t)(code >> 16) * kGT;
+    n0 = (int64_t)(code & 0xffff) * kGT;
+  }
+  if (n0 > m0) return;
+  constexpr int kSlab = kGK * kGT;                          // doubles of one operand's slab
+  __shared__ __attribute__((aligned(16))) double sm[kSyrkStages * 2 * kSlab];
+  typedef __attribute__((address_space(3))) void lds_void;
+  typedef __attribute__((address_space(1))) const void g_void;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  // this lane's source columns for its pieces p = 2·wave + j (rows 2p, 2p + 1): column pair (lane & 31) ^ 8·(row & 1),
+  // clamped into the matrix (columns past N feed C entries that are never stored)
+  const int prow0 = 4 * wave + (lane >> 5), q = lane & 31;
+  int64_t colA[2], colB[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = prow0 + 2 * j;
+    const int gq = q ^ ((row & 1) << 3);
+    colA[j] = m0 + 2 * gq < N - 1 ? m0 + 2 * gq : N - 2;
+    colB[j] = n0 + 2 * gq < N - 1 ? n0 + 2 * gq : N - 2;
+  }
+  const int ns = (int)(K / kGK);
+  auto issue = [&](int stage, int slab) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = prow0 + 2 * j;
+      const double* src = V + ((int64_t)slab * kGK + row) * ldv;
+      double* dA = sm + (stage * 2 + 0) * kSlab + (4 * wave + 2 * j) * kGT;   // wave-uniform: rows 2p, 2p + 1
+      double* dB = sm + (stage * 2 + 1) * kSlab + (4 * wave + 2 * j) * kGT;
+      __builtin_amdgcn_global_load_lds((g_void*)(src + colA[j]), (lds_void*)dA, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((g_void*)(src + colB[j]), (lds_void*)dB, 16, 0, 0);
+    }
+  };
+  d4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+  if (ns > 0) issue(0, 0);
+  if (ns > 1) issue(1, 1);
+  for (int sl = 0; sl < ns; ++sl) {
+    // slab sl's four DMAs of this wave retired (sl + 1's four may stay in flight), then every wave's
+    if (sl + 1 < ns)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    // stage (sl + 2) % 3 was last read by slab sl − 1, which every wave has finished (the barrier above)
+    if (sl + 2 < ns) issue((sl + 2) % kSyrkStages, sl + 2);
+    const double* As = sm + ((sl % kSyrkStages) * 2 + 0) * kSlab;
+    const double* Bs = sm + ((sl % kSyrkStages) * 2 + 1) * kSlab;
+#pragma unroll
+    for (int ks = 0; ks < kGK / 4; ++ks) {
+      const int kk = 4 * ks + (lane >> 4);
+      const double a0 = As[kk * kGT + syrk_swz(kk, 32 * wm + (lane & 15))];
+      const double a1 = As[kk * kGT + syrk_swz(kk, 32 * wm + 16 + (lane & 15))];
+      const double b0 = Bs[kk * kGT + syrk_swz(kk, 32 * wn + (lane & 15))];
+      const double b1 = Bs[kk * kGT + syrk_swz(kk, 32 * wn + 16 + (lane & 15))];
+      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  }
+  // the epilogue's cross-term scratch: stage 0's A / B tiles ([16][64], after its barrier)
+  cov_epilogue(m0, n0, N, N, acc, alpha, ce, C, ldc, sm, sm + kSlab, kGT);
 }
 
 template <bool TA, bool TB, bool BTRI, bool LOWER, bool ATRI = false>
@@ -411,12 +513,19 @@ constexpr bool g_syrk_xcd_map = true;
 #endif
 
 hipError_t launch_cov_syrk(hipStream_t s, int64_t N, int64_t K, const double* V, int64_t ldv, double* S, int64_t lds,
-                           const double* xs, const double* xsq, int kp, int kind, double variance, double diag_add) {
+                           const double* xs, const double* xsq, int kp, int kind, double variance, double diag_add,
+                           bool glds) {
   if (N <= 0) return hipSuccess;
   const int T = (int)((N + kGT - 1) / kGT);
   int g1 = 0;
   const int* tmap = g_syrk_xcd_map ? xcd_tile_map(kMapSyrk, T, T, &g1) : nullptr;
   const dim3 grid = tmap ? dim3((unsigned)g1) : dim3((unsigned)T, (unsigned)T);
+  // the direct-to-LDS pipeline needs whole 16-row slabs and 16-B column pairs inside each row
+  if (glds && K % kGK == 0 && N % 2 == 0 && N >= 2 && ldv % 2 == 0 && (reinterpret_cast<uintptr_t>(V) & 15) == 0) {
+    hipLaunchKernelGGL(syrk_glds_kernel, grid, dim3(256), 0, s, N, K, -1.0, V, ldv, S, lds,
+                       CovEpi{xs, xsq, kp, kind, variance, diag_add}, tmap);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL((gemm_kernel<true, false, false, true, false, true>), grid, dim3(256), 0, s, N, N, K, -1.0, V, ldv,
                      V, ldv, 0.0, S, lds, (const double*)nullptr, (int64_t)0, (int64_t)0,
                      CovEpi{xs, xsq, kp, kind, variance, diag_add}, tmap);

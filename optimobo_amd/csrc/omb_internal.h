@@ -135,9 +135,11 @@ hipError_t launch_cand_cov(hipStream_t stream, const GPDev& g, int d, int DP, co
 int launch_cand_scale(hipStream_t stream, const GPDev& g, int d, int DP, const double* Xc, int64_t N, double* ws,
                       hipError_t* err);
 // lower triangle of S = K(X*, X*) + diag_add·I − VᵀV, V (K, N): the covariance SYRK with K(X*, X*) formed in its
-// epilogue from launch_cand_scale's rows (omb_gemm.hip gemm_kernel<…, KSS>)
+// epilogue from launch_cand_scale's rows (omb_gemm.hip gemm_kernel<…, KSS>; glds: syrk_glds_kernel, the three-stage
+// direct-to-LDS operand pipeline, where K % 16 = 0 and N, ldv even — bitwise the same C)
 hipError_t launch_cov_syrk(hipStream_t s, int64_t N, int64_t K, const double* V, int64_t ldv, double* S, int64_t lds,
-                           const double* xs, const double* xsq, int kp, int kind, double variance, double diag_add);
+                           const double* xs, const double* xsq, int kp, int kind, double variance, double diag_add,
+                           bool glds = true);
 hipError_t launch_mirror_lower(hipStream_t stream, double* S, int64_t N, int64_t lds);
 hipError_t launch_add_diag(hipStream_t stream, double* S, int64_t N, int64_t lds, double v);
 // in-place lower Cholesky; info (device int, zeroed by the first kernel) = first bad column (1-based);

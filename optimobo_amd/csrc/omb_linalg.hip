@@ -2834,15 +2834,16 @@ void set_chol_hybrid_k0(int k0) { g_chol_hybrid_k0 = k0; }
 #else
 constexpr int g_chol_hybrid_k0 = -1;
 #endif
-// The persistent launch's trailing updates keep up with the walk once ≤ ≈ 32 block columns remain; before that the
-// per-step launches' (three workgroups per CU, LDS-staged) are faster.  GPU-side times, k0 swept
-// (tools/ablate/chol_hybrid_sweep, gpurun_out/r04_w): N = 3000 per-step 1.093, persistent 1.092, k0 = 12-16
-// 0.996-0.999 ms; N = 4000 1.701 / 2.166 / k0 = 24-32 1.583-1.586; N = 5000 2.566 / 3.889 / k0 = 48 2.487; N ≤ 2000
-// (t ≤ 32) the persistent launch alone.
-constexpr int kCholPersistSteps = 32;
+// Rounds 4-5: the persistent launch's trailing updates kept up with the walk only once ≤ ≈ 32 block columns remained,
+// so the first t − 32 steps ran as per-step launches (three workgroups per CU, LDS-staged).  Round 6: with the far
+// tiles' updates batched (chol_task_table) the persistent launch alone is the fastest schedule at every size measured
+// (GPU time, tools/ablate/chol_hybrid_sweep): N = 3000 0.910 ms (round 5's hybrid 0.98, per-step 1.10), 5000 2.358
+// (2.48, 2.56), 6500 4.55-4.69 for every k0 (per-step 4.68), 8000 7.38 (k0 = 16 … 93: 7.75-7.89, per-step 7.90;
+// profiles/r06_d_chol_sweep.txt, r06_e_chol_sweep.txt, r06_f_chol_sweep_large_n.txt).  The per-step prefix stays
+// available to the tools (k0 > 0).
 static int chol_hybrid_k0(int t) {
-  if (g_chol_hybrid_k0 >= 0) return g_chol_hybrid_k0;
-  return t > kCholPersistSteps ? t - kCholPersistSteps : 0;
+  (void)t;
+  return g_chol_hybrid_k0 >= 0 ? g_chol_hybrid_k0 : 0;
 }
 
 // Round 4: one persistent launch (chol_persist_kernel), kPersistWgPerCu workgroups per CU.
@@ -2881,7 +2882,9 @@ void set_chol_lookahead(int L) { g_chol_lookahead = L; }
 #else
 constexpr int g_chol_lookahead = -1;
 #endif
-constexpr int kCholLookahead = 3;
+// Round 6 (with the batched far updates below): L = 2 — N = 3000 0.910 against 0.920 ms at L = 3, N = 5000 2.358 against
+// 2.403 ms (tools/ablate/chol_hybrid_sweep, profiles/r06_e_chol_sweep.txt)
+constexpr int kCholLookahead = 2;
 
 // Round 6: far tiles take their updates in batches (chol_persist_update_batch).  Tile (i, j)'s worker steps are
 // [k0, e) — e = j below the diagonal, i − 1 on it (the walker applies step i − 1 to its own D); the last `window`
@@ -2900,7 +2903,9 @@ void set_chol_batch(int batch, int window) {
 #else
 constexpr int g_chol_batch = -1, g_chol_window = -1;
 #endif
-constexpr int kCholBatch = 4;
+// batch 16, window 4: N = 3000 0.910 ms (1 / 0: 1.045; 8 / 4: 0.932; 32 / 4: 1.011; 16 / 2: 0.979), N = 5000 2.358 ms
+// (profiles/r06_d_chol_sweep.txt, r06_e_chol_sweep.txt)
+constexpr int kCholBatch = 16;
 constexpr int kCholWindow = 4;
 
 struct CholTaskTab {

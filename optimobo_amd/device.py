@@ -80,7 +80,7 @@ class AcqContext:
                 "fused_chain": _lib.DEBUG_FUSED_CHAIN, "argmax_passes": _lib.DEBUG_ARGMAX_PASSES,
                 "chol_mode": _lib.DEBUG_CHOL_MODE, "timing_stride": _lib.DEBUG_TIMING_STRIDE,
                 "cov_fused": _lib.DEBUG_COV_FUSED,
-                "select_seq": _lib.DEBUG_SELECT_SEQ}[what]
+                "select_seq": _lib.DEBUG_SELECT_SEQ, "syrk_glds": _lib.DEBUG_SYRK_GLDS}[what]
         self._check(self.lib.omb_debug_set(self._h, code, int(value)), "omb_debug_set")
 
     # ------------------------------------------------------------------ GP state

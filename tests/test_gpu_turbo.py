@@ -88,6 +88,30 @@ def test_posterior_cov_fused_epilogue_bitwise(ctx, n, d, N, kernel):
     np.testing.assert_allclose(Y1.cpu().numpy(), Y0.cpu().numpy(), rtol=0, atol=1e-8 * np.sqrt(var))
 
 
+@pytest.mark.parametrize("n,d,N,kernel", [(512, 30, 3000, "matern52"), (32, 6, 66, "rbf"), (160, 6, 1002, "matern52"),
+                                          (48, 3, 64, "matern52"), (47, 3, 200, "matern52"), (64, 4, 201, "rbf")])
+def test_posterior_cov_syrk_glds_bitwise(ctx, n, d, N, kernel):
+    """Round 6, OMB_DEBUG_SYRK_GLDS: the covariance SYRK with its operands staged by direct-to-LDS loads three slabs
+    deep against the register-staged two-slab pipeline — the same products in the same k order and the same epilogue,
+    so Σ is bitwise the same (and so are the draws).  n_train % 16 != 0 or an odd N take the register path either
+    way (the last two shapes)."""
+    X, y, ls, var, og = fit(ctx, n, d, seed=n + d + 11, kernel=kernel)
+    rng = np.random.default_rng(N + 5)
+    Xc = dev(np.clip(X[0] + 0.4 * (rng.uniform(0, 1, (N, d)) - 0.5), 0, 1))
+    Z = dev(rng.standard_normal((8, N)))
+    mu1, cov1 = ctx.posterior_cov(0, Xc)
+    Y1, j1 = ctx.posterior_samples(0, Xc, Z)
+    ctx.debug_set("syrk_glds", 0)
+    try:
+        mu0, cov0 = ctx.posterior_cov(0, Xc)
+        Y0, j0 = ctx.posterior_samples(0, Xc, Z)
+    finally:
+        ctx.debug_set("syrk_glds", 1)
+    assert torch.equal(mu1, mu0)
+    assert np.array_equal(np.tril(cov1.cpu().numpy()), np.tril(cov0.cpu().numpy()))
+    assert j1 == j0 and torch.equal(Y1, Y0)
+
+
 # ----------------------------------------------------------------------------- Cholesky
 def spd(N, seed):
     rng = np.random.default_rng(seed)
@@ -95,18 +119,19 @@ def spd(N, seed):
     return G @ G.T / N + 0.5 * np.eye(N)
 
 
-@pytest.fixture(params=[0, 1, 2, 4, 5, 6], ids=["auto", "steps", "persistent", "auto-ar", "steps-ar", "persistent-ar"])
+@pytest.fixture(params=[0, 1, 8, 4, 5, 12], ids=["auto", "steps", "persistent-single", "auto-ar", "steps-ar",
+                                                 "persistent-single-ar"])
 def chol_mode(ctx, request):
-    """omb_debug_set(CHOL_MODE): the default schedule (per-step launches, then one persistent launch for the last 32
-    steps), the per-step launches, the whole factorisation in one persistent launch (mode 2 used to be
-    the default schedule again); + 4: the same schedule with release / acquire hand-offs."""
+    """omb_debug_set(CHOL_MODE): the default schedule (round 6: the whole factorisation in one persistent launch, far
+    tiles' trailing updates batched), the per-step launches, the persistent launch with one task per trailing update
+    (round 5's table, + 8); + 4: the same schedule with release / acquire hand-offs."""
     ctx.debug_set("chol_mode", request.param)
     yield request.param
     ctx.debug_set("chol_mode", 0)
 
 
-# 2048 / 2049 / 2112 / 2113: 32, 33, 33 and 34 steps — the default schedule's hand-over from per-step launches to the
-# persistent launch at k0 = 0, 1, 1, 2 (max(0, steps − 32))
+# 2048 / 2049 / 2112 / 2113: 32, 33, 33 and 34 steps — round 5's hand-over from per-step launches to the persistent
+# launch (k0 = 0, 1, 1, 2); kept as sizes where the batched far updates' windows and batches meet the last steps
 @pytest.mark.parametrize("N", [1, 2, 63, 64, 65, 130, 192, 193, 333, 1000, 2048, 2049, 2112, 2113, 3000])
 def test_cholesky_vs_lapack(ctx, chol_mode, N):
     A = spd(N, N)
@@ -173,12 +198,12 @@ def test_cholesky_randomized_stress(ctx, chol_mode):
         assert np.array_equal(got, first)
 
 
-@pytest.mark.parametrize("mode", [0, 2], ids=["auto", "persistent"])
+@pytest.mark.parametrize("mode", [0, 4], ids=["auto", "auto-ar"])
 def test_cholesky_batched_updates_bitwise_single_steps(ctx, mode):
     """Round 6: the persistent launch's workers take a far tile's trailing updates in batches of steps (one A-tile
     round trip per batch); each step's product is still summed from zero and subtracted in step order, so the factor
-    is bitwise the one-task-per-step schedule's (OMB_DEBUG_CHOL_MODE + 8) — at sizes with 3 … 65 block columns, under
-    the default hybrid (per-step launches first) and the pure persistent launch."""
+    is bitwise the one-task-per-step schedule's (OMB_DEBUG_CHOL_MODE + 8) — at sizes with 3 … 65 block columns, with
+    the default hand-offs and with release / acquire ones."""
     for N in [130, 333, 700, 1500, 2113, 3000, 4097]:
         A = spd(N, 77 + N)
         ctx.debug_set("chol_mode", mode)

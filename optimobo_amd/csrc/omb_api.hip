@@ -954,15 +954,21 @@ static hipError_t cov_prepare(omb_ctx* ctx, const ObjState& s, const double* Xc,
 
 // lower triangle of Σ = K(X*, X*) − VᵀV (GPy PosteriorExact._raw_predict, full_cov=True); cws:
 // cand_cov_ws_doubles(N, DP) doubles.
+// zero_ints / n_zero / zero_info: the next Cholesky's sync words and status, zeroed by the fused SYRK's workgroups on
+// the side (*zeroed = true when it did: that factorisation then skips its init launch)
 static hipError_t cov_build(omb_ctx* ctx, const ObjState& s, const double* Xc, int64_t N, const double* V, double* S,
-                            int64_t lds, double* cws, double jitter = 0.0, bool prescaled = false) {
+                            int64_t lds, double* cws, double jitter = 0.0, bool prescaled = false,
+                            int* zero_ints = nullptr, int n_zero = 0, int* zero_info = nullptr, bool* zeroed = nullptr) {
+  if (zeroed) *zeroed = false;
   if (cov_fused_path(ctx, s)) {
     // K(X*, X*) formed in the SYRK's epilogue (launch_cov_syrk): the two-launch result below to the ulp
     hipError_t e = hipSuccess;
     const int kp = prescaled ? (s.DP + 3) / 4 * 4 : launch_cand_scale(ctx->stream, s.dev, s.d, s.DP, Xc, N, cws, &e);
-    if (e == hipSuccess && kp > 0)
+    if (e == hipSuccess && kp > 0) {
+      if (zeroed) *zeroed = zero_ints != nullptr;
       return launch_cov_syrk(ctx->stream, N, s.n, V, N, S, lds, cws, cws + N * kp, kp, s.kind, s.variance, jitter,
-                             ctx->syrk_glds);
+                             ctx->syrk_glds, zero_ints, n_zero, zero_info);
+    }
     if (e != hipSuccess) return e;
   }
   hipError_t e = launch_cand_cov(ctx->stream, s.dev, s.d, s.DP, Xc, N, S, lds, cws, jitter, ctx->cov_table);
@@ -974,15 +980,24 @@ static hipError_t cov_build(omb_ctx* ctx, const ObjState& s, const double* Xc, i
 // The factorisation in two halves, so that a caller can queue work that reads the factor before it waits for the
 // status: chol_enqueue queues A += jitter·I, the factor and the status's copy into pinned memory; chol_wait
 // synchronises and reads it.
-static int chol_enqueue(omb_ctx* ctx, double* A, int64_t N, int64_t lda, double jitter) {
-  // [info int | pad to 16 B | factor workspace (chol_ws_doubles)]
+// The factorisation workspace: [info int | pad to 16 B | factor workspace (chol_ws_doubles)]
+static int chol_workspace(omb_ctx* ctx, int64_t N, int** dinfo, double** ws) {
   int rc = grow_dev(ctx, &ctx->ichol, &ctx->ichol_cap, 16 + sizeof(double) * chol_ws_doubles(N), "Cholesky workspace");
   if (rc) return rc;
-  int* dinfo = static_cast<int*>(ctx->ichol);
-  double* ws = reinterpret_cast<double*>(static_cast<char*>(ctx->ichol) + 16);
+  *dinfo = static_cast<int*>(ctx->ichol);
+  *ws = reinterpret_cast<double*>(static_cast<char*>(ctx->ichol) + 16);
+  return OMB_OK;
+}
+
+// sync_zeroed: the persistent launch's sync words and info were zeroed by the covariance SYRK (cov_build)
+static int chol_enqueue(omb_ctx* ctx, double* A, int64_t N, int64_t lda, double jitter, bool sync_zeroed = false) {
+  int* dinfo = nullptr;
+  double* ws = nullptr;
+  int rc = chol_workspace(ctx, N, &dinfo, &ws);
+  if (rc) return rc;
   OMB_HIP(ctx, launch_add_diag(ctx->stream, A, N, lda, jitter));
   OMB_HIP(ctx, launch_cholesky_mode(ctx->stream, A, N, lda, dinfo, ws, ctx->chol_mode, ctx->spin_limit,
-                                    ctx->chol_acq_rel, ctx->chol_single));
+                                    ctx->chol_acq_rel, ctx->chol_single, sync_zeroed));
   OMB_HIP(ctx, hipMemcpyAsync(ctx->info_host, dinfo, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   return OMB_OK;
 }
@@ -1017,7 +1032,7 @@ int omb_posterior_cov(omb_ctx* ctx, int obj, const double* Xc_dev, int64_t N, do
   double* V = Kst + nN;
   double* var = V + nN;
   double* cws = var + N;
-  hipError_t e = cov_prepare(ctx, s, Xc_dev, N, Kst, V, mu_dev, var);
+  hipError_t e = cov_prepare(ctx, s, Xc_dev, N, Kst, V, mu_dev, var, nullptr);
   if (e == hipSuccess) e = cov_build(ctx, s, Xc_dev, N, V, cov_dev, N, cws);
   if (e == hipSuccess) e = launch_mirror_lower(ctx->stream, cov_dev, N, N);
   if (e != hipSuccess) return hip_fail(ctx, e, "posterior_cov");
@@ -1068,12 +1083,20 @@ int omb_posterior_samples(omb_ctx* ctx, int obj, const double* Xc_dev, int64_t N
   const bool prescale = cov_fused_path(ctx, s);
   hipError_t e = cov_prepare(ctx, s, Xc_dev, N, Kst, V, mu, var, prescale ? cws : nullptr);
   if (e != hipSuccess) return hip_fail(ctx, e, "posterior_samples (posterior)");
+  // the factorisation's workspace placed before the covariance build, whose SYRK zeroes its sync words and status
+  int* dinfo = nullptr;
+  double* cws_chol = nullptr;
+  if ((rc = chol_workspace(ctx, N, &dinfo, &cws_chol))) return rc;
+  int* sync_ints = nullptr;
+  const int n_sync = chol_persist_sync_words(cws_chol, N, &sync_ints);
   double jit = jitter_rel * s.variance;
   int info = -1, t = 0;
   for (; t < max_tries; ++t, jit *= 10.0) {
-    if ((e = cov_build(ctx, s, Xc_dev, N, V, S, N, cws, jit, prescale && t == 0)) != hipSuccess)   // Σ + jit·I
+    bool zeroed = false;
+    if ((e = cov_build(ctx, s, Xc_dev, N, V, S, N, cws, jit, prescale && t == 0, sync_ints, n_sync, dinfo, &zeroed)) !=
+        hipSuccess)   // Σ + jit·I
       return hip_fail(ctx, e, "posterior_samples (cov)");
-    if ((rc = chol_enqueue(ctx, S, N, N, 0.0))) return rc;
+    if ((rc = chol_enqueue(ctx, S, N, N, 0.0, zeroed))) return rc;
     // the draws are queued before the status is read (no idle GPU between the factor and them); a failed factor's
     // draws are overwritten by the next try's
     if ((e = launch_chol_samples(ctx->stream, S, N, N, mu, Zt_dev, B, Y_dev, cws)) != hipSuccess)

@@ -41,7 +41,17 @@ struct CovEpi {
   int kind;
   double variance;
   double diag_add;
+  int* zero_ints;   // n_zero words every workgroup's share of which it sets to 0 (the next Cholesky's sync words)
+  int n_zero;
+  int* zero_info;   // set to 0 by workgroup 0 (that Cholesky's status)
 };
+
+// The launch's side job (zero_ints / zero_info), run by every workgroup before any early return
+__device__ __forceinline__ void cov_zero_side(const CovEpi& ce) {
+  const int64_t b = (int64_t)blockIdx.y * gridDim.x + blockIdx.x, nb = (int64_t)gridDim.x * gridDim.y;
+  for (int64_t x = b * blockDim.x + threadIdx.x; x < ce.n_zero; x += nb * blockDim.x) ce.zero_ints[x] = 0;
+  if (ce.zero_info && b == 0 && threadIdx.x == 0) *ce.zero_info = 0;
+}
 
 // KSS epilogue (gemm_kernel, syrk_glds_kernel): C = K(X*, X*) + α·acc on the tile's lower triangle, the kernel block's
 // cross term over kp dimensions in slabs of 16 staged through the LDS scratch As / Bs ([16][pitch] doubles each).
@@ -107,6 +117,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t Nc, int64_
                                                    const double* __restrict__ col_bias, int64_t kchunk,
                                                    int64_t zstride, CovEpi ce,
                                                    const int* __restrict__ tmap = nullptr) {
+  if constexpr (KSS) cov_zero_side(ce);
   // ATRI: the last row tiles carry the most slabs, so they are dispatched first
   int64_t m0 = (int64_t)(ATRI ? gridDim.y - 1 - blockIdx.y : blockIdx.y) * kGT, n0 = (int64_t)blockIdx.x * kGT;
   if (tmap) {   // 1-D grid, workgroup b → tile tmap[b] = (row tile << 16 | column tile), −1: none (syrk_tile_map)
@@ -263,12 +274,28 @@ __global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t Nc, int64_
 // Every LDS byte lives in the one __shared__ array (a second __shared__ object can make hipcc wait vmcnt(0) before
 // each ds_read).  Requires K a multiple of 16 and N even with V 16-B aligned (launch_cov_syrk checks); the products
 // are summed in gemm_kernel's k order, so C is bitwise gemm_kernel<…, KSS>'s.
-constexpr int kSyrkStages = 3;
 __device__ __forceinline__ int syrk_swz(int row, int col) { return ((((col >> 1) ^ ((row & 1) << 3)) << 1) | (col & 1)); }
 
-__global__ __launch_bounds__(256) void syrk_glds_kernel(int64_t N, int64_t K, double alpha, const double* __restrict__ V,
+// s_waitcnt vmcnt(n) for a wave-uniform n ≤ 15 (the immediate is an encoding field)
+__device__ __forceinline__ void wait_vmcnt_le(int n) {
+  switch (n) {
+#define OMB_VMC(X) \
+  case X: asm volatile("s_waitcnt vmcnt(" #X ")" ::: "memory"); break;
+    OMB_VMC(1) OMB_VMC(2) OMB_VMC(3) OMB_VMC(4) OMB_VMC(5) OMB_VMC(6) OMB_VMC(7) OMB_VMC(8) OMB_VMC(9) OMB_VMC(10)
+    OMB_VMC(11) OMB_VMC(12) OMB_VMC(13) OMB_VMC(14) OMB_VMC(15)
+#undef OMB_VMC
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+// STAGES slabs of SR rows in flight, MINB workgroups per CU for the register allocation (the library: 3 × 16, 1;
+// tools/ablate/ablate_syrk times the others)
+template <int STAGES, int SR, int MINB = 1>
+__global__ __launch_bounds__(256, MINB) void syrk_glds_kernel(int64_t N, int64_t K, double alpha, const double* __restrict__ V,
                                                         int64_t ldv, double* __restrict__ C, int64_t ldc, CovEpi ce,
                                                         const int* __restrict__ tmap) {
+  static_assert(SR % 8 == 0 && STAGES >= 2, "slabs of whole 8-row groups (one 2-row piece per wave)");
+  cov_zero_side(ce);
   int64_t m0 = (int64_t)blockIdx.y * kGT, n0 = (int64_t)blockIdx.x * kGT;
   if (tmap) {
     const int code = tmap[blockIdx.x];
@@ -277,34 +304,35 @@ __global__ __launch_bounds__(256) void syrk_glds_kernel(int64_t N, int64_t K, do
     n0 = (int64_t)(code & 0xffff) * kGT;
   }
   if (n0 > m0) return;
-  constexpr int kSlab = kGK * kGT;                          // doubles of one operand's slab
-  __shared__ __attribute__((aligned(16))) double sm[kSyrkStages * 2 * kSlab];
+  constexpr int kSlab = SR * kGT;                           // doubles of one operand's slab
+  constexpr int PPW = SR / 8;                               // 1-KiB pieces (2 rows) per wave per operand and slab
+  __shared__ __attribute__((aligned(16))) double sm[STAGES * 2 * kSlab];
   typedef __attribute__((address_space(3))) void lds_void;
   typedef __attribute__((address_space(1))) const void g_void;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  // this lane's source columns for its pieces p = 2·wave + j (rows 2p, 2p + 1): column pair (lane & 31) ^ 8·(row & 1),
-  // clamped into the matrix (columns past N feed C entries that are never stored)
-  const int prow0 = 4 * wave + (lane >> 5), q = lane & 31;
+  // piece p = PPW·wave + j covers rows 2p, 2p + 1; this lane's source column pair (lane & 31) ^ 8·(row & 1), clamped
+  // into the matrix (columns past N feed C entries that are never stored)
+  const int q = lane & 31;
   int64_t colA[2], colB[2];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int row = prow0 + 2 * j;
-    const int gq = q ^ ((row & 1) << 3);
-    colA[j] = m0 + 2 * gq < N - 1 ? m0 + 2 * gq : N - 2;
-    colB[j] = n0 + 2 * gq < N - 1 ? n0 + 2 * gq : N - 2;
+  for (int par = 0; par < 2; ++par) {                       // row parity of the lane's rows: (lane >> 5) of an even base
+    const int gq = q ^ (par << 3);
+    colA[par] = m0 + 2 * gq < N - 1 ? m0 + 2 * gq : N - 2;
+    colB[par] = n0 + 2 * gq < N - 1 ? n0 + 2 * gq : N - 2;
   }
-  const int ns = (int)(K / kGK);
+  const int par = lane >> 5;
+  const int ns = (int)(K / SR);
   auto issue = [&](int stage, int slab) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int row = prow0 + 2 * j;
-      const double* src = V + ((int64_t)slab * kGK + row) * ldv;
-      double* dA = sm + (stage * 2 + 0) * kSlab + (4 * wave + 2 * j) * kGT;   // wave-uniform: rows 2p, 2p + 1
-      double* dB = sm + (stage * 2 + 1) * kSlab + (4 * wave + 2 * j) * kGT;
-      __builtin_amdgcn_global_load_lds((g_void*)(src + colA[j]), (lds_void*)dA, 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((g_void*)(src + colB[j]), (lds_void*)dB, 16, 0, 0);
+    for (int j = 0; j < PPW; ++j) {
+      const int r0 = 2 * (PPW * wave + j);                  // even: the lane's row is r0 + par
+      const double* src = V + ((int64_t)slab * SR + r0 + par) * ldv;
+      double* dA = sm + (stage * 2 + 0) * kSlab + r0 * kGT;   // wave-uniform
+      double* dB = sm + (stage * 2 + 1) * kSlab + r0 * kGT;
+      __builtin_amdgcn_global_load_lds((g_void*)(src + colA[par]), (lds_void*)dA, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((g_void*)(src + colB[par]), (lds_void*)dB, 16, 0, 0);
     }
   };
   d4 acc[2][2];
@@ -312,22 +340,21 @@ __global__ __launch_bounds__(256) void syrk_glds_kernel(int64_t N, int64_t K, do
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
-  if (ns > 0) issue(0, 0);
-  if (ns > 1) issue(1, 1);
+#pragma unroll
+  for (int st = 0; st < STAGES - 1; ++st)
+    if (st < ns) issue(st, st);
   for (int sl = 0; sl < ns; ++sl) {
-    // slab sl's four DMAs of this wave retired (sl + 1's four may stay in flight), then every wave's
-    if (sl + 1 < ns)
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // slab sl's DMAs of this wave retired (the later ones already issued may stay in flight), then every wave's
+    const int later = ns - 1 - sl < STAGES - 2 ? ns - 1 - sl : STAGES - 2;
+    wait_vmcnt_le(2 * PPW * later);
     __builtin_amdgcn_s_barrier();
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    // stage (sl + 2) % 3 was last read by slab sl − 1, which every wave has finished (the barrier above)
-    if (sl + 2 < ns) issue((sl + 2) % kSyrkStages, sl + 2);
-    const double* As = sm + ((sl % kSyrkStages) * 2 + 0) * kSlab;
-    const double* Bs = sm + ((sl % kSyrkStages) * 2 + 1) * kSlab;
+    // the stage slab sl + STAGES − 1 refills was last read by slab sl − 1, which every wave has finished
+    if (sl + STAGES - 1 < ns) issue((sl + STAGES - 1) % STAGES, sl + STAGES - 1);
+    const double* As = sm + ((sl % STAGES) * 2 + 0) * kSlab;
+    const double* Bs = sm + ((sl % STAGES) * 2 + 1) * kSlab;
 #pragma unroll
-    for (int ks = 0; ks < kGK / 4; ++ks) {
+    for (int ks = 0; ks < SR / 4; ++ks) {
       const int kk = 4 * ks + (lane >> 4);
       const double a0 = As[kk * kGT + syrk_swz(kk, 32 * wm + (lane & 15))];
       const double a1 = As[kk * kGT + syrk_swz(kk, 32 * wm + 16 + (lane & 15))];
@@ -340,9 +367,10 @@ __global__ __launch_bounds__(256) void syrk_glds_kernel(int64_t N, int64_t K, do
     }
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
   }
-  // the epilogue's cross-term scratch: stage 0's A / B tiles ([16][64], after its barrier)
+  // the epilogue's cross-term scratch: stage 0's A / B tiles (16 of their rows, after the epilogue's first barrier)
   cov_epilogue(m0, n0, N, N, acc, alpha, ce, C, ldc, sm, sm + kSlab, kGT);
 }
+constexpr int kSyrkStages = 3, kSyrkRows = 16;
 
 template <bool TA, bool TB, bool BTRI, bool LOWER, bool ATRI = false>
 static hipError_t gemm(hipStream_t stream, int64_t M, int64_t Nc, int64_t K, double alpha, const double* A,
@@ -514,21 +542,22 @@ constexpr bool g_syrk_xcd_map = true;
 
 hipError_t launch_cov_syrk(hipStream_t s, int64_t N, int64_t K, const double* V, int64_t ldv, double* S, int64_t lds,
                            const double* xs, const double* xsq, int kp, int kind, double variance, double diag_add,
-                           bool glds) {
+                           bool glds, int* zero_ints, int n_zero, int* zero_info) {
   if (N <= 0) return hipSuccess;
   const int T = (int)((N + kGT - 1) / kGT);
   int g1 = 0;
   const int* tmap = g_syrk_xcd_map ? xcd_tile_map(kMapSyrk, T, T, &g1) : nullptr;
   const dim3 grid = tmap ? dim3((unsigned)g1) : dim3((unsigned)T, (unsigned)T);
   // the direct-to-LDS pipeline needs whole 16-row slabs and 16-B column pairs inside each row
-  if (glds && K % kGK == 0 && N % 2 == 0 && N >= 2 && ldv % 2 == 0 && (reinterpret_cast<uintptr_t>(V) & 15) == 0) {
-    hipLaunchKernelGGL(syrk_glds_kernel, grid, dim3(256), 0, s, N, K, -1.0, V, ldv, S, lds,
-                       CovEpi{xs, xsq, kp, kind, variance, diag_add}, tmap);
+  if (glds && K % kSyrkRows == 0 && N % 2 == 0 && N >= 2 && ldv % 2 == 0 &&
+      (reinterpret_cast<uintptr_t>(V) & 15) == 0) {
+    hipLaunchKernelGGL((syrk_glds_kernel<kSyrkStages, kSyrkRows>), grid, dim3(256), 0, s, N, K, -1.0, V, ldv, S, lds,
+                       CovEpi{xs, xsq, kp, kind, variance, diag_add, zero_ints, n_zero, zero_info}, tmap);
     return hipGetLastError();
   }
   hipLaunchKernelGGL((gemm_kernel<true, false, false, true, false, true>), grid, dim3(256), 0, s, N, N, K, -1.0, V, ldv,
                      V, ldv, 0.0, S, lds, (const double*)nullptr, (int64_t)0, (int64_t)0,
-                     CovEpi{xs, xsq, kp, kind, variance, diag_add}, tmap);
+                     CovEpi{xs, xsq, kp, kind, variance, diag_add, zero_ints, n_zero, zero_info}, tmap);
   return hipGetLastError();
 }
 

@@ -137,9 +137,11 @@ int launch_cand_scale(hipStream_t stream, const GPDev& g, int d, int DP, const d
 // lower triangle of S = K(X*, X*) + diag_add·I − VᵀV, V (K, N): the covariance SYRK with K(X*, X*) formed in its
 // epilogue from launch_cand_scale's rows (omb_gemm.hip gemm_kernel<…, KSS>; glds: syrk_glds_kernel, the three-stage
 // direct-to-LDS operand pipeline, where K % 16 = 0 and N, ldv even — bitwise the same C)
+// zero_ints (n_zero ints) and zero_info: words the launch's workgroups set to 0 on the side (the next persistent
+// Cholesky's sync words and status), so that factorisation needs no init launch
 hipError_t launch_cov_syrk(hipStream_t s, int64_t N, int64_t K, const double* V, int64_t ldv, double* S, int64_t lds,
                            const double* xs, const double* xsq, int kp, int kind, double variance, double diag_add,
-                           bool glds = true);
+                           bool glds = true, int* zero_ints = nullptr, int n_zero = 0, int* zero_info = nullptr);
 hipError_t launch_mirror_lower(hipStream_t stream, double* S, int64_t N, int64_t lds);
 hipError_t launch_add_diag(hipStream_t stream, double* S, int64_t N, int64_t lds, double v);
 // in-place lower Cholesky; info (device int, zeroed by the first kernel) = first bad column (1-based);
@@ -166,8 +168,12 @@ hipError_t launch_cholesky(hipStream_t stream, double* A, int64_t N, int64_t lda
 // model's form; the default relaxed / sc1 form is measured valid on gfx950 and checked bitwise against this one).
 // single_steps = 1: the persistent launch's workers take every trailing update as its own task (round 5's table; the
 // default batches far tiles' updates, bitwise the same factor — checked against this one)
+// sync_zeroed: the persistent launch's sync words (chol_persist_sync_words) and info are already zero (written by the
+// covariance SYRK of the Thompson chain), so the k0 = 0 persistent launch goes without its init kernel
 hipError_t launch_cholesky_mode(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws, int mode,
-                                int spin_limit = kDefaultSpinLimit, int acq_rel = 0, int single_steps = 0);
+                                int spin_limit = kDefaultSpinLimit, int acq_rel = 0, int single_steps = 0,
+                                bool sync_zeroed = false);
+int chol_persist_sync_words(double* ws, int64_t N, int** ints);
 // Y (B, N) = μ + Zt Lᵀ (L lower, N×N): row b of Y is the sample μ + L z_b.
 // ws: chol_samples_ws_doubles(N, B) device doubles (split-K partial products; 0 when unsplit).
 int64_t chol_samples_ws_doubles(int64_t N, int B);

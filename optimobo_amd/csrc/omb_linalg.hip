@@ -2773,6 +2773,14 @@ int64_t chol_ws_doubles(int64_t N) {
   return launches > persist ? launches : persist;
 }
 
+// The persistent launch's sync words inside ws (chol_persist_kernel's layout; all zero before a k0 = 0 launch, which
+// chol_persist_init_kernel or, in the Thompson chain, the covariance SYRK writes)
+int chol_persist_sync_words(double* ws, int64_t N, int** ints) {
+  const int t = (int)((N + kNB - 1) / kNB);
+  *ints = reinterpret_cast<int*>(ws + (int64_t)t * kCholWsDoubles);
+  return t + 2 * t * t + 2;
+}
+
 struct CholPersistInit {
   int* ints = nullptr;   // the persistent launch's sync words (nullptr: none to write)
   int t = 0, k0 = 0;
@@ -2973,7 +2981,8 @@ static const int* chol_task_table(int t, int k0, int L, int batch, int window, i
 // k0 > 0: steps 0 .. k0 − 1 as per-step launches (their bulk trailing updates run at three workgroups per CU), the
 // rest in one persistent launch (the diagonal walk without kernel boundaries once the trailing matrix is small).
 static hipError_t launch_cholesky_persist(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws,
-                                          int spin_limit, int k0 = 0, int acq_rel = 0, int single_steps = 0) {
+                                          int spin_limit, int k0 = 0, int acq_rel = 0, int single_steps = 0,
+                                          bool sync_zeroed = false) {
   const int t = (int)((N + kNB - 1) / kNB);
   if (k0 > t - 2) k0 = 0;
   hipError_t e = hipSuccess;
@@ -2991,7 +3000,7 @@ static hipError_t launch_cholesky_persist(hipStream_t stream, double* A, int64_t
   const int* tab = L > 0 ? chol_task_table(t, k0, L, batch, window, &tab_total) : nullptr;
   if (tab) total = tab_total;
   CholSync sync{ints, ints + t, ints + t + t * t, ints + t + 2 * t * t, ints + t + 2 * t * t + 1, tab};
-  if (k0 == 0) {   // with k0 > 0 step 0's panel launch wrote the sync words
+  if (k0 == 0 && !sync_zeroed) {   // with k0 > 0 step 0's panel launch wrote the sync words
     hipLaunchKernelGGL(chol_persist_init_kernel, dim3(1), dim3(256), 0, stream, ints, t, k0, info);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
@@ -3007,18 +3016,18 @@ static hipError_t launch_cholesky_persist(hipStream_t stream, double* A, int64_t
 }
 
 hipError_t launch_cholesky_mode(hipStream_t stream, double* A, int64_t N, int64_t lda, int* info, double* ws, int mode,
-                                int spin_limit, int acq_rel, int single_steps) {
+                                int spin_limit, int acq_rel, int single_steps, bool sync_zeroed) {
   if (N <= 0) return hipSuccess;
   if (mode == kCholAuto) mode = kCholPersistent;
   if (mode == kCholPersistOnly) {
     if (chol_persist_fits(N, lda))
-      return launch_cholesky_persist(stream, A, N, lda, info, ws, spin_limit, 0, acq_rel, single_steps);
+      return launch_cholesky_persist(stream, A, N, lda, info, ws, spin_limit, 0, acq_rel, single_steps, sync_zeroed);
     mode = kCholBlocked;
   }
   if (mode == kCholPersistent) {
     if (chol_persist_fits(N, lda))
       return launch_cholesky_persist(stream, A, N, lda, info, ws, spin_limit, chol_hybrid_k0((int)((N + kNB - 1) / kNB)),
-                                     acq_rel, single_steps);
+                                     acq_rel, single_steps, sync_zeroed);
     mode = kCholBlocked;
   }
   if (acq_rel && mode == kCholBlocked) mode = kCholBlockedAcqRel;

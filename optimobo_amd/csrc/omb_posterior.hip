@@ -901,7 +901,8 @@ __global__ __launch_bounds__(64 * NW, WPE) void posterior_kernel(GPArgs args, co
     // A (L⁻¹) k-step pairs are loaded PD pairs ahead of their MFMAs into a register ring (the sp
     // loop is fully unrolled, so ring indices are static).  With 2 waves per SIMD the ring hides
     // the L2 latency; with 4 the other waves do and the registers are worth more as occupancy.
-    constexpr int PD = (NW == 8) ? ((ABL & 64) ? 2 : 1) : 0;   // PD 2 measured no faster (11.19 vs 11.16 ms)
+    // PD 2 measured no faster (11.19 vs 11.16 ms); at 6 waves per SIMD (WPE, round 6) the other waves hide the latency
+    constexpr int PD = (NW == 8 && WPE <= 2) ? ((ABL & 64) ? 2 : 1) : 0;
     d2 a_ring[PD + 1][RT];
     auto load_a = [&](int sp, d2* dst) {
 #pragma unroll
@@ -1529,9 +1530,18 @@ static hipError_t launch_posterior_dp(hipStream_t stream, const GPArgs& args, in
   } else if (RTneed <= 2) {
     // 128 < n ≤ 256: 32-candidate blocks on the counter ring (48 KiB, several workgroups per CU);
     // tools/ablate at n = 256, 3 objectives, 2^17 candidates: 0.709 ms (CT 4, barrier) → 0.641 ms;
-    // the whole-tile kernel (RMAX 16, CT 2) takes 0.688 ms there (profiles/r02_v2_ablate_c4.txt)
+    // the whole-tile kernel (RMAX 16, CT 2) takes 0.688 ms there (profiles/r02_v2_ablate_c4.txt).
+    // Round 6: n_var ≤ 8 (51 KiB of LDS) with the register budget of 6 waves per SIMD — three workgroups per CU
+    // instead of two (80 VGPRs, a few spilled, no A-operand prefetch ring: the other waves hide its latency) — ≈ 4%
+    // faster, alternated against the 2-wave build in one process (0.557-0.571 against 0.583-0.593 ms at config 4,
+    // profiles/r06_s_ablate_posterior_c4_wpe6*.txt).  With staged candidates (n_var > 8) the LDS allows two.
     dim3 grid((unsigned)((N + 31) / 32), n_obj);
-    hipLaunchKernelGGL((posterior_kernel<2, 2, DP, KIND, 8, 0>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var);
+    if constexpr (DP <= 8)
+      hipLaunchKernelGGL((posterior_kernel<2, 2, DP, KIND, 8, 0, 6>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu,
+                         var);
+    else
+      hipLaunchKernelGGL((posterior_kernel<2, 2, DP, KIND, 8, 0>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu,
+                         var);
   } else if (RTneed <= 4) {
     dim3 grid((unsigned)((N + 63) / 64), n_obj);
     hipLaunchKernelGGL((posterior_kernel<4, 4, DP, KIND>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var);

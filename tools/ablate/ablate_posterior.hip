@@ -353,13 +353,14 @@ int main(int argc, char** argv) {
   const Variant small256[] = {
       {"(warm-up) library", run<2, 2, 8, 0>},
       {"RT2 CT2 counter ring (library n<=256)", run<2, 2, 8, 0>},
-      {"RT2 CT2 ring, global generation loads", run<2, 2, 8, 262144>},
-      {"RT2 CT2 counter ring (library) 2", run<2, 2, 8, 0>},
-      {"RT2 CT2 ring, global generation loads 2", run<2, 2, 8, 262144>},
-      {"RT2 CT2 counter ring (library) 3", run<2, 2, 8, 0>},
-      {"RT2 CT2 ring, global generation loads 3", run<2, 2, 8, 262144>},
-      {"RT2 CT2 ring, 5 waves/SIMD bound", run<2, 2, 8, 0, 6, 5>},
       {"RT2 CT2 ring, 6 waves/SIMD bound", run<2, 2, 8, 0, 6, 6>},
+      {"RT2 CT2 ring, 5 waves/SIMD bound", run<2, 2, 8, 0, 6, 5>},
+      {"RT2 CT2 counter ring (library) 2", run<2, 2, 8, 0>},
+      {"RT2 CT2 ring, 5 waves/SIMD bound 2", run<2, 2, 8, 0, 6, 5>},
+      {"RT2 CT2 ring, 6 waves/SIMD bound 2", run<2, 2, 8, 0, 6, 6>},
+      {"RT2 CT2 counter ring (library) 3", run<2, 2, 8, 0>},
+      {"RT2 CT2 ring, 6 waves/SIMD bound 3", run<2, 2, 8, 0, 6, 6>},
+      {"RT2 CT2 counter ring (library) 4", run<2, 2, 8, 0>},
   };
 
 

@@ -361,18 +361,21 @@ def load_traffic(n, N, kernel="posterior"):
 
 
 def load_pipe(config, kernel):
-    """FP64-pipe occupancy of a kernel from the committed PMC summary (tools/pmc_pipe.py → profiles/r05_zm_pmc_pipe.json):
-    MFMA-busy and VALU-issue fractions per SIMD (they never co-execute on gfx950), or None."""
-    path = os.path.join(REPO, "profiles", "r05_zm_pmc_pipe.json")
-    try:
-        with open(path) as f:
-            t = json.load(f)
-    except (OSError, ValueError):
-        return None
-    for k, v in t.items():
-        if f"pmc_c{config}:" in k and kernel in k:
-            return {x: v[x] for x in ("mfma_busy_frac", "valu_issue_frac", "fp64_pipe_busy_frac") if x in v} | \
-                {"source": "profiles/r05_zm_pmc_pipe.json (rocprofv3 --pmc, separate passes)"}
+    """FP64-pipe occupancy of a kernel from the committed PMC summaries (tools/pmc_pipe.py): round 6's
+    (profiles/r06_v_pmc_pipe.json: configs 3 and 4 after their occupancy changes) first, then round 5's
+    (profiles/r05_zm_pmc_pipe.json): MFMA-busy and VALU-issue fractions per SIMD (they never co-execute on gfx950),
+    or None."""
+    for name in ("r06_v_pmc_pipe.json", "r05_zm_pmc_pipe.json"):
+        path = os.path.join(REPO, "profiles", name)
+        try:
+            with open(path) as f:
+                t = json.load(f)
+        except (OSError, ValueError):
+            continue
+        for k, v in t.items():
+            if f"pmc_c{config}:" in k and kernel in k:
+                return {x: v[x] for x in ("mfma_busy_frac", "valu_issue_frac", "fp64_pipe_busy_frac") if x in v} | \
+                    {"source": f"profiles/{name} (rocprofv3 --pmc, separate passes)"}
     return None
 
 

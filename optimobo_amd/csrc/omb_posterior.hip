@@ -1543,8 +1543,20 @@ static hipError_t launch_posterior_dp(hipStream_t stream, const GPArgs& args, in
       hipLaunchKernelGGL((posterior_kernel<2, 2, DP, KIND, 8, 0>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu,
                          var);
   } else if (RTneed <= 4) {
-    dim3 grid((unsigned)((N + 63) / 64), n_obj);
-    hipLaunchKernelGGL((posterior_kernel<4, 4, DP, KIND>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var);
+    // 256 < n ≤ 512 (BASELINE config 3).  Round 6: n_var ≤ 8 as 32-candidate blocks (CT 2) in the register budget of
+    // 4 waves per SIMD — two workgroups per CU (118 VGPRs, 51 KiB of LDS each) instead of one 64-candidate workgroup
+    // (214 VGPRs, 100 KiB): one workgroup's prologue, chunk hand-offs and reduction overlap the other's multiply.
+    // Alternated in one process at config 3 (n 512, 2^20 candidates, 2 objectives): 9.57 against 9.97 ms, μ within
+    // 1.2e-14 relative (the per-wave μ partials meet in another order), σ² bitwise (profiles/r06_u_ablate_posterior_c3*.txt).
+    // Wider inputs stage the candidates in LDS and spill at this budget: they keep the 64-candidate kernel.
+    if constexpr (DP <= 8) {
+      dim3 grid((unsigned)((N + 31) / 32), n_obj);
+      hipLaunchKernelGGL((posterior_kernel<4, 2, DP, KIND, 8, 0, 4>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu,
+                         var);
+    } else {
+      dim3 grid((unsigned)((N + 63) / 64), n_obj);
+      hipLaunchKernelGGL((posterior_kernel<4, 4, DP, KIND>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var);
+    }
   } else if (RTneed <= 8) {
     dim3 grid((unsigned)((N + 31) / 32), n_obj);
     hipLaunchKernelGGL((posterior_kernel<8, 2, DP, KIND>), grid, dim3(kBlockThreads), 0, stream, args, Xc, N, mu, var);

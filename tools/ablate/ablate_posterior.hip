@@ -311,30 +311,13 @@ int main(int argc, char** argv) {
   };
   const Variant narrow[] = {
       {"default (ring, MFMA gen)", run<4, 4, 8, 0>},
-      {"global generation loads (262144)", run<4, 4, 8, 262144>},
-      {"default again", run<4, 4, 8, 0>},
-      {"global generation loads again", run<4, 4, 8, 262144>},
-      {"default again", run<4, 4, 8, 0>},
-      {"global A loads, r04 (131072)", run<4, 4, 8, 131072>},
-      {"RT4 CT2 counter ring", run<4, 2, 8, 0>},
-      {"tab64 exp (16384)", run<4, 4, 8, 16384>},
-      {"tab256 + short sqrt (32768)", run<4, 4, 8, 32768>},
-      {"generation only (2)", run<4, 4, 8, 2>},
-      {"tab64 gen only", run<4, 4, 8, 16384 + 2>},
-      {"short sqrt gen only", run<4, 4, 8, 32768 + 2>},
-      {"cross term only (4096)", run<4, 4, 8, 4096>},
-      {"polynomial exp (8192)", run<4, 4, 8, 8192>},
-      {"polynomial exp, gen only", run<4, 4, 8, 8194>},
-      {"VALU gen (2048)", run<4, 4, 8, 2048>},
-      {"A PD=2 (64)", run<4, 4, 8, 64>},
-      {"const A (4)", run<4, 4, 8, 4>},
-      {"barrier pipeline (32)", run<4, 4, 8, 32>},
-      {"VALU gen, libm exp/sqrt", run<4, 4, 8, 2048 + 16>},
-      {"VALU gen, no Matern", run<4, 4, 8, 2048 + 1>},
-      {"VALU gen, no MFMA", run<4, 4, 8, 2048 + 2>},
-      {"16 waves ring", run<2, 4, 16, 0>},
-      {"setprio waves 4-7 (128)", run<4, 4, 8, 128>},
-      {"no sigma_f^2 mul (256)", run<4, 4, 8, 256>},
+      {"RT4 CT2 ring, 4 waves/SIMD bound", run<4, 2, 8, 0, 6, 4>},
+      {"default 2", run<4, 4, 8, 0>},
+      {"RT4 CT2 ring, 4 waves/SIMD bound 2", run<4, 2, 8, 0, 6, 4>},
+      {"RT4 CT2 ring (2 waves/SIMD)", run<4, 2, 8, 0>},
+      {"default 3", run<4, 4, 8, 0>},
+      {"RT4 CT2 ring, 4 waves/SIMD bound 3", run<4, 2, 8, 0, 6, 4>},
+      {"default 4", run<4, 4, 8, 0>},
   };
   // n ≤ 256 (configs 2 and 4): the library launches RT = 2 (n ≤ 256) or 1 (n ≤ 128), CT = 4, barrier pipeline
   const Variant small128[] = {

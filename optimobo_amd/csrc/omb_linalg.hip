@@ -1450,6 +1450,38 @@ __device__ __forceinline__ void chol_persist_update_batch(__amdgpu_buffer_rsrc_t
       }
 }
 
+// Waves [w0, w0 + nw) copy a 64 × 64 tile of A (rows r0.., columns c0..; rows from `rows` on read row rows − 1 and
+// columns from `cols` on column cols − 1 or, 16-B aligned, cols — inside the row's padding, lda being even — values
+// the caller masks) into LDS at pitch kDP with direct-to-LDS loads (round 6, the walker's next tiles).  The
+// padded image is 64 rows of 528 B: with 16-B aligned rows (aligned: lda even, A 16-B aligned) 33 wave instructions of
+// 1 KiB — lane l of instruction m fills 16-B chunk 64m + l, a row's 32 data chunks or its pad chunk (which reads the
+// row's last two doubles again) — else 132 instructions of 4-B pieces.  sc1, as every cross-workgroup read of the
+// persistent launch.  The callers wait vmcnt(0) and pass a barrier.
+__device__ __forceinline__ void chol_dma_tile(const double* __restrict__ src, int64_t lda, int rows, int cols,
+                                              double* lds_dst, bool aligned, int w0, int nw) {
+  typedef __attribute__((address_space(3))) void lds_void;
+  typedef __attribute__((address_space(1))) const void g_void;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) - w0;
+  if (w < 0 || w >= nw) return;
+  if (aligned) {
+    for (int m = w; m < 33; m += nw) {
+      const int chunk = 64 * m + lane, row = chunk / 33, cc = chunk - 33 * row;
+      const int cq = cc < 32 ? cc : 31, cmax = (cols + 1) / 2 - 1;
+      const double* gp = src + (int64_t)(row < rows ? row : rows - 1) * lda + 2 * (cq < cmax ? cq : cmax);
+      __builtin_amdgcn_global_load_lds((g_void*)gp, (lds_void*)(lds_dst + 128 * m), 16, 0, 16);
+    }
+  } else {
+    for (int m = w; m < 132; m += nw) {
+      const int dw = 64 * m + lane, row = dw / 132, cd = dw - 132 * row;
+      const int cq = cd < 128 ? cd : 127, cmax = 2 * cols - 1;
+      const char* gp = reinterpret_cast<const char*>(src + (int64_t)(row < rows ? row : rows - 1) * lda) +
+                       4 * (cq < cmax ? cq : cmax);
+      __builtin_amdgcn_global_load_lds((g_void*)gp, (lds_void*)(lds_dst + 32 * m), 4, 0, 16);
+    }
+  }
+}
+
 // bulk tasks of step k (see above): P(i, k) for i = k+2 .. t−1, then the update tiles by columns
 // k0 > 0 (chol_persist_kernel after k0 per-step launches): step k0's panel column is already in A, so step k0 has
 // only its update tasks
@@ -1480,6 +1512,7 @@ __global__ __launch_bounds__(256, kPersistWgPerCu) void chol_persist_kernel(doub
   __shared__ __attribute__((aligned(16))) double Lp[kNB * kDP];
   __shared__ __attribute__((aligned(16))) double Wl[4 * kWlP];
   __shared__ __attribute__((aligned(16))) double Wfl[kCholWsDoubles];   // the walker's W fragments
+  __shared__ __attribute__((aligned(16))) double PD[kNB * kDP];       // the walker's next diagonal tile (round 6)
   __shared__ int fl[kBlkFlags];
   __shared__ int s_task[2];
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4;
@@ -1512,6 +1545,11 @@ __global__ __launch_bounds__(256, kPersistWgPerCu) void chol_persist_kernel(doub
     }
     load_av(kstart);
     if (tid < kBlkFlags) fl[tid] = 0;
+    // Round 6: the next panel tile and the next diagonal tile reach the walker through LDS (chol_dma_tile: all four
+    // waves, direct-to-LDS) and the panel product reads them there — one load latency for both tiles instead of the
+    // per-lane loads of load_av and chol_persist_panel (walk: panel phase 4.45 → 2.5 µs per step, the wait including
+    // the copies 1.0 → 2.2 µs; N = 3000 0.911-0.922 → 0.895-0.900 ms, profiles/r06_aa_*)
+    const bool aligned = (lda & 1) == 0 && (reinterpret_cast<uintptr_t>(A) & 15) == 0;
     __syncthreads();
     for (int k = kstart; k < t; ++k) {
       OMB_PDBG(0, 1000 * k + 1);
@@ -1554,13 +1592,16 @@ __global__ __launch_bounds__(256, kPersistWgPerCu) void chol_persist_kernel(doub
       OMB_PTIME(8 * k + 1);
       chol64_blocked<kCholDReady>(A, lda, r0, nb, 0, Wf + (int64_t)k * kCholWsDoubles, Ds, Wl, fl, k + 1, Wfl);
       OMB_PDBG(1 + w, 1000 * k + 3);
+      const int64_t rb1 = (int64_t)(k + 1) * kNB;
+      const int rows1 = (int)(N - rb1 < kNB ? N - rb1 : kNB);
       chol_signal<AR>(sync.wflag + k, 1);                           // W_k's fragments (wf_store: sc1) drained
       OMB_PDBG(0, 1000 * k + 4);
       if (w == 0 && (fl[20] || fl[21])) atomicCAS(info, 0, fl[21] ? kCholSpinFault : (int)(r0 + fl[20]));
       if (w == 0) fl[20] = 0;           // read above (wave 0, in order); the next step's writes follow a barrier
       OMB_PTIME(8 * k + 2);
       if (k + 1 < t) {
-        // the next panel tile and the next diagonal tile: both updated through step k − 1 by the workers
+        // the next panel tile and the next diagonal tile: both updated through step k − 1 by the workers, copied into
+        // Lp (free since the D tiles) and PD by all four waves
         if (w == 0) {
           const int i1 = (k + 1) * t;
           if (chol_poll_ge<AR>(sync.cnt + i1 + k, k, sync, spin_limit, info))
@@ -1568,9 +1609,39 @@ __global__ __launch_bounds__(256, kPersistWgPerCu) void chol_persist_kernel(doub
         }
         __syncthreads();
         OMB_PDBG(0, 1000 * k + 5);
+        chol_dma_tile(A + rb1 * lda + (int64_t)k * kNB, lda, rows1, kNB, Lp, aligned, 0, 4);
+        chol_dma_tile(A + rb1 * lda + rb1, lda, rows1, rows1, PD, aligned, 0, 4);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
         OMB_PTIME(8 * k + 3);
-        load_av(k + 1);
-        chol_persist_panel(ra, A, N, lda, k + 1, k, Wfl, Lp);
+        // A_{k+1,k+1}'s lower tiles into av (load_av's mask), and the panel tile L_{k+1,k} = A_{k+1,k} W_kᵀ formed in
+        // place in Lp — each wave reads its 16 rows into registers, then writes the same rows (chol_persist_panel's
+        // product, bitwise)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int row = 16 * w + 4 * e + g, col = 16 * j + c;
+            av[4 * j + e] = (j <= w && row < rows1 && col <= row) ? PD[row * kDP + col] : (row == col ? 1.0 : 0.0);
+          }
+        {
+          double x[16];
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              x[4 * q + u] = 16 * w + c < rows1 ? Lp[(16 * w + c) * kDP + 16 * q + 4 * g + u] : 0.0;
+#pragma unroll
+          for (int jb = 0; jb < 4; ++jb) {
+            d4 pa = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+              if (q < 4 * (jb + 1))
+                pa = __builtin_amdgcn_mfma_f64_16x16x4f64(x[q], Wfl[jb * 16 * 64 + q * 64 + lane], pa, 0, 0, 0);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) Lp[(16 * w + 4 * e + g) * kDP + 16 * jb + c] = pa[e];
+          }
+        }
         // Lp visible to every wave; waves 2 and 3 store the tile to A (32 rows each, sc1) and signal it in the next
         // step, after their D tiles, where they wait for W_00 anyway: the stores' drain (≈ 2.4 µs) stays off the
         // chain that waves 0 and 1 run (consumers wait for 4 = 2 + 2)

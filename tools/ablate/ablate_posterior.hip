@@ -291,33 +291,23 @@ int main(int argc, char** argv) {
   b.var = var;
   const Variant wide[] = {
       {"default RT8 CT2 (MFMA gen)", run<8, 2, 8, 0, 32>},
-      {"buffer generation loads (262144)", run<8, 2, 8, 262144, 32>},
-      {"default again", run<8, 2, 8, 0, 32>},
-      {"buffer generation loads again", run<8, 2, 8, 262144, 32>},
-      {"global A loads, r04 (131072)", run<8, 2, 8, 131072, 32>},
-      {"default again", run<8, 2, 8, 0, 32>},
-      {"global A loads again", run<8, 2, 8, 131072, 32>},
-      {"tab64 exp (16384)", run<8, 2, 8, 16384, 32>},
-      {"tab256 + short sqrt (32768)", run<8, 2, 8, 32768, 32>},
-      {"VALU gen (2048)", run<8, 2, 8, 2048, 32>},
-      {"polynomial exp (8192)", run<8, 2, 8, 8192, 32>},
-      {"const A (4)", run<8, 2, 8, 4, 32>},
-      {"generation only (2)", run<8, 2, 8, 2, 32>},
-      {"VALU generation only (2050)", run<8, 2, 8, 2050, 32>},
-      {"no Matern (1)", run<8, 2, 8, 1, 32>},
-      {"16 waves RT4 CT2 MFMA gen", run<4, 2, 16, 0, 32>},
-      {"16 waves RT4 CT2 VALU gen", run<4, 2, 16, 2048, 32>},
-      {"16 waves generation only", run<4, 2, 16, 2, 32>},
+      {"16 waves RT4 CT2 (4 waves/SIMD)", run<4, 2, 16, 0, 32>},
+      {"RT8 CT1, 4 waves/SIMD bound", run<8, 1, 8, 0, 32, 4>},
+      {"default 2", run<8, 2, 8, 0, 32>},
+      {"16 waves RT4 CT2 2", run<4, 2, 16, 0, 32>},
+      {"RT8 CT1, 4 waves/SIMD bound 2", run<8, 1, 8, 0, 32, 4>},
+      {"default 3", run<8, 2, 8, 0, 32>},
+      {"16 waves RT4 CT2 3", run<4, 2, 16, 0, 32>},
+      {"default 4", run<8, 2, 8, 0, 32>},
   };
   const Variant narrow[] = {
-      {"default (ring, MFMA gen)", run<4, 4, 8, 0>},
-      {"RT4 CT2 ring, 4 waves/SIMD bound", run<4, 2, 8, 0, 6, 4>},
-      {"default 2", run<4, 4, 8, 0>},
-      {"RT4 CT2 ring, 4 waves/SIMD bound 2", run<4, 2, 8, 0, 6, 4>},
-      {"RT4 CT2 ring (2 waves/SIMD)", run<4, 2, 8, 0>},
-      {"default 3", run<4, 4, 8, 0>},
-      {"RT4 CT2 ring, 4 waves/SIMD bound 3", run<4, 2, 8, 0, 6, 4>},
-      {"default 4", run<4, 4, 8, 0>},
+      {"RT4 CT2 4 waves/SIMD (library)", run<4, 2, 8, 0, 6, 4>},
+      {"16 waves RT2 CT4 (1 wg/CU, 4 waves/SIMD)", run<2, 4, 16, 0>},
+      {"RT4 CT2 library 2", run<4, 2, 8, 0, 6, 4>},
+      {"16 waves RT2 CT4 2", run<2, 4, 16, 0>},
+      {"RT4 CT2 library 3", run<4, 2, 8, 0, 6, 4>},
+      {"16 waves RT2 CT4 3", run<2, 4, 16, 0>},
+      {"RT4 CT2 library 4", run<4, 2, 8, 0, 6, 4>},
   };
   // n ≤ 256 (configs 2 and 4): the library launches RT = 2 (n ≤ 256) or 1 (n ≤ 128), CT = 4, barrier pipeline
   const Variant small128[] = {
@@ -334,16 +324,16 @@ int main(int argc, char** argv) {
       {"tile RMAX8 CT4", run_tile<8, 4, 0>},
   };
   const Variant small256[] = {
-      {"(warm-up) library", run<2, 2, 8, 0>},
-      {"RT2 CT2 counter ring (library n<=256)", run<2, 2, 8, 0>},
-      {"RT2 CT2 ring, 6 waves/SIMD bound", run<2, 2, 8, 0, 6, 6>},
-      {"RT2 CT2 ring, 5 waves/SIMD bound", run<2, 2, 8, 0, 6, 5>},
-      {"RT2 CT2 counter ring (library) 2", run<2, 2, 8, 0>},
-      {"RT2 CT2 ring, 5 waves/SIMD bound 2", run<2, 2, 8, 0, 6, 5>},
-      {"RT2 CT2 ring, 6 waves/SIMD bound 2", run<2, 2, 8, 0, 6, 6>},
-      {"RT2 CT2 counter ring (library) 3", run<2, 2, 8, 0>},
-      {"RT2 CT2 ring, 6 waves/SIMD bound 3", run<2, 2, 8, 0, 6, 6>},
-      {"RT2 CT2 counter ring (library) 4", run<2, 2, 8, 0>},
+      {"(warm-up) library", run<2, 2, 8, 0, 6, 6>},
+      {"RT2 CT2 6 waves/SIMD (library)", run<2, 2, 8, 0, 6, 6>},
+      {"RT2 CT2 6w, tab64 exp (16384)", run<2, 2, 8, 16384, 6, 6>},
+      {"RT2 CT1, 8 waves/SIMD bound", run<2, 1, 8, 0, 6, 8>},
+      {"RT2 CT1, 6 waves/SIMD bound", run<2, 1, 8, 0, 6, 6>},
+      {"RT2 CT2 6w library 2", run<2, 2, 8, 0, 6, 6>},
+      {"RT2 CT1, 6 waves/SIMD bound 2", run<2, 1, 8, 0, 6, 6>},
+      {"RT2 CT1, 8 waves/SIMD bound 2", run<2, 1, 8, 0, 6, 8>},
+      {"RT2 CT2 6w, tab64 exp 2", run<2, 2, 8, 16384, 6, 6>},
+      {"RT2 CT2 6w library 3", run<2, 2, 8, 0, 6, 6>},
   };
 
 

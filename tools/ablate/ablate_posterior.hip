@@ -312,15 +312,15 @@ int main(int argc, char** argv) {
   // n ≤ 256 (configs 2 and 4): the library launches RT = 2 (n ≤ 256) or 1 (n ≤ 128), CT = 4, barrier pipeline
   const Variant small128[] = {
       {"reg16 library (warm-up slot)", run_reg<0, 16, true>},
-      {"reg16 r02 staging + ls reload (128)", run_reg<128, 16, true>},
       {"reg16 library", run_reg<0, 16, true>},
-      {"reg16 prefetch next tile (64)", run_reg<64, 16, true>},
-      {"reg16 r02 staging + prefetch (192)", run_reg<192, 16, true>},
-      {"reg16 staging only (1)", run_reg<1, 16, true>},
-      {"reg16 r02 staging only (129)", run_reg<129, 16, true>},
-      {"reg16 gen only (2)", run_reg<2, 16, true>},
-      {"reg16 short sqrt (16)", run_reg<16, 16, true>},
-      {"reg16 library again", run_reg<0, 16, true>},
+      {"ring RT1 CT4, 4 waves/SIMD (2 wg/CU)", run<1, 4, 8, 0, 6, 4>},
+      {"ring RT1 CT2, 6 waves/SIMD (3 wg/CU)", run<1, 2, 8, 0, 6, 6>},
+      {"ring RT1 CT2, 8 waves/SIMD (4 wg/CU)", run<1, 2, 8, 0, 6, 8>},
+      {"reg16 library 2", run_reg<0, 16, true>},
+      {"ring RT1 CT4, 4 waves/SIMD 2", run<1, 4, 8, 0, 6, 4>},
+      {"ring RT1 CT2, 6 waves/SIMD 2", run<1, 2, 8, 0, 6, 6>},
+      {"ring RT1 CT2, 8 waves/SIMD 2", run<1, 2, 8, 0, 6, 8>},
+      {"reg16 library 3", run_reg<0, 16, true>},
       {"tile RMAX8 CT4", run_tile<8, 4, 0>},
   };
   const Variant small256[] = {

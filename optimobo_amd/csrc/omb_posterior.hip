@@ -601,7 +601,7 @@ __global__ __launch_bounds__(512) void kernel_block_persist_kernel(GPDev g, int 
 // operand instead of loading L⁻¹, bit 8 drops the per-chunk barrier (barrier mode only), bit 16
 // uses libm exp/sqrt, bit 32 selects the 2-buffer / block-barrier pipeline instead of the
 // counter-synchronised 3-buffer ring (tools/ablate: 12.03 → 11.23 ms at n = 512, N = 2^20); bit 128
-// gives waves 4-7 static priority 1, bit 256 drops the σ_f² multiply, bit 512 starts the distance
+// gives waves 4-7 static priority 1, bit 524288 applies exp's 2^m by an integer add to the high word (IEXP), bit 256 drops the σ_f² multiply, bit 512 starts the distance
 // chain at ‖x‖² + ‖x*‖² with −2x* pre-scaled (one fma fewer per element), bit 65536 forces a spin
 // bound of 0 on the counter-ring waits (the fault-word path).
 // NW = waves per workgroup (8 or 16): waves w, w+4, w+8, w+12 share a SIMD.
@@ -828,7 +828,7 @@ __global__ __launch_bounds__(64 * NW, WPE) void posterior_kernel(GPArgs args, co
           if constexpr (ABL & 8192)   // ablation: the 17-instruction polynomial exp, two sqrt corrections
             kernel_of_r2_k_x2<KIND>(r2a, r2b, sf2, args.ec, v0, v1);
           else if constexpr (kTab256)
-            matern_r2_tab256_x2<(ABL & 32768) != 0>(r2a, r2b, pm, args.ec, etab, v0, v1);
+            matern_r2_tab256_x2<(ABL & 32768) != 0, (ABL & 524288) != 0>(r2a, r2b, pm, args.ec, etab, v0, v1);
           else
             kernel_of_r2_tab_x2<KIND>(r2a, r2b, pm, args.ec, etab, v0, v1);
           if constexpr (!kAug) {

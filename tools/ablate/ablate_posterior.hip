@@ -302,6 +302,9 @@ int main(int argc, char** argv) {
   };
   const Variant narrow[] = {
       {"RT4 CT2 4 waves/SIMD (library)", run<4, 2, 8, 0, 6, 4>},
+      {"RT4 CT2 library, IEXP", run<4, 2, 8, 524288, 6, 4>},
+      {"RT4 CT2 library 1b", run<4, 2, 8, 0, 6, 4>},
+      {"RT4 CT2 library, IEXP 2", run<4, 2, 8, 524288, 6, 4>},
       {"16 waves RT2 CT4 (1 wg/CU, 4 waves/SIMD)", run<2, 4, 16, 0>},
       {"RT4 CT2 library 2", run<4, 2, 8, 0, 6, 4>},
       {"16 waves RT2 CT4 2", run<2, 4, 16, 0>},
@@ -326,6 +329,9 @@ int main(int argc, char** argv) {
   const Variant small256[] = {
       {"(warm-up) library", run<2, 2, 8, 0, 6, 6>},
       {"RT2 CT2 6 waves/SIMD (library)", run<2, 2, 8, 0, 6, 6>},
+      {"RT2 CT2 6w, IEXP", run<2, 2, 8, 524288, 6, 6>},
+      {"RT2 CT2 6w library 1b", run<2, 2, 8, 0, 6, 6>},
+      {"RT2 CT2 6w, IEXP 2", run<2, 2, 8, 524288, 6, 6>},
       {"RT2 CT2 6w, tab64 exp (16384)", run<2, 2, 8, 16384, 6, 6>},
       {"RT2 CT1, 8 waves/SIMD bound", run<2, 1, 8, 0, 6, 8>},
       {"RT2 CT1, 6 waves/SIMD bound", run<2, 1, 8, 0, 6, 6>},

@@ -508,9 +508,16 @@ __device__ __forceinline__ int chol16_factor(double (&a)[16], double (&x)[16]) {
       dj = 1.0;
     }
     const double y0 = __builtin_amdgcn_rsq(dj);
+#ifndef OMB_CHOL16_POLY2
     const double hd = 0.5 * dj;
     const double y1 = fma(y0, fma(-hd * y0, y0, 0.5), y0);
     const double inv = fma(y1, fma(-hd * y1, y1, 0.5), y1);
+#else
+    // tools (round 6, measured, not kept — DESIGN §11a): one second-order correction, y0 (1 − r/2 + 3r²/8) with
+    // r = d·y0² − 1, 4 dependent operations instead of 6; as accurate (profiles/r06_p2_mb_rsq.txt), N = 3000 0.5% faster
+    const double r = fma(dj * y0, y0, -1.0);
+    const double inv = fma(y0 * r, fma(r, 0.375, -0.5), y0);
+#endif
     if constexpr (j < 15) {
       const double s1 = a1 * inv;
       dj = fma(-s1, s1, ap);
